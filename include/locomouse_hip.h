@@ -1,0 +1,253 @@
+/*
+ * locomouse_hip.h — C-ABI of the MI355X-native LocoMouse per-frame detection path.
+ *
+ * This is the drop-in boundary between host code that keeps the reference's
+ * `LocoMouse` call surface (LocoMouse_class.hpp:169-350, main.cpp:54-82) and the
+ * hand-written gfx950 HIP kernels in liblocomouse_hip.so.  Plain C types only:
+ * no OpenCV, no torch, no HIP types in any signature.
+ *
+ * What each entry point replaces in the reference (paths relative to the
+ * reference root):
+ *
+ *   lm_ctx_create         LocoMouse::LocoMouse  LocoMouse_class.cpp:307-345 (parameters
+ *                         already parsed), LocoMouse_Model ctor :3095-3162 and the
+ *                         geometry of LocoMouse::initializeFeatureLoop :655-769.
+ *   lm_detect_batch       one iteration of the per-frame loop main.cpp:57-80, for n
+ *                         consecutive frames:  readFrame :1273-1333 (+ LocoMouse_TM::
+ *                         readFrame TM.cpp:243-249), cropBoundingBox :1408-1478,
+ *                         detectTail :2541-2767, detectBottomCandidates :771-807 +
+ *                         :841-854 + nmsMax :1610-1747, computeUnaryCostsBottom
+ *                         :873-894 + :1909-1952, computePairwiseCostsBottom :896-919 +
+ *                         :1954-2070, detectSideCandidates :809-838 + :856-870 +
+ *                         peakClustering :1749-1905, matchBottomSideCandidates
+ *                         :999-1267 and storePreviousImage :1508-1513.
+ *   lm_candidate          Candidate (Candidates.hpp:16-34) — byte-identical layout.
+ *   lm_p22d + side arrays P22D (Candidates.hpp:63-105).
+ *   unary / pw_* arrays   MyMat (column-major doubles, MyMat.cpp:64-70) and
+ *                         MATSPARSE (MATLAB CSC, MyMat.cpp:141-178).
+ *   lm_status + lm_last_error   the std::invalid_argument / std::runtime_error
+ *                         exceptions caught at main.cpp:94-101.
+ *
+ * Threading: one context per (device, host thread); a context is not re-entrant.
+ * Results returned through lm_batch_result are owned by the context and stay
+ * valid until the next lm_detect_batch* call on it or lm_ctx_destroy.
+ */
+#ifndef LOCOMOUSE_HIP_H
+#define LOCOMOUSE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LM_ABI_VERSION 1
+#define LM_N_PAWS 4          /* LocoMouse_class.hpp:84 */
+#define LM_N_TAIL_POINTS 15  /* LocoMouse_class.hpp:86 */
+#define LM_N_LISTS 4         /* candidate lists per frame */
+#define LM_N_FEATURES 2      /* paw, snout */
+
+typedef enum {
+  LM_OK = 0,
+  LM_ERR_INVALID_ARGUMENT = 1, /* reference: std::invalid_argument            */
+  LM_ERR_RUNTIME = 2,          /* reference: std::runtime_error / cv asserts  */
+  LM_ERR_HIP = 3               /* HIP runtime failure (no reference analogue) */
+} lm_status;
+
+/* cv::Rect */
+typedef struct {
+  int32_t x, y, width, height;
+} lm_rect;
+
+/* One row of config.yml `location_prior` (LocoMouse_class.cpp:132-145):
+ * [x y max_distance min_x max_x min_y max_y]. */
+typedef struct {
+  double x, y, max_distance, min_x, max_x, min_y, max_y;
+} lm_location_prior;
+
+/* config.yml keys the per-frame path reads (LocoMouse_class.cpp:18-249;
+ * defaults LocoMouse_class.hpp:53-74).  Keys that only feed the whole-video
+ * bounding-box pass (median_filter_size, min_pixel_visible,
+ * moving_average_window) are not part of this path. */
+typedef struct {
+  int32_t conn_comp_connectivity;               /* 4 or 8 */
+  int32_t max_displacement_bottom;
+  int32_t max_displacement_side;
+  int32_t occlusion_grid_spacing_pixels_side;
+  int32_t occlusion_grid_spacing_pixels_bottom;
+  int32_t use_provided_bounding_box;            /* must be 1 (BB pre-pass not on this path) */
+  int32_t transform_gray_values;                /* LUT on the bottom crop mask, :1445-1454 */
+  int32_t reserved0;
+  double side_bottom_min_overlap;
+  double occlusion_grid_max_width;
+  double tail_sub_bounding_box;
+  double alpha_vel_bottom;
+  double alpha_vel_side;
+  double pairwise_occluded_cost;
+  lm_location_prior location_prior[5];          /* rows 0-3 paws, row 4 snout */
+  lm_rect bounding_box_side;                    /* bounding_box_side  (x y w h) */
+  lm_rect bounding_box_bottom;                  /* bounding_box_bottom (x y w h) */
+  float gray_value_transformation[256];         /* used iff transform_gray_values */
+} lm_params;
+
+/* One linear detector (model.yml modelX_view / biasX_view, :3106-3148).
+ * Weights are row-major doubles as read from the model file; they are rounded
+ * to float exactly as cv::filter2D does with a CV_64F kernel on CV_8U input. */
+typedef struct {
+  const double* weights;
+  int32_t rows, cols;
+  double bias;
+} lm_detector;
+
+typedef struct {
+  lm_detector paw_bottom, paw_side;
+  lm_detector snout_bottom, snout_side;
+  lm_detector tail_bottom, tail_side;
+} lm_model;
+
+/* Video/background/calibration description (loadVideo/loadBackground/
+ * loadCalibration/loadFlip, :367-484). */
+typedef struct {
+  int32_t method;                 /* 0 LocoMouse, 1 LocoMouse_TM, 2 LocoMouse_TM_DE (Methods.cpp:3-26) */
+  int32_t flip;                   /* 1 when the side character is 'L' (:471-473) */
+  int32_t video_rows, video_cols; /* raw frame size (channel 0 of the decoded frame) */
+  const uint8_t* background;      /* video_rows x video_cols, row-major, copied at create */
+  int32_t calib_rows, calib_cols; /* N_ROWS x N_COLS of ind_warp_mapping */
+  const int32_t* ind_warp_mapping;/* calib_rows x calib_cols, copied at create */
+  lm_rect view_box_side, view_box_bottom;
+} lm_setup;
+
+/* Geometry derived at create time (initializeFeatureLoop :655-769 and the
+ * LocoMouse_Model pads :3157-3161 incl. the spost_b = spre_b move-assign at :3173). */
+typedef struct {
+  int32_t n_rows, n_cols;
+  int32_t pad_pre_rows, pad_pre_cols, pad_post_rows, pad_post_cols;
+  int32_t ipad_rows, ipad_cols;
+  int32_t spre_b_w, spre_b_h, spost_b_w, spost_b_h;
+  int32_t spre_t_w, spre_t_h, spost_t_w, spost_t_h;
+  lm_rect bb_bottom_mouse, bb_side_mouse;
+  lm_rect bb_bottom_mouse_pad, bb_side_mouse_pad;     /* x,y = 0; placed per frame */
+  lm_rect bb_unpad_mouse_bottom, bb_unpad_mouse_side;
+  lm_rect bb_bottom_tail_pad, bb_unpad_tail_bottom, bb_bottom_tail;
+  lm_rect bb_side_tail_pad, bb_unpad_tail_side;
+  int32_t tail_box_width;
+  int32_t ong_nx, ong_ny;                             /* ONG_size */
+  double ong_br_x, ong_br_y;                          /* ONG_BR_corner */
+  int32_t n_ong_side, ong_side_lowest;
+  lm_rect match_box_paw_bottom, match_box_paw_side;   /* LocoMouse_Feature :2954-2969 */
+  lm_rect match_box_snout_bottom, match_box_snout_side;
+} lm_geometry;
+
+/* Candidate: {Point_<int> p; double s;} — x@0, y@4, score@8 (16 bytes). */
+typedef struct {
+  int32_t x, y;
+  double score;
+} lm_candidate;
+
+/* P22D: bottom candidate + the raw yt/st vectors (always >= 1 entry; the
+ * "no side match" state is st[0] < 0, Candidates.cpp:148-156). */
+typedef struct {
+  lm_candidate bottom;
+  int32_t side_offset;  /* into side_y / side_s */
+  int32_t side_count;   /* yt.size() */
+} lm_p22d;
+
+/* Per-batch results, in frame order.  List k of frame f (k: 0 bottom paw,
+ * 1 bottom snout, 2 side paw, 3 side snout) is cand[cand_offset[4f+k] ..
+ * cand_offset[4f+k+1]).  Feature k (0 paw, 1 snout) of frame f owns
+ * p22d[p22d_offset[2f+k] ..), unary[unary_offset[2f+k] ..) (column-major,
+ * N_cand x 4 for paws, N_cand x 1 for the snout) and one MATSPARSE when its
+ * global frame index is > 0 (pw_dims[3(2f+k)+0] = n_rows, +1 = n_cols,
+ * +2 = nnz; n_rows = -1 when absent).  tail holds 3x15 int32 per frame
+ * (rows x, y, z; -1 = missing). */
+typedef struct {
+  int32_t n_frames;
+  int32_t first_frame;
+  const int64_t* cand_offset;   /* [4n+1] */
+  const lm_candidate* cand;
+  const int64_t* p22d_offset;   /* [2n+1] */
+  const lm_p22d* p22d;
+  const int32_t* side_y;
+  const double* side_s;
+  const int64_t* unary_offset;  /* [2n+1] */
+  const double* unary;
+  const int32_t* pw_dims;       /* [2n][3] */
+  const int64_t* pw_jc_offset;  /* [2n+1] */
+  const int32_t* pw_jc;
+  const int64_t* pw_nz_offset;  /* [2n+1] */
+  const int32_t* pw_ir;
+  const double* pw_pr;
+  const int32_t* tail;          /* [n][3][15] */
+} lm_batch_result;
+
+typedef struct lm_ctx lm_ctx;
+
+/* Library identity. */
+int32_t lm_abi_version(void);
+
+/* Error text of the last failing call on this thread (create errors
+ * included).  Never NULL. */
+const char* lm_last_error(void);
+
+/* Create a context on HIP device `device`.  Copies background, calibration and
+ * model weights to the device.  max_batch bounds n in lm_detect_batch*.
+ * Fails with LM_ERR_INVALID_ARGUMENT on the reference's validation errors
+ * (:35-249, :486-540, :3097-3140) and on use_provided_bounding_box == 0. */
+lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_params* params,
+                        const lm_model* model, int32_t max_batch, lm_ctx** out);
+void lm_ctx_destroy(lm_ctx* ctx);
+
+lm_status lm_get_geometry(const lm_ctx* ctx, lm_geometry* out);
+
+/* The ctx's HIP stream (hipStream_t as void*), for event timing by callers. */
+void* lm_ctx_stream(lm_ctx* ctx);
+
+/* Run frames [first_frame, first_frame + n) through the per-frame path.
+ * frames: host memory, n raw frames of video_rows x video_cols u8 at
+ * frame_pitch bytes apart.  bb: NULL for the provided bounding box (the only
+ * mode on this path), else per-frame bottom-right corners [n'][3] = {x,
+ * y_bottom, y_side} (LocoMouse_class.cpp:547-557), n' = n (+1 if prev_frame).
+ * prev_frame: the raw frame first_frame-1 when the context did not process it
+ * in its previous call (shard start); it is run as a 1-frame halo and its own
+ * results are not returned.  NULL continues from the context state (or starts
+ * the video when first_frame == 0). */
+lm_status lm_detect_batch(lm_ctx* ctx, const uint8_t* frames, int64_t frame_pitch,
+                          int32_t n, int32_t first_frame, const uint8_t* prev_frame,
+                          const int32_t* bb, lm_batch_result* out);
+
+/* Same, with frames (and prev_frame) already resident in device memory of the
+ * context's device.  Results are copied back to host memory owned by ctx. */
+lm_status lm_detect_batch_device(lm_ctx* ctx, const uint8_t* d_frames, int64_t frame_pitch,
+                                 int32_t n, int32_t first_frame, const uint8_t* d_prev_frame,
+                                 const int32_t* bb, lm_batch_result* out);
+
+/* ---- diagnostics (parity tests and benchmarks; not part of the reference surface) ---- */
+
+/* flags: bit 0 keep raw filter2D score maps of the last batch;
+ *        bit 1 record per-kernel HIP event timings. */
+lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags);
+
+/* Copy the raw correlation scores (before masking) of detector det
+ * (0 paw_b, 1 snout_b, 2 tail_b, 3 paw_s, 4 snout_s, 5 tail_s) for frame
+ * index f of the last batch: UNPAD region, row-major, rows x cols floats. */
+lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out, int32_t rows, int32_t cols);
+
+/* Copy the bottom TAIL_MASK (0/255, tail_box_width x bottom height) of frame f. */
+lm_status lm_debug_tail_mask(lm_ctx* ctx, int32_t f, uint8_t* out, int32_t rows, int32_t cols);
+
+/* Kernel timings of the last batch when debug bit 1 is set: fills up to cap
+ * (name, milliseconds) pairs; returns the number of kernels. */
+int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32_t cap);
+
+/* Benchmark/test input utility (not a reference interface): writes frames
+ * [first_frame, first_frame + n) of the synthetic scene of include/lm_synth.h
+ * (rows x cols u8, frame_pitch bytes apart) into device memory of `device`. */
+lm_status lm_synth_frames_device(int32_t device, uint8_t* d_out, int32_t rows, int32_t cols, int64_t first_frame,
+                                 int32_t n, int64_t frame_pitch);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LOCOMOUSE_HIP_H */

@@ -1,0 +1,122 @@
+/*
+ * lm_device.h — layouts shared by the gfx950 kernels (lm_kernels.hip) and the
+ * host runtime (lm_runtime.hip).
+ *
+ * Device-memory layout of one batch ("slots"): slot 0 is the previous frame
+ * (carried from the last batch or run as a 1-frame halo), slots 1..B are the
+ * frames of the batch.  Everything per slot is laid out slot-major so one
+ * launch covers a whole batch.
+ */
+#ifndef LM_DEVICE_H
+#define LM_DEVICE_H
+
+#include <stdint.h>
+
+// Correlation tile: 256 threads as 16 x 16, each LM_C x LM_R outputs.
+#define LM_C 5
+#define LM_R 3
+#define LM_TW (16 * LM_C)  // 80
+#define LM_TH (16 * LM_R)  // 48
+#define LM_JC 4            // tap chunk along a detector row (kw padded to a multiple)
+
+#define LM_NDET 6
+#define LM_NLIST 4
+#define LM_NFEAT 2
+
+// detector ids (also debug ids of lm_debug_scores)
+enum { DET_PAW_B = 0, DET_SNOUT_B = 1, DET_TAIL_B = 2, DET_PAW_S = 3, DET_SNOUT_S = 4, DET_TAIL_S = 5 };
+// list ids (lm_batch_result order)
+enum { LIST_PAW_B = 0, LIST_SNOUT_B = 1, LIST_PAW_S = 2, LIST_SNOUT_S = 3 };
+
+struct LmDet {
+  int32_t view;      // 0 bottom, 1 side
+  int32_t kind;      // 0 point detector (list), 1 tail detector (binary map)
+  int32_t list;      // list id for kind 0, 0/1 (bottom/side) for kind 1
+  int32_t kh, kw, kwp;
+  int32_t w_off;     // float offset of the kh x kwp zero-padded weights
+  float delta;       // (float)(-rho): filter2D delta (LocoMouse_class.cpp:845)
+  int32_t oh, ow;    // consumed output region (UNPAD)
+  int32_t in_y, in_x;  // ext-crop coords of tap (0,0) of output (0,0)
+  int32_t m_y, m_x;    // ext-crop coords of the I_*_MOUSE pixel of output (0,0)
+  int32_t tiles_x, tiles_y, tile_base;
+  int32_t box_w, box_h;  // NMS box (detector cols, rows)
+};
+
+struct LmConst {
+  LmDet det[LM_NDET];
+  int32_t n_tiles;
+  // per view (0 bottom, 1 side): extended crop (all taps of all detectors)
+  int32_t ext_h[2], ext_w[2];
+  int32_t ext_oy[2], ext_ox[2];  // origin relative to the padded crop (BB_*_MOUSE_PAD)
+  int32_t crop_h[2], crop_w[2];  // padded crop size
+  int32_t unpad_y[2], unpad_x[2];  // BB_UNPAD_MOUSE_* offset inside the padded crop
+  // images
+  int32_t video_rows, video_cols;
+  int32_t n_rows, n_cols;  // corrected image (calibration) size
+  int32_t pad_pre_rows, pad_pre_cols, ipad_rows, ipad_cols;
+  int32_t flip;
+  // tail
+  int32_t tail_w, tail_hb, tail_hs;  // tail box width, bottom/side heights
+  int32_t connectivity;
+  // per-list capacities (= output area) and list offsets inside a slot's key area
+  int32_t list_cap[LM_NLIST];
+  int64_t list_off[LM_NLIST];
+  int64_t keys_per_slot;
+  // matching / costs (config.yml)
+  double side_bottom_min_overlap;
+  double alpha_vel_bottom, pairwise_occluded_cost;
+  int32_t max_displacement_bottom, ong_spacing_bottom;
+  int32_t ong_nx, ong_ny;
+  double ong_br_x, ong_br_y;
+  int32_t bb_bottom_w, bb_bottom_h;
+  int32_t spre_b_w, spre_b_h, spre_t_w, spre_t_h;
+  int32_t match_b[LM_NFEAT][4];  // match_box_bottom x,y,w,h (paw, snout)
+  int32_t match_s[LM_NFEAT][4];
+  int32_t size_b[LM_NFEAT][2];   // detector (cols, rows) bottom
+  int32_t size_s[LM_NFEAT][2];   // side
+  double prior[5][7];            // location_prior rows
+};
+
+// per-slot frame info (uploaded per batch)
+struct LmSlot {
+  int32_t crop_x[2], crop_y[2];  // padded crop top-left in I_PAD coords (bottom, side)
+  int32_t frame;                 // global frame index (CURRENT_FRAME)
+  int32_t active;                // 1 when the slot is processed in this batch
+};
+
+// per-slot output header (device -> host)
+struct LmSlotOut {
+  int32_t n_pos[LM_NLIST];       // positive detections (after masking)
+  int32_t cand_off[LM_NLIST];    // into the candidate arena
+  int32_t cand_cnt[LM_NLIST];
+  int32_t p22d_off[LM_NFEAT], p22d_cnt[LM_NFEAT];
+  int32_t side_off[LM_NFEAT], side_cnt[LM_NFEAT];
+  int32_t unary_off[LM_NFEAT], unary_cnt[LM_NFEAT];
+  int32_t pw_rows[LM_NFEAT], pw_cols[LM_NFEAT], pw_nnz[LM_NFEAT];
+  int32_t pw_jc_off[LM_NFEAT], pw_nz_off[LM_NFEAT];
+  int32_t tail[45];
+  int32_t ties[LM_NLIST];        // 1 when the exact-tie std::sort replica ran
+  int32_t pad_[3];
+};
+
+// arena counters (device -> host)
+enum { AR_CAND = 0, AR_P22D, AR_SIDE, AR_UNARY, AR_PWJC, AR_PWNZ, AR_COUNT };
+struct LmArenaCtl {
+  int32_t used[AR_COUNT];
+  int32_t cap[AR_COUNT];
+  int32_t overflow;
+  int32_t pad_;
+};
+
+struct LmCand {  // == lm_candidate / Candidate
+  int32_t x, y;
+  double s;
+};
+
+struct LmP22D {  // == lm_p22d
+  LmCand bottom;
+  int32_t side_off;
+  int32_t side_cnt;
+};
+
+#endif  // LM_DEVICE_H

@@ -1,0 +1,232 @@
+/*
+ * lm_introsort.h — exact replica of libstdc++'s std::sort (GCC 11, the
+ * toolchain of this image and of the GPU box) for device code.
+ *
+ * Why: nmsMax / peakClustering sort their positive detections with
+ * std::sort(compareCandidate) (LocoMouse_class.cpp:1658, :1800;
+ * Candidates.cpp:33-36: a.s > b.s).  std::sort is unstable, so when two
+ * detections have exactly equal scores their relative order — and therefore
+ * cluster membership and candidate order — is whatever libstdc++'s
+ * introsort produces from the row-major input order.  The GPU path sorts with
+ * a bitonic network keyed (score desc, row-major index asc); that equals
+ * std::sort whenever all scores are distinct.  When a tie is detected the
+ * list is re-sorted with this replica from row-major order.
+ *
+ * Restated from the published libstdc++ algorithm (bits/stl_algo.h
+ * __introsort_loop / __unguarded_partition_pivot / __move_median_to_first /
+ * __final_insertion_sort with _S_threshold = 16, and bits/stl_heap.h
+ * __make_heap / __adjust_heap / __push_heap / __pop_heap / __sort_heap for
+ * the depth-limit fallback).  Every comparison and move happens in the same
+ * order as libstdc++, which is what makes the permutation identical.
+ * tests/test_introsort.py checks it against std::sort on tie-heavy inputs.
+ */
+#ifndef LM_INTROSORT_H
+#define LM_INTROSORT_H
+
+#if defined(__HIPCC__)
+#define LM_HD __host__ __device__
+#else
+#define LM_HD
+#endif
+
+namespace lm_sort {
+
+template <class T, class Less>
+LM_HD inline void iter_swap_(T* a, T* b) {
+  T t = *a;
+  *a = *b;
+  *b = t;
+}
+
+template <class T, class Less>
+LM_HD inline void move_median_to_first(T* result, T* a, T* b, T* c, Less comp) {
+  if (comp(*a, *b)) {
+    if (comp(*b, *c)) iter_swap_<T, Less>(result, b);
+    else if (comp(*a, *c)) iter_swap_<T, Less>(result, c);
+    else iter_swap_<T, Less>(result, a);
+  } else if (comp(*a, *c)) {
+    iter_swap_<T, Less>(result, a);
+  } else if (comp(*b, *c)) {
+    iter_swap_<T, Less>(result, c);
+  } else {
+    iter_swap_<T, Less>(result, b);
+  }
+}
+
+template <class T, class Less>
+LM_HD inline T* unguarded_partition(T* first, T* last, T* pivot, Less comp) {
+  while (true) {
+    while (comp(*first, *pivot)) ++first;
+    --last;
+    while (comp(*pivot, *last)) --last;
+    if (!(first < last)) return first;
+    iter_swap_<T, Less>(first, last);
+    ++first;
+  }
+}
+
+template <class T, class Less>
+LM_HD inline T* unguarded_partition_pivot(T* first, T* last, Less comp) {
+  T* mid = first + (last - first) / 2;
+  move_median_to_first<T, Less>(first, first + 1, mid, last - 1, comp);
+  return unguarded_partition<T, Less>(first + 1, last, first, comp);
+}
+
+// ---- heap (stl_heap.h), used when the depth limit is exhausted
+template <class T, class Less>
+LM_HD inline void push_heap_(T* first, long hole, long top, T value, Less comp) {
+  long parent = (hole - 1) / 2;
+  while (hole > top && comp(first[parent], value)) {
+    first[hole] = first[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  first[hole] = value;
+}
+
+template <class T, class Less>
+LM_HD inline void adjust_heap(T* first, long hole, long len, T value, Less comp) {
+  const long top = hole;
+  long second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (comp(first[second], first[second - 1])) second--;
+    first[hole] = first[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    first[hole] = first[second - 1];
+    hole = second - 1;
+  }
+  push_heap_<T, Less>(first, hole, top, value, comp);
+}
+
+template <class T, class Less>
+LM_HD inline void make_heap_(T* first, T* last, Less comp) {
+  const long len = last - first;
+  if (len < 2) return;
+  long parent = (len - 2) / 2;
+  while (true) {
+    T value = first[parent];
+    adjust_heap<T, Less>(first, parent, len, value, comp);
+    if (parent == 0) return;
+    parent--;
+  }
+}
+
+template <class T, class Less>
+LM_HD inline void pop_heap_(T* first, T* last, T* result, Less comp) {
+  T value = *result;
+  *result = *first;
+  adjust_heap<T, Less>(first, 0, (long)(last - first), value, comp);
+}
+
+template <class T, class Less>
+LM_HD inline void partial_sort_full(T* first, T* last, Less comp) {
+  // __heap_select(first, last, last) == __make_heap; then __sort_heap
+  make_heap_<T, Less>(first, last, comp);
+  while (last - first > 1) {
+    --last;
+    pop_heap_<T, Less>(first, last, last, comp);
+  }
+}
+
+// ---- insertion sorts
+template <class T, class Less>
+LM_HD inline void unguarded_linear_insert(T* last, Less comp) {
+  T val = *last;
+  T* next = last - 1;
+  while (comp(val, *next)) {
+    *last = *next;
+    last = next;
+    --next;
+  }
+  *last = val;
+}
+
+template <class T, class Less>
+LM_HD inline void insertion_sort(T* first, T* last, Less comp) {
+  if (first == last) return;
+  for (T* i = first + 1; i != last; ++i) {
+    if (comp(*i, *first)) {
+      T val = *i;
+      for (T* p = i; p != first; --p) *p = *(p - 1);  // move_backward
+      *first = val;
+    } else {
+      unguarded_linear_insert<T, Less>(i, comp);
+    }
+  }
+}
+
+enum { kThreshold = 16 };
+
+template <class T, class Less>
+LM_HD inline void final_insertion_sort(T* first, T* last, Less comp) {
+  if (last - first > kThreshold) {
+    insertion_sort<T, Less>(first, first + kThreshold, comp);
+    for (T* i = first + kThreshold; i != last; ++i) unguarded_linear_insert<T, Less>(i, comp);
+  } else {
+    insertion_sort<T, Less>(first, last, comp);
+  }
+}
+
+LM_HD inline int lg_(long n) {
+  int r = 0;
+  while (n > 1) {
+    n >>= 1;
+    ++r;
+  }
+  return r;  // floor(log2 n) == std::__lg
+}
+
+// __introsort_loop without recursion: the recursive call on [cut, last) is
+// pushed on an explicit stack and processed before the loop continues on
+// [first, cut) — the same visiting order as the recursive original.
+template <class T, class Less>
+LM_HD inline void introsort_loop(T* first, T* last, int depth_limit, Less comp) {
+  struct Frame {
+    T* first;
+    T* last;
+    int depth;
+    int stage;  // 0: fresh; 1: returned from right recursion
+    T* cut;
+  };
+  Frame stack[72];
+  int sp = 0;
+  stack[sp++] = Frame{first, last, depth_limit, 0, nullptr};
+  while (sp > 0) {
+    Frame& fr = stack[sp - 1];
+    if (fr.stage == 1) {
+      fr.last = fr.cut;  // __last = __cut after the recursive call
+      fr.stage = 0;
+    }
+    if (fr.last - fr.first > kThreshold) {
+      if (fr.depth == 0) {
+        partial_sort_full<T, Less>(fr.first, fr.last, comp);
+        --sp;
+        continue;
+      }
+      --fr.depth;
+      T* cut = unguarded_partition_pivot<T, Less>(fr.first, fr.last, comp);
+      fr.cut = cut;
+      fr.stage = 1;
+      Frame child{cut, fr.last, fr.depth, 0, nullptr};
+      stack[sp++] = child;
+    } else {
+      --sp;
+    }
+  }
+}
+
+template <class T, class Less>
+LM_HD inline void std_sort(T* first, T* last, Less comp) {
+  if (first != last) {
+    introsort_loop<T, Less>(first, last, lg_((long)(last - first)) * 2, comp);
+    final_insertion_sort<T, Less>(first, last, comp);
+  }
+}
+
+}  // namespace lm_sort
+
+#endif  // LM_INTROSORT_H

@@ -1,0 +1,1186 @@
+// lm_kernels.hip — gfx950 kernels of the LocoMouse per-frame detection path.
+//
+// Batch pipeline (one launch each, grid over frame slots; see lm_device.h):
+//   k_minmax_lut  per-frame min/max of sat(F - BKG) -> normalize LUT (+ TM imadjust)
+//                 LocoMouse_class.cpp:1304-1310, TM.cpp:247, :3204-3242
+//   k_ingest      calibration gather + flip + LUT -> extended padded crops (u8)
+//                 :1316-1327 (correctImage :1337-1406), cropBoundingBox :1408-1478
+//   k_corr        all six filter2D detectors, fp32 row-major FMA chains, LDS-tiled;
+//                 epilogue: brightness mask + score>0 compaction / tail binarisation
+//                 :845, :860, :2575-2576, :782, :817, :849, :864, :2593-2598
+//   k_tail        largest connected component (bottom, then side AND column mask),
+//                 TAIL_MASK, 15-segment binary moments  :2558-2767
+//   k_nms         tail-mask filter, sort (bitonic; libstdc++ introsort replica on
+//                 exact ties), nmsMax (bottom) / peakClustering (side)  :1610-1905
+//   k_post        unary costs, pairwise CSC, side<->bottom matching with the
+//                 motion criterion  :873-919, :999-1267, :1909-2070
+//   k_carry       previous frame's bottom candidates into slot 0 of the next batch
+//
+// All floating-point code is compiled with -ffp-contract=off; the correlation
+// uses explicit fmaf in the reference's row-major tap order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lm_device.h"
+#include "lm_introsort.h"
+
+#define DEV __device__ __forceinline__
+
+// ------------------------------------------------------------------ helpers
+
+DEV uint8_t ipad_pixel(const uint8_t* __restrict__ F, const uint8_t* __restrict__ bkg,
+                       const int32_t* __restrict__ cal, const uint8_t* lut, const LmConst& K, int R, int C) {
+  // I_PAD(R, C): zero outside I_UNPAD (:684-689); inside, the corrected,
+  // normalised, optionally flipped frame.
+  const int r = R - K.pad_pre_rows;
+  int c = C - K.pad_pre_cols;
+  if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) return 0;
+  if (K.flip) c = K.n_cols - 1 - c;
+  const int idx = cal[r * K.n_cols + c];
+  const int f = F[idx], b = bkg[idx];
+  return lut[f > b ? f - b : 0];
+}
+
+DEV float wave_min_u32(unsigned v) {
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
+  return v;
+}
+
+// ------------------------------------------------------------ k_minmax_lut
+// One 1024-thread block per frame slot.  16-byte loads of frame and
+// background; the per-frame LUT folds normalize(NORM_MINMAX) -> convertTo
+// (sat_u8(cvRound((float)p*(float)scale + (float)shift)), OpenCV 3.x) and the
+// LocoMouse_TM imadjust LUT.
+__global__ __launch_bounds__(1024) void k_minmax_lut(const uint8_t* const* __restrict__ frame_ptr,
+                                                     const uint8_t* __restrict__ bkg, int npix, int s0,
+                                                     const uint8_t* __restrict__ adj, int use_adj,
+                                                     uint8_t* __restrict__ luts) {
+  const int slot = s0 + blockIdx.x;
+  const uint8_t* __restrict__ F = frame_ptr[slot];
+  unsigned mn = 255, mx = 0;
+  const int nvec = npix >> 4;
+  const uint4* F4 = reinterpret_cast<const uint4*>(F);
+  const uint4* B4 = reinterpret_cast<const uint4*>(bkg);
+  for (int i = threadIdx.x; i < nvec; i += blockDim.x) {
+    uint4 f = F4[i];
+    uint4 b = B4[i];
+    unsigned fw[4] = {f.x, f.y, f.z, f.w}, bw[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        unsigned fv = (fw[q] >> (8 * k)) & 255u, bv = (bw[q] >> (8 * k)) & 255u;
+        unsigned d = fv > bv ? fv - bv : 0u;
+        mn = min(mn, d);
+        mx = max(mx, d);
+      }
+    }
+  }
+  for (int i = (nvec << 4) + threadIdx.x; i < npix; i += blockDim.x) {
+    unsigned fv = F[i], bv = bkg[i];
+    unsigned d = fv > bv ? fv - bv : 0u;
+    mn = min(mn, d);
+    mx = max(mx, d);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (unsigned)__shfl_xor((int)mn, o));
+    mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  }
+  __shared__ unsigned smn[16], smx[16];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    smn[wid] = mn;
+    smx[wid] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    unsigned a = 255, b = 0;
+    const int nw = blockDim.x >> 6;
+    for (int w = 0; w < nw; ++w) {
+      a = min(a, smn[w]);
+      b = max(b, smx[w]);
+    }
+    const double smin = (double)a, smax = (double)b, dmin = 0.0, dmax = 255.0;
+    const double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0.0);
+    const double shift = dmin - smin * scale;
+    const int p = threadIdx.x;
+    int v;
+    if (fabs(scale - 1.0) < 2.220446049250313e-16 && fabs(shift) < 2.220446049250313e-16) {
+      v = p;  // convertTo noScale -> copy
+    } else {
+      const float sf = (float)scale, hf = (float)shift;
+      float t = __fmul_rn((float)p, sf);
+      t = __fadd_rn(t, hf);
+      int iv = (int)rintf(t);
+      v = iv < 0 ? 0 : (iv > 255 ? 255 : iv);
+    }
+    if (use_adj) v = adj[v];
+    luts[slot * 256 + p] = (uint8_t)v;
+  }
+}
+
+// ---------------------------------------------------------------- k_ingest
+// Builds the extended padded crops of both views for each slot: every I_PAD
+// pixel any detector tap reads.  Each thread writes 4 consecutive bytes.
+__global__ __launch_bounds__(256) void k_ingest(const LmConst K, const uint8_t* const* __restrict__ frame_ptr,
+                                                const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+                                                const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
+                                                int s0, uint8_t* __restrict__ ext, int64_t ext_slot_bytes) {
+  const int slot = s0 + blockIdx.y;
+  __shared__ uint8_t lut[256];
+  lut[threadIdx.x] = luts[slot * 256 + threadIdx.x];
+  __syncthreads();
+  const uint8_t* __restrict__ F = frame_ptr[slot];
+  const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
+  const int64_t etot = e0 + (int64_t)K.ext_h[1] * K.ext_w[1];
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (q >= etot) return;
+  const int v = q < e0 ? 0 : 1;
+  const int64_t qq = v == 0 ? q : q - e0;
+  const int er = (int)(qq / K.ext_w[v]);
+  const int ec = (int)(qq % K.ext_w[v]);  // multiple of 4 (ext_w % 16 == 0)
+  const LmSlot sl = slots[slot];
+  const int R = sl.crop_y[v] + K.ext_oy[v] + er;
+  const int C0 = sl.crop_x[v] + K.ext_ox[v] + ec;
+  uint32_t word = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) word |= (uint32_t)ipad_pixel(F, bkg, cal, lut, K, R, C0 + k) << (8 * k);
+  *reinterpret_cast<uint32_t*>(ext + (int64_t)slot * ext_slot_bytes + q) = word;
+}
+
+// ------------------------------------------------------------------ k_corr
+// One block = one 80x48 output tile of one detector of one slot; 256 threads
+// as 16x16, each LM_R rows x LM_C columns.  The input tile is staged in LDS as
+// float.  For every output the taps are accumulated as
+//     acc = (float)(-rho);  for i in rows, j in cols: acc = fmaf(w[i][j], I, acc)
+// i.e. exactly cv::filter2D's row-major chain (zero-padded taps add +0).
+// Pixel rows are walked once per thread (t = r + i), so a loaded row feeds all
+// LM_R accumulator rows; weights are wave-uniform scalar loads.
+#define LM_MAXK 64
+
+__global__ __launch_bounds__(256) void k_corr(const LmConst K, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                              const float* __restrict__ weights, int s0,
+                                              unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                              uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  extern __shared__ float lds[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  int d = 0;
+#pragma unroll
+  for (int k = 1; k < LM_NDET; ++k)
+    if ((int)blockIdx.x >= K.det[k].tile_base) d = k;
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - D.tile_base;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1, cols = LM_TW + D.kwp - 1;
+  int stride = cols;
+  stride += (16 - (stride & 31) + 32) & 31;  // stride == 16 (mod 32): conflict-free row pairs
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  // stage: 4 bytes per thread-iteration (columns padded to a multiple of 4)
+  const int cols4 = (cols + 3) >> 2;
+  for (int e = threadIdx.x; e < rows * cols4; e += 256) {
+    const int r = e / cols4, c4 = (e - r * cols4) << 2;
+    const uint8_t* p = src + (int64_t)r * ew + c4;
+    float* o = lds + r * stride + c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c4 + k < stride) o[k] = (float)p[k];
+  }
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
+  float acc[LM_R][LM_C];
+#pragma unroll
+  for (int r = 0; r < LM_R; ++r)
+#pragma unroll
+    for (int c = 0; c < LM_C; ++c) acc[r][c] = D.delta;
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  for (int t = 0; t < LM_R + kh - 1; ++t) {
+    const float* prow = lds + (ly * LM_R + t) * stride + lx * LM_C;
+    for (int jc = 0; jc < kwp; jc += LM_JC) {
+      float px[LM_C + LM_JC - 1];
+#pragma unroll
+      for (int q = 0; q < LM_C + LM_JC - 1; ++q) px[q] = prow[jc + q];
+#pragma unroll
+      for (int r = 0; r < LM_R; ++r) {
+        const int i = t - r;
+        if (i >= 0 && i < kh) {
+          const float* wr = W + i * kwp + jc;
+#pragma unroll
+          for (int j = 0; j < LM_JC; ++j) {
+            const float w = wr[j];
+#pragma unroll
+            for (int c = 0; c < LM_C; ++c) acc[r][c] = __builtin_fmaf(w, px[c + j], acc[r][c]);
+          }
+        }
+      }
+    }
+  }
+
+  // epilogue
+  const int my = D.m_y - D.in_y, mx = D.m_x - D.in_x;  // anchor inside the LDS tile
+  unsigned long long mykeys[LM_R * LM_C];
+  int nk = 0;
+#pragma unroll
+  for (int r = 0; r < LM_R; ++r)
+#pragma unroll
+    for (int c = 0; c < LM_C; ++c) {
+      const int y = oy0 + ly * LM_R + r, x = ox0 + lx * LM_C + c;
+      if (y < D.oh && x < D.ow) {
+        const float s = acc[r][c];
+        if (D.kind == 0) {
+          const float pix = lds[(ly * LM_R + r + my) * stride + lx * LM_C + c + mx];
+          if (pix > 25.0f && s > 0.0f) {  // threshold(25.5 -> 25, BINARY_INV) mask, setTo(0), > 0
+            mykeys[nk++] = ((unsigned long long)(~__float_as_uint(s)) << 32) | (unsigned)(y * D.ow + x);
+          }
+        } else {
+          tailbin[(int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0) +
+                  (int64_t)y * D.ow + x] = s > 0.0f ? 1 : 0;
+        }
+      }
+    }
+  if (D.kind != 0) return;
+  int off = nk ? atomicAdd(&s_cnt, nk) : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
+  __syncthreads();
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + s_base + off;
+  for (int k = 0; k < nk; ++k) kl[k] = mykeys[k];
+}
+
+// Debug copy of raw scores: same arithmetic as k_corr, no compaction.
+__global__ __launch_bounds__(256) void k_corr_dbg(const LmConst K, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                  const float* __restrict__ weights, int s0, float* __restrict__ dbg,
+                                                  const int64_t* __restrict__ dbg_off, int64_t dbg_slot_floats) {
+  extern __shared__ float lds[];
+  const int slot = s0 + blockIdx.y;
+  int d = 0;
+#pragma unroll
+  for (int k = 1; k < LM_NDET; ++k)
+    if ((int)blockIdx.x >= K.det[k].tile_base) d = k;
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - D.tile_base;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1, cols = LM_TW + D.kwp - 1;
+  int stride = cols;
+  stride += (16 - (stride & 31) + 32) & 31;
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  const int cols4 = (cols + 3) >> 2;
+  for (int e = threadIdx.x; e < rows * cols4; e += 256) {
+    const int r = e / cols4, c4 = (e - r * cols4) << 2;
+    const uint8_t* p = src + (int64_t)r * ew + c4;
+    float* o = lds + r * stride + c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c4 + k < stride) o[k] = (float)p[k];
+  }
+  __syncthreads();
+  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
+  const float* __restrict__ W = weights + D.w_off;
+  for (int r = 0; r < LM_R; ++r)
+    for (int c = 0; c < LM_C; ++c) {
+      const int y = oy0 + ly * LM_R + r, x = ox0 + lx * LM_C + c;
+      if (y >= D.oh || x >= D.ow) continue;
+      float a = D.delta;
+      for (int i = 0; i < D.kh; ++i)
+        for (int j = 0; j < D.kwp; ++j)
+          a = __builtin_fmaf(W[i * D.kwp + j], lds[(ly * LM_R + r + i) * stride + lx * LM_C + c + j], a);
+      dbg[(int64_t)slot * dbg_slot_floats + dbg_off[d] + (int64_t)y * D.ow + x] = a;
+    }
+}
+
+// ------------------------------------------------------------------ k_tail
+// Connected components by lock-free union-find (atomicMin hooking) over the
+// compacted foreground of a tail binary map, in LDS.  The largest component
+// wins; on equal areas the one OpenCV labels first (8-connectivity: Grana
+// BBDT 2x2-block raster order; 4-connectivity: Wu pixel raster order).
+#define LM_TAIL_FG_MAX 6144
+
+struct CCWork {
+  unsigned* fg;      // pixel index of each foreground element
+  unsigned* parent;  // union-find forest over element ids
+  unsigned* area;    // per root
+  unsigned* key;     // per root: first-label key
+};
+
+DEV unsigned cc_find(unsigned* parent, unsigned a) {
+  unsigned p = parent[a];
+  while (p != a) {
+    a = p;
+    p = parent[a];
+  }
+  return a;
+}
+
+DEV void cc_union(unsigned* parent, unsigned a, unsigned b) {
+  while (true) {
+    a = cc_find(parent, a);
+    b = cc_find(parent, b);
+    if (a == b) return;
+    if (a < b) {
+      unsigned t = a;
+      a = b;
+      b = t;
+    }
+    // a > b: hook a under b
+    unsigned old = atomicMin(&parent[a], b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+// Labels the foreground (given as element list fg[0..n) with pixel indices
+// into a rows x cols map where `is_fg(p)` tells membership and `id_of(p)`
+// maps a foreground pixel to its element id).  Returns the chosen root (or
+// 0xFFFFFFFF when n == 0) in *s_best.  Block-wide; all threads call.
+template <class IsFg, class IdOf>
+DEV void cc_largest(CCWork W, int n, int rows, int cols, int conn, IsFg is_fg, IdOf id_of, unsigned* s_best) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    W.parent[k] = k;
+    W.area[k] = 0;
+    W.key[k] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const unsigned p = W.fg[k];
+    const int y = p / cols, x = p % cols;
+    if (x > 0 && is_fg(p - 1)) cc_union(W.parent, k, id_of(p - 1));
+    if (y > 0) {
+      if (is_fg(p - cols)) cc_union(W.parent, k, id_of(p - cols));
+      if (conn == 8) {
+        if (x > 0 && is_fg(p - cols - 1)) cc_union(W.parent, k, id_of(p - cols - 1));
+        if (x + 1 < cols && is_fg(p - cols + 1)) cc_union(W.parent, k, id_of(p - cols + 1));
+      }
+    }
+  }
+  __syncthreads();
+  const int nbx = (cols + 1) / 2;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const unsigned root = cc_find(W.parent, k);
+    const unsigned p = W.fg[k];
+    const int y = p / cols, x = p % cols;
+    const unsigned key = conn == 8 ? (unsigned)((y >> 1) * nbx + (x >> 1)) : p;
+    atomicAdd(&W.area[root], 1u);
+    atomicMin(&W.key[root], key);
+  }
+  __syncthreads();
+  // max area, then min key
+  unsigned long long best = 0;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    if (W.parent[k] == (unsigned)k) {  // root (parents are final roots after find? roots satisfy parent==self)
+      unsigned long long v = ((unsigned long long)W.area[k] << 32) | (0xFFFFFFFFu - W.key[k]);
+      if (v > best) best = v;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long other = __shfl_xor(best, o);
+    if (other > best) best = other;
+  }
+  __shared__ unsigned long long s_red[16];
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w)
+      if (s_red[w] > b) b = s_red[w];
+    unsigned chosen = 0xFFFFFFFFu;
+    if (b) {
+      // find the root with this (area, key): keys are unique per component
+      const unsigned key = 0xFFFFFFFFu - (unsigned)(b & 0xFFFFFFFFu);
+      for (int k = 0; k < n; ++k)
+        if (W.parent[k] == (unsigned)k && W.key[k] == key) {
+          chosen = k;
+          break;
+        }
+    }
+    *s_best = chosen;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_tail(const LmConst K, int s0, const uint8_t* __restrict__ tailbin,
+                                               int64_t tailbin_slot_bytes, uint8_t* __restrict__ tailmask,
+                                               unsigned* __restrict__ scratch, int64_t scratch_slot_words,
+                                               LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err) {
+  const int slot = s0 + blockIdx.x;
+  const int TW = K.tail_w, HB = K.tail_hb, HS = K.tail_hs;
+  const uint8_t* __restrict__ binb = tailbin + (int64_t)slot * tailbin_slot_bytes;
+  const uint8_t* __restrict__ bins = binb + (int64_t)HB * TW;
+  uint8_t* __restrict__ mask = tailmask + (int64_t)slot * HB * TW;
+  unsigned* __restrict__ idmap = scratch + (int64_t)slot * scratch_slot_words;  // [HB*TW] element ids
+
+  __shared__ unsigned s_fg[LM_TAIL_FG_MAX], s_parent[LM_TAIL_FG_MAX], s_area[LM_TAIL_FG_MAX], s_key[LM_TAIL_FG_MAX];
+  __shared__ int s_n;
+  __shared__ unsigned s_best;
+  __shared__ int s_first, s_last;
+  __shared__ uint8_t s_col[1024];
+  // moments accumulators: [segment 15][tile rows <= 16][tile cols <= 2] x (n, sx, sy)
+  __shared__ unsigned s_mb[15][16][2][3];
+  __shared__ unsigned s_ms[15][16][2];  // side: per track column, per tile row: (n, sy)
+
+  CCWork Wk{s_fg, s_parent, s_area, s_key};
+  const int conn = K.connectivity;
+
+  // zero TAIL_MASK, column mask
+  for (int p = threadIdx.x; p < HB * TW; p += blockDim.x) mask[p] = 0;
+  for (int c = threadIdx.x; c < TW; c += blockDim.x) s_col[c] = 0;
+  if (threadIdx.x == 0) {
+    s_n = 0;
+    s_first = 0x7FFFFFFF;
+    s_last = -1;
+  }
+  for (int e = threadIdx.x; e < 15 * 16 * 2 * 3; e += blockDim.x) (&s_mb[0][0][0][0])[e] = 0;
+  for (int e = threadIdx.x; e < 15 * 16 * 2; e += blockDim.x) (&s_ms[0][0][0])[e] = 0;
+  __syncthreads();
+
+  // ---- bottom: compact foreground
+  for (int p = threadIdx.x; p < HB * TW; p += blockDim.x)
+    if (binb[p]) {
+      int k = atomicAdd(&s_n, 1);
+      if (k < LM_TAIL_FG_MAX) {
+        s_fg[k] = p;
+        idmap[p] = k;
+      }
+    }
+  __syncthreads();
+  int n = s_n;
+  if (n > LM_TAIL_FG_MAX) {
+    if (threadIdx.x == 0) atomicOr(err, 2);  // tail foreground exceeds the LDS capacity
+    return;
+  }
+  cc_largest(Wk, n, HB, TW, conn, [&](unsigned p) { return binb[p] != 0; }, [&](unsigned p) { return idmap[p]; }, &s_best);
+  const unsigned best_b = s_best;
+  if (best_b != 0xFFFFFFFFu) {
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      if (cc_find(s_parent, k) == best_b) {
+        const unsigned p = s_fg[k];
+        mask[p] = 255;
+        const int x = p % TW;
+        s_col[x] = 255;
+        atomicMin(&s_first, x);
+        atomicMax(&s_last, x);
+      }
+    }
+  }
+  __syncthreads();
+  const int first = s_first, last = s_last;
+  const bool have = best_b != 0xFFFFFFFFu;
+  // segment geometry (:2677-2685)
+  const int tail_width = have ? last - first : 0;
+  const int rem = tail_width % 15, reg = (tail_width - rem) / 15;
+  // bottom segment moments: per selected pixel, integer per-tile sums
+  if (have) {
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      if (cc_find(s_parent, k) != best_b) continue;
+      const unsigned p = s_fg[k];
+      const int y = p / TW, x = p % TW;
+      if (x < first || x >= first + tail_width) continue;  // segments cover [first, last)
+      const int rx = x - first;
+      int seg, sx;
+      if (rx < rem * (reg + 1)) {
+        seg = rx / (reg + 1);
+        sx = seg * (reg + 1);
+      } else {
+        seg = rem + (rx - rem * (reg + 1)) / reg;
+        sx = rem * (reg + 1) + (seg - rem) * reg;
+      }
+      const int lxs = rx - sx;  // x inside the segment ROI
+      const int ty = y >> 5, tx = lxs >> 5;
+      atomicAdd(&s_mb[seg][ty][tx][0], 1u);
+      atomicAdd(&s_mb[seg][ty][tx][1], (unsigned)(lxs & 31));
+      atomicAdd(&s_mb[seg][ty][tx][2], (unsigned)(y & 31));
+    }
+  }
+  __syncthreads();
+
+  // ---- side: (tail_s > 0) & repeat(colmax) -> largest component
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  for (int p = threadIdx.x; p < HS * TW; p += blockDim.x)
+    if (bins[p] && s_col[p % TW]) {
+      int k = atomicAdd(&s_n, 1);
+      if (k < LM_TAIL_FG_MAX) {
+        s_fg[k] = p;
+        idmap[p] = k;
+      }
+    }
+  __syncthreads();
+  n = s_n;
+  if (n > LM_TAIL_FG_MAX) {
+    if (threadIdx.x == 0) atomicOr(err, 2);
+    return;
+  }
+  auto side_fg = [&](unsigned p) { return bins[p] != 0 && s_col[p % TW] != 0; };
+  cc_largest(Wk, n, HS, TW, conn, side_fg, [&](unsigned p) { return idmap[p]; }, &s_best);
+  const unsigned best_s = s_best;
+
+  // track x (per segment) — needed to know which side columns to measure
+  __shared__ int s_tx[15];
+  if (threadIdx.x < 15) {
+    const int i = threadIdx.x;
+    int tx_ = -1, ty_ = -1;
+    if (have) {
+      const int sx = first + (i < rem ? i * (reg + 1) : rem * (reg + 1) + (i - rem) * reg);
+      const int wseg = i < rem ? reg + 1 : reg;
+      double m00 = 0, m10 = 0, m01 = 0;
+      const double s = 1. / 255;
+      const int ntr = (HB + 31) >> 5, ntc = (wseg + 31) >> 5;
+      for (int ty = 0; ty < ntr; ++ty)
+        for (int tx = 0; tx < ntc; ++tx) {
+          const unsigned cnt = s_mb[i][ty][tx][0];
+          const double mom0 = (double)(255u * cnt) * s;
+          const double mom1 = (double)(255u * s_mb[i][ty][tx][1] + 0u) * s;
+          const double mom2 = (double)(255u * s_mb[i][ty][tx][2]) * s;
+          const double xm = (double)(tx * 32) * mom0, ym = (double)(ty * 32) * mom0;
+          m00 += mom0;
+          m10 += mom1 + xm;
+          m01 += mom2 + ym;
+        }
+      if (m00 > 0) {
+        tx_ = (int)(m10 / m00) + sx;
+        ty_ = (int)(m01 / m00) + 0;
+      }
+    }
+    s_tx[i] = tx_;
+    hdr[slot].tail[i] = tx_;
+    hdr[slot].tail[15 + i] = ty_;
+  }
+  __syncthreads();
+  if (best_s != 0xFFFFFFFFu) {
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      if (cc_find(s_parent, k) != best_s) continue;
+      const unsigned p = s_fg[k];
+      const int y = p / TW, x = p % TW;
+      for (int i = 0; i < 15; ++i)
+        if (s_tx[i] > 0 && s_tx[i] == x) {
+          atomicAdd(&s_ms[i][y >> 5][0], 1u);
+          atomicAdd(&s_ms[i][y >> 5][1], (unsigned)(y & 31));
+        }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 15) {
+    const int i = threadIdx.x;
+    int tz = -1;
+    if (s_tx[i] > 0) {
+      double m00 = 0, m01 = 0;
+      const double s = 1. / 255;
+      const int ntr = (HS + 31) >> 5;
+      for (int ty = 0; ty < ntr; ++ty) {
+        const double mom0 = (double)(255u * s_ms[i][ty][0]) * s;
+        const double mom2 = (double)(255u * s_ms[i][ty][1]) * s;
+        const double xm = 0.0 * mom0, ym = (double)(ty * 32) * mom0;
+        (void)xm;
+        m00 += mom0;
+        m01 += mom2 + ym;
+      }
+      if (m00 > 0) tz = (int)(m01 / m00) + 0;
+    }
+    hdr[slot].tail[30 + i] = tz;
+  }
+}
+
+// ------------------------------------------------------------------- k_nms
+#define LM_NMS_THREADS 512
+#define LM_NMS_CAP 4096  // entries sorted in LDS; larger lists take the global path
+
+DEV float key_score(unsigned long long k) { return __uint_as_float(~(unsigned)(k >> 32)); }
+DEV unsigned key_idx(unsigned long long k) { return (unsigned)(k & 0xFFFFFFFFu); }
+
+// in-place ascending bitonic sort of a[0..np), np power of two, block-wide
+DEV void bitonic_sort(unsigned long long* a, int np) {
+  for (int k = 2; k <= np; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < np; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long x = a[i], y = a[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            a[i] = y;
+            a[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+struct ReplicaLess {  // compareCandidate on (idx << 32 | score bits) words
+  DEV bool operator()(unsigned long long a, unsigned long long b) const {
+    return __uint_as_float((unsigned)(a & 0xFFFFFFFFu)) > __uint_as_float((unsigned)(b & 0xFFFFFFFFu));
+  }
+};
+
+// Rect overlap test of nmsMax / peakClustering (:1698-1709, :1833-1844):
+// inter / (2wh - inter) > 0.5  <=>  3*inter > 2wh  (exact for these integers)
+DEV bool overlaps(int xa, int ya, int xb, int yb, int bw, int bh) {
+  const int dx = abs(xa - xb), dy = abs(ya - yb);
+  if (dx >= bw || dy >= bh) return false;
+  const int inter = (bw - dx) * (bh - dy);
+  const double a = (double)inter;
+  return a / (2.0 * (bw * bh) - a) > 0.5;
+}
+
+__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0, int side, unsigned long long* __restrict__ keys,
+                                                       const int32_t* __restrict__ n_pos, const uint8_t* __restrict__ tailmask,
+                                                       unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
+                                                       LmSlotOut* __restrict__ hdr, LmCand* __restrict__ arena_cand,
+                                                       LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err) {
+  const int slot = s0 + blockIdx.x;
+  const int feat = blockIdx.y;                 // 0 paw, 1 snout
+  const int list = side ? 2 + feat : feat;
+  const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
+  const LmDet D = K.det[det];
+  LmSlotOut* H = hdr + slot;
+  __shared__ unsigned long long s_keys[LM_NMS_CAP];
+  __shared__ int s_assign[LM_NMS_CAP];
+  __shared__ int s_n, s_flag, s_ncand, s_base;
+
+  if (side && H->cand_cnt[feat] == 0) {  // detectSideCandidates skips (:820-833)
+    if (threadIdx.x == 0) {
+      H->n_pos[list] = 0;
+      H->cand_off[list] = 0;
+      H->cand_cnt[list] = 0;
+      H->ties[list] = 0;
+    }
+    return;
+  }
+  const int n_in = n_pos[slot * LM_NLIST + list];
+  const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
+  unsigned long long* a = s_keys;
+  int* assign = s_assign;
+  const bool global_path = n_in > LM_NMS_CAP;
+  if (global_path) {
+    a = gscratch + (int64_t)(blockIdx.y + 2 * blockIdx.x) * gscratch_slot;
+    assign = reinterpret_cast<int*>(a + gscratch_slot / 2);
+  }
+  if (threadIdx.x == 0) {
+    s_n = 0;
+    s_flag = 0;
+  }
+  __syncthreads();
+  // load + TAIL_MASK filter (bottom lists: mask(BB_BOTTOM_TAIL).setTo(255, TAIL_MASK), :783)
+  const uint8_t* __restrict__ tm = tailmask + (int64_t)slot * K.tail_hb * K.tail_w;
+  for (int k = threadIdx.x; k < n_in; k += blockDim.x) {
+    const unsigned long long v = src[k];
+    bool keep = true;
+    if (!side) {
+      const unsigned idx = key_idx(v);
+      const int y = idx / D.ow, x = idx % D.ow;
+      if (x < K.tail_w && y < K.tail_hb && tm[y * K.tail_w + x]) keep = false;
+    }
+    if (keep) a[atomicAdd(&s_n, 1)] = v;
+  }
+  __syncthreads();
+  const int n = s_n;
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
+  __syncthreads();
+  if (np > 1) bitonic_sort(a, np);
+  // exact score ties -> libstdc++ order
+  for (int k = threadIdx.x; k + 1 < n; k += blockDim.x)
+    if ((a[k] >> 32) == (a[k + 1] >> 32)) s_flag = 1;
+  __syncthreads();
+  const int tie = s_flag;
+  if (tie) {
+    // row-major order (the order nmsMax pushes detections, :1638-1648)
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      const unsigned long long v = a[k];
+      a[k] = ((unsigned long long)key_idx(v) << 32) | (unsigned)(~(unsigned)(v >> 32));
+    }
+    __syncthreads();
+    if (np > 1) bitonic_sort(a, np);
+    if (threadIdx.x == 0) lm_sort::std_sort(a, a + n, ReplicaLess());
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      const unsigned long long v = a[k];
+      a[k] = ((unsigned long long)(~(unsigned)(v & 0xFFFFFFFFu)) << 32) | (unsigned)(v >> 32);
+    }
+    __syncthreads();
+  }
+  const int bw = D.box_w, bh = D.box_h, ow = D.ow;
+  int ncand = 0;
+  if (!side) {
+    // nmsMax: assign[j] = first i < j overlapping j (suppressed points keep
+    // suppressing, :1677-1720); maxima resolved by pointer jumping.
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+      const unsigned ij = key_idx(a[j]);
+      const int xj = ij % ow, yj = ij / ow;
+      int as = -1;
+      for (int i = 0; i < j; ++i) {
+        const unsigned ii = key_idx(a[i]);
+        if (overlaps(ii % ow, ii / ow, xj, yj, bw, bh)) {
+          as = i;
+          break;
+        }
+      }
+      assign[j] = as < 0 ? j : as;
+    }
+    __syncthreads();
+    while (true) {
+      if (threadIdx.x == 0) s_flag = 0;
+      __syncthreads();
+      for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const int m = assign[j], mm = assign[m];
+        if (mm != m) {
+          assign[j] = mm;
+          s_flag = 1;
+        }
+      }
+      __syncthreads();
+      if (!s_flag) break;
+      __syncthreads();
+    }
+  } else {
+    // peakClustering: leaders in sorted order; each suppresses the undecided
+    // points overlapping it (:1815-1850).  assign[j] = leader id (-1 undecided)
+    for (int j = threadIdx.x; j < n; j += blockDim.x) assign[j] = -1;
+    __syncthreads();
+    __shared__ int s_lead;
+    int lead = 0;
+    while (lead < n) {
+      if (threadIdx.x == 0) assign[lead] = lead;
+      const unsigned il = key_idx(a[lead]);
+      const int xl = il % ow, yl = il / ow;
+      for (int j = lead + 1 + threadIdx.x; j < n; j += blockDim.x) {
+        if (assign[j] >= 0) continue;
+        const unsigned ij = key_idx(a[j]);
+        if (overlaps(xl, yl, ij % ow, ij / ow, bw, bh)) assign[j] = lead;
+      }
+      if (threadIdx.x == 0) s_lead = n;
+      __syncthreads();
+      for (int j = lead + 1 + threadIdx.x; j < n; j += blockDim.x)
+        if (assign[j] < 0) atomicMin(&s_lead, j);
+      __syncthreads();
+      lead = s_lead;
+      __syncthreads();
+    }
+  }
+  // maxima / leaders in sorted order -> output slots
+  if (threadIdx.x == 0) {
+    int c = 0;
+    for (int j = 0; j < n; ++j)
+      if (assign[j] == j) ++c;
+    s_ncand = c;
+    int base = atomicAdd(&ctl->used[AR_CAND], c);
+    if (base + c > ctl->cap[AR_CAND]) {
+      atomicOr(&ctl->overflow, 1);
+      base = -1;
+    }
+    s_base = base;
+  }
+  __syncthreads();
+  ncand = s_ncand;
+  const int base = s_base;
+  if (base >= 0) {
+    // rank of each maximum among maxima (prefix count), then the weighted
+    // mean over its members in sorted order (double, :1731-1744 / :1865-1883)
+    for (int m = threadIdx.x; m < n; m += blockDim.x) {
+      if (assign[m] != m) continue;
+      int rank = 0;
+      for (int j = 0; j < m; ++j) rank += assign[j] == j;
+      double wx = 0, wy = 0, ss = 0;
+      int members = 0;
+      for (int j = m; j < n; ++j) {
+        if (assign[j] != m) continue;
+        const unsigned ij = key_idx(a[j]);
+        const double s = (double)key_score(a[j]);
+        wx += (double)(int)(ij % ow) * s;
+        wy += (double)(int)(ij / ow) * s;
+        ss += s;
+        ++members;
+      }
+      const unsigned im = key_idx(a[m]);
+      LmCand c;
+      c.s = (double)key_score(a[m]);
+      if (!side) {  // Point_<double> / double -> Point_<int>: cvRound (half even)
+        c.x = (int)rint(wx / ss);
+        c.y = (int)rint(wy / ss);
+      } else if (members > 1) {  // std::round (half away from zero)
+        c.x = (int)round(wx / ss);
+        c.y = (int)round(wy / ss);
+      } else {
+        c.x = (int)(im % ow);
+        c.y = (int)(im / ow);
+      }
+      arena_cand[base + rank] = c;
+    }
+  }
+  if (threadIdx.x == 0) {
+    H->n_pos[list] = n;
+    H->cand_off[list] = base;
+    H->cand_cnt[list] = ncand;
+    H->ties[list] = tie;
+  }
+}
+
+// ------------------------------------------------------------------ k_post
+#define LM_POST_THREADS 256
+#define LM_POST_MAXC 512     // candidates per list handled in LDS
+#define LM_POST_MAXOFF 2048  // CSC columns (Ni + Nong) + 1
+
+DEV bool vel_criterion(const LmConst& K, const uint8_t* Fc, const uint8_t* Fp, const uint8_t* bkg, const int32_t* cal,
+                       const uint8_t* lutc, const uint8_t* lutp, int crop_x, int crop_y, int crop_w, int crop_h,
+                       int bx, int by, int bwid, int bhei, int area, double alpha, int32_t* err) {
+  // checkVelCriterion (:1256-1267): sum(sat_u8(I - I_prev) > 25) >= area*alpha
+  if (bx < 0 || by < 0 || bwid < 0 || bhei < 0 || bx + bwid > crop_w || by + bhei > crop_h) {
+    atomicOr(err, 4);  // cv::Mat ROI assertion in the reference
+    return false;
+  }
+  int sum = 0;
+  for (int r = 0; r < bhei; ++r)
+    for (int c = 0; c < bwid; ++c) {
+      const int R = crop_y + by + r, C = crop_x + bx + c;
+      const int a = ipad_pixel(Fc, bkg, cal, lutc, K, R, C);
+      const int b = ipad_pixel(Fp, bkg, cal, lutp, K, R, C);
+      const int s = a > b ? a - b : 0;
+      sum += s > 25;
+    }
+  return (double)sum >= ((double)area) * alpha;
+}
+
+__global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const LmSlot* __restrict__ slots,
+                                                         const uint8_t* const* __restrict__ frame_ptr,
+                                                         const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+                                                         const uint8_t* __restrict__ luts, LmSlotOut* __restrict__ hdr,
+                                                         LmCand* __restrict__ arena_cand, LmP22D* __restrict__ arena_p22d,
+                                                         int32_t* __restrict__ arena_side_y, double* __restrict__ arena_side_s,
+                                                         double* __restrict__ arena_unary, int32_t* __restrict__ arena_jc,
+                                                         int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
+                                                         LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err) {
+  const int slot = 1 + blockIdx.x;
+  const int feat = blockIdx.y;
+  LmSlotOut* H = hdr + slot;
+  const LmSlotOut* HP = hdr + slot - 1;
+  const int frame = slots[slot].frame;
+  __shared__ LmCand sb[LM_POST_MAXC], st[LM_POST_MAXC], sp[LM_POST_MAXC];
+  __shared__ int s_off[LM_POST_MAXOFF];
+  __shared__ int s_mb[LM_POST_MAXC], s_mt[LM_POST_MAXC];  // motion status (-1 unknown)
+  __shared__ float s_bps[LM_POST_MAXC], s_tpb[LM_POST_MAXC];
+  __shared__ int s_all_equal, s_any1, s_any0, s_base[4];
+  const int Nb = H->cand_cnt[feat], Ns = H->cand_cnt[2 + feat];
+  const int Ni = frame > 0 ? HP->cand_cnt[feat] : 0;
+  if (Nb > LM_POST_MAXC || Ns > LM_POST_MAXC || Ni > LM_POST_MAXC || Ni + K.ong_nx * K.ong_ny + 1 > LM_POST_MAXOFF) {
+    if (threadIdx.x == 0) atomicOr(err, 8);
+    return;
+  }
+  const LmCand* cb = arena_cand + H->cand_off[feat];
+  const LmCand* ct = arena_cand + H->cand_off[2 + feat];
+  const LmCand* cp = arena_cand + HP->cand_off[feat];
+  for (int k = threadIdx.x; k < Nb; k += blockDim.x) sb[k] = cb[k];
+  for (int k = threadIdx.x; k < Ns; k += blockDim.x) st[k] = ct[k];
+  for (int k = threadIdx.x; k < Ni; k += blockDim.x) sp[k] = cp[k];
+  __syncthreads();
+
+  // ---------------- unary (unaryCostBox :1909-1952), column-major Nb x nprior
+  const int nprior = feat == 0 ? 4 : 1;
+  const int p0 = feat == 0 ? 0 : 4;
+  if (threadIdx.x == 0) {
+    int b = atomicAdd(&ctl->used[AR_UNARY], Nb * nprior);
+    if (b + Nb * nprior > ctl->cap[AR_UNARY]) {
+      atomicOr(&ctl->overflow, 1);
+      b = -1;
+    }
+    s_base[0] = b;
+  }
+  __syncthreads();
+  if (s_base[0] >= 0) {
+    const double norm_fact = 1 / sqrt(2.0);
+    for (int e = threadIdx.x; e < Nb * nprior; e += blockDim.x) {
+      const int j = e / Nb, i = e % Nb;  // column-major: values[j*nrows + i]
+      const double* pr = K.prior[p0 + j];
+      const double cx = (double)sb[i].x / (double)K.bb_bottom_w, cy = (double)sb[i].y / (double)K.bb_bottom_h;
+      const double ax = pr[3], aw = pr[4] - pr[3], ay = pr[5], ah = pr[6] - pr[5];
+      double v = 0.0;
+      if (ax <= cx && cx < ax + aw && ay <= cy && cy < ay + ah) {
+        const double dx = cx - pr[0], dy = cy - pr[1];
+        const double dd = __dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy));
+        const double val = sqrt(dd) * norm_fact;
+        if (val <= pr[2]) v = (1 - val) * sb[i].s;
+      }
+      arena_unary[s_base[0] + e] = v;
+    }
+  }
+  if (threadIdx.x == 0) {
+    H->unary_off[feat] = s_base[0];
+    H->unary_cnt[feat] = Nb * nprior;
+  }
+
+  // ---------------- pairwise (pairwisePotential :1954-2070) when frame > 0
+  if (frame > 0) {
+    const int Nong = K.ong_nx * K.ong_ny;
+    const int ncols = Ni + Nong, nrows = Nb + Nong;
+    const double gs = (double)K.ong_spacing_bottom, maxd = (double)K.max_displacement_bottom;
+    const double alpha = K.alpha_vel_bottom, occ = K.pairwise_occluded_cost * alpha;
+    auto ong_of = [&](const LmCand& c) {
+      const int xc = (int)round((K.ong_br_x - (double)c.x) / gs);
+      const int yc = (int)round((K.ong_br_y - (double)c.y) / gs);
+      const int ox = xc < 0 ? 0 : (xc > K.ong_nx - 1 ? K.ong_nx - 1 : xc);
+      const int oy = yc < 0 ? 0 : (yc > K.ong_ny - 1 ? K.ong_ny - 1 : yc);
+      return oy * K.ong_nx + ox;
+    };
+    auto trans = [&](int i, int j) {  // D(j, i) candidate -> candidate
+      const double dx = (double)sb[j].x - (double)sp[i].x, dy = (double)sb[j].y - (double)sp[i].y;
+      const double dist = sqrt(__dadd_rn(__dmul_rn(dx, dx), __dmul_rn(dy, dy)));
+      if (!(dist < maxd)) return 0.0;
+      double inv = 1 - (dist / maxd);
+      return inv * alpha;
+    };
+    // column counts -> Jc
+    for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
+      int cnt = 0;
+      if (c < Ni) {
+        for (int j = 0; j < Nb; ++j) cnt += trans(c, j) != 0.0;
+        cnt += occ != 0.0;
+      } else {
+        const int q = c - Ni;
+        if (Ni > 0)
+          for (int j = 0; j < Nb; ++j) cnt += (ong_of(sb[j]) == q && occ != 0.0);
+        cnt += occ != 0.0;
+      }
+      s_off[c] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int acc = 0;
+      for (int c = 0; c < ncols; ++c) {
+        const int t = s_off[c];
+        s_off[c] = acc;
+        acc += t;
+      }
+      s_off[ncols] = acc;
+      int bj = atomicAdd(&ctl->used[AR_PWJC], ncols + 1);
+      int bn = atomicAdd(&ctl->used[AR_PWNZ], acc);
+      if (bj + ncols + 1 > ctl->cap[AR_PWJC] || bn + acc > ctl->cap[AR_PWNZ]) {
+        atomicOr(&ctl->overflow, 1);
+        bj = -1;
+      }
+      s_base[1] = bj;
+      s_base[2] = bn;
+    }
+    __syncthreads();
+    const int bj = s_base[1], bn = s_base[2];
+    if (bj >= 0) {
+      for (int c = threadIdx.x; c <= ncols; c += blockDim.x) arena_jc[bj + c] = s_off[c];
+      for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
+        int o = bn + s_off[c];
+        if (c < Ni) {
+          for (int j = 0; j < Nb; ++j) {
+            const double v = trans(c, j);
+            if (v != 0.0) {
+              arena_ir[o] = j;
+              arena_pr[o] = v;
+              ++o;
+            }
+          }
+          if (occ != 0.0) {
+            arena_ir[o] = Nb + ong_of(sp[c]);
+            arena_pr[o] = occ;
+            ++o;
+          }
+        } else {
+          const int q = c - Ni;
+          if (Ni > 0 && occ != 0.0)
+            for (int j = 0; j < Nb; ++j)
+              if (ong_of(sb[j]) == q) {
+                arena_ir[o] = j;
+                arena_pr[o] = occ;
+                ++o;
+              }
+          if (occ != 0.0) {
+            arena_ir[o] = Nb + q;
+            arena_pr[o] = occ;
+            ++o;
+          }
+        }
+      }
+    }
+    if (threadIdx.x == 0) {
+      H->pw_rows[feat] = nrows;
+      H->pw_cols[feat] = ncols;
+      H->pw_nnz[feat] = s_off[ncols];
+      H->pw_jc_off[feat] = bj;
+      H->pw_nz_off[feat] = bn;
+    }
+    __syncthreads();
+  } else if (threadIdx.x == 0) {
+    H->pw_rows[feat] = -1;
+    H->pw_cols[feat] = -1;
+    H->pw_nnz[feat] = 0;
+    H->pw_jc_off[feat] = 0;
+    H->pw_nz_off[feat] = 0;
+  }
+
+  // ---------------- matching (:1023-1254)
+  const int ovlp = (int)(K.size_b[feat][0] * (1 - K.side_bottom_min_overlap));
+  const bool vel_check = frame > 0;
+  if (threadIdx.x == 0) {
+    s_any1 = 0;
+    s_any0 = 0;
+  }
+  for (int k = threadIdx.x; k < LM_POST_MAXC; k += blockDim.x) {
+    s_mb[k] = -1;
+    s_mt[k] = -1;
+    s_bps[k] = 0.f;
+    s_tpb[k] = 0.f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < Nb * Ns; e += blockDim.x) {
+    const int i = e / Ns, j = e % Ns;
+    if (abs(sb[i].x - st[j].x) <= ovlp) s_any1 = 1;
+    else s_any0 = 1;
+  }
+  __syncthreads();
+  const bool mixed = s_any1 && s_any0;  // normalize(NORM_MINMAX) all-equal -> all 0 (:1065)
+  auto boolD = [&](int i, int j) { return mixed && abs(sb[i].x - st[j].x) <= ovlp; };
+  for (int j = threadIdx.x; j < Ns; j += blockDim.x) {
+    float s = 0.f;
+    for (int i = 0; i < Nb; ++i) s += boolD(i, j) ? 1.f : 0.f;
+    s_bps[j] = s;
+  }
+  for (int i = threadIdx.x; i < Nb; i += blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < Ns; ++j) s += boolD(i, j) ? 1.f : 0.f;
+    s_tpb[i] = s;
+  }
+  __syncthreads();
+  // motion status where the reference evaluates it
+  const LmSlot sl = slots[slot];
+  const uint8_t* Fc = frame_ptr[slot];
+  const uint8_t* Fp = frame_ptr[slot - 1];
+  const uint8_t* lutc = luts + slot * 256;
+  const uint8_t* lutp = luts + (slot - 1) * 256;
+  const int* mbox = K.match_b[feat];
+  const int* tbox = K.match_s[feat];
+  if (vel_check) {
+    for (int i = threadIdx.x; i < Nb; i += blockDim.x) {
+      bool need = false;
+      for (int j = 0; j < Ns; ++j) need |= boolD(i, j) && s_bps[j] > 1;
+      if (need)
+        s_mb[i] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl.crop_x[0], sl.crop_y[0], K.crop_w[0], K.crop_h[0],
+                                mbox[0] + sb[i].x + K.spre_b_w, mbox[1] + sb[i].y + K.spre_b_h, mbox[2], mbox[3],
+                                K.size_b[feat][0] * K.size_b[feat][1], 0.02, err);
+    }
+    for (int j = threadIdx.x; j < Ns; j += blockDim.x) {
+      bool need = false;
+      if (s_bps[j] > 1)
+        for (int i = 0; i < Nb; ++i) need |= boolD(i, j);
+      if (need)
+        s_mt[j] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl.crop_x[1], sl.crop_y[1], K.crop_w[1], K.crop_h[1],
+                                tbox[0] + st[j].x + K.spre_t_w, tbox[1] + st[j].y + K.spre_t_h, tbox[2], tbox[3],
+                                K.size_s[feat][0] * K.size_s[feat][1], 0.05, err);
+    }
+  }
+  __syncthreads();
+  const double walpha = -(1. / (double)ovlp);
+  auto matches = [&](int i, int j) {
+    if (!boolD(i, j)) return false;
+    if ((s_bps[j] > 1) & vel_check) return s_mb[i] == s_mt[j];
+    return true;
+  };
+  // side entries per bottom candidate (>= 1: the "no match" entry)
+  for (int i = threadIdx.x; i < Nb; i += blockDim.x) {
+    int cnt = 0;
+    if (Ns > 0 && s_tpb[i] != 0)
+      for (int j = 0; j < Ns; ++j) cnt += matches(i, j);
+    s_off[i] = cnt > 0 ? cnt : 1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int i = 0; i < Nb; ++i) {
+      const int t = s_off[i];
+      s_off[i] = acc;
+      acc += t;
+    }
+    s_off[Nb] = acc;
+    int bp = atomicAdd(&ctl->used[AR_P22D], Nb);
+    int bs = atomicAdd(&ctl->used[AR_SIDE], acc);
+    if (bp + Nb > ctl->cap[AR_P22D] || bs + acc > ctl->cap[AR_SIDE]) {
+      atomicOr(&ctl->overflow, 1);
+      bp = -1;
+    }
+    s_base[0] = bp;
+    s_base[1] = bs;
+  }
+  __syncthreads();
+  const int bp = s_base[0], bs = s_base[1];
+  if (bp >= 0) {
+    for (int i = threadIdx.x; i < Nb; i += blockDim.x) {
+      const int o = bs + s_off[i];
+      int cnt = 0;
+      double st0 = -1;
+      if (Ns > 0 && s_tpb[i] != 0) {
+        for (int j = 0; j < Ns; ++j) {
+          if (!matches(i, j)) continue;
+          const double wgt = __dadd_rn(__dmul_rn((double)abs(sb[i].x - st[j].x), walpha), 1.0);
+          const double sv = st[j].s * wgt;
+          // P22D(C_b, C_temp) then add_side_candidate (Candidates.cpp:106-115)
+          if (cnt == 0) {
+            arena_side_y[o] = st[j].y;
+            arena_side_s[o] = sv;
+            st0 = sv;
+            cnt = 1;
+          } else if (st0 < 0) {
+            arena_side_y[o] = st[j].y;
+            arena_side_s[o] = sv;
+            st0 = sv;
+          } else {
+            if (!(sv >= 0)) atomicOr(err, 16);  // CV_Assert(S >= 0)
+            arena_side_y[o + cnt] = st[j].y;
+            arena_side_s[o + cnt] = sv;
+            ++cnt;
+          }
+        }
+      }
+      if (cnt == 0) {
+        arena_side_y[o] = -1;  // Candidate(-1, -1, -1)
+        arena_side_s[o] = -1;
+        cnt = 1;
+      }
+      LmP22D p;
+      p.bottom = sb[i];
+      p.side_off = o;
+      p.side_cnt = cnt;
+      arena_p22d[bp + i] = p;
+    }
+  }
+  if (threadIdx.x == 0) {
+    H->p22d_off[feat] = bp;
+    H->p22d_cnt[feat] = Nb;
+    H->side_off[feat] = bs;
+    H->side_cnt[feat] = s_off[Nb];
+  }
+}
+
+// ----------------------------------------------------------------- k_carry
+// Copies the bottom candidate lists of the last slot of the previous batch
+// (frame first-1) to the carry buffer read by k_post for slot 0.
+// Runs first in a batch (arena counters reset by the host): the carried
+// candidates occupy arena_cand[0, n0 + n1).
+__global__ void k_carry(const LmSlotOut* __restrict__ prev_hdr, int prev_slot, const LmCand* __restrict__ prev_cand,
+                        LmCand* __restrict__ arena_cand, LmSlotOut* __restrict__ hdr, LmArenaCtl* __restrict__ ctl) {
+  const LmSlotOut P = prev_hdr[prev_slot];
+  const int n0 = P.cand_cnt[0], n1 = P.cand_cnt[1];
+  for (int k = threadIdx.x; k < n0; k += blockDim.x) arena_cand[k] = prev_cand[P.cand_off[0] + k];
+  for (int k = threadIdx.x; k < n1; k += blockDim.x) arena_cand[n0 + k] = prev_cand[P.cand_off[1] + k];
+  if (threadIdx.x == 0) {
+    hdr[0].cand_off[0] = 0;
+    hdr[0].cand_cnt[0] = n0;
+    hdr[0].cand_off[1] = n0;
+    hdr[0].cand_cnt[1] = n1;
+    ctl->used[AR_CAND] = n0 + n1;
+  }
+}
+

@@ -1,0 +1,918 @@
+// lm_runtime.hip — host runtime behind include/locomouse_hip.h.
+//
+// Owns the device state of one LocoMouse context: setup validation and
+// geometry (LocoMouse::LocoMouse :307-345, validateImageVideoSize :486-540,
+// initializeFeatureLoop :655-769, LocoMouse_Model :3095-3179), the per-batch
+// buffers, the kernel chain of lm_kernels.hip and the assembly of results
+// into the reference's container layout (Candidate / P22D / MyMat /
+// MATSPARSE, in frame order).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "locomouse_hip.h"
+#include "lm_kernels.hip"
+
+#define LM_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+thread_local std::string g_err = "";
+
+struct HipError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIPCHK(x) hip_check((x), #x)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    release();
+    if (count == 0) count = 1;
+    HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    n = count;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DevBuf() { release(); }
+};
+
+template <class T>
+struct HostBuf {  // pinned
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count) {
+    release();
+    if (count == 0) count = 1;
+    HIPCHK(hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault));
+    n = count;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~HostBuf() { release(); }
+};
+
+struct Rect {
+  int x = 0, y = 0, w = 0, h = 0;
+};
+
+int ceil_half(int v) { return (int)std::ceil((double)v / 2); }
+
+struct Arena {
+  DevBuf<LmCand> cand;
+  DevBuf<LmP22D> p22d;
+  DevBuf<int32_t> side_y;
+  DevBuf<double> side_s;
+  DevBuf<double> unary;
+  DevBuf<int32_t> jc, ir;
+  DevBuf<double> pr;
+  DevBuf<LmSlotOut> hdr;
+  DevBuf<LmArenaCtl> ctl;
+  int cap[AR_COUNT] = {0};
+  void alloc(const int* c, int nslots) {
+    for (int k = 0; k < AR_COUNT; ++k) cap[k] = c[k];
+    cand.alloc(cap[AR_CAND]);
+    p22d.alloc(cap[AR_P22D]);
+    side_y.alloc(cap[AR_SIDE]);
+    side_s.alloc(cap[AR_SIDE]);
+    unary.alloc(cap[AR_UNARY]);
+    jc.alloc(cap[AR_PWJC]);
+    ir.alloc(cap[AR_PWNZ]);
+    pr.alloc(cap[AR_PWNZ]);
+    if (!hdr.p) hdr.alloc(nslots);
+    if (!ctl.p) ctl.alloc(1);
+  }
+};
+
+}  // namespace
+
+struct lm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int max_batch = 0, nslots = 0;
+  int debug = 0;
+  lm_setup setup{};
+  lm_params params{};
+  lm_geometry geo{};
+  LmConst K{};
+  int npix = 0;
+  int bb_x = 0, bb_yb = 0, bb_ys = 0;  // provided-box bottom-right corners
+  int spost_b_w = 0, spost_b_h = 0, spost_t_w = 0, spost_t_h = 0;
+  int64_t ext_slot_bytes = 0, tailbin_slot_bytes = 0, dbg_slot_floats = 0;
+  int64_t dbg_off[LM_NDET] = {0};
+  int64_t gscratch_slot = 0;
+  size_t corr_lds = 0;
+  // device buffers
+  DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin, tailmask;
+  DevBuf<int32_t> cal, npos, err;
+  DevBuf<float> weights, dbg;
+  DevBuf<int64_t> dbg_offd;
+  DevBuf<const uint8_t*> frame_ptr;
+  DevBuf<LmSlot> slots;
+  DevBuf<unsigned long long> keys, gscratch;
+  DevBuf<unsigned> tscratch;
+  Arena arena[2];
+  int parity = 0;
+  // host
+  HostBuf<LmSlot> h_slots;
+  HostBuf<const uint8_t*> h_frame_ptr;
+  HostBuf<LmSlotOut> h_hdr;
+  HostBuf<LmArenaCtl> h_ctl;
+  HostBuf<int32_t> h_err;
+  std::vector<LmCand> h_cand;
+  std::vector<LmP22D> h_p22d;
+  std::vector<int32_t> h_side_y, h_jc, h_ir;
+  std::vector<double> h_side_s, h_unary, h_pr;
+  // state carried between batches
+  bool have_state = false;
+  int last_frame = -1, last_n = 0, last_parity = 0;
+  // last batch info
+  int batch_n = 0, batch_s0 = 1;
+  // results
+  std::vector<int64_t> r_cand_off, r_p22d_off, r_unary_off, r_jc_off, r_nz_off;
+  std::vector<lm_candidate> r_cand;
+  std::vector<lm_p22d> r_p22d;
+  std::vector<int32_t> r_side_y, r_pw_dims, r_jc, r_ir, r_tail;
+  std::vector<double> r_side_s, r_unary, r_pr;
+  // timing
+  std::vector<std::string> t_names;
+  std::vector<double> t_ms;
+
+  ~lm_ctx() {
+    if (stream) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+};
+
+namespace {
+
+void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const lm_model* M) {
+  if (!su || !P || !M) throw std::invalid_argument("null setup/params/model");
+  // LocoMouse_Parameters (:33-249)
+  if (P->conn_comp_connectivity != 4 && P->conn_comp_connectivity != 8)
+    throw std::invalid_argument("Invalid configuration parameter: conn_comp_connectivity must be either 4 or 8.");
+  if (P->side_bottom_min_overlap < 0 || P->side_bottom_min_overlap > 1)
+    throw std::invalid_argument("Invalid configuration parameter: side_bottom_min_overlap must belong to [0,1].");
+  if (P->max_displacement_bottom < 0 || P->max_displacement_side < 0 || P->occlusion_grid_spacing_pixels_side < 0 ||
+      P->occlusion_grid_spacing_pixels_bottom < 0 || P->alpha_vel_bottom < 0 || P->alpha_vel_side < 0 ||
+      P->pairwise_occluded_cost < 0)
+    throw std::invalid_argument("Invalid configuration parameter: must be non-negative.");
+  if (P->occlusion_grid_max_width < 0 || P->occlusion_grid_max_width > 1 || P->tail_sub_bounding_box < 0 ||
+      P->tail_sub_bounding_box > 1)
+    throw std::invalid_argument("Invalid configuration parameter: must belong to [0,1].");
+  for (int k = 0; k < 5; ++k) {
+    const lm_location_prior& q = P->location_prior[k];
+    if (!(q.min_x < q.max_x) || !(q.min_y < q.max_y))
+      throw std::invalid_argument("location_prior: CV_Assert(minx < maxx && miny < maxy)");
+  }
+  if (!P->use_provided_bounding_box)
+    throw std::invalid_argument("use_provided_bounding_box = 0 needs the whole-video BB pass (not on this path).");
+  if (P->transform_gray_values)
+    throw std::runtime_error(
+        "transform_gray_values: LUT re-types the bottom mask to CV_32F and Mat::setTo asserts (LocoMouse_class.cpp:1448, :849).");
+  if (P->occlusion_grid_spacing_pixels_bottom <= 0) throw std::invalid_argument("occlusion_grid_spacing_pixels_bottom must be > 0.");
+  // loaders / validateImageVideoSize
+  if (!su->background || !su->ind_warp_mapping) throw std::invalid_argument("background / calibration missing.");
+  if (su->video_rows <= 0 || su->video_cols <= 0 || su->calib_rows <= 0 || su->calib_cols <= 0)
+    throw std::invalid_argument("empty video or calibration.");
+  if (su->method < 0 || su->method > 2) throw std::invalid_argument("method must be 0, 1 or 2.");
+  const int64_t nv = (int64_t)su->video_rows * su->video_cols;
+  const int64_t nc = (int64_t)su->calib_rows * su->calib_cols;
+  int32_t mn = INT32_MAX, mx = INT32_MIN;
+  for (int64_t i = 0; i < nc; ++i) {
+    mn = std::min(mn, su->ind_warp_mapping[i]);
+    mx = std::max(mx, su->ind_warp_mapping[i]);
+  }
+  if (mn < 0 || mx >= nv) throw std::runtime_error("Calibration mapping indices out of range.");
+  const int NR = su->calib_rows, NC = su->calib_cols;
+  const lm_rect ub = P->bounding_box_bottom, us = P->bounding_box_side;
+  if (ub.x < 0 || ub.y < 0 || ub.x + ub.width >= NC || ub.y + ub.height >= NR)
+    throw std::runtime_error("Provided bounding box for the bottom view exceeds the image dimensions.");
+  if (us.x < 0 || us.y < 0 || us.x + us.width >= NC || us.y + us.height >= NR)
+    throw std::runtime_error("Provided bounding box for the side view exceeds the image dimensions.");
+  // model (:3095-3162)
+  const lm_detector* dets[6] = {&M->paw_bottom, &M->snout_bottom, &M->tail_bottom, &M->paw_side, &M->snout_side, &M->tail_side};
+  const char* names[6] = {"modelPaw_bottom", "modelSnout_bottom", "modelTail_bottom", "modelPaw_side", "modelSnout_side", "modelTail_side"};
+  for (int d = 0; d < 6; ++d) {
+    if (!dets[d]->weights || dets[d]->rows <= 0 || dets[d]->cols <= 0)
+      throw std::invalid_argument(std::string("Error: ") + names[d] + " cannot be empty.");
+    if (dets[d]->rows > LM_MAXK || dets[d]->cols > LM_MAXK)
+      throw std::invalid_argument(std::string(names[d]) + ": detectors larger than 64x64 are not supported.");
+  }
+
+  c->setup = *su;
+  c->params = *P;
+  lm_geometry& g = c->geo;
+  std::memset(&g, 0, sizeof(g));
+  g.n_rows = NR;
+  g.n_cols = NC;
+  const int mts_c = std::max(M->paw_side.cols, M->snout_side.cols), mts_r = std::max(M->paw_side.rows, M->snout_side.rows);
+  const int mtb_c = std::max(M->paw_bottom.cols, M->snout_bottom.cols), mtb_r = std::max(M->paw_bottom.rows, M->snout_bottom.rows);
+  g.spre_t_w = ceil_half(mts_c - 1);
+  g.spre_t_h = ceil_half(mts_r - 1);
+  g.spre_b_w = ceil_half(mtb_c - 1);
+  g.spre_b_h = ceil_half(mtb_r - 1);
+  g.spost_t_w = (mts_c - 1) / 2;
+  g.spost_t_h = (mts_r - 1) / 2;
+  g.spost_b_w = g.spre_b_w;  // LocoMouse_Model move-assign: spost_b = other.size_pre_bottom() (:3173)
+  g.spost_b_h = g.spre_b_h;
+  g.bb_bottom_mouse = lm_rect{0, 0, ub.width, ub.height};
+  g.bb_side_mouse = lm_rect{0, 0, us.width, us.height};
+  g.pad_pre_rows = std::max({us.height, g.spre_t_h, g.spre_b_h});
+  g.pad_post_rows = g.spost_b_h > g.spost_t_h ? g.spost_b_h : g.spost_t_h;
+  g.pad_pre_cols = std::max({ub.width, g.spre_t_w, g.spre_b_w});
+  g.pad_post_cols = g.spost_b_w > g.spost_t_w ? g.spost_b_w : g.spost_t_w;
+  g.ipad_rows = g.pad_pre_rows + NR + g.pad_post_rows;
+  g.ipad_cols = g.pad_pre_cols + NC + g.pad_post_cols;
+  g.bb_bottom_mouse_pad = lm_rect{0, 0, g.spre_b_w + ub.width + g.spost_b_w, g.spre_b_h + ub.height + g.spost_b_h};
+  g.bb_side_mouse_pad = lm_rect{0, 0, g.spre_t_w + us.width + g.spost_t_w, g.spre_t_h + us.height + g.spost_t_h};
+  g.bb_unpad_mouse_bottom = lm_rect{g.spre_b_w, g.spre_b_h, ub.width, ub.height};
+  g.bb_unpad_mouse_side = lm_rect{g.spre_t_w, g.spre_t_h, us.width, us.height};
+  const int tw = (int)(unsigned)((int)(double)(ub.width) * P->tail_sub_bounding_box);
+  g.tail_box_width = tw;
+  g.bb_bottom_tail_pad = lm_rect{0, 0, tw + g.spre_b_w + g.spost_b_w, ub.height + g.spre_b_h + g.spost_b_h};
+  g.bb_unpad_tail_bottom = lm_rect{g.spre_b_w, g.spre_b_h, tw, ub.height};
+  g.bb_bottom_tail = lm_rect{0, 0, tw, ub.height};
+  g.bb_side_tail_pad = lm_rect{0, 0, tw + g.spre_t_w + g.spost_t_w, us.height + g.spre_t_h + g.spost_t_h};
+  g.bb_unpad_tail_side = lm_rect{g.spre_t_w, g.spre_t_h, tw, us.height};
+  const int sp = P->occlusion_grid_spacing_pixels_bottom;
+  g.ong_ny = (int)(unsigned)(((ub.height - sp) / sp) + 1);
+  g.ong_nx = (int)(unsigned)(((P->occlusion_grid_max_width * ub.width) - sp) / sp + 1);
+  g.ong_br_x = (double)(ub.width - 1 - sp / 2);
+  g.ong_br_y = (double)(ub.height - 1 - sp / 2);
+  const int sps = P->occlusion_grid_spacing_pixels_side;
+  g.n_ong_side = sps > 0 ? (int)(unsigned)(((us.height - sps) / sps) + 1) : 0;
+  g.ong_side_lowest = (int)(unsigned)(us.height - 1 - sps / 2);
+  auto mrect = [](const lm_detector& d) {  // LocoMouse_Feature :2954-2969
+    const int nw = (int)std::round((double)d.cols / 2), nh = (int)std::round((double)d.rows / 2);
+    return lm_rect{-(nw / 2), -(nh / 2), nw, nh};
+  };
+  g.match_box_paw_bottom = mrect(M->paw_bottom);
+  g.match_box_paw_side = mrect(M->paw_side);
+  g.match_box_snout_bottom = mrect(M->snout_bottom);
+  g.match_box_snout_side = mrect(M->snout_side);
+  if (g.ong_nx <= 0 || g.ong_ny <= 0) throw std::invalid_argument("occlusion grid is empty for this bounding box.");
+  if (tw <= 0) throw std::invalid_argument("tail box width is 0.");
+
+  c->bb_x = ub.x + ub.width;  // getBoundingBox provided-box branch (:547-557)
+  c->bb_ys = us.y + us.height;
+  c->bb_yb = ub.y + ub.height;
+  c->npix = (int)nv;
+
+  // ---------------- kernel constants
+  LmConst& K = c->K;
+  std::memset(&K, 0, sizeof(K));
+  const int view_of[6] = {0, 0, 0, 1, 1, 1};
+  const int kind_of[6] = {0, 0, 1, 0, 0, 1};
+  const int list_of[6] = {LIST_PAW_B, LIST_SNOUT_B, 0, LIST_PAW_S, LIST_SNOUT_S, 1};
+  Rect out_rel[6];  // output region relative to the padded crop
+  out_rel[DET_PAW_B] = out_rel[DET_SNOUT_B] = Rect{g.spre_b_w, g.spre_b_h, ub.width, ub.height};
+  out_rel[DET_TAIL_B] = Rect{g.spre_b_w, g.spre_b_h, tw, ub.height};
+  out_rel[DET_PAW_S] = out_rel[DET_SNOUT_S] = Rect{g.spre_t_w, g.spre_t_h, us.width, us.height};
+  out_rel[DET_TAIL_S] = Rect{g.spre_t_w, g.spre_t_h, tw, us.height};
+  int tile = 0, w_off = 0;
+  int ey0[2] = {INT32_MAX, INT32_MAX}, ex0[2] = {INT32_MAX, INT32_MAX}, ey1[2] = {INT32_MIN, INT32_MIN},
+      ex1[2] = {INT32_MIN, INT32_MIN};
+  for (int d = 0; d < 6; ++d) {
+    LmDet& D = K.det[d];
+    const lm_detector& src = *dets[d];
+    D.view = view_of[d];
+    D.kind = kind_of[d];
+    D.list = list_of[d];
+    D.kh = src.rows;
+    D.kw = src.cols;
+    D.kwp = (src.cols + LM_JC - 1) / LM_JC * LM_JC;
+    D.w_off = w_off;
+    w_off += D.kh * D.kwp;
+    D.delta = (float)(-src.bias);  // saturate_cast<float>(delta)
+    D.oh = out_rel[d].h;
+    D.ow = out_rel[d].w;
+    D.tiles_x = (D.ow + LM_TW - 1) / LM_TW;
+    D.tiles_y = (D.oh + LM_TH - 1) / LM_TH;
+    D.tile_base = tile;
+    tile += D.tiles_x * D.tiles_y;
+    D.box_w = src.cols;
+    D.box_h = src.rows;
+    const int ay = src.rows / 2, ax = src.cols / 2;  // anchor Point(-1,-1)
+    const int y0 = out_rel[d].y - ay, x0 = out_rel[d].x - ax;
+    const int v = D.view;
+    ey0[v] = std::min(ey0[v], y0);
+    ex0[v] = std::min(ex0[v], x0);
+    ey1[v] = std::max(ey1[v], y0 + D.tiles_y * LM_TH + D.kh - 1);
+    ex1[v] = std::max(ex1[v], x0 + D.tiles_x * LM_TW + D.kwp - 1 + 4);
+    D.in_y = y0;  // rebased below
+    D.in_x = x0;
+    D.m_y = out_rel[d].y;
+    D.m_x = out_rel[d].x;
+  }
+  K.n_tiles = tile;
+  for (int v = 0; v < 2; ++v) {
+    K.ext_oy[v] = ey0[v];
+    K.ext_ox[v] = ex0[v];
+    K.ext_h[v] = ey1[v] - ey0[v];
+    K.ext_w[v] = ((ex1[v] - ex0[v]) + 15) / 16 * 16;
+  }
+  for (int d = 0; d < 6; ++d) {
+    LmDet& D = K.det[d];
+    D.in_y -= K.ext_oy[D.view];
+    D.in_x -= K.ext_ox[D.view];
+    D.m_y -= K.ext_oy[D.view];
+    D.m_x -= K.ext_ox[D.view];
+  }
+  K.crop_h[0] = g.bb_bottom_mouse_pad.height;
+  K.crop_w[0] = g.bb_bottom_mouse_pad.width;
+  K.crop_h[1] = g.bb_side_mouse_pad.height;
+  K.crop_w[1] = g.bb_side_mouse_pad.width;
+  K.unpad_y[0] = g.spre_b_h;
+  K.unpad_x[0] = g.spre_b_w;
+  K.unpad_y[1] = g.spre_t_h;
+  K.unpad_x[1] = g.spre_t_w;
+  K.video_rows = su->video_rows;
+  K.video_cols = su->video_cols;
+  K.n_rows = NR;
+  K.n_cols = NC;
+  K.pad_pre_rows = g.pad_pre_rows;
+  K.pad_pre_cols = g.pad_pre_cols;
+  K.ipad_rows = g.ipad_rows;
+  K.ipad_cols = g.ipad_cols;
+  K.flip = su->flip ? 1 : 0;
+  K.tail_w = tw;
+  K.tail_hb = ub.height;
+  K.tail_hs = us.height;
+  K.connectivity = P->conn_comp_connectivity;
+  int64_t off = 0;
+  for (int l = 0; l < LM_NLIST; ++l) {
+    const int d = l == 0 ? DET_PAW_B : l == 1 ? DET_SNOUT_B : l == 2 ? DET_PAW_S : DET_SNOUT_S;
+    K.list_cap[l] = K.det[d].oh * K.det[d].ow;
+    K.list_off[l] = off;
+    off += K.list_cap[l];
+  }
+  K.keys_per_slot = off;
+  K.side_bottom_min_overlap = P->side_bottom_min_overlap;
+  K.alpha_vel_bottom = P->alpha_vel_bottom;
+  K.pairwise_occluded_cost = P->pairwise_occluded_cost;
+  K.max_displacement_bottom = P->max_displacement_bottom;
+  K.ong_spacing_bottom = sp;
+  K.ong_nx = g.ong_nx;
+  K.ong_ny = g.ong_ny;
+  K.ong_br_x = g.ong_br_x;
+  K.ong_br_y = g.ong_br_y;
+  K.bb_bottom_w = ub.width;
+  K.bb_bottom_h = ub.height;
+  K.spre_b_w = g.spre_b_w;
+  K.spre_b_h = g.spre_b_h;
+  K.spre_t_w = g.spre_t_w;
+  K.spre_t_h = g.spre_t_h;
+  const lm_rect mb[2] = {g.match_box_paw_bottom, g.match_box_snout_bottom};
+  const lm_rect ms[2] = {g.match_box_paw_side, g.match_box_snout_side};
+  for (int f = 0; f < 2; ++f) {
+    K.match_b[f][0] = mb[f].x;
+    K.match_b[f][1] = mb[f].y;
+    K.match_b[f][2] = mb[f].width;
+    K.match_b[f][3] = mb[f].height;
+    K.match_s[f][0] = ms[f].x;
+    K.match_s[f][1] = ms[f].y;
+    K.match_s[f][2] = ms[f].width;
+    K.match_s[f][3] = ms[f].height;
+    const lm_detector& db = f == 0 ? M->paw_bottom : M->snout_bottom;
+    const lm_detector& ds = f == 0 ? M->paw_side : M->snout_side;
+    K.size_b[f][0] = db.cols;
+    K.size_b[f][1] = db.rows;
+    K.size_s[f][0] = ds.cols;
+    K.size_s[f][1] = ds.rows;
+  }
+  for (int k = 0; k < 5; ++k) {
+    const lm_location_prior& q = P->location_prior[k];
+    const double row[7] = {q.x, q.y, q.max_distance, q.min_x, q.max_x, q.min_y, q.max_y};
+    for (int j = 0; j < 7; ++j) K.prior[k][j] = row[j];
+  }
+  if (g.ong_nx * g.ong_ny + 1 + 512 > LM_POST_MAXOFF) throw std::invalid_argument("occlusion grid too large.");
+
+  // per-slot sizes
+  c->ext_slot_bytes = ((int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1] + 255) / 256 * 256;
+  c->tailbin_slot_bytes = (int64_t)(K.tail_hb + K.tail_hs) * K.tail_w;
+  int64_t doff = 0;
+  for (int d = 0; d < 6; ++d) {
+    c->dbg_off[d] = doff;
+    doff += (int64_t)K.det[d].oh * K.det[d].ow;
+  }
+  c->dbg_slot_floats = doff;
+  int np = 1;
+  while (np < std::max(K.list_cap[0], K.list_cap[2])) np <<= 1;
+  c->gscratch_slot = 2 * (int64_t)np;
+  size_t lds = 0;
+  for (int d = 0; d < 6; ++d) {
+    const LmDet& D = K.det[d];
+    int cols = LM_TW + D.kwp - 1;
+    int stride = cols + ((16 - (cols & 31) + 32) & 31);
+    lds = std::max(lds, (size_t)(LM_TH + D.kh - 1) * stride * sizeof(float) + 16);
+  }
+  c->corr_lds = lds;
+
+  // weights (float, rows zero-padded to kwp) and TM imadjust LUT
+  std::vector<float> wts((size_t)w_off, 0.f);
+  for (int d = 0; d < 6; ++d) {
+    const LmDet& D = K.det[d];
+    for (int i = 0; i < D.kh; ++i)
+      for (int j = 0; j < D.kw; ++j) wts[(size_t)D.w_off + i * D.kwp + j] = (float)dets[d]->weights[(size_t)i * D.kw + j];
+  }
+  uint8_t adj[256];
+  {
+    // imadjust(I, I, 0, 0.6, 0, 1) (LocoMouse_class.cpp:3204-3242)
+    double low_in = 0 * 255, high_in = 0.6 * 255, low_out = 0 * 255, high_out = 1 * 255.0;
+    double range_in = high_in - low_in, range_out = high_out - low_out, range_div = range_out / range_in;
+    for (int i = 0; i < 256; ++i) {
+      double temp;
+      if (i <= low_in) temp = 0;
+      else if (i >= high_in) temp = range_out;
+      else temp = (i - low_in) * (range_div);
+      adj[i] = (uint8_t)std::round((temp + low_out));
+    }
+  }
+
+  // ---------------- device allocations
+  const int ns = c->nslots;
+  c->bkg.alloc(nv);
+  HIPCHK(hipMemcpy(c->bkg.p, su->background, nv, hipMemcpyHostToDevice));
+  c->cal.alloc(nc);
+  HIPCHK(hipMemcpy(c->cal.p, su->ind_warp_mapping, nc * sizeof(int32_t), hipMemcpyHostToDevice));
+  c->weights.alloc(wts.size());
+  HIPCHK(hipMemcpy(c->weights.p, wts.data(), wts.size() * sizeof(float), hipMemcpyHostToDevice));
+  c->adj.alloc(256);
+  HIPCHK(hipMemcpy(c->adj.p, adj, 256, hipMemcpyHostToDevice));
+  const int64_t fstride = (nv + 255) / 256 * 256;
+  c->frames.alloc((size_t)fstride * ns);
+  c->halo.alloc(fstride);
+  HIPCHK(hipMemset(c->halo.p, 0, fstride));
+  c->luts.alloc((size_t)256 * ns);
+  c->ext.alloc((size_t)c->ext_slot_bytes * ns);
+  c->tailbin.alloc((size_t)c->tailbin_slot_bytes * ns);
+  c->tailmask.alloc((size_t)K.tail_hb * K.tail_w * ns);
+  c->tscratch.alloc((size_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w * ns);
+  c->keys.alloc((size_t)K.keys_per_slot * ns);
+  c->npos.alloc((size_t)LM_NLIST * ns);
+  c->err.alloc(1);
+  c->frame_ptr.alloc(ns);
+  c->slots.alloc(ns);
+  c->h_slots.alloc(ns);
+  c->h_frame_ptr.alloc(ns);
+  c->h_hdr.alloc(ns);
+  c->h_ctl.alloc(1);
+  c->h_err.alloc(1);
+  int cap[AR_COUNT];
+  cap[AR_CAND] = ns * LM_NLIST * 64;
+  cap[AR_P22D] = ns * LM_NFEAT * 64;
+  cap[AR_SIDE] = ns * LM_NFEAT * 256;
+  cap[AR_UNARY] = ns * LM_NFEAT * 64 * 4;
+  cap[AR_PWJC] = ns * LM_NFEAT * (64 + g.ong_nx * g.ong_ny + 1);
+  cap[AR_PWNZ] = ns * LM_NFEAT * 1024;
+  for (int a = 0; a < 2; ++a) c->arena[a].alloc(cap, ns);
+  HIPCHK(hipFuncSetAttribute((const void*)k_corr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->corr_lds));
+  HIPCHK(hipFuncSetAttribute((const void*)k_corr_dbg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->corr_lds));
+}
+
+lm_status fail(lm_status s, const std::string& m) {
+  g_err = m;
+  return s;
+}
+
+template <class F>
+lm_status guarded(F&& f) {
+  try {
+    f();
+    return LM_OK;
+  } catch (const std::invalid_argument& e) {
+    return fail(LM_ERR_INVALID_ARGUMENT, e.what());
+  } catch (const HipError& e) {
+    return fail(LM_ERR_HIP, e.what());
+  } catch (const std::exception& e) {
+    return fail(LM_ERR_RUNTIME, e.what());
+  }
+}
+
+struct Timer {
+  lm_ctx* c;
+  bool on;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> ev;
+  explicit Timer(lm_ctx* cc) : c(cc), on(cc->debug & 2) {}
+  void begin(const char* name) {
+    if (!on) return;
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, c->stream));
+    ev.push_back({name, {a, b}});
+  }
+  void end() {
+    if (!on) return;
+    HIPCHK(hipEventRecord(ev.back().second.second, c->stream));
+  }
+  void collect() {
+    if (!on) return;
+    c->t_names.clear();
+    c->t_ms.clear();
+    for (auto& e : ev) {
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, e.second.first, e.second.second));
+      c->t_names.push_back(e.first);
+      c->t_ms.push_back(ms);
+      (void)hipEventDestroy(e.second.first);
+      (void)hipEventDestroy(e.second.second);
+    }
+    ev.clear();
+  }
+};
+
+void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev, const int32_t* bb,
+               bool device_frames, lm_batch_result* out) {
+  if (n <= 0 || n > c->max_batch) throw std::invalid_argument("n must be in [1, max_batch].");
+  if (first < 0) throw std::invalid_argument("first_frame must be >= 0.");
+  if (!frames) throw std::invalid_argument("frames is NULL.");
+  if (pitch < c->npix) throw std::invalid_argument("frame_pitch smaller than one frame.");
+  HIPCHK(hipSetDevice(c->device));
+  const bool halo = prev != nullptr && first > 0;
+  const bool carry = !halo && first > 0;
+  if (carry && !(c->have_state && c->last_frame == first - 1))
+    throw std::invalid_argument("frame first_frame-1 was not processed by this context: pass prev_frame (shard start).");
+  const LmConst& K = c->K;
+  const lm_geometry& g = c->geo;
+  const int64_t fstride = (c->npix + 255) / 256 * 256;
+  hipStream_t st = c->stream;
+  Timer T(c);
+
+  // ---- slots: frame pointers and crop rectangles (cropBoundingBox :1420-1470)
+  const int s_lut0 = first > 0 ? 0 : 1, s_proc0 = halo ? 0 : 1;
+  for (int s = 0; s <= n; ++s) {
+    LmSlot& S = c->h_slots.p[s];
+    std::memset(&S, 0, sizeof(S));
+    const int gframe = first - 1 + s;
+    S.frame = gframe;
+    S.active = s >= s_lut0;
+    if (s == 0) c->h_frame_ptr.p[0] = c->halo.p;
+    else c->h_frame_ptr.p[s] = device_frames ? frames + (int64_t)(s - 1) * pitch : c->frames.p + (int64_t)s * fstride;
+    if (s < s_lut0) continue;
+    const int bi = halo ? s : s - 1;  // index into bb[]
+    int bx = c->bb_x, byb = c->bb_yb, bys = c->bb_ys;
+    if (bb && (s > 0 || halo)) {
+      bx = bb[3 * bi];
+      byb = bb[3 * bi + 1];
+      bys = bb[3 * bi + 2];
+    }
+    S.crop_x[0] = (int)((unsigned)(bx + g.pad_pre_cols) - (unsigned)(g.bb_bottom_mouse_pad.width - g.spost_b_w) + 1u);
+    S.crop_y[0] = (int)((unsigned)(byb + g.pad_pre_rows) - (unsigned)(g.bb_bottom_mouse_pad.height - g.spost_b_h) + 1u);
+    S.crop_x[1] = (int)((unsigned)(g.pad_pre_cols + bx) - (unsigned)(g.bb_side_mouse_pad.width - g.spost_t_w) + 1u);
+    S.crop_y[1] = (int)((unsigned)(g.pad_pre_rows + bys) - (unsigned)(g.bb_side_mouse_pad.height - g.spost_t_h) + 1u);
+    const int w[2] = {g.bb_bottom_mouse_pad.width, g.bb_side_mouse_pad.width};
+    const int h[2] = {g.bb_bottom_mouse_pad.height, g.bb_side_mouse_pad.height};
+    if (s >= s_proc0)
+      for (int v = 0; v < 2; ++v)
+        if (S.crop_x[v] < 0 || S.crop_y[v] < 0 || S.crop_x[v] + w[v] > g.ipad_cols || S.crop_y[v] + h[v] > g.ipad_rows)
+          throw std::runtime_error(std::string("ROI out of image bounds: ") + (v ? "BB_SIDE_MOUSE_PAD" : "BB_BOTTOM_MOUSE_PAD"));
+  }
+  (void)K;
+
+  // ---- inputs
+  if (!device_frames) {
+    for (int s = 1; s <= n; ++s)
+      HIPCHK(hipMemcpyAsync(c->frames.p + (int64_t)s * fstride, frames + (int64_t)(s - 1) * pitch, c->npix,
+                            hipMemcpyHostToDevice, st));
+  }
+  if (halo)
+    HIPCHK(hipMemcpyAsync(c->halo.p, prev, c->npix, device_frames ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->slots.p, c->h_slots.p, sizeof(LmSlot) * (n + 1), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->frame_ptr.p, c->h_frame_ptr.p, sizeof(void*) * (n + 1), hipMemcpyHostToDevice, st));
+
+  const int cur = c->parity, prv = c->last_parity;
+  for (int attempt = 0;; ++attempt) {
+    Arena& A = c->arena[cur];
+    LmArenaCtl& hc = *c->h_ctl.p;
+    std::memset(&hc, 0, sizeof(hc));
+    for (int k = 0; k < AR_COUNT; ++k) hc.cap[k] = A.cap[k];
+    HIPCHK(hipMemcpyAsync(A.ctl.p, &hc, sizeof(hc), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(c->npos.p, 0, sizeof(int32_t) * LM_NLIST * (n + 1), st));
+    HIPCHK(hipMemsetAsync(c->err.p, 0, sizeof(int32_t), st));
+    if (carry) {
+      T.begin("k_carry");
+      k_carry<<<1, 256, 0, st>>>(c->arena[prv].hdr.p, c->last_n, c->arena[prv].cand.p, A.cand.p, A.hdr.p, A.ctl.p);
+      T.end();
+    }
+    T.begin("k_minmax_lut");
+    k_minmax_lut<<<n + 1 - s_lut0, 1024, 0, st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0, c->adj.p,
+                                                 c->setup.method != 0, c->luts.p);
+    T.end();
+    const int nproc = n + 1 - s_proc0;
+    const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
+    T.begin("k_ingest");
+    k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
+        K, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
+    T.end();
+    T.begin("k_corr");
+    k_corr<<<dim3(K.n_tiles, nproc), 256, c->corr_lds, st>>>(K, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0,
+                                                             c->keys.p, c->npos.p, c->tailbin.p, c->tailbin_slot_bytes);
+    T.end();
+    if (c->debug & 1) {
+      if (!c->dbg.p) {
+        c->dbg.alloc((size_t)c->dbg_slot_floats * c->nslots);
+        c->dbg_offd.alloc(LM_NDET);
+        HIPCHK(hipMemcpy(c->dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice));
+      }
+      k_corr_dbg<<<dim3(K.n_tiles, nproc), 256, c->corr_lds, st>>>(K, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0,
+                                                                   c->dbg.p, c->dbg_offd.p, c->dbg_slot_floats);
+    }
+    T.begin("k_tail");
+    k_tail<<<nproc, 1024, 0, st>>>(K, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p, c->tscratch.p,
+                                   (int64_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w, A.hdr.p, c->err.p);
+    T.end();
+    if (!c->gscratch.p) c->gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
+    T.begin("k_nms_bottom");
+    k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(K, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+                                                    c->gscratch_slot, A.hdr.p, A.cand.p, A.ctl.p, c->err.p);
+    T.end();
+    T.begin("k_nms_side");
+    k_nms<<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(K, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+                                                c->gscratch_slot, A.hdr.p, A.cand.p, A.ctl.p, c->err.p);
+    T.end();
+    T.begin("k_post");
+    k_post<<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(K, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
+                                                   A.cand.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
+                                                   A.pr.p, A.ctl.p, c->err.p);
+    T.end();
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_hdr.p, A.hdr.p, sizeof(LmSlotOut) * (n + 1), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_ctl.p, A.ctl.p, sizeof(LmArenaCtl), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_err.p, c->err.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const int e = *c->h_err.p;
+    if (e & 4) throw std::runtime_error("checkVelCriterion: match box outside the padded crop (cv::Mat ROI assertion).");
+    if (e & 16) throw std::runtime_error("P22D::add_side_candidate_safe: CV_Assert(S >= 0) failed.");
+    if (e & 2) throw std::runtime_error("tail foreground exceeds the kernel's LDS capacity.");
+    if (e & 8) throw std::runtime_error("candidate list exceeds the k_post LDS capacity.");
+    if (!c->h_ctl.p->overflow) break;
+    if (attempt >= 3) throw std::runtime_error("result arena overflow persists.");
+    int ncap[AR_COUNT];
+    for (int k = 0; k < AR_COUNT; ++k) ncap[k] = std::max(A.cap[k], (int)(c->h_ctl.p->used[k] * 1.25) + 1024);
+    if (carry) {
+      // keep the carried candidates readable: grow only the current arena
+    }
+    A.alloc(ncap, c->nslots);
+  }
+  T.collect();
+
+  // ---- D2H arena (used prefixes)
+  Arena& A = c->arena[cur];
+  const LmArenaCtl ctl = *c->h_ctl.p;
+  c->h_cand.resize(ctl.used[AR_CAND]);
+  c->h_p22d.resize(ctl.used[AR_P22D]);
+  c->h_side_y.resize(ctl.used[AR_SIDE]);
+  c->h_side_s.resize(ctl.used[AR_SIDE]);
+  c->h_unary.resize(ctl.used[AR_UNARY]);
+  c->h_jc.resize(ctl.used[AR_PWJC]);
+  c->h_ir.resize(ctl.used[AR_PWNZ]);
+  c->h_pr.resize(ctl.used[AR_PWNZ]);
+  auto d2h = [&](void* dst, const void* src, size_t bytes) {
+    if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+  };
+  d2h(c->h_cand.data(), A.cand.p, c->h_cand.size() * sizeof(LmCand));
+  d2h(c->h_p22d.data(), A.p22d.p, c->h_p22d.size() * sizeof(LmP22D));
+  d2h(c->h_side_y.data(), A.side_y.p, c->h_side_y.size() * sizeof(int32_t));
+  d2h(c->h_side_s.data(), A.side_s.p, c->h_side_s.size() * sizeof(double));
+  d2h(c->h_unary.data(), A.unary.p, c->h_unary.size() * sizeof(double));
+  d2h(c->h_jc.data(), A.jc.p, c->h_jc.size() * sizeof(int32_t));
+  d2h(c->h_ir.data(), A.ir.p, c->h_ir.size() * sizeof(int32_t));
+  d2h(c->h_pr.data(), A.pr.p, c->h_pr.size() * sizeof(double));
+  // keep frame first+n-1 as the next batch's previous frame (storePreviousImage :1508-1513)
+  HIPCHK(hipMemcpyAsync(c->halo.p, c->h_frame_ptr.p[n], c->npix, hipMemcpyDeviceToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+
+  // ---- assemble in frame order
+  c->r_cand_off.assign(1, 0);
+  c->r_p22d_off.assign(1, 0);
+  c->r_unary_off.assign(1, 0);
+  c->r_jc_off.assign(1, 0);
+  c->r_nz_off.assign(1, 0);
+  c->r_cand.clear();
+  c->r_p22d.clear();
+  c->r_side_y.clear();
+  c->r_side_s.clear();
+  c->r_unary.clear();
+  c->r_pw_dims.clear();
+  c->r_jc.clear();
+  c->r_ir.clear();
+  c->r_pr.clear();
+  c->r_tail.clear();
+  for (int s = 1; s <= n; ++s) {
+    const LmSlotOut& H = c->h_hdr.p[s];
+    for (int l = 0; l < LM_NLIST; ++l) {
+      for (int k = 0; k < H.cand_cnt[l]; ++k) {
+        const LmCand& q = c->h_cand[H.cand_off[l] + k];
+        c->r_cand.push_back(lm_candidate{q.x, q.y, q.s});
+      }
+      c->r_cand_off.push_back((int64_t)c->r_cand.size());
+    }
+    for (int f = 0; f < LM_NFEAT; ++f) {
+      const int side_base = (int)c->r_side_y.size();
+      for (int k = 0; k < H.p22d_cnt[f]; ++k) {
+        const LmP22D& q = c->h_p22d[H.p22d_off[f] + k];
+        lm_p22d o;
+        o.bottom = lm_candidate{q.bottom.x, q.bottom.y, q.bottom.s};
+        o.side_offset = side_base + (q.side_off - H.side_off[f]);
+        o.side_count = q.side_cnt;
+        c->r_p22d.push_back(o);
+      }
+      c->r_p22d_off.push_back((int64_t)c->r_p22d.size());
+      c->r_side_y.insert(c->r_side_y.end(), c->h_side_y.begin() + H.side_off[f],
+                         c->h_side_y.begin() + H.side_off[f] + H.side_cnt[f]);
+      c->r_side_s.insert(c->r_side_s.end(), c->h_side_s.begin() + H.side_off[f],
+                         c->h_side_s.begin() + H.side_off[f] + H.side_cnt[f]);
+      c->r_unary.insert(c->r_unary.end(), c->h_unary.begin() + H.unary_off[f],
+                        c->h_unary.begin() + H.unary_off[f] + H.unary_cnt[f]);
+      c->r_unary_off.push_back((int64_t)c->r_unary.size());
+      if (H.pw_rows[f] >= 0) {
+        c->r_pw_dims.insert(c->r_pw_dims.end(), {H.pw_rows[f], H.pw_cols[f], H.pw_nnz[f]});
+        c->r_jc.insert(c->r_jc.end(), c->h_jc.begin() + H.pw_jc_off[f], c->h_jc.begin() + H.pw_jc_off[f] + H.pw_cols[f] + 1);
+        c->r_ir.insert(c->r_ir.end(), c->h_ir.begin() + H.pw_nz_off[f], c->h_ir.begin() + H.pw_nz_off[f] + H.pw_nnz[f]);
+        c->r_pr.insert(c->r_pr.end(), c->h_pr.begin() + H.pw_nz_off[f], c->h_pr.begin() + H.pw_nz_off[f] + H.pw_nnz[f]);
+      } else {
+        c->r_pw_dims.insert(c->r_pw_dims.end(), {-1, -1, 0});
+      }
+      c->r_jc_off.push_back((int64_t)c->r_jc.size());
+      c->r_nz_off.push_back((int64_t)c->r_ir.size());
+    }
+    c->r_tail.insert(c->r_tail.end(), H.tail, H.tail + 45);
+  }
+  c->have_state = true;
+  c->last_frame = first + n - 1;
+  c->last_n = n;
+  c->last_parity = cur;
+  c->parity = 1 - cur;
+  c->batch_n = n;
+  c->batch_s0 = s_proc0;
+
+  out->n_frames = n;
+  out->first_frame = first;
+  out->cand_offset = c->r_cand_off.data();
+  out->cand = c->r_cand.data();
+  out->p22d_offset = c->r_p22d_off.data();
+  out->p22d = c->r_p22d.data();
+  out->side_y = c->r_side_y.data();
+  out->side_s = c->r_side_s.data();
+  out->unary_offset = c->r_unary_off.data();
+  out->unary = c->r_unary.data();
+  out->pw_dims = c->r_pw_dims.data();
+  out->pw_jc_offset = c->r_jc_off.data();
+  out->pw_jc = c->r_jc.data();
+  out->pw_nz_offset = c->r_nz_off.data();
+  out->pw_ir = c->r_ir.data();
+  out->pw_pr = c->r_pr.data();
+  out->tail = c->r_tail.data();
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- C ABI
+
+LM_API int32_t lm_abi_version(void) { return LM_ABI_VERSION; }
+
+LM_API const char* lm_last_error(void) { return g_err.c_str(); }
+
+LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_params* params, const lm_model* model,
+                               int32_t max_batch, lm_ctx** out) {
+  if (!out) return fail(LM_ERR_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  if (max_batch <= 0) return fail(LM_ERR_INVALID_ARGUMENT, "max_batch must be > 0");
+  lm_ctx* c = new lm_ctx();
+  lm_status s = guarded([&] {
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) throw HipError("invalid HIP device index");
+    c->device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->max_batch = max_batch;
+    c->nslots = max_batch + 1;
+    validate_and_build(c, setup, params, model);
+  });
+  if (s != LM_OK) {
+    delete c;
+    return s;
+  }
+  *out = c;
+  return LM_OK;
+}
+
+LM_API void lm_ctx_destroy(lm_ctx* ctx) { delete ctx; }
+
+LM_API lm_status lm_get_geometry(const lm_ctx* ctx, lm_geometry* out) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  *out = ctx->geo;
+  return LM_OK;
+}
+
+LM_API void* lm_ctx_stream(lm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+LM_API lm_status lm_detect_batch(lm_ctx* ctx, const uint8_t* frames, int64_t frame_pitch, int32_t n, int32_t first_frame,
+                                 const uint8_t* prev_frame, const int32_t* bb, lm_batch_result* out) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  return guarded([&] { run_batch(ctx, frames, frame_pitch, n, first_frame, prev_frame, bb, false, out); });
+}
+
+LM_API lm_status lm_detect_batch_device(lm_ctx* ctx, const uint8_t* d_frames, int64_t frame_pitch, int32_t n,
+                                        int32_t first_frame, const uint8_t* d_prev_frame, const int32_t* bb,
+                                        lm_batch_result* out) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  return guarded([&] { run_batch(ctx, d_frames, frame_pitch, n, first_frame, d_prev_frame, bb, true, out); });
+}
+
+LM_API lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags) {
+  if (!ctx) return fail(LM_ERR_INVALID_ARGUMENT, "null ctx");
+  ctx->debug = flags;
+  return LM_OK;
+}
+
+LM_API lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out, int32_t rows, int32_t cols) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  if (!(ctx->debug & 1) || !ctx->dbg.p) return fail(LM_ERR_INVALID_ARGUMENT, "debug scores not enabled");
+  if (f < 0 || f >= ctx->batch_n || det < 0 || det >= LM_NDET) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
+  const LmDet& D = ctx->K.det[det];
+  if (rows != D.oh || cols != D.ow) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
+  return guarded([&] {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpy(out, ctx->dbg.p + (int64_t)(f + 1) * ctx->dbg_slot_floats + ctx->dbg_off[det],
+                     sizeof(float) * rows * cols, hipMemcpyDeviceToHost));
+  });
+}
+
+LM_API lm_status lm_debug_tail_mask(lm_ctx* ctx, int32_t f, uint8_t* out, int32_t rows, int32_t cols) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  if (f < 0 || f >= ctx->batch_n) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
+  if (rows != ctx->K.tail_hb || cols != ctx->K.tail_w) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
+  return guarded([&] {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpy(out, ctx->tailmask.p + (int64_t)(f + 1) * rows * cols, (size_t)rows * cols, hipMemcpyDeviceToHost));
+  });
+}
+
+LM_API int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32_t cap) {
+  if (!ctx) return 0;
+  const int32_t n = (int32_t)ctx->t_names.size();
+  for (int32_t i = 0; i < n && i < cap; ++i) {
+    if (names) names[i] = ctx->t_names[i].c_str();
+    if (ms) ms[i] = ctx->t_ms[i];
+  }
+  return n;
+}
+
+// ------------------------------------------------------- synthetic source
+#include "lm_synth.h"
+
+__global__ void k_synth(uint8_t* __restrict__ out, lm_synth_scene sc, int64_t first, int64_t pitch) {
+  const int64_t f = blockIdx.y;
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t np = (int64_t)sc.rows * sc.cols;
+  if (q >= np) return;
+  uint32_t w = 0;
+  for (int k = 0; k < 4 && q + k < np; ++k) {
+    const int64_t p = q + k;
+    w |= (uint32_t)lm_synth_pixel(&sc, first + f, (int32_t)(p / sc.cols), (int32_t)(p % sc.cols)) << (8 * k);
+  }
+  uint8_t* o = out + f * pitch + q;
+  if (q + 4 <= np && ((uintptr_t)o & 3) == 0) {
+    *reinterpret_cast<uint32_t*>(o) = w;
+  } else {
+    for (int k = 0; k < 4 && q + k < np; ++k) o[k] = (uint8_t)(w >> (8 * k));
+  }
+}
+
+LM_API lm_status lm_synth_frames_device(int32_t device, uint8_t* d_out, int32_t rows, int32_t cols, int64_t first_frame,
+                                        int32_t n, int64_t frame_pitch) {
+  if (!d_out || rows <= 0 || cols <= 0 || n <= 0 || frame_pitch < (int64_t)rows * cols)
+    return fail(LM_ERR_INVALID_ARGUMENT, "bad synth arguments");
+  return guarded([&] {
+    HIPCHK(hipSetDevice(device));
+    const lm_synth_scene sc = lm_synth_default_scene(rows, cols);
+    const int64_t np = (int64_t)rows * cols;
+    k_synth<<<dim3((unsigned)((np / 4 + 255) / 256 + 1), n), 256>>>(d_out, sc, first_frame, frame_pitch);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+  });
+}

@@ -1,0 +1,166 @@
+"""ctypes binding of liblocomouse_hip.so (the C-ABI in include/locomouse_hip.h).
+
+This is how tests and bench.py drive the HIP path.  There is no CPU fallback:
+if the shared library is missing or no HIP device is present, Context()
+raises.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from .abi import LM_OK, lm_batch_result, lm_geometry, result_to_numpy
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "liblocomouse_hip.so")
+CSRC = os.path.join(PKG, "csrc")
+
+EXPORTED = (
+    "lm_abi_version", "lm_last_error", "lm_ctx_create", "lm_ctx_destroy", "lm_get_geometry", "lm_ctx_stream",
+    "lm_detect_batch", "lm_detect_batch_device", "lm_ctx_set_debug", "lm_debug_scores", "lm_debug_tail_mask",
+    "lm_debug_kernel_times", "lm_synth_frames_device",
+)
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+               "-fvisibility=hidden", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+
+
+def build(verbose=False):
+    """Compile liblocomouse_hip.so for gfx950 in-tree (hipcc cross-compiles
+    without a GPU)."""
+    cmd = ["hipcc", *HIPCC_FLAGS, "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-o", LIB_PATH,
+           os.path.join(CSRC, "lm_runtime.hip")]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run locomouse_cpp_amd.runtime.build() (no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        L.lm_abi_version.restype = C.c_int32
+        L.lm_last_error.restype = C.c_char_p
+        L.lm_ctx_create.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
+        L.lm_ctx_destroy.argtypes = [C.c_void_p]
+        L.lm_get_geometry.argtypes = [C.c_void_p, C.POINTER(lm_geometry)]
+        L.lm_ctx_stream.argtypes = [C.c_void_p]
+        L.lm_ctx_stream.restype = C.c_void_p
+        for fn in (L.lm_detect_batch, L.lm_detect_batch_device):
+            fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
+                           C.POINTER(lm_batch_result)]
+        L.lm_ctx_set_debug.argtypes = [C.c_void_p, C.c_int32]
+        L.lm_debug_scores.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
+        L.lm_debug_tail_mask.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
+        L.lm_debug_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int32]
+        L.lm_debug_kernel_times.restype = C.c_int32
+        L.lm_synth_frames_device.argtypes = [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32,
+                                             C.c_int64]
+        _lib = L
+    return _lib
+
+
+class LMError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"lm status {code}: {msg}")
+        self.code = code
+
+
+def _check(rc):
+    if rc != LM_OK:
+        raise LMError(rc, lib().lm_last_error().decode())
+
+
+def synth_frames_device(d_ptr, rows, cols, first, n, pitch, device=0):
+    """Fill device memory with synthetic frames (bench/test input utility)."""
+    _check(lib().lm_synth_frames_device(device, C.c_void_p(d_ptr), rows, cols, first, n, pitch))
+
+
+class Context:
+    """One lm_ctx on one HIP device (the per-frame loop's state)."""
+
+    def __init__(self, cfg, max_batch=64, device=0):
+        self.cfg = cfg  # keeps the arrays behind the structs alive
+        self._h = C.c_void_p()
+        _check(lib().lm_ctx_create(device, C.byref(cfg.setup), C.byref(cfg.params), C.byref(cfg.model), max_batch,
+                                   C.byref(self._h)))
+        self.max_batch = max_batch
+
+    def geometry(self):
+        g = lm_geometry()
+        _check(lib().lm_get_geometry(self._h, C.byref(g)))
+        return g
+
+    def stream(self):
+        return lib().lm_ctx_stream(self._h)
+
+    def set_debug(self, flags):
+        _check(lib().lm_ctx_set_debug(self._h, flags))
+
+    def detect(self, frames, first_frame, prev_frame=None, bb=None, raw=False):
+        """Host frames [n, rows, cols] u8 -> result dict (abi.result_to_numpy)."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        n = frames.shape[0]
+        res = lm_batch_result()
+        pp = None
+        if prev_frame is not None:
+            self._prev = np.ascontiguousarray(prev_frame, dtype=np.uint8)
+            pp = self._prev.ctypes.data
+        bbp = None
+        if bb is not None:
+            self._bb = np.ascontiguousarray(bb, dtype=np.int32)
+            bbp = self._bb.ctypes.data
+        _check(lib().lm_detect_batch(self._h, frames.ctypes.data, frames.shape[1] * frames.shape[2], n, first_frame,
+                                     pp, bbp, C.byref(res)))
+        return res if raw else result_to_numpy(res)
+
+    def detect_device(self, d_frames_ptr, pitch, n, first_frame, d_prev_ptr=None, bb=None, raw=True):
+        """Frames already in device memory (e.g. a torch.cuda uint8 tensor's data_ptr())."""
+        res = lm_batch_result()
+        bbp = None
+        if bb is not None:
+            self._bb = np.ascontiguousarray(bb, dtype=np.int32)
+            bbp = self._bb.ctypes.data
+        _check(lib().lm_detect_batch_device(self._h, C.c_void_p(d_frames_ptr), pitch, n, first_frame,
+                                            C.c_void_p(d_prev_ptr) if d_prev_ptr else None, bbp, C.byref(res)))
+        return res if raw else result_to_numpy(res)
+
+    def debug_scores(self, f, det):
+        g = self.geometry()
+        shapes = {0: (g.bb_bottom_mouse.height, g.bb_bottom_mouse.width), 1: (g.bb_bottom_mouse.height, g.bb_bottom_mouse.width),
+                  2: (g.bb_bottom_mouse.height, g.tail_box_width), 3: (g.bb_side_mouse.height, g.bb_side_mouse.width),
+                  4: (g.bb_side_mouse.height, g.bb_side_mouse.width), 5: (g.bb_side_mouse.height, g.tail_box_width)}
+        out = np.zeros(shapes[det], dtype=np.float32)
+        _check(lib().lm_debug_scores(self._h, f, det, out.ctypes.data, out.shape[0], out.shape[1]))
+        return out
+
+    def debug_tail_mask(self, f):
+        g = self.geometry()
+        out = np.zeros((g.bb_bottom_mouse.height, g.tail_box_width), dtype=np.uint8)
+        _check(lib().lm_debug_tail_mask(self._h, f, out.ctypes.data, out.shape[0], out.shape[1]))
+        return out
+
+    def kernel_times(self):
+        names = (C.c_char_p * 64)()
+        ms = (C.c_double * 64)()
+        n = lib().lm_debug_kernel_times(self._h, names, ms, 64)
+        return [(names[i].decode(), ms[i]) for i in range(min(n, 64))]
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().lm_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,160 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU restatement
+oracle on the same synthetic frames.  Integer/index outputs must be
+bit-identical; scores are compared bit-exactly too (the HIP correlation uses
+the same fmaf chain as the oracle) and, separately, within 1e-5 relative of
+the float64 cross-check in test_oracle.py.
+"""
+import numpy as np
+import pytest
+
+from locomouse_cpp_amd import synthetic as S
+from locomouse_cpp_amd.abi import frame_views
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(cfg, max_batch=16):
+    from locomouse_cpp_amd.runtime import Context
+    return Context(cfg, max_batch=max_batch)
+
+
+def _oracle(cfg, frames, flags=0):
+    from oracle import oracle as O
+    return O.OracleRun(cfg, frames, flags=flags)
+
+
+KEYS = ("cand_offset", "cand", "p22d_offset", "p22d", "side_y", "side_s", "unary_offset", "unary", "pw_dims",
+        "pw_jc_offset", "pw_jc", "pw_nz_offset", "pw_ir", "pw_pr", "tail")
+
+
+def concat_results(parts):
+    """Concatenate per-batch result dicts into one (offsets rebased)."""
+    out = {}
+    for k in KEYS:
+        if k.endswith("offset"):
+            acc, base = [np.zeros(1, np.int64)], 0
+            for p in parts:
+                acc.append(p[k][1:] + base)
+                base += int(p[k][-1])
+            out[k] = np.concatenate(acc)
+        elif k == "p22d":
+            arrs, base = [], 0
+            for p in parts:
+                a = p[k].copy()
+                a["side_offset"] += base
+                base += len(p["side_y"])
+                arrs.append(a)
+            out[k] = np.concatenate(arrs)
+        else:
+            out[k] = np.concatenate([p[k] for p in parts])
+    out["n_frames"] = sum(p["n_frames"] for p in parts)
+    return out
+
+
+def assert_same(got, ref, label=""):
+    for k in KEYS:
+        a, b = got[k], ref[k]
+        if a.dtype.names:
+            ok = a.shape == b.shape and all(np.array_equal(a[n], b[n]) for n in a.dtype.names)
+        else:
+            ok = a.shape == b.shape and np.array_equal(a, b)
+        if not ok:
+            # locate the first differing frame for a readable message
+            n = ref["n_frames"]
+            for f in range(n):
+                vg, vr = frame_views(got, f), frame_views(ref, f)
+                for lk in range(4):
+                    if not (len(vg["cand"][lk]) == len(vr["cand"][lk]) and
+                            all(np.array_equal(vg["cand"][lk][x], vr["cand"][lk][x]) for x in ("x", "y", "score"))):
+                        raise AssertionError(f"{label}{k}: frame {f} list {lk}\n gpu {vg['cand'][lk]}\n ref {vr['cand'][lk]}")
+                if not np.array_equal(vg["tail"], vr["tail"]):
+                    raise AssertionError(f"{label}{k}: frame {f} tail\n gpu {vg['tail']}\n ref {vr['tail']}")
+                for fk in range(2):
+                    if vg["p22d"][fk] != vr["p22d"][fk]:
+                        raise AssertionError(f"{label}{k}: frame {f} p22d {fk}\n gpu {vg['p22d'][fk]}\n ref {vr['p22d'][fk]}")
+                    if not np.array_equal(vg["unary"][fk], vr["unary"][fk]):
+                        raise AssertionError(f"{label}{k}: frame {f} unary {fk}\n gpu {vg['unary'][fk]}\n ref {vr['unary'][fk]}")
+                    pg, pr = vg["pairwise"][fk], vr["pairwise"][fk]
+                    if (pg is None) != (pr is None) or (pg is not None and not all(
+                            np.array_equal(pg[x], pr[x]) for x in ("jc", "ir", "pr")) or (pg and pg["n_rows"] != pr["n_rows"])):
+                        raise AssertionError(f"{label}{k}: frame {f} pairwise {fk}\n gpu {pg}\n ref {pr}")
+            raise AssertionError(f"{label}{k} differs: {a[:8]} vs {b[:8]}")
+
+
+@pytest.fixture(scope="module")
+def cfg():
+    return S.SyntheticConfig()
+
+
+def test_raw_scores_bit_exact(cfg):
+    frames = cfg.frames(0, 3)
+    ctx = _ctx(cfg)
+    ctx.set_debug(1)
+    ctx.detect(frames, 0)
+    from oracle import oracle as O
+    ref = _oracle(cfg, frames, flags=O.KEEP_DEBUG)
+    g = ctx.geometry()
+    for f in range(3):
+        for det in range(6):
+            got = ctx.debug_scores(f, det)
+            exp = ref.scores(f, det, got.shape)
+            assert exp is not None
+            assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), (f, det, np.abs(got - exp).max())
+        assert np.array_equal(ctx.debug_tail_mask(f), ref.tail_mask(f, (g.bb_bottom_mouse.height, g.tail_box_width)))
+
+
+def test_geometry_matches_oracle(cfg):
+    from oracle import oracle as O
+    assert _ctx(cfg).geometry().as_dict() == O.geometry(cfg).as_dict()
+
+
+def test_full_path_one_batch(cfg):
+    frames = cfg.frames(0, 12)
+    got = _ctx(cfg).detect(frames, 0)
+    ref = _oracle(cfg, frames).result
+    assert_same(got, ref)
+
+
+def test_batches_carry_state(cfg):
+    frames = cfg.frames(0, 12)
+    ctx = _ctx(cfg, max_batch=5)
+    parts = [ctx.detect(frames[i:i + 5], i) for i in range(0, 12, 5)]
+    assert_same(concat_results(parts), _oracle(cfg, frames).result, "carry: ")
+
+
+def test_shard_with_halo_frame(cfg):
+    frames = cfg.frames(0, 12)
+    ref = _oracle(cfg, frames).result
+    ctx = _ctx(cfg, max_batch=8)
+    a = _ctx(cfg, max_batch=8).detect(frames[:6], 0)
+    b = ctx.detect(frames[6:], 6, prev_frame=frames[5])
+    assert_same(concat_results([a, b]), ref, "halo: ")
+
+
+@pytest.mark.parametrize("kw", [{"method": 1}, {"method": 2}, {"flip": True}, {"connectivity": 4}])
+def test_variants(kw):
+    c = S.SyntheticConfig(**kw)
+    frames = c.frames(20, 6)
+    assert_same(_ctx(c).detect(frames, 0), _oracle(c, frames).result, f"{kw}: ")
+
+
+def test_device_frames_api(cfg):
+    torch = pytest.importorskip("torch")
+    frames = cfg.frames(30, 6)
+    d = torch.from_numpy(frames).cuda()
+    torch.cuda.synchronize()
+    from locomouse_cpp_amd.abi import result_to_numpy
+    ctx = _ctx(cfg)
+    got = result_to_numpy(ctx.detect_device(d.data_ptr(), frames.shape[1] * frames.shape[2], 6, 0))
+    assert_same(got, _oracle(cfg, frames).result, "device: ")
+
+
+def test_error_mapping(cfg):
+    from locomouse_cpp_amd.runtime import LMError
+    with pytest.raises(LMError) as e:
+        _ctx(S.SyntheticConfig(connectivity=5))
+    assert e.value.code == 1
+    ctx = _ctx(cfg)
+    with pytest.raises(LMError) as e:
+        ctx.detect(cfg.frames(3, 2), 3)  # frame 2 never seen and no halo
+    assert e.value.code == 1
