@@ -44,6 +44,12 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
+        # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's):
+        # load it first so this library and torch share one HIP runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: run locomouse_cpp_amd.runtime.build() (no CPU fallback)")
         L = C.CDLL(LIB_PATH)
