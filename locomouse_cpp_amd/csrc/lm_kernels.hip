@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 #include "lm_device.h"
 #include "lm_introsort.h"
 
@@ -158,19 +160,83 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst K, const uint8_t* 
 // LM_R accumulator rows; weights are wave-uniform scalar loads.
 #define LM_MAXK 64
 
-__global__ __launch_bounds__(256) void k_corr(const LmConst K, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
-                                              const float* __restrict__ weights, int s0,
+// Shared epilogue: point detectors apply the brightness mask of
+// detectBottom/SideCandidates (threshold(25.5 -> 25, BINARY_INV), :782/:817;
+// setTo(0, mask) :849/:864) and append every score > 0 as a sort key
+// (~score_bits << 32 | row-major index) to the frame's list; tail detectors
+// write the binarised map (threshold(>0) + convertTo 8U, :2593-2598).
+// Two passes over a register bitmask keep the accumulators statically indexed.
+template <int R_, int C_>
+DEV void corr_epilogue(const LmConst& K, const LmDet& D, const float (&acc)[R_][C_], const float* lds, int stride, int ly,
+                       int lx, int oy0, int ox0, int slot, unsigned long long* __restrict__ keys,
+                       int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes, int* s_cnt,
+                       int* s_base) {
+  static_assert(R_ * C_ <= 32, "bitmask");
+  const int my = D.m_y - D.in_y, mx = D.m_x - D.in_x;  // I_*_MOUSE pixel inside the LDS tile
+  if (D.kind != 0) {
+    uint8_t* __restrict__ tb = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
+#pragma unroll
+    for (int r = 0; r < R_; ++r)
+#pragma unroll
+      for (int c = 0; c < C_; ++c) {
+        const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
+        if (y < D.oh && x < D.ow) tb[(int64_t)y * D.ow + x] = acc[r][c] > 0.0f ? 1 : 0;
+      }
+    return;
+  }
+  unsigned bits = 0;
+#pragma unroll
+  for (int r = 0; r < R_; ++r)
+#pragma unroll
+    for (int c = 0; c < C_; ++c) {
+      const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
+      const float pix = lds[(ly * R_ + r + my) * stride + lx * C_ + c + mx];
+      if (y < D.oh && x < D.ow && pix > 25.0f && acc[r][c] > 0.0f) bits |= 1u << (r * C_ + c);
+    }
+  const int nk = __popc(bits);
+  const int off = nk ? atomicAdd(s_cnt, nk) : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) *s_base = *s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], *s_cnt) : 0;
+  __syncthreads();
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + *s_base + off;
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < R_; ++r)
+#pragma unroll
+    for (int c = 0; c < C_; ++c)
+      if (bits & (1u << (r * C_ + c))) {
+        const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
+        kl[k++] = ((unsigned long long)(~__float_as_uint(acc[r][c])) << 32) | (unsigned)(y * D.ow + x);
+      }
+}
+
+// LDS row stride of the packed kernel: == 4 (mod 8) so the two 16-lane row
+// groups of a ds_read2_b32 (4 rows apart) hit disjoint bank halves.
+__host__ __device__ inline int pk_stride(int cols) { return cols + ((4 - (cols & 7)) + 8) % 8; }
+
+struct LmDetGroup {
+  int32_t n;
+  int32_t ids[LM_NDET];
+  int32_t tile_end[LM_NDET];  // cumulative tile counts
+};
+
+__global__ __launch_bounds__(256) void k_corr(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+                                              int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
                                               unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                               uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
   extern __shared__ float lds[];
   __shared__ int s_cnt, s_base;
   const int slot = s0 + blockIdx.y;
-  int d = 0;
+  int gi = 0, tb = 0;
 #pragma unroll
-  for (int k = 1; k < LM_NDET; ++k)
-    if ((int)blockIdx.x >= K.det[k].tile_base) d = k;
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
   const LmDet D = K.det[d];
-  const int lt = blockIdx.x - D.tile_base;
+  const int lt = blockIdx.x - tb;
   const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
   const int rows = LM_TH + D.kh - 1, cols = LM_TW + D.kwp - 1;
   int stride = cols;
@@ -222,36 +288,256 @@ __global__ __launch_bounds__(256) void k_corr(const LmConst K, const uint8_t* __
     }
   }
 
-  // epilogue
-  const int my = D.m_y - D.in_y, mx = D.m_x - D.in_x;  // anchor inside the LDS tile
-  unsigned long long mykeys[LM_R * LM_C];
-  int nk = 0;
+  corr_epilogue<LM_R, LM_C>(K, D, acc, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes, &s_cnt, &s_base);
+}
+
+// k_corr_kw: k_corr specialised on the detector width KW (a weight row is
+// fully unrolled: one scalar-load wait per detector row instead of one per
+// 4 taps).  One launch covers the detectors of one width (ids in G).
+
+template <int KW>
+__global__ __launch_bounds__(256) void k_corr_kw(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
+                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  extern __shared__ float lds[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - tb;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
+  int stride = cols;
+  stride += (16 - (stride & 31) + 32) & 31;
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  const int cols4 = (cols + 3) >> 2;
+  for (int e = threadIdx.x; e < rows * cols4; e += 256) {
+    const int r = e / cols4, c4 = (e - r * cols4) << 2;
+    const uint8_t* p = src + (int64_t)r * ew + c4;
+    float* o = lds + r * stride + c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c4 + k < stride) o[k] = (float)p[k];
+  }
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
+  float acc[LM_R][LM_C];
 #pragma unroll
   for (int r = 0; r < LM_R; ++r)
 #pragma unroll
-    for (int c = 0; c < LM_C; ++c) {
-      const int y = oy0 + ly * LM_R + r, x = ox0 + lx * LM_C + c;
-      if (y < D.oh && x < D.ow) {
-        const float s = acc[r][c];
-        if (D.kind == 0) {
-          const float pix = lds[(ly * LM_R + r + my) * stride + lx * LM_C + c + mx];
-          if (pix > 25.0f && s > 0.0f) {  // threshold(25.5 -> 25, BINARY_INV) mask, setTo(0), > 0
-            mykeys[nk++] = ((unsigned long long)(~__float_as_uint(s)) << 32) | (unsigned)(y * D.ow + x);
-          }
-        } else {
-          tailbin[(int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0) +
-                  (int64_t)y * D.ow + x] = s > 0.0f ? 1 : 0;
+    for (int c = 0; c < LM_C; ++c) acc[r][c] = D.delta;
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  for (int t = 0; t < LM_R + kh - 1; ++t) {
+    const float* prow = lds + (ly * LM_R + t) * stride + lx * LM_C;
+    float px[LM_C + KW - 1];
+#pragma unroll
+    for (int q = 0; q < LM_C + KW - 1; ++q) px[q] = prow[q];
+#pragma unroll
+    for (int r = 0; r < LM_R; ++r) {
+      const int i = t - r;
+      if (i >= 0 && i < kh) {
+        const float* wr = W + i * kwp;
+#pragma unroll
+        for (int j = 0; j < KW; ++j) {
+          const float w = wr[j];
+#pragma unroll
+          for (int c = 0; c < LM_C; ++c) acc[r][c] = __builtin_fmaf(w, px[c + j], acc[r][c]);
         }
       }
     }
-  if (D.kind != 0) return;
-  int off = nk ? atomicAdd(&s_cnt, nk) : 0;
-  __syncthreads();
-  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
-  __syncthreads();
-  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + s_base + off;
-  for (int k = 0; k < nk; ++k) kl[k] = mykeys[k];
+  }
+
+  corr_epilogue<LM_R, LM_C>(K, D, acc, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes, &s_cnt, &s_base);
 }
+
+// k_corr_pk: packed-FP32 correlation.  gfx950 issues one v_fma_f32 (wave64)
+// per 4 cycles per SIMD; v_pk_fma_f32 does two FMAs per lane in the same slot.
+// Each accumulator pair holds two vertically adjacent outputs (rows 2p, 2p+1)
+// of one column: for tap (i, j) both use weight w[i][j] (SGPR, broadcast) and
+// pixels (t, t+1) of one column, which one ds_read2_b32 loads into an aligned
+// register pair.  Every output still accumulates its taps in row-major order
+// with single-rounding FMAs, so results are bit-identical to k_corr.
+// 192 threads as 16 (x) x 12 (y), each 5 columns x 4 rows: the 80x48 tile.
+#define PK_C 5
+#define PK_R 4
+#define PK_TY 12
+
+typedef float lm_f2 __attribute__((ext_vector_type(2)));
+
+// Pixel pairs (row t, row t+1) of one column straight into an aligned VGPR
+// pair: ds_read2_b32 with offset1 = offset0 + STRIDE (dwords).  At most 15
+// LDS reads in flight (lgkmcnt is 4 bits); one wait at the end.
+constexpr int pk_stride_c(int cols) { return cols + ((4 - (cols & 7)) + 8) % 8; }
+
+template <int STRIDE, int Q>
+DEV void lds_pair(lm_f2& dst, unsigned base) {
+  static_assert(Q + STRIDE <= 255, "ds_read2_b32 offset range");
+  if constexpr (Q >= 15) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
+  asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(dst) : "v"(base), "i"(Q), "i"(Q + STRIDE) : "memory");
+}
+
+template <int STRIDE, int N, int... Qs>
+DEV void lds_pairs_impl(lm_f2 (&px)[N], unsigned base, std::integer_sequence<int, Qs...>) {
+  (lds_pair<STRIDE, Qs>(px[Qs], base), ...);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int STRIDE, int N>
+DEV void lds_pairs(lm_f2 (&px)[N], unsigned base) {
+  lds_pairs_impl<STRIDE, N>(px, base, std::make_integer_sequence<int, N>{});
+}
+
+template <int KW, bool WLDS, bool ASMLD = false>
+__global__ __launch_bounds__(192) void k_corr_pk(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
+                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  // WLDS: detector weights staged in LDS (broadcast reads) instead of scalar
+  // loads, so every lgkm wait is an in-order LDS wait the compiler can count.
+  extern __shared__ float lds[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - tb;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
+  const int stride = pk_stride(cols);
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  const int cols4 = (cols + 3) >> 2;
+  for (int e = threadIdx.x; e < rows * cols4; e += blockDim.x) {
+    const int r = e / cols4, c4 = (e - r * cols4) << 2;
+    const uint8_t* p = src + (int64_t)r * ew + c4;
+    float* o = lds + r * stride + c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c4 + k < stride) o[k] = (float)p[k];
+  }
+  float* wl = lds + ((rows * stride + 3) & ~3);
+  if (WLDS)
+    for (int e = threadIdx.x; e < D.kh * D.kwp; e += blockDim.x) wl[e] = weights[D.w_off + e];
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
+  lm_f2 acc[PK_R / 2][PK_C];
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) acc[p][c] = (lm_f2){D.delta, D.delta};
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  for (int t = 0; t < kh + PK_R - 2; ++t) {
+    const float* p0 = lds + (ly * PK_R + t) * stride + lx * PK_C;
+    lm_f2 px[PK_C + KW - 1];
+    if constexpr (ASMLD) {
+      constexpr int STR = pk_stride_c(LM_TW + KW - 1);
+      const unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p0;
+      lds_pairs<STR, PK_C + KW - 1>(px, base);
+    } else {
+#pragma unroll
+      for (int q = 0; q < PK_C + KW - 1; ++q) px[q] = (lm_f2){p0[q], p0[q + stride]};
+    }
+#pragma unroll
+    for (int p = 0; p < PK_R / 2; ++p) {
+      const int i = t - 2 * p;
+      if (i >= 0 && i < kh) {
+        const float* wr = (WLDS ? wl : W) + i * kwp;
+#pragma unroll
+        for (int j = 0; j < KW; ++j) {
+          const float w = wr[j];
+          const lm_f2 w2 = (lm_f2){w, w};
+#pragma unroll
+          for (int c = 0; c < PK_C; ++c) acc[p][c] = __builtin_elementwise_fma(w2, px[c + j], acc[p][c]);
+        }
+      }
+    }
+  }
+  float accf[PK_R][PK_C];
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) {
+      accf[2 * p][c] = acc[p][c].x;
+      accf[2 * p + 1][c] = acc[p][c].y;
+    }
+  corr_epilogue<PK_R, PK_C>(K, D, accf, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
+                            &s_cnt, &s_base);
+}
+
+// widths with a specialised kernel; others use the generic k_corr
+#define LM_KW_LIST(X) \
+  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+
+// Correlation variants: 0 generic (runtime width), 1 width-specialised plain
+// FMA (k_corr_kw), 2 packed FMA with compiler-scheduled LDS loads, 3 packed
+// FMA with explicit (row t, row t+1) ds_read2_b32 pair loads (default).
+enum { CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3 };
+
+template <int n>
+static inline const void* corr_fn(int variant) {
+  if (variant == CORR_PK_ASM) return (const void*)&k_corr_pk<n, false, true>;
+  if (variant == CORR_PK) return (const void*)&k_corr_pk<n, false, false>;
+  return (const void*)&k_corr_kw<n>;
+}
+
+static inline const void* corr_kernel(int variant, int kw, int* threads) {
+  *threads = (variant == CORR_PK || variant == CORR_PK_ASM) ? 192 : 256;
+  if (variant != CORR_GENERIC) switch (kw) {
+#define LM_KW_CASE(n) \
+  case n:             \
+    return corr_fn<n>(variant);
+      LM_KW_LIST(LM_KW_CASE)
+#undef LM_KW_CASE
+      default:
+        break;
+    }
+  *threads = 256;
+  return (const void*)&k_corr;
+}
+
+static inline hipError_t corr_set_lds(int variant, int kw, size_t lds) {
+  int th;
+  return hipFuncSetAttribute(corr_kernel(variant, kw, &th), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
+// Launch the correlation for one detector group (all detectors of one width).
+static inline hipError_t launch_corr(int variant, int kw, dim3 grid, size_t lds, hipStream_t st, const LmConst& K,
+                                     const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes,
+                                     const float* weights, int s0, unsigned long long* keys, int32_t* n_pos,
+                                     uint8_t* tailbin, int64_t tailbin_slot_bytes) {
+  int th;
+  const void* fn = corr_kernel(variant, kw, &th);
+  void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
+                  (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
+  return hipLaunchKernel(fn, grid, dim3(th), args, lds, st);
+}
+
 
 // Debug copy of raw scores: same arithmetic as k_corr, no compaction.
 __global__ __launch_bounds__(256) void k_corr_dbg(const LmConst K, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,

@@ -119,6 +119,8 @@ struct lm_ctx {
   int64_t dbg_off[LM_NDET] = {0};
   int64_t gscratch_slot = 0;
   size_t corr_lds = 0;
+  int corr_variant = 2;
+  std::vector<std::pair<int, LmDetGroup>> corr_groups;  // (detector width, detectors)
   // device buffers
   DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin, tailmask;
   DevBuf<int32_t> cal, npos, err;
@@ -424,10 +426,29 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   for (int d = 0; d < 6; ++d) {
     const LmDet& D = K.det[d];
     int cols = LM_TW + D.kwp - 1;
-    int stride = cols + ((16 - (cols & 31) + 32) & 31);
-    lds = std::max(lds, (size_t)(LM_TH + D.kh - 1) * stride * sizeof(float) + 16);
+    int stride = std::max(cols + ((16 - (cols & 31) + 32) & 31), pk_stride(cols));
+    lds = std::max(lds, (size_t)(LM_TH + D.kh - 1) * stride * sizeof(float) + 16 + (size_t)D.kh * D.kwp * sizeof(float));
   }
   c->corr_lds = lds;
+  c->corr_variant = CORR_PK_ASM;
+  if (const char* v = getenv("LM_CORR_VARIANT")) c->corr_variant = atoi(v);
+  // detectors grouped by width: one width-specialised correlation launch each
+  c->corr_groups.clear();
+  for (int d = 0; d < 6; ++d) {
+    const int kw = K.det[d].kw;
+    auto it = std::find_if(c->corr_groups.begin(), c->corr_groups.end(), [&](const auto& p) { return p.first == kw; });
+    if (it == c->corr_groups.end()) {
+      LmDetGroup G;
+      std::memset(&G, 0, sizeof(G));
+      c->corr_groups.push_back({kw, G});
+      it = c->corr_groups.end() - 1;
+    }
+    LmDetGroup& G = it->second;
+    const int prev = G.n ? G.tile_end[G.n - 1] : 0;
+    G.ids[G.n] = d;
+    G.tile_end[G.n] = prev + K.det[d].tiles_x * K.det[d].tiles_y;
+    ++G.n;
+  }
 
   // weights (float, rows zero-padded to kwp) and TM imadjust LUT
   std::vector<float> wts((size_t)w_off, 0.f);
@@ -487,7 +508,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   cap[AR_PWJC] = ns * LM_NFEAT * (64 + g.ong_nx * g.ong_ny + 1);
   cap[AR_PWNZ] = ns * LM_NFEAT * 1024;
   for (int a = 0; a < 2; ++a) c->arena[a].alloc(cap, ns);
-  HIPCHK(hipFuncSetAttribute((const void*)k_corr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->corr_lds));
+  for (const auto& grp : c->corr_groups) HIPCHK(corr_set_lds(c->corr_variant, grp.first, c->corr_lds));
   HIPCHK(hipFuncSetAttribute((const void*)k_corr_dbg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->corr_lds));
 }
 
@@ -627,8 +648,12 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
         K, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
     T.end();
     T.begin("k_corr");
-    k_corr<<<dim3(K.n_tiles, nproc), 256, c->corr_lds, st>>>(K, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0,
-                                                             c->keys.p, c->npos.p, c->tailbin.p, c->tailbin_slot_bytes);
+    for (const auto& grp : c->corr_groups) {
+      const LmDetGroup& G = grp.second;
+      HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_lds, st, K, G,
+                         c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->keys.p, c->npos.p, c->tailbin.p,
+                         c->tailbin_slot_bytes));
+    }
     T.end();
     if (c->debug & 1) {
       if (!c->dbg.p) {

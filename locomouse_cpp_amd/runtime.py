@@ -23,7 +23,7 @@ EXPORTED = (
     "lm_debug_kernel_times", "lm_synth_frames_device",
 )
 
-HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
                "-fvisibility=hidden", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
 
