@@ -182,37 +182,39 @@ LM_HD inline int lg_(long n) {
 
 // __introsort_loop without recursion: the recursive call on [cut, last) is
 // pushed on an explicit stack and processed before the loop continues on
-// [first, cut) — the same visiting order as the recursive original.
+// [first, cut) — the same visiting order as the recursive original.  The
+// stack (kStackInts ints: first, last, depth, cut per frame; depth <=
+// 2*lg(n)+1 <= 64 frames) is caller-provided so device code can keep it in
+// LDS instead of per-lane scratch.
+enum { kStackFrames = 66, kStackInts = 4 * kStackFrames };
+
 template <class T, class Less>
-LM_HD inline void introsort_loop(T* first, T* last, int depth_limit, Less comp) {
-  struct Frame {
-    T* first;
-    T* last;
-    int depth;
-    int stage;  // 0: fresh; 1: returned from right recursion
-    T* cut;
-  };
-  Frame stack[72];
+LM_HD inline void introsort_loop(T* base, int first, int last, int depth_limit, Less comp, int* stk) {
   int sp = 0;
-  stack[sp++] = Frame{first, last, depth_limit, 0, nullptr};
+  auto push = [&](int f, int l, int d) {
+    stk[4 * sp + 0] = f;
+    stk[4 * sp + 1] = l;
+    stk[4 * sp + 2] = d;
+    stk[4 * sp + 3] = -1;  // cut (set once the frame partitions)
+    ++sp;
+  };
+  push(first, last, depth_limit);
   while (sp > 0) {
-    Frame& fr = stack[sp - 1];
-    if (fr.stage == 1) {
-      fr.last = fr.cut;  // __last = __cut after the recursive call
-      fr.stage = 0;
+    int* fr = stk + 4 * (sp - 1);
+    if (fr[3] >= 0) {  // returned from the recursive call on [cut, last)
+      fr[1] = fr[3];   // __last = __cut
+      fr[3] = -1;
     }
-    if (fr.last - fr.first > kThreshold) {
-      if (fr.depth == 0) {
-        partial_sort_full<T, Less>(fr.first, fr.last, comp);
+    if (fr[1] - fr[0] > kThreshold) {
+      if (fr[2] == 0) {
+        partial_sort_full<T, Less>(base + fr[0], base + fr[1], comp);
         --sp;
         continue;
       }
-      --fr.depth;
-      T* cut = unguarded_partition_pivot<T, Less>(fr.first, fr.last, comp);
-      fr.cut = cut;
-      fr.stage = 1;
-      Frame child{cut, fr.last, fr.depth, 0, nullptr};
-      stack[sp++] = child;
+      --fr[2];
+      T* cut = unguarded_partition_pivot<T, Less>(base + fr[0], base + fr[1], comp);
+      fr[3] = (int)(cut - base);
+      push(fr[3], fr[1], fr[2]);
     } else {
       --sp;
     }
@@ -220,11 +222,17 @@ LM_HD inline void introsort_loop(T* first, T* last, int depth_limit, Less comp) 
 }
 
 template <class T, class Less>
-LM_HD inline void std_sort(T* first, T* last, Less comp) {
+LM_HD inline void std_sort(T* first, T* last, Less comp, int* stk) {
   if (first != last) {
-    introsort_loop<T, Less>(first, last, lg_((long)(last - first)) * 2, comp);
+    introsort_loop<T, Less>(first, 0, (int)(last - first), lg_((long)(last - first)) * 2, comp, stk);
     final_insertion_sort<T, Less>(first, last, comp);
   }
+}
+
+template <class T, class Less>
+inline void std_sort(T* first, T* last, Less comp) {  // host convenience
+  int stk[kStackInts];
+  std_sort<T, Less>(first, last, comp, stk);
 }
 
 }  // namespace lm_sort

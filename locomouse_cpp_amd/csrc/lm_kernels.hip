@@ -875,13 +875,19 @@ __global__ __launch_bounds__(1024) void k_tail(const LmConst K, int s0, const ui
 }
 
 // ------------------------------------------------------------------- k_nms
+// One 512-thread block per (frame, list).  Positive detections are filtered by
+// TAIL_MASK (bottom lists), sorted by (score desc, row-major index asc) with an
+// LDS bitonic network (== std::sort whenever scores are distinct; on an exact
+// tie the list is re-sorted from row-major order with the libstdc++ introsort
+// replica, lm_introsort.h), then clustered: nmsMax for the bottom view,
+// peakClustering for the side view.
 #define LM_NMS_THREADS 512
-#define LM_NMS_CAP 4096  // entries sorted in LDS; larger lists take the global path
+#define LM_NMS_CAP 2048  // entries kept in LDS; larger lists use the global-memory path
 
 DEV float key_score(unsigned long long k) { return __uint_as_float(~(unsigned)(k >> 32)); }
-DEV unsigned key_idx(unsigned long long k) { return (unsigned)(k & 0xFFFFFFFFu); }
+DEV unsigned key_lo(unsigned long long k) { return (unsigned)(k & 0xFFFFFFFFu); }
 
-// in-place ascending bitonic sort of a[0..np), np power of two, block-wide
+// in-place ascending bitonic sort of a[0..np), np a power of two, block-wide
 DEV void bitonic_sort(unsigned long long* a, int np) {
   for (int k = 2; k <= np; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
@@ -907,14 +913,50 @@ struct ReplicaLess {  // compareCandidate on (idx << 32 | score bits) words
   }
 };
 
-// Rect overlap test of nmsMax / peakClustering (:1698-1709, :1833-1844):
-// inter / (2wh - inter) > 0.5  <=>  3*inter > 2wh  (exact for these integers)
-DEV bool overlaps(int xa, int ya, int xb, int yb, int bw, int bh) {
-  const int dx = abs(xa - xb), dy = abs(ya - yb);
-  if (dx >= bw || dy >= bh) return false;
-  const int inter = (bw - dx) * (bh - dy);
-  const double a = (double)inter;
-  return a / (2.0 * (bw * bh) - a) > 0.5;
+// Rect overlap test of nmsMax / peakClustering (:1698-1709, :1833-1844) on
+// packed x | y << 16: inter / (2wh - inter) > 0.5  <=>  3*inter > 2wh.  The two
+// are equal for these integers: the margin of the double quotient over 0.5 is
+// >= 1/(4wh), far above its rounding error.
+DEV bool overlaps_xy(unsigned a, unsigned b, int bw, int bh) {
+  const int dx = abs((int)(a & 0xFFFFu) - (int)(b & 0xFFFFu));
+  const int dy = abs((int)(a >> 16) - (int)(b >> 16));
+  if (dx >= bw || dy >= bh) return false;  // R.area() == 0
+  return 3 * (bw - dx) * (bh - dy) > 2 * bw * bh;
+}
+
+// exclusive prefix count of flags f(j), j in [0, n): returns per-thread chunk
+// start offsets via out[j] for flagged j; returns the total
+template <class F>
+DEV int block_rank(int n, F flag, int* out, int* s_wsum) {
+  const int T = blockDim.x, chunk = (n + T - 1) / T;
+  const int j0 = threadIdx.x * chunk, j1 = min(n, j0 + chunk);
+  int c = 0;
+  for (int j = j0; j < j1; ++j) c += flag(j);
+  // inclusive wave scan
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int v = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) s_wsum[wid] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int w = 0; w < (T >> 6); ++w) {
+      const int t = s_wsum[w];
+      s_wsum[w] = acc;
+      acc += t;
+    }
+    s_wsum[T >> 6] = acc;
+  }
+  __syncthreads();
+  int r = s_wsum[wid] + v - c;
+  for (int j = j0; j < j1; ++j)
+    if (flag(j)) out[j] = r++;
+  const int total = s_wsum[T >> 6];
+  __syncthreads();
+  return total;
 }
 
 __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0, int side, unsigned long long* __restrict__ keys,
@@ -923,14 +965,16 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
                                                        LmSlotOut* __restrict__ hdr, LmCand* __restrict__ arena_cand,
                                                        LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err) {
   const int slot = s0 + blockIdx.x;
-  const int feat = blockIdx.y;                 // 0 paw, 1 snout
+  const int feat = blockIdx.y;  // 0 paw, 1 snout
   const int list = side ? 2 + feat : feat;
   const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
   const LmDet D = K.det[det];
   LmSlotOut* H = hdr + slot;
   __shared__ unsigned long long s_keys[LM_NMS_CAP];
-  __shared__ int s_assign[LM_NMS_CAP];
-  __shared__ int s_n, s_flag, s_ncand, s_base;
+  __shared__ int s_assign[LM_NMS_CAP], s_rank[LM_NMS_CAP];
+  __shared__ int s_stk[lm_sort::kStackInts];
+  __shared__ int s_wsum[LM_NMS_THREADS / 64 + 1];
+  __shared__ int s_n, s_flag, s_base, s_lead;
 
   if (side && H->cand_cnt[feat] == 0) {  // detectSideCandidates skips (:820-833)
     if (threadIdx.x == 0) {
@@ -945,24 +989,25 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
   const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
   unsigned long long* a = s_keys;
   int* assign = s_assign;
-  const bool global_path = n_in > LM_NMS_CAP;
-  if (global_path) {
+  int* rank = s_rank;
+  if (n_in > LM_NMS_CAP) {  // rare: whole crop positive; same algorithm in global scratch
     a = gscratch + (int64_t)(blockIdx.y + 2 * blockIdx.x) * gscratch_slot;
     assign = reinterpret_cast<int*>(a + gscratch_slot / 2);
+    rank = assign + gscratch_slot / 2;
   }
   if (threadIdx.x == 0) {
     s_n = 0;
     s_flag = 0;
   }
   __syncthreads();
-  // load + TAIL_MASK filter (bottom lists: mask(BB_BOTTOM_TAIL).setTo(255, TAIL_MASK), :783)
+  // load + TAIL_MASK filter (bottom: mask(BB_BOTTOM_TAIL).setTo(255, TAIL_MASK), :783)
   const uint8_t* __restrict__ tm = tailmask + (int64_t)slot * K.tail_hb * K.tail_w;
   for (int k = threadIdx.x; k < n_in; k += blockDim.x) {
     const unsigned long long v = src[k];
     bool keep = true;
     if (!side) {
-      const unsigned idx = key_idx(v);
-      const int y = idx / D.ow, x = idx % D.ow;
+      const unsigned idx = key_lo(v);
+      const int y = idx / D.ow, x = idx - y * D.ow;
       if (x < K.tail_w && y < K.tail_hb && tm[y * K.tail_w + x]) keep = false;
     }
     if (keep) a[atomicAdd(&s_n, 1)] = v;
@@ -974,20 +1019,19 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
   for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
   __syncthreads();
   if (np > 1) bitonic_sort(a, np);
-  // exact score ties -> libstdc++ order
   for (int k = threadIdx.x; k + 1 < n; k += blockDim.x)
     if ((a[k] >> 32) == (a[k + 1] >> 32)) s_flag = 1;
   __syncthreads();
   const int tie = s_flag;
   if (tie) {
-    // row-major order (the order nmsMax pushes detections, :1638-1648)
+    // exact score tie: std::sort from the row-major order nmsMax builds (:1638-1648)
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
       const unsigned long long v = a[k];
-      a[k] = ((unsigned long long)key_idx(v) << 32) | (unsigned)(~(unsigned)(v >> 32));
+      a[k] = ((unsigned long long)key_lo(v) << 32) | (unsigned)(~(unsigned)(v >> 32));
     }
     __syncthreads();
     if (np > 1) bitonic_sort(a, np);
-    if (threadIdx.x == 0) lm_sort::std_sort(a, a + n, ReplicaLess());
+    if (threadIdx.x == 0) lm_sort::std_sort(a, a + n, ReplicaLess(), s_stk);
     __syncthreads();
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
       const unsigned long long v = a[k];
@@ -995,23 +1039,28 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
     }
     __syncthreads();
   }
-  const int bw = D.box_w, bh = D.box_h, ow = D.ow;
-  int ncand = 0;
+  // row-major index -> packed (x | y << 16), once per detection
+  const int ow = D.ow, bw = D.box_w, bh = D.box_h;
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const unsigned long long v = a[k];
+    const unsigned idx = key_lo(v);
+    const unsigned y = idx / ow, x = idx - y * ow;
+    a[k] = (v & 0xFFFFFFFF00000000ull) | (x | (y << 16));
+  }
+  __syncthreads();
   if (!side) {
-    // nmsMax: assign[j] = first i < j overlapping j (suppressed points keep
-    // suppressing, :1677-1720); maxima resolved by pointer jumping.
+    // nmsMax: every point, suppressed or not, suppresses the later points it
+    // overlaps (:1677-1720) => j belongs to the first i < j overlapping it;
+    // maxima by pointer jumping.
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      const unsigned ij = key_idx(a[j]);
-      const int xj = ij % ow, yj = ij / ow;
-      int as = -1;
-      for (int i = 0; i < j; ++i) {
-        const unsigned ii = key_idx(a[i]);
-        if (overlaps(ii % ow, ii / ow, xj, yj, bw, bh)) {
+      const unsigned xj = key_lo(a[j]);
+      int as = j;
+      for (int i = 0; i < j; ++i)
+        if (overlaps_xy(key_lo(a[i]), xj, bw, bh)) {
           as = i;
           break;
         }
-      }
-      assign[j] = as < 0 ? j : as;
+      assign[j] = as;
     }
     __syncthreads();
     while (true) {
@@ -1025,26 +1074,24 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
         }
       }
       __syncthreads();
-      if (!s_flag) break;
+      const int again = s_flag;
       __syncthreads();
+      if (!again) break;
     }
   } else {
     // peakClustering: leaders in sorted order; each suppresses the undecided
-    // points overlapping it (:1815-1850).  assign[j] = leader id (-1 undecided)
+    // points overlapping it (:1815-1850).  assign[j] = leader (-1 undecided).
     for (int j = threadIdx.x; j < n; j += blockDim.x) assign[j] = -1;
     __syncthreads();
-    __shared__ int s_lead;
     int lead = 0;
     while (lead < n) {
-      if (threadIdx.x == 0) assign[lead] = lead;
-      const unsigned il = key_idx(a[lead]);
-      const int xl = il % ow, yl = il / ow;
-      for (int j = lead + 1 + threadIdx.x; j < n; j += blockDim.x) {
-        if (assign[j] >= 0) continue;
-        const unsigned ij = key_idx(a[j]);
-        if (overlaps(xl, yl, ij % ow, ij / ow, bw, bh)) assign[j] = lead;
+      const unsigned xl = key_lo(a[lead]);
+      if (threadIdx.x == 0) {
+        assign[lead] = lead;
+        s_lead = n;
       }
-      if (threadIdx.x == 0) s_lead = n;
+      for (int j = lead + 1 + threadIdx.x; j < n; j += blockDim.x)
+        if (assign[j] < 0 && overlaps_xy(xl, key_lo(a[j]), bw, bh)) assign[j] = lead;
       __syncthreads();
       for (int j = lead + 1 + threadIdx.x; j < n; j += blockDim.x)
         if (assign[j] < 0) atomicMin(&s_lead, j);
@@ -1053,41 +1100,36 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
       __syncthreads();
     }
   }
-  // maxima / leaders in sorted order -> output slots
+  // maxima (leaders) in sorted order -> output ranks
+  const int ncand = block_rank(n, [&](int j) { return assign[j] == j; }, rank, s_wsum);
   if (threadIdx.x == 0) {
-    int c = 0;
-    for (int j = 0; j < n; ++j)
-      if (assign[j] == j) ++c;
-    s_ncand = c;
-    int base = atomicAdd(&ctl->used[AR_CAND], c);
-    if (base + c > ctl->cap[AR_CAND]) {
+    int base = atomicAdd(&ctl->used[AR_CAND], ncand);
+    if (base + ncand > ctl->cap[AR_CAND]) {
       atomicOr(&ctl->overflow, 1);
       base = -1;
     }
     s_base = base;
   }
   __syncthreads();
-  ncand = s_ncand;
   const int base = s_base;
   if (base >= 0) {
-    // rank of each maximum among maxima (prefix count), then the weighted
-    // mean over its members in sorted order (double, :1731-1744 / :1865-1883)
+    // weighted mean over each cluster's members in sorted order, double
+    // (:1731-1744 / :1865-1883)
     for (int m = threadIdx.x; m < n; m += blockDim.x) {
       if (assign[m] != m) continue;
-      int rank = 0;
-      for (int j = 0; j < m; ++j) rank += assign[j] == j;
       double wx = 0, wy = 0, ss = 0;
       int members = 0;
       for (int j = m; j < n; ++j) {
         if (assign[j] != m) continue;
-        const unsigned ij = key_idx(a[j]);
-        const double s = (double)key_score(a[j]);
-        wx += (double)(int)(ij % ow) * s;
-        wy += (double)(int)(ij / ow) * s;
+        const unsigned long long v = a[j];
+        const unsigned xy = key_lo(v);
+        const double s = (double)key_score(v);
+        wx += (double)(int)(xy & 0xFFFFu) * s;
+        wy += (double)(int)(xy >> 16) * s;
         ss += s;
         ++members;
       }
-      const unsigned im = key_idx(a[m]);
+      const unsigned xm = key_lo(a[m]);
       LmCand c;
       c.s = (double)key_score(a[m]);
       if (!side) {  // Point_<double> / double -> Point_<int>: cvRound (half even)
@@ -1097,10 +1139,10 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
         c.x = (int)round(wx / ss);
         c.y = (int)round(wy / ss);
       } else {
-        c.x = (int)(im % ow);
-        c.y = (int)(im / ow);
+        c.x = (int)(xm & 0xFFFFu);
+        c.y = (int)(xm >> 16);
       }
-      arena_cand[base + rank] = c;
+      arena_cand[base + rank[m]] = c;
     }
   }
   if (threadIdx.x == 0) {

@@ -1114,6 +1114,13 @@ LMO_API int lmo_debug_scores(const lmo_result* r, int32_t f, int32_t det, float*
   return LM_OK;
 }
 
+LMO_API int lmo_debug_scores_dims(const lmo_result* r, int32_t f, int32_t det, int32_t* rows, int32_t* cols) {
+  if (!r || !rows || !cols || f < 0 || f >= (int)r->r.scores.size() || det < 0 || det >= 6) return LM_ERR_INVALID_ARGUMENT;
+  *rows = r->r.scores[f][det].rows;
+  *cols = r->r.scores[f][det].cols;
+  return LM_OK;
+}
+
 LMO_API int lmo_debug_tail_mask(const lmo_result* r, int32_t f, uint8_t* out, int32_t rows, int32_t cols) {
   if (!r || f < 0 || f >= (int)r->r.tail_mask.size()) return LM_ERR_INVALID_ARGUMENT;
   const lmo::Mat8& m = r->r.tail_mask[f];

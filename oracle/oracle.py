@@ -37,6 +37,7 @@ def lib():
         L.lmo_free.argtypes = [C.c_void_p]
         L.lmo_geometry.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(lm_geometry)]
         L.lmo_debug_scores.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
+        L.lmo_debug_scores_dims.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.lmo_debug_tail_mask.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
         L.lmo_debug_ipad.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
         L.lmo_std_sort_perm.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
@@ -79,7 +80,12 @@ class OracleRun:
             raise OracleError(rc, lib().lmo_last_error().decode())
         self.result = result_to_numpy(view)
 
-    def scores(self, f, det, shape):
+    def scores(self, f, det, shape=None):
+        if shape is None:
+            r, c = C.c_int32(), C.c_int32()
+            if lib().lmo_debug_scores_dims(self._h, f, det, C.byref(r), C.byref(c)) or r.value == 0:
+                return None
+            shape = (r.value, c.value)
         out = np.zeros(shape, dtype=np.float32)
         rc = lib().lmo_debug_scores(self._h, f, det, out.ctypes.data, shape[0], shape[1])
         if rc:

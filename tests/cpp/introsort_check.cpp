@@ -57,7 +57,8 @@ int main() {
       std::vector<Cand> b = a;
       std::__introsort_loop(a.begin(), a.end(), (long)depth, __gnu_cxx::__ops::__iter_comp_iter(cmp));
       std::__final_insertion_sort(a.begin(), a.end(), __gnu_cxx::__ops::__iter_comp_iter(cmp));
-      lm_sort::introsort_loop(b.data(), b.data() + n, depth, cmp);
+      int stk[lm_sort::kStackInts];
+      lm_sort::introsort_loop(b.data(), 0, n, depth, cmp, stk);
       lm_sort::final_insertion_sort(b.data(), b.data() + n, cmp);
       ++cases;
       for (int i = 0; i < n; ++i)

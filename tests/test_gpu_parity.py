@@ -158,3 +158,39 @@ def test_error_mapping(cfg):
     with pytest.raises(LMError) as e:
         ctx.detect(cfg.frames(3, 2), 3)  # frame 2 never seen and no halo
     assert e.value.code == 1
+
+
+def _quantized_config(rank):
+    """Detector weights on a 2^-12 grid, so the fp32 correlation is exact and
+    equal-sum windows tie exactly; biases put ~`rank` pixels above zero."""
+    from oracle import oracle as O
+    base = S.SyntheticConfig()
+    W = {}
+    for name in ("paw_bottom", "snout_bottom", "paw_side", "snout_side"):
+        w = base.weights[name]
+        W[name] = np.round(w * w.size * 4) / 4 / 1024
+    c0 = S.SyntheticConfig(weights=W, biases={n: 0.0 for n in W})
+    r0 = O.OracleRun(c0, c0.frames(0, 1), flags=O.KEEP_DEBUG)
+    biases, dups = {}, 0
+    for det, name in ((0, "paw_bottom"), (1, "snout_bottom"), (3, "paw_side"), (4, "snout_side")):
+        v = np.sort(r0.scores(0, det).ravel())[::-1]
+        biases[name] = float(v[rank])
+        pos = v[v > v[rank]]
+        dups += len(pos) - len(np.unique(pos))
+    return S.SyntheticConfig(weights=W, biases=biases), dups
+
+
+def test_nms_exact_score_ties():
+    """Exact ties take the std::sort replica path (lm_introsort.h)."""
+    c, dups = _quantized_config(400)
+    assert dups > 20  # the case really has ties
+    frames = c.frames(0, 6)
+    assert_same(_ctx(c).detect(frames, 0), _oracle(c, frames).result, "ties: ")
+
+
+def test_nms_large_lists_global_path():
+    """> LM_NMS_CAP positives per list: NMS runs from global scratch."""
+    c, dups = _quantized_config(5000)
+    assert dups > 1000
+    frames = c.frames(0, 4)
+    assert_same(_ctx(c).detect(frames, 0), _oracle(c, frames).result, "large: ")
