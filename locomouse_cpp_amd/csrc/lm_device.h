@@ -119,4 +119,57 @@ struct LmP22D {  // == lm_p22d
   int32_t side_cnt;
 };
 
+// Candidate staging: k_nms writes the candidates of (slot, list) over that
+// list's key area (list_cap[l] u64 = room for list_cap[l]/2 candidates),
+// after it has read the keys.  k_post reads them there; k_pack packs them.
+#define LM_CAND_STAGE(K, keys, slot, list) \
+  ((LmCand*)((keys) + (int64_t)(slot) * (K).keys_per_slot + (K).list_off[list]))
+
+// Packed per-batch results, laid out exactly as lm_batch_result's arrays
+// (frame order), so the host does one D2H and hands out pointers.
+enum { PK_CAND = 0, PK_P22D, PK_SIDE, PK_UNARY, PK_JC, PK_NZ, PK_COUNT };
+struct LmPackHdr {
+  int64_t tot[PK_COUNT];
+  int64_t bytes;        // packed size for this batch
+  int32_t overflow;     // bit0: pack buffer too small, bit1: staging arena overflow
+  int32_t err;          // copy of the kernels' error bits
+  int32_t used[AR_COUNT];
+  int32_t pad_[2];
+};
+
+struct LmPackLayout {  // byte offsets inside the packed buffer
+  int64_t cand_off, p22d_off, unary_off, jc_off, nz_off, pw_dims, tail;
+  int64_t cand, p22d, side_y, side_s, unary, jc, ir, pr, bytes;
+};
+
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline LmPackLayout lm_pack_layout(int n, const int64_t* tot) {
+  LmPackLayout L;
+  int64_t o = 0;
+  auto take = [&o](int64_t bytes) {
+    const int64_t r = o;
+    o += (bytes + 15) / 16 * 16;
+    return r;
+  };
+  L.cand_off = take(8 * (4 * (int64_t)n + 1));
+  L.p22d_off = take(8 * (2 * (int64_t)n + 1));
+  L.unary_off = take(8 * (2 * (int64_t)n + 1));
+  L.jc_off = take(8 * (2 * (int64_t)n + 1));
+  L.nz_off = take(8 * (2 * (int64_t)n + 1));
+  L.pw_dims = take(4 * 6 * (int64_t)n);
+  L.tail = take(4 * 45 * (int64_t)n);
+  L.cand = take(16 * tot[PK_CAND]);
+  L.p22d = take(24 * tot[PK_P22D]);
+  L.side_y = take(4 * tot[PK_SIDE]);
+  L.side_s = take(8 * tot[PK_SIDE]);
+  L.unary = take(8 * tot[PK_UNARY]);
+  L.jc = take(4 * tot[PK_JC]);
+  L.ir = take(4 * tot[PK_NZ]);
+  L.pr = take(8 * tot[PK_NZ]);
+  L.bytes = o;
+  return L;
+}
+
 #endif  // LM_DEVICE_H

@@ -876,13 +876,14 @@ __global__ __launch_bounds__(1024) void k_tail(const LmConst K, int s0, const ui
 
 // ------------------------------------------------------------------- k_nms
 // One 512-thread block per (frame, list).  Positive detections are filtered by
-// TAIL_MASK (bottom lists), sorted by (score desc, row-major index asc) with an
-// LDS bitonic network (== std::sort whenever scores are distinct; on an exact
-// tie the list is re-sorted from row-major order with the libstdc++ introsort
-// replica, lm_introsort.h), then clustered: nmsMax for the bottom view,
+// TAIL_MASK (bottom lists), sorted by (score desc, row-major index asc) —
+// equal to std::sort whenever scores are distinct; on an exact tie the list is
+// re-sorted from row-major order with the libstdc++ introsort replica
+// (lm_introsort.h) — then clustered: nmsMax for the bottom view,
 // peakClustering for the side view.
 #define LM_NMS_THREADS 512
-#define LM_NMS_CAP 2048  // entries kept in LDS; larger lists use the global-memory path
+#define LM_NMS_CAP 2048     // entries kept in LDS; larger lists use the global-memory path
+#define LM_NMS_RANKSORT 1024  // up to this many entries: O(n^2/T) rank sort instead of bitonic
 
 DEV float key_score(unsigned long long k) { return __uint_as_float(~(unsigned)(k >> 32)); }
 DEV unsigned key_lo(unsigned long long k) { return (unsigned)(k & 0xFFFFFFFFu); }
@@ -907,6 +908,30 @@ DEV void bitonic_sort(unsigned long long* a, int np) {
   }
 }
 
+// ascending sort of n DISTINCT keys by rank counting: every key's position is
+// the number of smaller keys.  All lanes of a wave read the same a[i]
+// (LDS broadcast), no barrier inside.  tmp holds n keys.
+DEV void rank_sort(unsigned long long* a, unsigned long long* tmp, int n) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
+    const unsigned long long key = a[k];
+    int r = 0;
+    int i = 0;
+    for (; i + 8 <= n; i += 8) {  // 4 x 16 B loads in flight per iteration
+      const ulonglong2 q0 = *reinterpret_cast<const ulonglong2*>(a + i);
+      const ulonglong2 q1 = *reinterpret_cast<const ulonglong2*>(a + i + 2);
+      const ulonglong2 q2 = *reinterpret_cast<const ulonglong2*>(a + i + 4);
+      const ulonglong2 q3 = *reinterpret_cast<const ulonglong2*>(a + i + 6);
+      r += (q0.x < key) + (q0.y < key) + (q1.x < key) + (q1.y < key) + (q2.x < key) + (q2.y < key) +
+           (q3.x < key) + (q3.y < key);
+    }
+    for (; i < n; ++i) r += a[i] < key;
+    tmp[r] = key;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < n; k += blockDim.x) a[k] = tmp[k];
+  __syncthreads();
+}
+
 struct ReplicaLess {  // compareCandidate on (idx << 32 | score bits) words
   DEV bool operator()(unsigned long long a, unsigned long long b) const {
     return __uint_as_float((unsigned)(a & 0xFFFFFFFFu)) > __uint_as_float((unsigned)(b & 0xFFFFFFFFu));
@@ -924,17 +949,16 @@ DEV bool overlaps_xy(unsigned a, unsigned b, int bw, int bh) {
   return 3 * (bw - dx) * (bh - dy) > 2 * bw * bh;
 }
 
-// exclusive prefix count of flags f(j), j in [0, n): returns per-thread chunk
-// start offsets via out[j] for flagged j; returns the total
+// Enumerates the j in [0, n) with flag(j) in increasing order: out[r] = j.
+// Returns their count.
 template <class F>
-DEV int block_rank(int n, F flag, int* out, int* s_wsum) {
+DEV int block_compact(int n, F flag, int* out, int* s_wsum) {
   const int T = blockDim.x, chunk = (n + T - 1) / T;
   const int j0 = threadIdx.x * chunk, j1 = min(n, j0 + chunk);
   int c = 0;
   for (int j = j0; j < j1; ++j) c += flag(j);
-  // inclusive wave scan
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int v = c;
+  int v = c;  // inclusive wave scan
   for (int o = 1; o < 64; o <<= 1) {
     const int u = __shfl_up(v, o);
     if (lane >= o) v += u;
@@ -953,33 +977,43 @@ DEV int block_rank(int n, F flag, int* out, int* s_wsum) {
   __syncthreads();
   int r = s_wsum[wid] + v - c;
   for (int j = j0; j < j1; ++j)
-    if (flag(j)) out[j] = r++;
+    if (flag(j)) out[r++] = j;
   const int total = s_wsum[T >> 6];
   __syncthreads();
   return total;
 }
 
+DEV double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
 __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0, int side, unsigned long long* __restrict__ keys,
                                                        const int32_t* __restrict__ n_pos, const uint8_t* __restrict__ tailmask,
                                                        unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
-                                                       LmSlotOut* __restrict__ hdr, LmCand* __restrict__ arena_cand,
-                                                       LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err) {
+                                                       LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
+                                                       long long* __restrict__ prof) {
   const int slot = s0 + blockIdx.x;
   const int feat = blockIdx.y;  // 0 paw, 1 snout
+  // optional phase timestamps (LM_KPROF=1): clock64() of thread 0 per phase
+#define NMS_PROF(k) \
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = clock64();
+  NMS_PROF(0)
   const int list = side ? 2 + feat : feat;
   const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
   const LmDet D = K.det[det];
   LmSlotOut* H = hdr + slot;
   __shared__ unsigned long long s_keys[LM_NMS_CAP];
-  __shared__ int s_assign[LM_NMS_CAP], s_rank[LM_NMS_CAP];
+  __shared__ int s_assign[LM_NMS_CAP], s_mlist[LM_NMS_CAP];
+  __shared__ unsigned s_xy[LM_NMS_CAP + 16];
   __shared__ int s_stk[lm_sort::kStackInts];
   __shared__ int s_wsum[LM_NMS_THREADS / 64 + 1];
-  __shared__ int s_n, s_flag, s_base, s_lead;
+  __shared__ int s_n, s_flag, s_base;
 
   if (side && H->cand_cnt[feat] == 0) {  // detectSideCandidates skips (:820-833)
     if (threadIdx.x == 0) {
       H->n_pos[list] = 0;
-      H->cand_off[list] = 0;
       H->cand_cnt[list] = 0;
       H->ties[list] = 0;
     }
@@ -989,11 +1023,15 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
   const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
   unsigned long long* a = s_keys;
   int* assign = s_assign;
-  int* rank = s_rank;
-  if (n_in > LM_NMS_CAP) {  // rare: whole crop positive; same algorithm in global scratch
+  int* mlist = s_mlist;
+  unsigned* xy = s_xy;
+  const bool glob = n_in > LM_NMS_CAP;
+  if (glob) {  // rare: most of the crop positive; same algorithm in global scratch
+    const int64_t npg = gscratch_slot / 3;
     a = gscratch + (int64_t)(blockIdx.y + 2 * blockIdx.x) * gscratch_slot;
-    assign = reinterpret_cast<int*>(a + gscratch_slot / 2);
-    rank = assign + gscratch_slot / 2;
+    assign = reinterpret_cast<int*>(a + npg);
+    mlist = assign + npg;
+    xy = reinterpret_cast<unsigned*>(mlist + npg);
   }
   if (threadIdx.x == 0) {
     s_n = 0;
@@ -1013,12 +1051,18 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
     if (keep) a[atomicAdd(&s_n, 1)] = v;
   }
   __syncthreads();
+  NMS_PROF(1)
   const int n = s_n;
   int np = 1;
   while (np < n) np <<= 1;
-  for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
-  __syncthreads();
-  if (np > 1) bitonic_sort(a, np);
+  if (n <= LM_NMS_RANKSORT) {
+    rank_sort(a, reinterpret_cast<unsigned long long*>(s_assign), n);  // s_assign+s_mlist: 16 KB scratch
+  } else {
+    for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
+    __syncthreads();
+    bitonic_sort(a, np);
+  }
+  NMS_PROF(2)
   for (int k = threadIdx.x; k + 1 < n; k += blockDim.x)
     if ((a[k] >> 32) == (a[k + 1] >> 32)) s_flag = 1;
   __syncthreads();
@@ -1029,6 +1073,7 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
       const unsigned long long v = a[k];
       a[k] = ((unsigned long long)key_lo(v) << 32) | (unsigned)(~(unsigned)(v >> 32));
     }
+    for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
     __syncthreads();
     if (np > 1) bitonic_sort(a, np);
     if (threadIdx.x == 0) lm_sort::std_sort(a, a + n, ReplicaLess(), s_stk);
@@ -1042,27 +1087,35 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
   // row-major index -> packed (x | y << 16), once per detection
   const int ow = D.ow, bw = D.box_w, bh = D.box_h;
   for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    const unsigned long long v = a[k];
-    const unsigned idx = key_lo(v);
+    const unsigned idx = key_lo(a[k]);
     const unsigned y = idx / ow, x = idx - y * ow;
-    a[k] = (v & 0xFFFFFFFF00000000ull) | (x | (y << 16));
+    xy[k] = x | (y << 16);
   }
+  for (int k = n + threadIdx.x; k < ((n + 15) & ~15); k += blockDim.x) xy[k] = 0;
   __syncthreads();
+  NMS_PROF(3)
   if (!side) {
     // nmsMax: every point, suppressed or not, suppresses the later points it
     // overlaps (:1677-1720) => j belongs to the first i < j overlapping it;
     // maxima by pointer jumping.
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      const unsigned xj = key_lo(a[j]);
+      const unsigned xj = xy[j];
       int as = j;
-      for (int i = 0; i < j; ++i)
-        if (overlaps_xy(key_lo(a[i]), xj, bw, bh)) {
-          as = i;
-          break;
-        }
+      for (int i0 = 0; i0 < j && as == j; i0 += 16) {  // 4 x 16 B loads in flight
+        unsigned v[16];
+        *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(xy + i0);
+        *reinterpret_cast<uint4*>(v + 4) = *reinterpret_cast<const uint4*>(xy + i0 + 4);
+        *reinterpret_cast<uint4*>(v + 8) = *reinterpret_cast<const uint4*>(xy + i0 + 8);
+        *reinterpret_cast<uint4*>(v + 12) = *reinterpret_cast<const uint4*>(xy + i0 + 12);
+        unsigned hit = 0;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) hit |= (unsigned)(i0 + t < j && overlaps_xy(v[t], xj, bw, bh)) << t;
+        if (hit) as = i0 + __ffs(hit) - 1;
+      }
       assign[j] = as;
     }
     __syncthreads();
+    NMS_PROF(4)
     while (true) {
       if (threadIdx.x == 0) s_flag = 0;
       __syncthreads();
@@ -1078,58 +1131,70 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
       __syncthreads();
       if (!again) break;
     }
-  } else {
-    // peakClustering: leaders in sorted order; each suppresses the undecided
-    // points overlapping it (:1815-1850).  assign[j] = leader (-1 undecided).
-    for (int j = threadIdx.x; j < n; j += blockDim.x) assign[j] = -1;
-    __syncthreads();
+  } else if (threadIdx.x < 64) {
+    // peakClustering: leaders in sorted order; each claims the undecided
+    // points overlapping it (:1815-1850).  One wave, no block barriers:
+    // assign[j] = leader, -1 undecided.
+    const int lane = threadIdx.x;
+    for (int j = lane; j < n; j += 64) assign[j] = -1;
     int lead = 0;
     while (lead < n) {
-      const unsigned xl = key_lo(a[lead]);
-      if (threadIdx.x == 0) {
-        assign[lead] = lead;
-        s_lead = n;
+      const unsigned xl = xy[lead];
+      if (lane == 0) assign[lead] = lead;
+      int next = n;
+      for (int b = lead + 1; b < n; b += 64) {
+        const int j = b + lane;
+        bool und = false;
+        if (j < n && assign[j] < 0) {
+          if (overlaps_xy(xl, xy[j], bw, bh)) assign[j] = lead;
+          else und = true;
+        }
+        const unsigned long long m = __ballot(und);
+        if (m && next == n) next = b + __ffsll((long long)m) - 1;
       }
-      for (int j = lead + 1 + threadIdx.x; j < n; j += blockDim.x)
-        if (assign[j] < 0 && overlaps_xy(xl, key_lo(a[j]), bw, bh)) assign[j] = lead;
-      __syncthreads();
-      for (int j = lead + 1 + threadIdx.x; j < n; j += blockDim.x)
-        if (assign[j] < 0) atomicMin(&s_lead, j);
-      __syncthreads();
-      lead = s_lead;
-      __syncthreads();
+      lead = next;
     }
-  }
-  // maxima (leaders) in sorted order -> output ranks
-  const int ncand = block_rank(n, [&](int j) { return assign[j] == j; }, rank, s_wsum);
-  if (threadIdx.x == 0) {
-    int base = atomicAdd(&ctl->used[AR_CAND], ncand);
-    if (base + ncand > ctl->cap[AR_CAND]) {
-      atomicOr(&ctl->overflow, 1);
-      base = -1;
-    }
-    s_base = base;
   }
   __syncthreads();
-  const int base = s_base;
-  if (base >= 0) {
-    // weighted mean over each cluster's members in sorted order, double
-    // (:1731-1744 / :1865-1883)
-    for (int m = threadIdx.x; m < n; m += blockDim.x) {
-      if (assign[m] != m) continue;
-      double wx = 0, wy = 0, ss = 0;
-      int members = 0;
-      for (int j = m; j < n; ++j) {
-        if (assign[j] != m) continue;
-        const unsigned long long v = a[j];
-        const unsigned xy = key_lo(v);
-        const double s = (double)key_score(v);
-        wx += (double)(int)(xy & 0xFFFFu) * s;
-        wy += (double)(int)(xy >> 16) * s;
-        ss += s;
-        ++members;
+  NMS_PROF(5)
+  // maxima (leaders) in sorted order
+  const int ncand = block_compact(n, [&](int j) { return assign[j] == j; }, mlist, s_wsum);
+  LmCand* __restrict__ out = LM_CAND_STAGE(K, keys, slot, list);
+  const bool fits = ncand <= K.list_cap[list] / 2;  // always: maxima are >= w/3 apart
+  if (!fits && threadIdx.x == 0) atomicOr(err, 32);
+  NMS_PROF(6)
+  // weighted mean over each cluster's members in sorted order, in double
+  // (:1731-1744 / :1865-1883).  One wave per cluster: members are found 64 at
+  // a time with a ballot; the products x*s, y*s are exact in double, so they
+  // are formed per lane and only the additions run in member order.
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int r = wid; r < ncand && fits; r += nw) {
+    const int m = mlist[r];
+    double wx = 0, wy = 0, ss = 0;
+    int members = 0;
+    for (int b = m; b < n; b += 64) {
+      const int j = b + lane;
+      bool mem = false;
+      double px = 0, py = 0, ps = 0;
+      if (j < n && assign[j] == m) {
+        mem = true;
+        const unsigned q = xy[j];
+        ps = (double)key_score(a[j]);
+        px = (double)(int)(q & 0xFFFFu) * ps;
+        py = (double)(int)(q >> 16) * ps;
       }
-      const unsigned xm = key_lo(a[m]);
+      unsigned long long mask = __ballot(mem);
+      members += __popcll(mask);
+      while (mask) {
+        const int sl = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        wx += readlane_f64(px, sl);
+        wy += readlane_f64(py, sl);
+        ss += readlane_f64(ps, sl);
+      }
+    }
+    if (lane == 0) {
+      const unsigned xm = xy[m];
       LmCand c;
       c.s = (double)key_score(a[m]);
       if (!side) {  // Point_<double> / double -> Point_<int>: cvRound (half even)
@@ -1142,15 +1207,16 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
         c.x = (int)(xm & 0xFFFFu);
         c.y = (int)(xm >> 16);
       }
-      arena_cand[base + rank[m]] = c;
+      out[r] = c;
     }
   }
+  NMS_PROF(7)
   if (threadIdx.x == 0) {
     H->n_pos[list] = n;
-    H->cand_off[list] = base;
-    H->cand_cnt[list] = ncand;
+    H->cand_cnt[list] = fits ? ncand : 0;
     H->ties[list] = tie;
   }
+#undef NMS_PROF
 }
 
 // ------------------------------------------------------------------ k_post
@@ -1182,7 +1248,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const
                                                          const uint8_t* const* __restrict__ frame_ptr,
                                                          const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
                                                          const uint8_t* __restrict__ luts, LmSlotOut* __restrict__ hdr,
-                                                         LmCand* __restrict__ arena_cand, LmP22D* __restrict__ arena_p22d,
+                                                         const unsigned long long* __restrict__ keys, LmP22D* __restrict__ arena_p22d,
                                                          int32_t* __restrict__ arena_side_y, double* __restrict__ arena_side_s,
                                                          double* __restrict__ arena_unary, int32_t* __restrict__ arena_jc,
                                                          int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
@@ -1203,9 +1269,9 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const
     if (threadIdx.x == 0) atomicOr(err, 8);
     return;
   }
-  const LmCand* cb = arena_cand + H->cand_off[feat];
-  const LmCand* ct = arena_cand + H->cand_off[2 + feat];
-  const LmCand* cp = arena_cand + HP->cand_off[feat];
+  const LmCand* cb = LM_CAND_STAGE(K, keys, slot, feat);
+  const LmCand* ct = LM_CAND_STAGE(K, keys, slot, 2 + feat);
+  const LmCand* cp = LM_CAND_STAGE(K, keys, slot - 1, feat);
   for (int k = threadIdx.x; k < Nb; k += blockDim.x) sb[k] = cb[k];
   for (int k = threadIdx.x; k < Ns; k += blockDim.x) st[k] = ct[k];
   for (int k = threadIdx.x; k < Ni; k += blockDim.x) sp[k] = cp[k];
@@ -1494,21 +1560,157 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const
 
 // ----------------------------------------------------------------- k_carry
 // Copies the bottom candidate lists of the last slot of the previous batch
-// (frame first-1) to the carry buffer read by k_post for slot 0.
-// Runs first in a batch (arena counters reset by the host): the carried
-// candidates occupy arena_cand[0, n0 + n1).
-__global__ void k_carry(const LmSlotOut* __restrict__ prev_hdr, int prev_slot, const LmCand* __restrict__ prev_cand,
-                        LmCand* __restrict__ arena_cand, LmSlotOut* __restrict__ hdr, LmArenaCtl* __restrict__ ctl) {
-  const LmSlotOut P = prev_hdr[prev_slot];
-  const int n0 = P.cand_cnt[0], n1 = P.cand_cnt[1];
-  for (int k = threadIdx.x; k < n0; k += blockDim.x) arena_cand[k] = prev_cand[P.cand_off[0] + k];
-  for (int k = threadIdx.x; k < n1; k += blockDim.x) arena_cand[n0 + k] = prev_cand[P.cand_off[1] + k];
+// (frame first-1) into slot 0's candidate staging, where k_post reads the
+// previous frame's candidates (pairwisePotential, :896-919).  Runs first in a
+// batch, before k_corr reuses the key areas of slots >= 1.
+__global__ void k_carry(const LmConst K, unsigned long long* __restrict__ keys, const LmSlotOut* __restrict__ prev_hdr,
+                        int prev_slot, LmSlotOut* __restrict__ hdr) {
+  for (int l = 0; l < LM_NFEAT; ++l) {
+    const int cnt = prev_hdr[prev_slot].cand_cnt[l];
+    const LmCand* src = LM_CAND_STAGE(K, keys, prev_slot, l);
+    LmCand* dst = LM_CAND_STAGE(K, keys, 0, l);
+    for (int k = threadIdx.x; k < cnt; k += blockDim.x) dst[k] = src[k];
+    if (threadIdx.x == 0) hdr[0].cand_cnt[l] = cnt;
+  }
+}
+
+// ------------------------------------------------------------------ k_pack
+// Packs the batch's results into lm_batch_result's layout (frame order) in one
+// buffer: k_pack_scan computes every offset array (exclusive scans over the
+// frames) and the totals, k_pack_copy moves each (frame, feature)'s data.
+// Unit = one batch; a few KB per frame, launch-latency bound.
+template <class F>
+DEV int64_t block_exscan64(int L, F count, int64_t* out, int64_t* s_w) {
+  const int T = blockDim.x, chunk = (L + T - 1) / T;
+  const int i0 = threadIdx.x * chunk, i1 = min(L, i0 + chunk);
+  int64_t c = 0;
+  for (int i = i0; i < i1; ++i) c += count(i);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t v = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) s_w[wid] = v;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    hdr[0].cand_off[0] = 0;
-    hdr[0].cand_cnt[0] = n0;
-    hdr[0].cand_off[1] = n0;
-    hdr[0].cand_cnt[1] = n1;
-    ctl->used[AR_CAND] = n0 + n1;
+    int64_t acc = 0;
+    for (int w = 0; w < (T >> 6); ++w) {
+      const int64_t t = s_w[w];
+      s_w[w] = acc;
+      acc += t;
+    }
+    s_w[T >> 6] = acc;
+  }
+  __syncthreads();
+  int64_t r = s_w[wid] + v - c;
+  for (int i = i0; i < i1; ++i) {
+    out[i] = r;
+    r += count(i);
+  }
+  const int64_t total = s_w[T >> 6];
+  if (threadIdx.x == 0) out[L] = total;
+  __syncthreads();
+  return total;
+}
+
+__global__ __launch_bounds__(1024) void k_pack_scan(const LmSlotOut* __restrict__ hdr, int n,
+                                                    const LmArenaCtl* __restrict__ ctl, const int32_t* __restrict__ err,
+                                                    LmPackHdr* __restrict__ ph, uint8_t* __restrict__ pack, int64_t pack_cap,
+                                                    int64_t* __restrict__ side_base) {
+  __shared__ int64_t s_w[1024 / 64 + 1];
+  const int64_t zero[PK_COUNT] = {0, 0, 0, 0, 0, 0};
+  const LmPackLayout L0 = lm_pack_layout(n, zero);  // offset arrays do not depend on the totals
+  const LmSlotOut* H = hdr + 1;
+  int64_t tot[PK_COUNT];
+  tot[PK_CAND] = block_exscan64(4 * n, [&](int i) { return (int64_t)H[i >> 2].cand_cnt[i & 3]; },
+                                reinterpret_cast<int64_t*>(pack + L0.cand_off), s_w);
+  tot[PK_P22D] = block_exscan64(2 * n, [&](int i) { return (int64_t)H[i >> 1].p22d_cnt[i & 1]; },
+                                reinterpret_cast<int64_t*>(pack + L0.p22d_off), s_w);
+  tot[PK_UNARY] = block_exscan64(2 * n, [&](int i) { return (int64_t)H[i >> 1].unary_cnt[i & 1]; },
+                                 reinterpret_cast<int64_t*>(pack + L0.unary_off), s_w);
+  tot[PK_JC] = block_exscan64(2 * n, [&](int i) {
+    const LmSlotOut& h = H[i >> 1];
+    return h.pw_rows[i & 1] >= 0 ? (int64_t)h.pw_cols[i & 1] + 1 : (int64_t)0;
+  }, reinterpret_cast<int64_t*>(pack + L0.jc_off), s_w);
+  tot[PK_NZ] = block_exscan64(2 * n, [&](int i) {
+    const LmSlotOut& h = H[i >> 1];
+    return h.pw_rows[i & 1] >= 0 ? (int64_t)h.pw_nnz[i & 1] : (int64_t)0;
+  }, reinterpret_cast<int64_t*>(pack + L0.nz_off), s_w);
+  tot[PK_SIDE] = block_exscan64(2 * n, [&](int i) { return (int64_t)H[i >> 1].side_cnt[i & 1]; }, side_base, s_w);
+  if (threadIdx.x == 0) {
+    const LmPackLayout L = lm_pack_layout(n, tot);
+    for (int k = 0; k < PK_COUNT; ++k) ph->tot[k] = tot[k];
+    ph->bytes = L.bytes;
+    ph->overflow = (L.bytes > pack_cap ? 1 : 0) | (ctl->overflow ? 2 : 0);
+    ph->err = *err;
+    for (int k = 0; k < AR_COUNT; ++k) ph->used[k] = ctl->used[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pack_copy(const LmConst K, const LmSlotOut* __restrict__ hdr, int n,
+                                                   const unsigned long long* __restrict__ keys,
+                                                   const LmP22D* __restrict__ arena_p22d, const int32_t* __restrict__ arena_side_y,
+                                                   const double* __restrict__ arena_side_s, const double* __restrict__ arena_unary,
+                                                   const int32_t* __restrict__ arena_jc, const int32_t* __restrict__ arena_ir,
+                                                   const double* __restrict__ arena_pr, const LmPackHdr* __restrict__ ph,
+                                                   uint8_t* __restrict__ pack, const int64_t* __restrict__ side_base) {
+  if (ph->overflow || ph->err) return;  // the host raises or reruns; offsets may be garbage
+  const int f = blockIdx.x, feat = blockIdx.y, slot = 1 + f;
+  const LmSlotOut& H = hdr[slot];
+  int64_t tot[PK_COUNT];
+  for (int k = 0; k < PK_COUNT; ++k) tot[k] = ph->tot[k];
+  const LmPackLayout L = lm_pack_layout(n, tot);
+  const int64_t* cand_off = reinterpret_cast<const int64_t*>(pack + L.cand_off);
+  const int64_t* p22d_off = reinterpret_cast<const int64_t*>(pack + L.p22d_off);
+  const int64_t* unary_off = reinterpret_cast<const int64_t*>(pack + L.unary_off);
+  const int64_t* jc_off = reinterpret_cast<const int64_t*>(pack + L.jc_off);
+  const int64_t* nz_off = reinterpret_cast<const int64_t*>(pack + L.nz_off);
+  LmCand* cand = reinterpret_cast<LmCand*>(pack + L.cand);
+  for (int l = feat; l < LM_NLIST; l += 2) {
+    const LmCand* src = LM_CAND_STAGE(K, keys, slot, l);
+    LmCand* dst = cand + cand_off[4 * f + l];
+    for (int k = threadIdx.x; k < H.cand_cnt[l]; k += blockDim.x) dst[k] = src[k];
+  }
+  const int q = 2 * f + feat;
+  const int64_t sb = side_base[q];
+  LmP22D* p22d = reinterpret_cast<LmP22D*>(pack + L.p22d) + p22d_off[q];
+  for (int k = threadIdx.x; k < H.p22d_cnt[feat]; k += blockDim.x) {
+    LmP22D v = arena_p22d[H.p22d_off[feat] + k];
+    v.side_off = (int32_t)(sb + (v.side_off - H.side_off[feat]));
+    p22d[k] = v;
+  }
+  int32_t* side_y = reinterpret_cast<int32_t*>(pack + L.side_y) + sb;
+  double* side_s = reinterpret_cast<double*>(pack + L.side_s) + sb;
+  for (int k = threadIdx.x; k < H.side_cnt[feat]; k += blockDim.x) {
+    side_y[k] = arena_side_y[H.side_off[feat] + k];
+    side_s[k] = arena_side_s[H.side_off[feat] + k];
+  }
+  double* unary = reinterpret_cast<double*>(pack + L.unary) + unary_off[q];
+  for (int k = threadIdx.x; k < H.unary_cnt[feat]; k += blockDim.x) unary[k] = arena_unary[H.unary_off[feat] + k];
+  int32_t* dims = reinterpret_cast<int32_t*>(pack + L.pw_dims) + 3 * q;
+  if (H.pw_rows[feat] >= 0) {
+    int32_t* jc = reinterpret_cast<int32_t*>(pack + L.jc) + jc_off[q];
+    int32_t* ir = reinterpret_cast<int32_t*>(pack + L.ir) + nz_off[q];
+    double* pr = reinterpret_cast<double*>(pack + L.pr) + nz_off[q];
+    for (int k = threadIdx.x; k <= H.pw_cols[feat]; k += blockDim.x) jc[k] = arena_jc[H.pw_jc_off[feat] + k];
+    for (int k = threadIdx.x; k < H.pw_nnz[feat]; k += blockDim.x) {
+      ir[k] = arena_ir[H.pw_nz_off[feat] + k];
+      pr[k] = arena_pr[H.pw_nz_off[feat] + k];
+    }
+    if (threadIdx.x == 0) {
+      dims[0] = H.pw_rows[feat];
+      dims[1] = H.pw_cols[feat];
+      dims[2] = H.pw_nnz[feat];
+    }
+  } else if (threadIdx.x == 0) {
+    dims[0] = -1;
+    dims[1] = -1;
+    dims[2] = 0;
+  }
+  if (feat == 0) {
+    int32_t* tail = reinterpret_cast<int32_t*>(pack + L.tail) + 45 * f;
+    for (int k = threadIdx.x; k < 45; k += blockDim.x) tail[k] = H.tail[k];
   }
 }
 

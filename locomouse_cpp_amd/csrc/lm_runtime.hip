@@ -76,7 +76,7 @@ struct Rect {
 int ceil_half(int v) { return (int)std::ceil((double)v / 2); }
 
 struct Arena {
-  DevBuf<LmCand> cand;
+  // k_post's per-(frame, feature) outputs, bump-allocated (unordered)
   DevBuf<LmP22D> p22d;
   DevBuf<int32_t> side_y;
   DevBuf<double> side_s;
@@ -85,10 +85,14 @@ struct Arena {
   DevBuf<double> pr;
   DevBuf<LmSlotOut> hdr;
   DevBuf<LmArenaCtl> ctl;
+  // packed results (lm_batch_result layout), its header and side-array bases
+  DevBuf<uint8_t> pack;
+  DevBuf<LmPackHdr> ph;
+  DevBuf<int64_t> side_base;
+  int64_t pack_cap = 0;
   int cap[AR_COUNT] = {0};
   void alloc(const int* c, int nslots) {
     for (int k = 0; k < AR_COUNT; ++k) cap[k] = c[k];
-    cand.alloc(cap[AR_CAND]);
     p22d.alloc(cap[AR_P22D]);
     side_y.alloc(cap[AR_SIDE]);
     side_s.alloc(cap[AR_SIDE]);
@@ -98,6 +102,15 @@ struct Arena {
     pr.alloc(cap[AR_PWNZ]);
     if (!hdr.p) hdr.alloc(nslots);
     if (!ctl.p) ctl.alloc(1);
+    if (!ph.p) ph.alloc(1);
+    if (!side_base.p) side_base.alloc(2 * (size_t)nslots + 1);
+    const int64_t tot[PK_COUNT] = {cap[AR_CAND], cap[AR_P22D], cap[AR_SIDE], cap[AR_UNARY], cap[AR_PWJC], cap[AR_PWNZ]};
+    alloc_pack(lm_pack_layout(nslots, tot).bytes);
+  }
+  void alloc_pack(int64_t bytes) {
+    if (bytes <= pack_cap) return;
+    pack.alloc((size_t)bytes);
+    pack_cap = bytes;
   }
 };
 
@@ -130,29 +143,22 @@ struct lm_ctx {
   DevBuf<LmSlot> slots;
   DevBuf<unsigned long long> keys, gscratch;
   DevBuf<unsigned> tscratch;
+  DevBuf<long long> kprof;  // LM_KPROF=1: k_nms phase timestamps
+  bool kprof_on = false;
   Arena arena[2];
   int parity = 0;
   // host
   HostBuf<LmSlot> h_slots;
   HostBuf<const uint8_t*> h_frame_ptr;
-  HostBuf<LmSlotOut> h_hdr;
   HostBuf<LmArenaCtl> h_ctl;
   HostBuf<int32_t> h_err;
-  std::vector<LmCand> h_cand;
-  std::vector<LmP22D> h_p22d;
-  std::vector<int32_t> h_side_y, h_jc, h_ir;
-  std::vector<double> h_side_s, h_unary, h_pr;
+  HostBuf<LmPackHdr> h_ph;
+  HostBuf<uint8_t> h_pack;  // packed results of the last batch (lm_batch_result points here)
   // state carried between batches
   bool have_state = false;
   int last_frame = -1, last_n = 0, last_parity = 0;
   // last batch info
   int batch_n = 0, batch_s0 = 1;
-  // results
-  std::vector<int64_t> r_cand_off, r_p22d_off, r_unary_off, r_jc_off, r_nz_off;
-  std::vector<lm_candidate> r_cand;
-  std::vector<lm_p22d> r_p22d;
-  std::vector<int32_t> r_side_y, r_pw_dims, r_jc, r_ir, r_tail;
-  std::vector<double> r_side_s, r_unary, r_pr;
   // timing
   std::vector<std::string> t_names;
   std::vector<double> t_ms;
@@ -421,7 +427,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->dbg_slot_floats = doff;
   int np = 1;
   while (np < std::max(K.list_cap[0], K.list_cap[2])) np <<= 1;
-  c->gscratch_slot = 2 * (int64_t)np;
+  c->gscratch_slot = 3 * (int64_t)np;  // keys (u64) + assign, cluster list, xy (32-bit) per entry
   size_t lds = 0;
   for (int d = 0; d < 6; ++d) {
     const LmDet& D = K.det[d];
@@ -432,6 +438,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->corr_lds = lds;
   c->corr_variant = CORR_PK_ASM;
   if (const char* v = getenv("LM_CORR_VARIANT")) c->corr_variant = atoi(v);
+  if (const char* v = getenv("LM_KPROF")) c->kprof_on = atoi(v) != 0;
   // detectors grouped by width: one width-specialised correlation launch each
   c->corr_groups.clear();
   for (int d = 0; d < 6; ++d) {
@@ -497,8 +504,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->slots.alloc(ns);
   c->h_slots.alloc(ns);
   c->h_frame_ptr.alloc(ns);
-  c->h_hdr.alloc(ns);
   c->h_ctl.alloc(1);
+  c->h_ph.alloc(1);
   c->h_err.alloc(1);
   int cap[AR_COUNT];
   cap[AR_CAND] = ns * LM_NLIST * 64;
@@ -563,6 +570,37 @@ struct Timer {
     ev.clear();
   }
 };
+
+// LM_KPROF=1: mean cycles per k_nms phase over the batch's blocks (stderr)
+void kprof_report(lm_ctx* c, int n) {
+  std::vector<long long> h((size_t)2 * 16 * 2 * c->nslots);
+  HIPCHK(hipMemcpy(h.data(), c->kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+  for (int side = 0; side < 2; ++side) {
+    double acc[16] = {0}, life = 0;
+    int cnt[16] = {0}, nb = 0;
+    long long t_min = 0, t_max = 0;
+    for (int b = 0; b < 2 * n; ++b) {
+      const long long* t = h.data() + (size_t)side * 16 * 2 * c->nslots + (size_t)b * 16;
+      long long last = t[0];
+      if (!last) continue;
+      for (int k = 1; k < 16; ++k)
+        if (t[k]) {
+          acc[k] += (double)(t[k] - last);
+          ++cnt[k];
+          last = t[k];
+        }
+      life += (double)(last - t[0]);
+      ++nb;
+      t_min = t_min ? std::min(t_min, t[0]) : t[0];
+      t_max = std::max(t_max, last);
+    }
+    fprintf(stderr, "kprof k_nms %s: blocks=%d life=%.0f span=%lld", side ? "side" : "bottom", nb, nb ? life / nb : 0.0,
+            t_max - t_min);
+    for (int k = 1; k < 16; ++k)
+      if (cnt[k]) fprintf(stderr, " p%d=%.0f", k, acc[k] / cnt[k]);
+    fprintf(stderr, "\n");
+  }
+}
 
 void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev, const int32_t* bb,
                bool device_frames, lm_batch_result* out) {
@@ -632,9 +670,9 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
     HIPCHK(hipMemcpyAsync(A.ctl.p, &hc, sizeof(hc), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(c->npos.p, 0, sizeof(int32_t) * LM_NLIST * (n + 1), st));
     HIPCHK(hipMemsetAsync(c->err.p, 0, sizeof(int32_t), st));
-    if (carry) {
+    if (carry && attempt == 0) {  // a rerun keeps slot 0's staged candidates
       T.begin("k_carry");
-      k_carry<<<1, 256, 0, st>>>(c->arena[prv].hdr.p, c->last_n, c->arena[prv].cand.p, A.cand.p, A.hdr.p, A.ctl.p);
+      k_carry<<<1, 256, 0, st>>>(K, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
       T.end();
     }
     T.begin("k_minmax_lut");
@@ -669,122 +707,64 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
                                    (int64_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w, A.hdr.p, c->err.p);
     T.end();
     if (!c->gscratch.p) c->gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
+    long long *kp0 = nullptr, *kp1 = nullptr;
+    if (c->kprof_on) {
+      if (!c->kprof.p) c->kprof.alloc((size_t)2 * 16 * 2 * c->nslots);
+      HIPCHK(hipMemsetAsync(c->kprof.p, 0, sizeof(long long) * 2 * 16 * 2 * c->nslots, st));
+      kp0 = c->kprof.p;
+      kp1 = c->kprof.p + 16 * 2 * c->nslots;
+    }
     T.begin("k_nms_bottom");
     k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(K, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                    c->gscratch_slot, A.hdr.p, A.cand.p, A.ctl.p, c->err.p);
+                                                    c->gscratch_slot, A.hdr.p, c->err.p, kp0);
     T.end();
     T.begin("k_nms_side");
     k_nms<<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(K, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                c->gscratch_slot, A.hdr.p, A.cand.p, A.ctl.p, c->err.p);
+                                                c->gscratch_slot, A.hdr.p, c->err.p, kp1);
     T.end();
     T.begin("k_post");
     k_post<<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(K, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
-                                                   A.cand.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
+                                                   c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
                                                    A.pr.p, A.ctl.p, c->err.p);
     T.end();
+    T.begin("k_pack");
+    k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
+    k_pack_copy<<<dim3(n, 2), 256, 0, st>>>(K, A.hdr.p, n, c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p,
+                                            A.ir.p, A.pr.p, A.ph.p, A.pack.p, A.side_base.p);
+    T.end();
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->h_hdr.p, A.hdr.p, sizeof(LmSlotOut) * (n + 1), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(c->h_ctl.p, A.ctl.p, sizeof(LmArenaCtl), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(c->h_err.p, c->err.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(c->h_ph.p, A.ph.p, sizeof(LmPackHdr), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    const int e = *c->h_err.p;
+    const LmPackHdr& ph = *c->h_ph.p;
+    const int e = ph.err;
     if (e & 4) throw std::runtime_error("checkVelCriterion: match box outside the padded crop (cv::Mat ROI assertion).");
     if (e & 16) throw std::runtime_error("P22D::add_side_candidate_safe: CV_Assert(S >= 0) failed.");
     if (e & 2) throw std::runtime_error("tail foreground exceeds the kernel's LDS capacity.");
     if (e & 8) throw std::runtime_error("candidate list exceeds the k_post LDS capacity.");
-    if (!c->h_ctl.p->overflow) break;
+    if (e & 32) throw std::runtime_error("candidate staging overflow.");
+    if (e) throw std::runtime_error("device error flags " + std::to_string(e));
+    if (!ph.overflow) break;
     if (attempt >= 3) throw std::runtime_error("result arena overflow persists.");
-    int ncap[AR_COUNT];
-    for (int k = 0; k < AR_COUNT; ++k) ncap[k] = std::max(A.cap[k], (int)(c->h_ctl.p->used[k] * 1.25) + 1024);
-    if (carry) {
-      // keep the carried candidates readable: grow only the current arena
+    if (ph.overflow & 2) {
+      int ncap[AR_COUNT];
+      for (int k = 0; k < AR_COUNT; ++k) ncap[k] = std::max(A.cap[k], (int)(ph.used[k] * 1.25) + 1024);
+      A.alloc(ncap, c->nslots);
     }
-    A.alloc(ncap, c->nslots);
+    A.alloc_pack(ph.bytes + ph.bytes / 4);
   }
   T.collect();
+  if (c->kprof_on) kprof_report(c, n);
 
-  // ---- D2H arena (used prefixes)
+  // ---- one D2H of the packed results (already in lm_batch_result layout)
   Arena& A = c->arena[cur];
-  const LmArenaCtl ctl = *c->h_ctl.p;
-  c->h_cand.resize(ctl.used[AR_CAND]);
-  c->h_p22d.resize(ctl.used[AR_P22D]);
-  c->h_side_y.resize(ctl.used[AR_SIDE]);
-  c->h_side_s.resize(ctl.used[AR_SIDE]);
-  c->h_unary.resize(ctl.used[AR_UNARY]);
-  c->h_jc.resize(ctl.used[AR_PWJC]);
-  c->h_ir.resize(ctl.used[AR_PWNZ]);
-  c->h_pr.resize(ctl.used[AR_PWNZ]);
-  auto d2h = [&](void* dst, const void* src, size_t bytes) {
-    if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
-  };
-  d2h(c->h_cand.data(), A.cand.p, c->h_cand.size() * sizeof(LmCand));
-  d2h(c->h_p22d.data(), A.p22d.p, c->h_p22d.size() * sizeof(LmP22D));
-  d2h(c->h_side_y.data(), A.side_y.p, c->h_side_y.size() * sizeof(int32_t));
-  d2h(c->h_side_s.data(), A.side_s.p, c->h_side_s.size() * sizeof(double));
-  d2h(c->h_unary.data(), A.unary.p, c->h_unary.size() * sizeof(double));
-  d2h(c->h_jc.data(), A.jc.p, c->h_jc.size() * sizeof(int32_t));
-  d2h(c->h_ir.data(), A.ir.p, c->h_ir.size() * sizeof(int32_t));
-  d2h(c->h_pr.data(), A.pr.p, c->h_pr.size() * sizeof(double));
+  const LmPackHdr ph = *c->h_ph.p;
+  if ((int64_t)c->h_pack.n < ph.bytes) c->h_pack.alloc((size_t)(ph.bytes + ph.bytes / 4));
+  HIPCHK(hipMemcpyAsync(c->h_pack.p, A.pack.p, (size_t)ph.bytes, hipMemcpyDeviceToHost, st));
   // keep frame first+n-1 as the next batch's previous frame (storePreviousImage :1508-1513)
   HIPCHK(hipMemcpyAsync(c->halo.p, c->h_frame_ptr.p[n], c->npix, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipStreamSynchronize(st));
-
-  // ---- assemble in frame order
-  c->r_cand_off.assign(1, 0);
-  c->r_p22d_off.assign(1, 0);
-  c->r_unary_off.assign(1, 0);
-  c->r_jc_off.assign(1, 0);
-  c->r_nz_off.assign(1, 0);
-  c->r_cand.clear();
-  c->r_p22d.clear();
-  c->r_side_y.clear();
-  c->r_side_s.clear();
-  c->r_unary.clear();
-  c->r_pw_dims.clear();
-  c->r_jc.clear();
-  c->r_ir.clear();
-  c->r_pr.clear();
-  c->r_tail.clear();
-  for (int s = 1; s <= n; ++s) {
-    const LmSlotOut& H = c->h_hdr.p[s];
-    for (int l = 0; l < LM_NLIST; ++l) {
-      for (int k = 0; k < H.cand_cnt[l]; ++k) {
-        const LmCand& q = c->h_cand[H.cand_off[l] + k];
-        c->r_cand.push_back(lm_candidate{q.x, q.y, q.s});
-      }
-      c->r_cand_off.push_back((int64_t)c->r_cand.size());
-    }
-    for (int f = 0; f < LM_NFEAT; ++f) {
-      const int side_base = (int)c->r_side_y.size();
-      for (int k = 0; k < H.p22d_cnt[f]; ++k) {
-        const LmP22D& q = c->h_p22d[H.p22d_off[f] + k];
-        lm_p22d o;
-        o.bottom = lm_candidate{q.bottom.x, q.bottom.y, q.bottom.s};
-        o.side_offset = side_base + (q.side_off - H.side_off[f]);
-        o.side_count = q.side_cnt;
-        c->r_p22d.push_back(o);
-      }
-      c->r_p22d_off.push_back((int64_t)c->r_p22d.size());
-      c->r_side_y.insert(c->r_side_y.end(), c->h_side_y.begin() + H.side_off[f],
-                         c->h_side_y.begin() + H.side_off[f] + H.side_cnt[f]);
-      c->r_side_s.insert(c->r_side_s.end(), c->h_side_s.begin() + H.side_off[f],
-                         c->h_side_s.begin() + H.side_off[f] + H.side_cnt[f]);
-      c->r_unary.insert(c->r_unary.end(), c->h_unary.begin() + H.unary_off[f],
-                        c->h_unary.begin() + H.unary_off[f] + H.unary_cnt[f]);
-      c->r_unary_off.push_back((int64_t)c->r_unary.size());
-      if (H.pw_rows[f] >= 0) {
-        c->r_pw_dims.insert(c->r_pw_dims.end(), {H.pw_rows[f], H.pw_cols[f], H.pw_nnz[f]});
-        c->r_jc.insert(c->r_jc.end(), c->h_jc.begin() + H.pw_jc_off[f], c->h_jc.begin() + H.pw_jc_off[f] + H.pw_cols[f] + 1);
-        c->r_ir.insert(c->r_ir.end(), c->h_ir.begin() + H.pw_nz_off[f], c->h_ir.begin() + H.pw_nz_off[f] + H.pw_nnz[f]);
-        c->r_pr.insert(c->r_pr.end(), c->h_pr.begin() + H.pw_nz_off[f], c->h_pr.begin() + H.pw_nz_off[f] + H.pw_nnz[f]);
-      } else {
-        c->r_pw_dims.insert(c->r_pw_dims.end(), {-1, -1, 0});
-      }
-      c->r_jc_off.push_back((int64_t)c->r_jc.size());
-      c->r_nz_off.push_back((int64_t)c->r_ir.size());
-    }
-    c->r_tail.insert(c->r_tail.end(), H.tail, H.tail + 45);
-  }
+  const LmPackLayout L = lm_pack_layout(n, ph.tot);
+  const uint8_t* hp = c->h_pack.p;
   c->have_state = true;
   c->last_frame = first + n - 1;
   c->last_n = n;
@@ -795,21 +775,21 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
 
   out->n_frames = n;
   out->first_frame = first;
-  out->cand_offset = c->r_cand_off.data();
-  out->cand = c->r_cand.data();
-  out->p22d_offset = c->r_p22d_off.data();
-  out->p22d = c->r_p22d.data();
-  out->side_y = c->r_side_y.data();
-  out->side_s = c->r_side_s.data();
-  out->unary_offset = c->r_unary_off.data();
-  out->unary = c->r_unary.data();
-  out->pw_dims = c->r_pw_dims.data();
-  out->pw_jc_offset = c->r_jc_off.data();
-  out->pw_jc = c->r_jc.data();
-  out->pw_nz_offset = c->r_nz_off.data();
-  out->pw_ir = c->r_ir.data();
-  out->pw_pr = c->r_pr.data();
-  out->tail = c->r_tail.data();
+  out->cand_offset = reinterpret_cast<const int64_t*>(hp + L.cand_off);
+  out->cand = reinterpret_cast<const lm_candidate*>(hp + L.cand);
+  out->p22d_offset = reinterpret_cast<const int64_t*>(hp + L.p22d_off);
+  out->p22d = reinterpret_cast<const lm_p22d*>(hp + L.p22d);
+  out->side_y = reinterpret_cast<const int32_t*>(hp + L.side_y);
+  out->side_s = reinterpret_cast<const double*>(hp + L.side_s);
+  out->unary_offset = reinterpret_cast<const int64_t*>(hp + L.unary_off);
+  out->unary = reinterpret_cast<const double*>(hp + L.unary);
+  out->pw_dims = reinterpret_cast<const int32_t*>(hp + L.pw_dims);
+  out->pw_jc_offset = reinterpret_cast<const int64_t*>(hp + L.jc_off);
+  out->pw_jc = reinterpret_cast<const int32_t*>(hp + L.jc);
+  out->pw_nz_offset = reinterpret_cast<const int64_t*>(hp + L.nz_off);
+  out->pw_ir = reinterpret_cast<const int32_t*>(hp + L.ir);
+  out->pw_pr = reinterpret_cast<const double*>(hp + L.pr);
+  out->tail = reinterpret_cast<const int32_t*>(hp + L.tail);
 }
 
 }  // namespace

@@ -9,6 +9,7 @@ import pytest
 
 from locomouse_cpp_amd import synthetic as S
 from locomouse_cpp_amd.abi import frame_views
+from locomouse_cpp_amd.results import KEYS, concat_results
 
 pytestmark = pytest.mark.gpu
 
@@ -21,34 +22,6 @@ def _ctx(cfg, max_batch=16):
 def _oracle(cfg, frames, flags=0):
     from oracle import oracle as O
     return O.OracleRun(cfg, frames, flags=flags)
-
-
-KEYS = ("cand_offset", "cand", "p22d_offset", "p22d", "side_y", "side_s", "unary_offset", "unary", "pw_dims",
-        "pw_jc_offset", "pw_jc", "pw_nz_offset", "pw_ir", "pw_pr", "tail")
-
-
-def concat_results(parts):
-    """Concatenate per-batch result dicts into one (offsets rebased)."""
-    out = {}
-    for k in KEYS:
-        if k.endswith("offset"):
-            acc, base = [np.zeros(1, np.int64)], 0
-            for p in parts:
-                acc.append(p[k][1:] + base)
-                base += int(p[k][-1])
-            out[k] = np.concatenate(acc)
-        elif k == "p22d":
-            arrs, base = [], 0
-            for p in parts:
-                a = p[k].copy()
-                a["side_offset"] += base
-                base += len(p["side_y"])
-                arrs.append(a)
-            out[k] = np.concatenate(arrs)
-        else:
-            out[k] = np.concatenate([p[k] for p in parts])
-    out["n_frames"] = sum(p["n_frames"] for p in parts)
-    return out
 
 
 def assert_same(got, ref, label=""):
