@@ -72,7 +72,8 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--resident", type=int, default=1024, help="frames resident in HBM per rank (cycled)")
+    ap.add_argument("--resident", type=int, default=1024, help="frames resident in HBM per stream (cycled)")
+    ap.add_argument("--streams", type=int, default=1, help="contexts (HIP streams + host threads) per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -93,44 +94,72 @@ def main():
     from locomouse_cpp_amd.runtime import Context, synth_frames_device
 
     B = args.batch
+    NS = max(1, args.streams)
     R = max(B, args.resident // B * B)
     cfg = S.SyntheticConfig()
-    ctx = Context(cfg, max_batch=B, device=local)
-    frames = torch.empty((R, 256, 1024), dtype=torch.uint8, device=f"cuda:{local}")
+    # NS contexts per GPU, each with its own HIP stream and host thread, each
+    # on its own contiguous range of the rank's frames (its first batch gets
+    # the previous frame as a 1-frame halo, like a shard start)
+    ctxs = [Context(cfg, max_batch=B, device=local) for _ in range(NS)]
+    frames = torch.empty((NS, R + 1, 256, 1024), dtype=torch.uint8, device=f"cuda:{local}")
     first0 = rank * 10_000_000  # each rank its own stream of frames
-    synth_frames_device(frames.data_ptr(), 256, 1024, first0, R, FRAME_BYTES, device=local)
+    for k in range(NS):
+        # sub-stream k: frames first0 + k*5_000_000 - 1 ... (index 0 is the halo frame)
+        synth_frames_device(frames[k].data_ptr(), 256, 1024, first0 + k * 5_000_000, R + 1, FRAME_BYTES, device=local)
     torch.cuda.synchronize()
 
-    state = {"frame": 0}
+    state = [{"frame": 1} for _ in range(NS)]  # global index 0 of a sub-stream is its halo
 
-    def step():
-        f = state["frame"]
-        off = (f % R) * FRAME_BYTES
-        ctx.detect_device(frames.data_ptr() + off, FRAME_BYTES, B, f)
-        state["frame"] = f + B
+    def step(k, timing):
+        st = state[k]
+        f = st["frame"]
+        i = (f - 1) % R + 1
+        halo = None
+        if f == 1 or i == 1:
+            # start (or wrap-around of the resident window): pass the previous frame
+            halo = frames[k].data_ptr() + ((i - 1) * FRAME_BYTES if f == 1 else R * FRAME_BYTES)
+        ctxs[k].detect_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)
+        st["frame"] = f + B
+        if timing:
+            for name, ms in ctxs[k].kernel_times():
+                kernel_ms.setdefault(name, []).append(ms)
 
-    for _ in range(args.warmup):
-        step()
-    ctx.set_debug(2)  # HIP events around every kernel on the ctx stream
+    def run(k, n, timing):
+        for _ in range(n):
+            step(k, timing)
+
+    def run_all(n, timing):
+        if NS == 1:
+            run(0, n, timing)
+            return
+        import threading
+        th = [threading.Thread(target=run, args=(k, n, timing)) for k in range(NS)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+
     kernel_ms = {}
+    run_all(args.warmup, False)
+    for c in ctxs:
+        c.set_debug(2)  # HIP events around every kernel on the ctx stream
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        for name, ms in ctx.kernel_times():
-            kernel_ms.setdefault(name, []).append(ms)
+    run_all(args.steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.set_debug(0)
+    for c in ctxs:
+        c.set_debug(0)
+    ctx = ctxs[0]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    total_frames = args.steps * B * world
+    total_frames = args.steps * B * NS * world
     fps = total_frames / elapsed
 
     flops = algorithmic_flops_per_frame(ctx)
@@ -157,7 +186,8 @@ def main():
         "data": "synthetic (lm_synth.h scene, resident in HBM)",
         "config": {"workload": "C3: 1024x256 u8 synthetic stream, 6 detectors (paw/snout/tail x bottom/side), "
                                "full per-frame path incl. D2H of results",
-                   "batch_frames": B, "frames_per_rank": args.steps * B, "resident_frames_per_rank": R,
+                   "batch_frames": B, "streams_per_gpu": NS, "frames_per_rank": args.steps * B * NS,
+                   "resident_frames_per_stream": R,
                    "parallelism": f"frame shards x{world} (no collective)"},
         "hbm_gbs": round(fps * FRAME_BYTES / 1e9, 3),
         "roofline": {"bound": "mfma", "compute_roof": "fp32 (v_fma_f32 VALU; equals the f32 MFMA peak)",
@@ -170,7 +200,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

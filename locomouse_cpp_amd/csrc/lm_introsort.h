@@ -235,6 +235,68 @@ inline void std_sort(T* first, T* last, Less comp) {  // host convenience
   std_sort<T, Less>(first, last, comp, stk);
 }
 
+// ---- level-order formulation (for parallel execution)
+//
+// __introsort_loop only ever works on disjoint sub-ranges, and what it does to
+// a range depends on the range's contents and depth alone, so the ranges can
+// be processed level by level (in any order within a level) with the same
+// result.  The final insertion sort never moves an element across the
+// boundary of a leaf range (partitioning leaves every left-part element
+// !(right < left)), so it equals an insertion sort of each leaf on its own.
+// A leaf is a range of <= kThreshold elements or one heap-sorted at depth 0.
+//
+// process_range: returns true and the cut when the range was partitioned
+// (children [first, cut) and [cut, last), both with depth - 1), false when it
+// is a leaf.
+template <class T, class Less>
+LM_HD inline bool process_range(T* base, int first, int last, int depth, Less comp, int* cut) {
+  if (last - first <= kThreshold) return false;
+  if (depth == 0) {
+    partial_sort_full<T, Less>(base + first, base + last, comp);
+    return false;
+  }
+  *cut = (int)(unguarded_partition_pivot<T, Less>(base + first, base + last, comp) - base);
+  return true;
+}
+
+template <class T, class Less>
+inline void std_sort_levels(T* a, int n, Less comp, int depth0 = -1) {  // host reference of the level-order form
+  if (n <= 0) return;
+  int cur[3 * 4096], nxt[3 * 4096];
+  static thread_local unsigned char leaf[1 << 20];
+  for (int i = 0; i < n; ++i) leaf[i] = 0;
+  int qn = 1;
+  cur[0] = 0;
+  cur[1] = n;
+  cur[2] = depth0 >= 0 ? depth0 : 2 * lg_(n);
+  while (qn > 0) {
+    int nn = 0;
+    for (int r = qn - 1; r >= 0; --r) {  // any order within a level
+      int cut = 0;
+      if (process_range<T, Less>(a, cur[3 * r], cur[3 * r + 1], cur[3 * r + 2], comp, &cut)) {
+        const int d = cur[3 * r + 2] - 1;
+        nxt[3 * nn] = cur[3 * r];
+        nxt[3 * nn + 1] = cut;
+        nxt[3 * nn + 2] = d;
+        nxt[3 * nn + 3] = cut;
+        nxt[3 * nn + 4] = cur[3 * r + 1];
+        nxt[3 * nn + 5] = d;
+        nn += 2;
+      } else {
+        leaf[cur[3 * r]] = 1;
+      }
+    }
+    for (int k = 0; k < 3 * nn; ++k) cur[k] = nxt[k];
+    qn = nn;
+  }
+  for (int i = n - 1; i >= 0; --i)  // leaves in any order
+    if (leaf[i]) {
+      int e = i + 1;
+      while (e < n && !leaf[e]) ++e;
+      insertion_sort<T, Less>(a + i, a + e, comp);
+    }
+}
+
 }  // namespace lm_sort
 
 #endif  // LM_INTROSORT_H

@@ -490,6 +490,89 @@ __global__ __launch_bounds__(192) void k_corr_pk(const LmConst K, const LmDetGro
                             &s_cnt, &s_base);
 }
 
+// k_corr_p2: one row-pair per thread, 10 columns wide (192 threads as 8 x 24:
+// the same 80x48 tile).  Per input row-pair t only kernel row i = t is
+// needed, so the next row's weights are prefetched into SGPRs one iteration
+// ahead and the FMA block never waits on a scalar load.  LDS traffic: (KW+9)
+// ds_read2 per 10*KW packed FMAs.
+#define P2_C 10
+
+template <int KW>
+__global__ __launch_bounds__(192) void k_corr_p2(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
+                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  extern __shared__ float lds[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - tb;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
+  const int stride = pk_stride(cols);
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  const int cols4 = (cols + 3) >> 2;
+  for (int e = threadIdx.x; e < rows * cols4; e += blockDim.x) {
+    const int r = e / cols4, c4 = (e - r * cols4) << 2;
+    const uint8_t* p = src + (int64_t)r * ew + c4;
+    float* o = lds + r * stride + c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c4 + k < stride) o[k] = (float)p[k];
+  }
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
+  lm_f2 acc[P2_C];
+#pragma unroll
+  for (int c = 0; c < P2_C; ++c) acc[c] = (lm_f2){D.delta, D.delta};
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  float wc[KW];
+#pragma unroll
+  for (int j = 0; j < KW; ++j) wc[j] = W[j];
+  constexpr int STR = pk_stride_c(LM_TW + KW - 1);
+  for (int t = 0; t < kh; ++t) {
+    const float* p0 = lds + (ly * 2 + t) * stride + lx * P2_C;
+    lm_f2 px[P2_C + KW - 1];
+    const unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p0;
+    lds_pairs<STR, P2_C + KW - 1>(px, base);
+    const float* wnr = W + min(t + 1, kh - 1) * kwp;
+    float wn[KW];
+#pragma unroll
+    for (int j = 0; j < KW; ++j) wn[j] = wnr[j];
+    __builtin_amdgcn_sched_barrier(0);  // scalar loads of row t+1 issue before the FMAs of row t
+#pragma unroll
+    for (int j = 0; j < KW; ++j) {
+      const lm_f2 w2 = (lm_f2){wc[j], wc[j]};
+#pragma unroll
+      for (int c = 0; c < P2_C; ++c) acc[c] = __builtin_elementwise_fma(w2, px[c + j], acc[c]);
+    }
+#pragma unroll
+    for (int j = 0; j < KW; ++j) wc[j] = wn[j];
+  }
+  float accf[2][P2_C];
+#pragma unroll
+  for (int c = 0; c < P2_C; ++c) {
+    accf[0][c] = acc[c].x;
+    accf[1][c] = acc[c].y;
+  }
+  corr_epilogue<2, P2_C>(K, D, accf, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
+                         &s_cnt, &s_base);
+}
+
 // widths with a specialised kernel; others use the generic k_corr
 #define LM_KW_LIST(X) \
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
@@ -497,17 +580,18 @@ __global__ __launch_bounds__(192) void k_corr_pk(const LmConst K, const LmDetGro
 // Correlation variants: 0 generic (runtime width), 1 width-specialised plain
 // FMA (k_corr_kw), 2 packed FMA with compiler-scheduled LDS loads, 3 packed
 // FMA with explicit (row t, row t+1) ds_read2_b32 pair loads (default).
-enum { CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3 };
+enum { CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3, CORR_P2 = 4 };
 
 template <int n>
 static inline const void* corr_fn(int variant) {
+  if (variant == CORR_P2) return (const void*)&k_corr_p2<n>;
   if (variant == CORR_PK_ASM) return (const void*)&k_corr_pk<n, false, true>;
   if (variant == CORR_PK) return (const void*)&k_corr_pk<n, false, false>;
   return (const void*)&k_corr_kw<n>;
 }
 
 static inline const void* corr_kernel(int variant, int kw, int* threads) {
-  *threads = (variant == CORR_PK || variant == CORR_PK_ASM) ? 192 : 256;
+  *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2) ? 192 : 256;
   if (variant != CORR_GENERIC) switch (kw) {
 #define LM_KW_CASE(n) \
   case n:             \
@@ -949,6 +1033,147 @@ DEV bool overlaps_xy(unsigned a, unsigned b, int bw, int bh) {
   return 3 * (bw - dx) * (bh - dy) > 2 * bw * bh;
 }
 
+// std::sort(compareCandidate) replica in level order (lm_introsort.h
+// process_range / std_sort_levels; tests/cpp/introsort_check.cpp proves the
+// level-order form equal to libstdc++).  Every range of a level is handled
+// by one wave:
+//  * median-of-3 to the front (lane 0), then libstdc++'s unguarded Hoare
+//    partition computed in parallel: with f_k the k-th element from the left
+//    that is !(a < pivot) and l_k the k-th from the right that is
+//    !(pivot < a) (both in the range as it was before the loop), the loop
+//    swaps a[f_k] <-> a[l_k] for k < K, K = first k with f_k >= l_k, and
+//    returns min(f_K, l_{K-1}) (f_0 when K = 0);
+//  * depth 0: heap sort by lane 0 (libstdc++'s fallback; never seen here);
+//  * leaves (<= 16 elements): the final insertion sort is a stable sort of
+//    each leaf, done in registers by one thread per leaf.
+// q: two queues of qcap (first, last, depth); leaf: n flags; tf, tr: n ints.
+DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+DEV int wave_partition(unsigned long long* a, int F, int L, int* tf, int* tr) {
+  const ReplicaLess comp;
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) {
+    const int mid = F + (L - F) / 2;
+    lm_sort::move_median_to_first(a + F, a + F + 1, a + mid, a + L - 1, comp);
+  }
+  wave_sync();
+  const unsigned long long pv = a[F];
+  const int lo = F + 1, hi = L;
+  // ranks of the stoppers; tf[lo + k] = f_k, tr[lo + k] = k-th R-stopper from the LEFT
+  int nl = 0, nr = 0;
+  for (int b = lo; b < hi; b += 64) {
+    const int i = b + lane;
+    bool lf = false, rf = false;
+    if (i < hi) {
+      const unsigned long long v = a[i];
+      lf = !comp(v, pv);
+      rf = !comp(pv, v);
+    }
+    const unsigned long long ml = __ballot(lf), mr = __ballot(rf);
+    const unsigned long long below = (1ull << lane) - 1;
+    if (lf) tf[lo + nl + __popcll(ml & below)] = i;
+    if (rf) tr[lo + nr + __popcll(mr & below)] = i;
+    nl += __popcll(ml);
+    nr += __popcll(mr);
+  }
+  wave_sync();
+  // K: f_k < l_k holds for a prefix of k
+  int K = 0;
+  const int kmax = min(nl, nr);
+  for (int b = 0; b < kmax; b += 64) {
+    const int k = b + lane;
+    const bool ok = k < kmax && tf[lo + k] < tr[lo + nr - 1 - k];
+    const unsigned long long m = __ballot(ok);
+    K += __popcll(m);
+    if (m != ~0ull) break;
+  }
+  int cut;
+  if (K == 0) cut = tf[lo];
+  else cut = min(K < nl ? tf[lo + K] : 0x7fffffff, tr[lo + nr - K]);
+  for (int k = lane; k < K; k += 64) {
+    const int i = tf[lo + k], j = tr[lo + nr - 1 - k];
+    const unsigned long long x = a[i], y = a[j];
+    a[i] = y;
+    a[j] = x;
+  }
+  wave_sync();
+  return cut;
+}
+
+DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int* leaf, int* tf, int* tr, int* s_cnt) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) leaf[i] = 0;
+  if (threadIdx.x == 0) {
+    q[0] = 0;
+    q[1] = n;
+    q[2] = 2 * lm_sort::lg_(n);
+    s_cnt[0] = n > 0 ? 1 : 0;
+    s_cnt[1] = 0;
+  }
+  __syncthreads();
+  int sel = 0;
+  while (true) {
+    const int qn = s_cnt[sel];
+    if (qn == 0) break;
+    const int* cur = q + sel * 3 * qcap;
+    int* nxt = q + (1 - sel) * 3 * qcap;
+    for (int r = wid; r < qn; r += nw) {
+      const int f = cur[3 * r], l = cur[3 * r + 1], d = cur[3 * r + 2];
+      if (l - f <= lm_sort::kThreshold) {
+        if (lane == 0) leaf[f] = 1;
+      } else if (d == 0) {
+        if (lane == 0) {
+          lm_sort::partial_sort_full(a + f, a + l, ReplicaLess());
+          leaf[f] = 2;  // sorted; its insertion sort is a no-op
+        }
+      } else {
+        const int cut = wave_partition(a, f, l, tf, tr);
+        if (lane == 0) {
+          const int k = atomicAdd(&s_cnt[1 - sel], 2);
+          nxt[3 * k] = f;
+          nxt[3 * k + 1] = cut;
+          nxt[3 * k + 2] = d - 1;
+          nxt[3 * k + 3] = cut;
+          nxt[3 * k + 4] = l;
+          nxt[3 * k + 5] = d - 1;
+        }
+      }
+      wave_sync();
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_cnt[sel] = 0;
+    sel = 1 - sel;
+    __syncthreads();
+  }
+  // final insertion sort == stable sort of each leaf (<= 16 elements)
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    if (leaf[i] != 1) continue;
+    int e = i + 1;
+    while (e < n && e - i < lm_sort::kThreshold && !leaf[e]) ++e;
+    const int m = e - i;
+    unsigned long long v[lm_sort::kThreshold];
+    float sc[lm_sort::kThreshold];
+#pragma unroll
+    for (int t = 0; t < lm_sort::kThreshold; ++t) {
+      v[t] = t < m ? a[i + t] : 0ull;
+      sc[t] = __uint_as_float((unsigned)(v[t] & 0xFFFFFFFFu));
+    }
+#pragma unroll
+    for (int t = 0; t < lm_sort::kThreshold; ++t) {
+      if (t >= m) break;
+      int r = 0;
+#pragma unroll
+      for (int u = 0; u < lm_sort::kThreshold; ++u)
+        if (u < m) r += (sc[u] > sc[t]) || (u < t && !(sc[t] > sc[u]));
+      a[i + r] = v[t];
+    }
+  }
+  __syncthreads();
+}
+
 // Enumerates the j in [0, n) with flag(j) in increasing order: out[r] = j.
 // Returns their count.
 template <class F>
@@ -1000,6 +1225,7 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
 #define NMS_PROF(k) \
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = clock64();
   NMS_PROF(0)
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 14] = wall_clock64();
   const int list = side ? 2 + feat : feat;
   const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
   const LmDet D = K.det[det];
@@ -1007,9 +1233,10 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
   __shared__ unsigned long long s_keys[LM_NMS_CAP];
   __shared__ int s_assign[LM_NMS_CAP], s_mlist[LM_NMS_CAP];
   __shared__ unsigned s_xy[LM_NMS_CAP + 16];
+  __shared__ int s_tmp[LM_NMS_CAP];
   __shared__ int s_stk[lm_sort::kStackInts];
   __shared__ int s_wsum[LM_NMS_THREADS / 64 + 1];
-  __shared__ int s_n, s_flag, s_base;
+  __shared__ int s_n, s_flag, s_qcnt[2];
 
   if (side && H->cand_cnt[feat] == 0) {  // detectSideCandidates skips (:820-833)
     if (threadIdx.x == 0) {
@@ -1053,10 +1280,11 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
   __syncthreads();
   NMS_PROF(1)
   const int n = s_n;
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 13] = n;
   int np = 1;
   while (np < n) np <<= 1;
   if (n <= LM_NMS_RANKSORT) {
-    rank_sort(a, reinterpret_cast<unsigned long long*>(s_assign), n);  // s_assign+s_mlist: 16 KB scratch
+    rank_sort(a, reinterpret_cast<unsigned long long*>(s_assign), n);  // s_assign: 8 KB = 1024 keys
   } else {
     for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
     __syncthreads();
@@ -1073,11 +1301,22 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
       const unsigned long long v = a[k];
       a[k] = ((unsigned long long)key_lo(v) << 32) | (unsigned)(~(unsigned)(v >> 32));
     }
-    for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
-    __syncthreads();
-    if (np > 1) bitonic_sort(a, np);
-    if (threadIdx.x == 0) lm_sort::std_sort(a, a + n, ReplicaLess(), s_stk);
-    __syncthreads();
+    if (!glob) {
+      if (n <= LM_NMS_RANKSORT) {  // back to row-major order
+        rank_sort(a, reinterpret_cast<unsigned long long*>(s_assign), n);
+      } else {
+        for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
+        __syncthreads();
+        bitonic_sort(a, np);
+      }
+      std_sort_levels_dev(a, n, s_mlist, LM_NMS_CAP / 6, s_assign, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt);
+    } else {  // rare and slow: one thread, explicit stack
+      for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
+      __syncthreads();
+      if (np > 1) bitonic_sort(a, np);
+      if (threadIdx.x == 0) lm_sort::std_sort(a, a + n, ReplicaLess(), s_stk);
+      __syncthreads();
+    }
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
       const unsigned long long v = a[k];
       a[k] = ((unsigned long long)(~(unsigned)(v & 0xFFFFFFFFu)) << 32) | (unsigned)(v >> 32);
@@ -1211,6 +1450,7 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
     }
   }
   NMS_PROF(7)
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 15] = wall_clock64();
   if (threadIdx.x == 0) {
     H->n_pos[list] = n;
     H->cand_cnt[list] = fits ? ncand : 0;

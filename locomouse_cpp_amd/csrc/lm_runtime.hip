@@ -11,6 +11,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -116,8 +118,20 @@ struct Arena {
 
 }  // namespace
 
+// Contexts on one device chain their correlation launches (LM_CORR_SERIALIZE,
+// default on): a context's k_corr waits for the previous k_corr issued on the
+// device by any context.  Several contexts then overlap their small kernels,
+// host work and copies with each other's correlation instead of splitting
+// the CUs between two correlation grids.
+namespace {
+std::mutex g_corr_mu;
+std::map<int, hipEvent_t> g_corr_last;  // device -> event after the last issued k_corr
+}  // namespace
+
 struct lm_ctx {
   int device = 0;
+  hipEvent_t corr_done = nullptr;
+  bool corr_serialize = true;
   hipStream_t stream = nullptr;
   int max_batch = 0, nslots = 0;
   int debug = 0;
@@ -168,6 +182,12 @@ struct lm_ctx {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
+    }
+    if (corr_done) {
+      std::lock_guard<std::mutex> lk(g_corr_mu);
+      auto it = g_corr_last.find(device);
+      if (it != g_corr_last.end() && it->second == corr_done) g_corr_last.erase(it);
+      (void)hipEventDestroy(corr_done);
     }
   }
 };
@@ -576,27 +596,49 @@ void kprof_report(lm_ctx* c, int n) {
   std::vector<long long> h((size_t)2 * 16 * 2 * c->nslots);
   HIPCHK(hipMemcpy(h.data(), c->kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
   for (int side = 0; side < 2; ++side) {
-    double acc[16] = {0}, life = 0;
+    double acc[16] = {0}, life = 0, wlife = 0;
     int cnt[16] = {0}, nb = 0;
     long long t_min = 0, t_max = 0;
     for (int b = 0; b < 2 * n; ++b) {
       const long long* t = h.data() + (size_t)side * 16 * 2 * c->nslots + (size_t)b * 16;
       long long last = t[0];
       if (!last) continue;
-      for (int k = 1; k < 16; ++k)
+      for (int k = 1; k < 13; ++k)
         if (t[k]) {
           acc[k] += (double)(t[k] - last);
           ++cnt[k];
           last = t[k];
         }
       life += (double)(last - t[0]);
+      wlife += t[15] ? (double)(t[15] - t[14]) * 0.01 : 0.0;
       ++nb;
-      t_min = t_min ? std::min(t_min, t[0]) : t[0];
-      t_max = std::max(t_max, last);
+      t_min = t_min ? std::min(t_min, t[14]) : t[14];
+      t_max = std::max(t_max, t[15]);
     }
-    fprintf(stderr, "kprof k_nms %s: blocks=%d life=%.0f span=%lld", side ? "side" : "bottom", nb, nb ? life / nb : 0.0,
-            t_max - t_min);
-    for (int k = 1; k < 16; ++k)
+    long long s_max = 0;
+    for (int b = 0; b < 2 * n; ++b) {
+      const long long* t = h.data() + (size_t)side * 16 * 2 * c->nslots + (size_t)b * 16;
+      if (t[14]) s_max = std::max(s_max, t[14] - t_min);
+    }
+    {
+      std::vector<std::pair<long long, int>> lv;
+      for (int b = 0; b < 2 * n; ++b) {
+        const long long* t = h.data() + (size_t)side * 16 * 2 * c->nslots + (size_t)b * 16;
+        if (t[15]) lv.push_back({t[15] - t[14], b});
+      }
+      std::sort(lv.rbegin(), lv.rend());
+      fprintf(stderr, "kprof slowest:");
+      for (size_t i = 0; i < lv.size() && i < 6; ++i) {
+        const long long* t = h.data() + (size_t)side * 16 * 2 * c->nslots + (size_t)lv[i].second * 16;
+        fprintf(stderr, " [blk %d n=%lld %.1fus cyc=%lld:", lv[i].second, t[13], lv[i].first * 0.01, t[7] - t[0]);
+        for (int k = 1; k <= 7; ++k) fprintf(stderr, " %lld", t[k] ? t[k] - t[0] : -1);
+        fprintf(stderr, "]");
+      }
+      fprintf(stderr, "\n");
+    }
+    fprintf(stderr, "kprof k_nms %s: blocks=%d life=%.0f cyc = %.1f us, span=%.1f us, last start=%.1f us", side ? "side" : "bottom",
+            nb, nb ? life / nb : 0.0, nb ? wlife / nb : 0.0, (t_max - t_min) * 0.01, s_max * 0.01);
+    for (int k = 1; k < 13; ++k)
       if (cnt[k]) fprintf(stderr, " p%d=%.0f", k, acc[k] / cnt[k]);
     fprintf(stderr, "\n");
   }
@@ -685,6 +727,12 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
     k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
         K, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
     T.end();
+    std::unique_lock<std::mutex> corr_lk(g_corr_mu, std::defer_lock);
+    if (c->corr_serialize) {
+      corr_lk.lock();
+      auto it = g_corr_last.find(c->device);
+      if (it != g_corr_last.end() && it->second != c->corr_done) HIPCHK(hipStreamWaitEvent(st, it->second, 0));
+    }
     T.begin("k_corr");
     for (const auto& grp : c->corr_groups) {
       const LmDetGroup& G = grp.second;
@@ -693,6 +741,11 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
                          c->tailbin_slot_bytes));
     }
     T.end();
+    if (c->corr_serialize) {
+      HIPCHK(hipEventRecord(c->corr_done, st));
+      g_corr_last[c->device] = c->corr_done;
+      corr_lk.unlock();
+    }
     if (c->debug & 1) {
       if (!c->dbg.p) {
         c->dbg.alloc((size_t)c->dbg_slot_floats * c->nslots);
@@ -813,6 +866,8 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     c->device = device;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->corr_done, hipEventDisableTiming));
+    if (const char* v = getenv("LM_CORR_SERIALIZE")) c->corr_serialize = atoi(v) != 0;
     c->max_batch = max_batch;
     c->nslots = max_batch + 1;
     validate_and_build(c, setup, params, model);

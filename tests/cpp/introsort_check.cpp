@@ -35,14 +35,16 @@ int main() {
           else s = (double)((i / 8) % levels) + (r % 2) * 0.5;       // blocky
           a[i] = Cand{i, 0, (float)s};
         }
-        std::vector<Cand> b = a;
+        std::vector<Cand> b = a, c = a;
         std::sort(a.begin(), a.end(), cmp);
         lm_sort::std_sort(b.data(), b.data() + n, cmp);
+        lm_sort::std_sort_levels(c.data(), n, cmp);
         ++cases;
         for (int i = 0; i < n; ++i)
-          if (a[i].x != b[i].x) {
+          if (a[i].x != b[i].x || a[i].x != c[i].x) {
             ++fails;
-            std::printf("MISMATCH n=%d levels=%d pattern=%d at %d\n", n, levels, pattern, i);
+            std::printf("MISMATCH n=%d levels=%d pattern=%d at %d (%s)\n", n, levels, pattern, i,
+                        a[i].x != b[i].x ? "replica" : "level-order");
             break;
           }
       }
@@ -54,7 +56,8 @@ int main() {
     for (int depth : {0, 1, 2, 3}) {
       std::vector<Cand> a(n);
       for (int i = 0; i < n; ++i) a[i] = Cand{i, 0, (double)(sm(i * 31 + n) % 9)};
-      std::vector<Cand> b = a;
+      std::vector<Cand> b = a, c = a;
+      lm_sort::std_sort_levels(c.data(), n, cmp, depth);
       std::__introsort_loop(a.begin(), a.end(), (long)depth, __gnu_cxx::__ops::__iter_comp_iter(cmp));
       std::__final_insertion_sort(a.begin(), a.end(), __gnu_cxx::__ops::__iter_comp_iter(cmp));
       int stk[lm_sort::kStackInts];
@@ -62,7 +65,7 @@ int main() {
       lm_sort::final_insertion_sort(b.data(), b.data() + n, cmp);
       ++cases;
       for (int i = 0; i < n; ++i)
-        if (a[i].x != b[i].x) {
+        if (a[i].x != b[i].x || a[i].x != c[i].x) {
           ++fails;
           std::printf("HEAP MISMATCH n=%d depth=%d at %d\n", n, depth, i);
           break;

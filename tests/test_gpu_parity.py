@@ -153,9 +153,11 @@ def _quantized_config(rank):
     return S.SyntheticConfig(weights=W, biases=biases), dups
 
 
-def test_nms_exact_score_ties():
-    """Exact ties take the std::sort replica path (lm_introsort.h)."""
-    c, dups = _quantized_config(400)
+@pytest.mark.parametrize("rank", [400, 1500])
+def test_nms_exact_score_ties(rank):
+    """Exact ties take the std::sort replica path (lm_introsort.h); 1500
+    positives also exercise the bitonic (> LM_NMS_RANKSORT) branch."""
+    c, dups = _quantized_config(rank)
     assert dups > 20  # the case really has ties
     frames = c.frames(0, 6)
     assert_same(_ctx(c).detect(frames, 0), _oracle(c, frames).result, "ties: ")
