@@ -11,6 +11,7 @@ scaling "weak".  Rank 0 prints one JSON line.
 """
 import argparse
 import json
+import math
 import os
 import platform
 import sys
@@ -72,8 +73,9 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--resident", type=int, default=1024, help="frames resident in HBM per stream (cycled)")
+    ap.add_argument("--resident", type=int, default=6400, help="frames resident in HBM per stream (cycled)")
     ap.add_argument("--streams", type=int, default=1, help="contexts (HIP streams + host threads) per GPU")
+    ap.add_argument("--round-robin", action="store_true", help="one host thread drives all streams in turn")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -95,29 +97,33 @@ def main():
 
     B = args.batch
     NS = max(1, args.streams)
-    R = max(B, args.resident // B * B)
+    # Frames resident per stream, cycled: a multiple of the batch and of the
+    # scene's motion period (100 frames), so the wrap-around is a continuous
+    # step of the video, not a jump.
+    unit = B * 100 // math.gcd(B, 100)
+    R = max(unit, args.resident // unit * unit)
     cfg = S.SyntheticConfig()
     # NS contexts per GPU, each with its own HIP stream and host thread, each
-    # on its own contiguous range of the rank's frames (its first batch gets
-    # the previous frame as a 1-frame halo, like a shard start)
+    # on its own contiguous range of the video (rank-major): like a shard, its
+    # first batch gets the previous frame as a 1-frame halo.
     ctxs = [Context(cfg, max_batch=B, device=local) for _ in range(NS)]
     frames = torch.empty((NS, R + 1, 256, 1024), dtype=torch.uint8, device=f"cuda:{local}")
-    first0 = rank * 10_000_000  # each rank its own stream of frames
+    vbase = [(rank * NS + k) * R for k in range(NS)]
     for k in range(NS):
-        # sub-stream k: frames first0 + k*5_000_000 - 1 ... (index 0 is the halo frame)
-        synth_frames_device(frames[k].data_ptr(), 256, 1024, first0 + k * 5_000_000, R + 1, FRAME_BYTES, device=local)
+        # index 0 holds frame vbase-1 (the halo), index i frame vbase+i-1
+        synth_frames_device(frames[k].data_ptr(), 256, 1024, vbase[k] - 1, R + 1, FRAME_BYTES, device=local)
     torch.cuda.synchronize()
 
-    state = [{"frame": 1} for _ in range(NS)]  # global index 0 of a sub-stream is its halo
+    state = [{"frame": vbase[k]} for k in range(NS)]
 
     def step(k, timing):
         st = state[k]
         f = st["frame"]
-        i = (f - 1) % R + 1
+        i = (f - vbase[k]) % R + 1
         halo = None
-        if f == 1 or i == 1:
-            # start (or wrap-around of the resident window): pass the previous frame
-            halo = frames[k].data_ptr() + ((i - 1) * FRAME_BYTES if f == 1 else R * FRAME_BYTES)
+        if i == 1 and f > 0:
+            # stream start (vbase > 0) or wrap-around: pass the previous frame
+            halo = frames[k].data_ptr() + (0 if f == vbase[k] else R * FRAME_BYTES)
         ctxs[k].detect_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)
         st["frame"] = f + B
         if timing:
@@ -129,15 +135,27 @@ def main():
             step(k, timing)
 
     def run_all(n, timing):
-        if NS == 1:
-            run(0, n, timing)
+        if NS == 1 or args.round_robin:
+            for _ in range(n):
+                for k in range(NS):
+                    step(k, timing)
             return
         import threading
-        th = [threading.Thread(target=run, args=(k, n, timing)) for k in range(NS)]
+        errors = []
+
+        def guarded(k):
+            try:
+                run(k, n, timing)
+            except BaseException as e:  # re-raised below: a failed stream must fail the bench
+                errors.append(e)
+
+        th = [threading.Thread(target=guarded, args=(k,)) for k in range(NS)]
         for t in th:
             t.start()
         for t in th:
             t.join()
+        if errors:
+            raise errors[0]
 
     kernel_ms = {}
     run_all(args.warmup, False)

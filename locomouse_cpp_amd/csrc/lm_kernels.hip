@@ -573,6 +573,122 @@ __global__ __launch_bounds__(192) void k_corr_p2(const LmConst K, const LmDetGro
                          &s_cnt, &s_base);
 }
 
+// k_corr_db: k_corr_p2's shape with the LDS loads double-buffered.  Two
+// pixel-pair buffers: while the FMAs of row-pair t run on one, the ds_read2
+// loads of row-pair t+1 fill the other, so a wave waits on LDS only when its
+// loads have not landed after a whole row of FMAs.  The detector weights of
+// both rows of an iteration are scalar-loaded first and consumed by an empty
+// asm statement, so the compiler's own lgkmcnt(0) for them comes before the
+// pixel loads are issued and never drains the pixel queue.
+template <int STRIDE, int... Qs>
+DEV void db_issue(lm_f2 (&px)[sizeof...(Qs)], unsigned base, std::integer_sequence<int, Qs...>) {
+  (lds_pair<STRIDE, Qs>(px[Qs], base), ...);
+}
+
+DEV void db_use_sgpr(float w) { asm volatile("; weight %0" ::"s"(w)); }
+
+template <int N>
+DEV void db_use_sgprs(const float (&w)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) db_use_sgpr(w[i]);
+}
+
+template <int KW>
+DEV void db_fma(lm_f2 (&acc)[P2_C], const lm_f2 (&px)[P2_C + KW - 1], const float (&w)[KW]) {
+#pragma unroll
+  for (int j = 0; j < KW; ++j) {
+    const lm_f2 w2 = (lm_f2){w[j], w[j]};
+#pragma unroll
+    for (int c = 0; c < P2_C; ++c) acc[c] = __builtin_elementwise_fma(w2, px[c + j], acc[c]);
+  }
+}
+
+template <int KW>
+__global__ __launch_bounds__(192, 2) void k_corr_db(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+                                                    int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
+                                                    unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                                    uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  constexpr int NQ = P2_C + KW - 1;
+  constexpr int STR = pk_stride_c(LM_TW + KW - 1);
+  extern __shared__ float lds[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - tb;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
+  const int stride = pk_stride(cols);
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  const int cols4 = (cols + 3) >> 2;
+  for (int e = threadIdx.x; e < rows * cols4; e += blockDim.x) {
+    const int r = e / cols4, c4 = (e - r * cols4) << 2;
+    const uint8_t* p = src + (int64_t)r * ew + c4;
+    float* o = lds + r * stride + c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c4 + k < stride) o[k] = (float)p[k];
+  }
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
+  lm_f2 acc[P2_C];
+#pragma unroll
+  for (int c = 0; c < P2_C; ++c) acc[c] = (lm_f2){D.delta, D.delta};
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  const unsigned base0 =
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(lds + (ly * 2) * stride + lx * P2_C);
+  const unsigned rstep = (unsigned)stride * 4u;
+  lm_f2 pa[NQ], pb[NQ];
+  db_issue<STR>(pa, base0, std::make_integer_sequence<int, NQ>{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  for (int t = 0; t < kh; t += 2) {
+    const bool two = t + 1 < kh;
+    float wa[KW], wb[KW];
+#pragma unroll
+    for (int j = 0; j < KW; ++j) wa[j] = W[t * kwp + j];
+#pragma unroll
+    for (int j = 0; j < KW; ++j) wb[j] = W[(two ? t + 1 : t) * kwp + j];
+    db_use_sgprs<KW>(wa);  // the compiler's wait for the scalar loads lands here
+    db_use_sgprs<KW>(wb);
+    __builtin_amdgcn_sched_barrier(0);
+    if (two) db_issue<STR>(pb, base0 + (unsigned)(t + 1) * rstep, std::make_integer_sequence<int, NQ>{});
+    __builtin_amdgcn_sched_barrier(0);
+    db_fma<KW>(acc, pa, wa);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (!two) break;
+    if (t + 2 < kh) db_issue<STR>(pa, base0 + (unsigned)(t + 2) * rstep, std::make_integer_sequence<int, NQ>{});
+    __builtin_amdgcn_sched_barrier(0);
+    db_fma<KW>(acc, pb, wb);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float accf[2][P2_C];
+#pragma unroll
+  for (int c = 0; c < P2_C; ++c) {
+    accf[0][c] = acc[c].x;
+    accf[1][c] = acc[c].y;
+  }
+  corr_epilogue<2, P2_C>(K, D, accf, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
+                         &s_cnt, &s_base);
+}
+
 // widths with a specialised kernel; others use the generic k_corr
 #define LM_KW_LIST(X) \
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
@@ -580,10 +696,11 @@ __global__ __launch_bounds__(192) void k_corr_p2(const LmConst K, const LmDetGro
 // Correlation variants: 0 generic (runtime width), 1 width-specialised plain
 // FMA (k_corr_kw), 2 packed FMA with compiler-scheduled LDS loads, 3 packed
 // FMA with explicit (row t, row t+1) ds_read2_b32 pair loads (default).
-enum { CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3, CORR_P2 = 4 };
+enum { CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3, CORR_P2 = 4, CORR_DB = 5 };
 
 template <int n>
 static inline const void* corr_fn(int variant) {
+  if (variant == CORR_DB) return (const void*)&k_corr_db<n>;
   if (variant == CORR_P2) return (const void*)&k_corr_p2<n>;
   if (variant == CORR_PK_ASM) return (const void*)&k_corr_pk<n, false, true>;
   if (variant == CORR_PK) return (const void*)&k_corr_pk<n, false, false>;
@@ -591,7 +708,7 @@ static inline const void* corr_fn(int variant) {
 }
 
 static inline const void* corr_kernel(int variant, int kw, int* threads) {
-  *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2) ? 192 : 256;
+  *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2 || variant == CORR_DB) ? 192 : 256;
   if (variant != CORR_GENERIC) switch (kw) {
 #define LM_KW_CASE(n) \
   case n:             \

@@ -11,8 +11,6 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
-#include <map>
-#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -118,20 +116,8 @@ struct Arena {
 
 }  // namespace
 
-// Contexts on one device chain their correlation launches (LM_CORR_SERIALIZE,
-// default on): a context's k_corr waits for the previous k_corr issued on the
-// device by any context.  Several contexts then overlap their small kernels,
-// host work and copies with each other's correlation instead of splitting
-// the CUs between two correlation grids.
-namespace {
-std::mutex g_corr_mu;
-std::map<int, hipEvent_t> g_corr_last;  // device -> event after the last issued k_corr
-}  // namespace
-
 struct lm_ctx {
   int device = 0;
-  hipEvent_t corr_done = nullptr;
-  bool corr_serialize = true;
   hipStream_t stream = nullptr;
   int max_batch = 0, nslots = 0;
   int debug = 0;
@@ -182,12 +168,6 @@ struct lm_ctx {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
       (void)hipStreamDestroy(stream);
-    }
-    if (corr_done) {
-      std::lock_guard<std::mutex> lk(g_corr_mu);
-      auto it = g_corr_last.find(device);
-      if (it != g_corr_last.end() && it->second == corr_done) g_corr_last.erase(it);
-      (void)hipEventDestroy(corr_done);
     }
   }
 };
@@ -727,12 +707,6 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
     k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
         K, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
     T.end();
-    std::unique_lock<std::mutex> corr_lk(g_corr_mu, std::defer_lock);
-    if (c->corr_serialize) {
-      corr_lk.lock();
-      auto it = g_corr_last.find(c->device);
-      if (it != g_corr_last.end() && it->second != c->corr_done) HIPCHK(hipStreamWaitEvent(st, it->second, 0));
-    }
     T.begin("k_corr");
     for (const auto& grp : c->corr_groups) {
       const LmDetGroup& G = grp.second;
@@ -741,11 +715,6 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
                          c->tailbin_slot_bytes));
     }
     T.end();
-    if (c->corr_serialize) {
-      HIPCHK(hipEventRecord(c->corr_done, st));
-      g_corr_last[c->device] = c->corr_done;
-      corr_lk.unlock();
-    }
     if (c->debug & 1) {
       if (!c->dbg.p) {
         c->dbg.alloc((size_t)c->dbg_slot_floats * c->nslots);
@@ -866,8 +835,6 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     c->device = device;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&c->corr_done, hipEventDisableTiming));
-    if (const char* v = getenv("LM_CORR_SERIALIZE")) c->corr_serialize = atoi(v) != 0;
     c->max_batch = max_batch;
     c->nslots = max_batch + 1;
     validate_and_build(c, setup, params, model);

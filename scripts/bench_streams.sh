@@ -1,8 +1,7 @@
 #!/bin/bash
-# Throughput vs contexts per GPU (and k_corr serialisation across contexts).
+# Throughput vs contexts (HIP streams + host threads) per GPU.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
-for cfg in "1 1" "2 1" "2 0" "3 1" "4 1"; do
-  set -- $cfg
-  LM_CORR_SERIALIZE=$2 timeout -k 10 200 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu --streams $1 2>/dev/null | python -c "import json,sys; d=json.load(sys.stdin); print('streams $1 serialize $2:', d['value'], 'corr_ms', d['kernel_avg_ms']['k_corr'], 'TF', d['roofline']['achieved'], d['kernel_avg_ms'])" || exit 1
+for ns in ${STREAMS:-1 2 3 4}; do
+  timeout -k 10 200 python bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu --streams $ns 2>gpurun_out/streams_$ns.err | python -c "import json,sys; d=json.load(sys.stdin); print('streams $ns:', d['value'], 'corr_ms', d['kernel_avg_ms']['k_corr'], 'TF', d['roofline']['achieved'], d['kernel_avg_ms'])" || exit 1
 done
