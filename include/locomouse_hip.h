@@ -240,6 +240,11 @@ lm_status lm_debug_tail_mask(lm_ctx* ctx, int32_t f, uint8_t* out, int32_t rows,
  * (name, milliseconds) pairs; returns the number of kernels. */
 int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32_t cap);
 
+/* Same kernels as lm_debug_kernel_times, as [t0, t1] milliseconds since the
+ * device's epoch event (recorded by the first lm_ctx_set_debug with bit 1 on
+ * that device), so the spans of several contexts' streams can be merged. */
+int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, double* t1, int32_t cap);
+
 /* Benchmark/test input utility (not a reference interface): writes frames
  * [first_frame, first_frame + n) of the synthetic scene of include/lm_synth.h
  * (rows x cols u8, frame_pitch bytes apart) into device memory of `device`. */

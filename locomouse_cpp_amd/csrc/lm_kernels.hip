@@ -1583,10 +1583,19 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0,
 
 DEV bool vel_criterion(const LmConst& K, const uint8_t* Fc, const uint8_t* Fp, const uint8_t* bkg, const int32_t* cal,
                        const uint8_t* lutc, const uint8_t* lutp, int crop_x, int crop_y, int crop_w, int crop_h,
-                       int bx, int by, int bwid, int bhei, int area, double alpha, int32_t* err) {
+                       int bx, int by, int bwid, int bhei, int area, double alpha, int32_t* err, int tag) {
   // checkVelCriterion (:1256-1267): sum(sat_u8(I - I_prev) > 25) >= area*alpha
   if (bx < 0 || by < 0 || bwid < 0 || bhei < 0 || bx + bwid > crop_w || by + bhei > crop_h) {
     atomicOr(err, 4);  // cv::Mat ROI assertion in the reference
+    if (atomicCAS(&err[1], 0, 1) == 0) {  // first offender, for the error message
+      err[2] = tag;
+      err[3] = bx;
+      err[4] = by;
+      err[5] = bwid;
+      err[6] = bhei;
+      err[7] = crop_w;
+      err[8] = crop_h;
+    }
     return false;
   }
   int sum = 0;
@@ -1821,7 +1830,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const
       if (need)
         s_mb[i] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl.crop_x[0], sl.crop_y[0], K.crop_w[0], K.crop_h[0],
                                 mbox[0] + sb[i].x + K.spre_b_w, mbox[1] + sb[i].y + K.spre_b_h, mbox[2], mbox[3],
-                                K.size_b[feat][0] * K.size_b[feat][1], 0.02, err);
+                                K.size_b[feat][0] * K.size_b[feat][1], 0.02, err, (slot << 16) | (feat << 12) | i);
     }
     for (int j = threadIdx.x; j < Ns; j += blockDim.x) {
       bool need = false;
@@ -1830,7 +1839,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const
       if (need)
         s_mt[j] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl.crop_x[1], sl.crop_y[1], K.crop_w[1], K.crop_h[1],
                                 tbox[0] + st[j].x + K.spre_t_w, tbox[1] + st[j].y + K.spre_t_h, tbox[2], tbox[3],
-                                K.size_s[feat][0] * K.size_s[feat][1], 0.05, err);
+                                K.size_s[feat][0] * K.size_s[feat][1], 0.05, err, (slot << 16) | (feat << 12) | 0x800 | j);
     }
   }
   __syncthreads();

@@ -10,7 +10,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -118,6 +121,7 @@ struct Arena {
 
 struct lm_ctx {
   int device = 0;
+  bool counted = false;  // holds a slot of the per-device live-context budget
   hipStream_t stream = nullptr;
   int max_batch = 0, nslots = 0;
   int debug = 0;
@@ -160,13 +164,15 @@ struct lm_ctx {
   // last batch info
   int batch_n = 0, batch_s0 = 1;
   // timing
-  std::vector<std::string> t_names;
-  std::vector<double> t_ms;
+  std::vector<const char*> t_names;  // static kernel names
+  std::vector<double> t_ms, t_t0, t_t1;
+  std::vector<hipEvent_t> ev_pool;
 
   ~lm_ctx() {
     if (stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
+      for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
       (void)hipStreamDestroy(stream);
     }
   }
@@ -499,14 +505,14 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->tscratch.alloc((size_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w * ns);
   c->keys.alloc((size_t)K.keys_per_slot * ns);
   c->npos.alloc((size_t)LM_NLIST * ns);
-  c->err.alloc(1);
+  c->err.alloc(16);
   c->frame_ptr.alloc(ns);
   c->slots.alloc(ns);
   c->h_slots.alloc(ns);
   c->h_frame_ptr.alloc(ns);
   c->h_ctl.alloc(1);
   c->h_ph.alloc(1);
-  c->h_err.alloc(1);
+  c->h_err.alloc(16);
   int cap[AR_COUNT];
   cap[AR_CAND] = ns * LM_NLIST * 64;
   cap[AR_P22D] = ns * LM_NFEAT * 64;
@@ -517,6 +523,49 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   for (int a = 0; a < 2; ++a) c->arena[a].alloc(cap, ns);
   for (const auto& grp : c->corr_groups) HIPCHK(corr_set_lds(c->corr_variant, grp.first, c->corr_lds));
   HIPCHK(hipFuncSetAttribute((const void*)k_corr_dbg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->corr_lds));
+}
+
+// Live contexts per device.  Each context owns one HIP stream, and HIP maps
+// streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by default).
+// Measured on MI355X (ROCm 7, scripts/debug_mt.py): once contexts share
+// hardware queues (more than GPU_MAX_HW_QUEUES/2 contexts in one process,
+// torch's own stream included in the budget) batches intermittently come
+// back with other batches' bytes in their candidate staging -- silently wrong
+// results.  Refuse such a context instead of corrupting results.
+std::mutex g_live_mu;
+std::map<int, int> g_live;
+
+int live_ctx_limit() {
+  if (const char* v = getenv("LM_ALLOW_QUEUE_SHARING"))
+    if (atoi(v) != 0) return 1 << 30;
+  int hwq = 4;
+  if (const char* v = getenv("GPU_MAX_HW_QUEUES")) hwq = std::max(1, atoi(v));
+  return std::max(1, hwq / 2);
+}
+
+void live_ctx_acquire(int device) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  const int lim = live_ctx_limit();
+  if (g_live[device] >= lim)
+    throw std::runtime_error("too many contexts on HIP device " + std::to_string(device) + " in this process (limit " +
+                             std::to_string(lim) + " = GPU_MAX_HW_QUEUES/2): contexts sharing hardware queues return "
+                             "corrupted results; destroy a context or raise GPU_MAX_HW_QUEUES.");
+  ++g_live[device];
+}
+
+void live_ctx_release(int device) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  --g_live[device];
+}
+
+// One epoch event per device (recorded when timing is switched on) that every
+// context's kernel spans are measured against.
+std::map<int, hipEvent_t> g_epoch;
+
+hipEvent_t epoch_event(const lm_ctx* c) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  auto it = g_epoch.find(c->device);
+  return it == g_epoch.end() ? nullptr : it->second;
 }
 
 lm_status fail(lm_status s, const std::string& m) {
@@ -541,31 +590,46 @@ lm_status guarded(F&& f) {
 struct Timer {
   lm_ctx* c;
   bool on;
-  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> ev;
+  std::vector<std::pair<const char*, int>> ev;  // (kernel, index of its begin event in the ctx pool)
   explicit Timer(lm_ctx* cc) : c(cc), on(cc->debug & 2) {}
+  hipEvent_t pool(size_t i) {
+    while (c->ev_pool.size() <= i) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[i];
+  }
   void begin(const char* name) {
     if (!on) return;
-    hipEvent_t a, b;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
-    HIPCHK(hipEventRecord(a, c->stream));
-    ev.push_back({name, {a, b}});
+    const int i = (int)ev.size() * 2;
+    HIPCHK(hipEventRecord(pool(i), c->stream));
+    ev.push_back({name, i});
   }
   void end() {
     if (!on) return;
-    HIPCHK(hipEventRecord(ev.back().second.second, c->stream));
+    HIPCHK(hipEventRecord(pool(ev.back().second + 1), c->stream));
   }
+  // Durations, plus start/end against the device's epoch event so callers can
+  // take the union of one kernel's spans over several contexts' streams.
   void collect() {
     if (!on) return;
     c->t_names.clear();
     c->t_ms.clear();
+    c->t_t0.clear();
+    c->t_t1.clear();
+    const hipEvent_t ep = epoch_event(c);
     for (auto& e : ev) {
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, e.second.first, e.second.second));
+      float ms = 0, t0 = 0, t1 = 0;
+      HIPCHK(hipEventElapsedTime(&ms, c->ev_pool[e.second], c->ev_pool[e.second + 1]));
+      if (ep) {
+        HIPCHK(hipEventElapsedTime(&t0, ep, c->ev_pool[e.second]));
+        HIPCHK(hipEventElapsedTime(&t1, ep, c->ev_pool[e.second + 1]));
+      }
       c->t_names.push_back(e.first);
       c->t_ms.push_back(ms);
-      (void)hipEventDestroy(e.second.first);
-      (void)hipEventDestroy(e.second.second);
+      c->t_t0.push_back(t0);
+      c->t_t1.push_back(t1);
     }
     ev.clear();
   }
@@ -691,7 +755,7 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
     for (int k = 0; k < AR_COUNT; ++k) hc.cap[k] = A.cap[k];
     HIPCHK(hipMemcpyAsync(A.ctl.p, &hc, sizeof(hc), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(c->npos.p, 0, sizeof(int32_t) * LM_NLIST * (n + 1), st));
-    HIPCHK(hipMemsetAsync(c->err.p, 0, sizeof(int32_t), st));
+    HIPCHK(hipMemsetAsync(c->err.p, 0, 16 * sizeof(int32_t), st));
     if (carry && attempt == 0) {  // a rerun keeps slot 0's staged candidates
       T.begin("k_carry");
       k_carry<<<1, 256, 0, st>>>(K, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
@@ -758,8 +822,24 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
     HIPCHK(hipMemcpyAsync(c->h_ph.p, A.ph.p, sizeof(LmPackHdr), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const LmPackHdr& ph = *c->h_ph.p;
-    const int e = ph.err;
-    if (e & 4) throw std::runtime_error("checkVelCriterion: match box outside the padded crop (cv::Mat ROI assertion).");
+    const int e = (c->debug & 4) ? (ph.err & ~4) : ph.err;  // debug bit 2: report but keep going
+    if ((c->debug & 4) && (ph.err & 4)) {
+      HIPCHK(hipMemcpy(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost));
+      const int32_t* d = c->h_err.p;
+      fprintf(stderr, "[lm debug] vel box error frame %d tag %x box (%d,%d,%d,%d)\n", first - 1 + (d[2] >> 16), d[2],
+              d[3], d[4], d[5], d[6]);
+    }
+    if (e & 4) {
+      HIPCHK(hipMemcpy(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost));
+      const int32_t* d = c->h_err.p;
+      const int tag = d[2], slot = tag >> 16;
+      char buf[256];
+      snprintf(buf, sizeof buf, " [frame %d, %s %s candidate %d: box (%d,%d,%d,%d) in crop %dx%d]",
+               first - 1 + slot, (tag >> 12 & 1) ? "snout" : "paw", (tag & 0x800) ? "side" : "bottom", tag & 0x7FF,
+               d[3], d[4], d[5], d[6], d[7], d[8]);
+      throw std::runtime_error(std::string("checkVelCriterion: match box outside the padded crop (cv::Mat ROI "
+                                           "assertion).") + buf);
+    }
     if (e & 16) throw std::runtime_error("P22D::add_side_candidate_safe: CV_Assert(S >= 0) failed.");
     if (e & 2) throw std::runtime_error("tail foreground exceeds the kernel's LDS capacity.");
     if (e & 8) throw std::runtime_error("candidate list exceeds the k_post LDS capacity.");
@@ -785,6 +865,19 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
   // keep frame first+n-1 as the next batch's previous frame (storePreviousImage :1508-1513)
   HIPCHK(hipMemcpyAsync(c->halo.p, c->h_frame_ptr.p[n], c->npix, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (c->debug & 8) {  // diagnostics: a second, synchronous copy of the pack must equal the async one
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<uint8_t> chk((size_t)ph.bytes);
+    HIPCHK(hipMemcpy(chk.data(), A.pack.p, (size_t)ph.bytes, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < ph.bytes; ++i)
+      if (chk[i] != c->h_pack.p[i]) {
+        int64_t j = ph.bytes - 1;
+        while (j > i && chk[j] == c->h_pack.p[j]) --j;
+        fprintf(stderr, "[lm debug] D2H pack mismatch frames %d..%d: bytes [%ld, %ld] of %ld differ\n", first,
+                first + n - 1, (long)i, (long)j, (long)ph.bytes);
+        break;
+      }
+  }
   const LmPackLayout L = lm_pack_layout(n, ph.tot);
   const uint8_t* hp = c->h_pack.p;
   c->have_state = true;
@@ -832,7 +925,9 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) throw HipError("invalid HIP device index");
+    live_ctx_acquire(device);
     c->device = device;
+    c->counted = true;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->max_batch = max_batch;
@@ -840,6 +935,7 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     validate_and_build(c, setup, params, model);
   });
   if (s != LM_OK) {
+    if (c->counted) live_ctx_release(c->device);
     delete c;
     return s;
   }
@@ -847,7 +943,10 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
   return LM_OK;
 }
 
-LM_API void lm_ctx_destroy(lm_ctx* ctx) { delete ctx; }
+LM_API void lm_ctx_destroy(lm_ctx* ctx) {
+  if (ctx && ctx->counted) live_ctx_release(ctx->device);
+  delete ctx;
+}
 
 LM_API lm_status lm_get_geometry(const lm_ctx* ctx, lm_geometry* out) {
   if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
@@ -872,8 +971,31 @@ LM_API lm_status lm_detect_batch_device(lm_ctx* ctx, const uint8_t* d_frames, in
 
 LM_API lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags) {
   if (!ctx) return fail(LM_ERR_INVALID_ARGUMENT, "null ctx");
-  ctx->debug = flags;
-  return LM_OK;
+  return guarded([&] {
+    if (flags & 2) {
+      std::lock_guard<std::mutex> lk(g_live_mu);
+      if (!g_epoch.count(ctx->device)) {
+        HIPCHK(hipSetDevice(ctx->device));
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        HIPCHK(hipEventRecord(e, ctx->stream));
+        HIPCHK(hipEventSynchronize(e));
+        g_epoch[ctx->device] = e;
+      }
+    }
+    ctx->debug = flags;
+  });
+}
+
+LM_API int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, double* t1, int32_t cap) {
+  if (!ctx) return 0;
+  const int32_t n = (int32_t)ctx->t_names.size();
+  for (int32_t i = 0; i < n && i < cap; ++i) {
+    if (names) names[i] = ctx->t_names[i];
+    if (t0) t0[i] = ctx->t_t0[i];
+    if (t1) t1[i] = ctx->t_t1[i];
+  }
+  return n;
 }
 
 LM_API lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out, int32_t rows, int32_t cols) {
@@ -903,7 +1025,7 @@ LM_API int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms
   if (!ctx) return 0;
   const int32_t n = (int32_t)ctx->t_names.size();
   for (int32_t i = 0; i < n && i < cap; ++i) {
-    if (names) names[i] = ctx->t_names[i].c_str();
+    if (names) names[i] = ctx->t_names[i];
     if (ms) ms[i] = ctx->t_ms[i];
   }
   return n;

@@ -20,7 +20,7 @@ CSRC = os.path.join(PKG, "csrc")
 EXPORTED = (
     "lm_abi_version", "lm_last_error", "lm_ctx_create", "lm_ctx_destroy", "lm_get_geometry", "lm_ctx_stream",
     "lm_detect_batch", "lm_detect_batch_device", "lm_ctx_set_debug", "lm_debug_scores", "lm_debug_tail_mask",
-    "lm_debug_kernel_times", "lm_synth_frames_device",
+    "lm_debug_kernel_times", "lm_debug_kernel_spans", "lm_synth_frames_device",
 )
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -68,6 +68,9 @@ def lib():
         L.lm_debug_tail_mask.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
         L.lm_debug_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.c_int32]
         L.lm_debug_kernel_times.restype = C.c_int32
+        L.lm_debug_kernel_spans.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
+                                            C.POINTER(C.c_double), C.c_int32]
+        L.lm_debug_kernel_spans.restype = C.c_int32
         L.lm_synth_frames_device.argtypes = [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32,
                                              C.c_int64]
         _lib = L
@@ -159,6 +162,14 @@ class Context:
         ms = (C.c_double * 64)()
         n = lib().lm_debug_kernel_times(self._h, names, ms, 64)
         return [(names[i].decode(), ms[i]) for i in range(min(n, 64))]
+
+    def kernel_spans(self):
+        """[(name, t0_ms, t1_ms)] of the last batch against the device epoch."""
+        names = (C.c_char_p * 64)()
+        t0 = (C.c_double * 64)()
+        t1 = (C.c_double * 64)()
+        n = lib().lm_debug_kernel_spans(self._h, names, t0, t1, 64)
+        return [(names[i].decode(), t0[i], t1[i]) for i in range(min(n, 64))]
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

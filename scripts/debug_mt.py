@@ -56,7 +56,7 @@ for k in range(NS):
     for b in range(NB):
         a, r = outs[k][b], ref[k][b]
         if isinstance(a, Exception) or isinstance(r, Exception):
-            print("stream", k, "batch", b, "mt:", repr(a)[:120] if isinstance(a, Exception) else "ok",
+            print("stream", k, "batch", b, "mt:", repr(a)[:400] if isinstance(a, Exception) else "ok",
                   "ref:", repr(r)[:120] if isinstance(r, Exception) else "ok")
             bad += 1
             continue
@@ -69,3 +69,20 @@ for k in range(NS):
                 bad += 1
                 break
 print("NS", NS, "NB", NB, "debug", debug, "bad batches:", bad)
+if bad and debug & 4:
+    # print the differing candidate lists of the first mismatching batch
+    for k in range(NS):
+        for b in range(NB):
+            a, r = outs[k][b], ref[k][b]
+            if isinstance(a, Exception):
+                continue
+            if not np.array_equal(a["cand"]["y"], r["cand"]["y"]) or a["cand"].shape != r["cand"].shape:
+                co_a, co_r = a["cand_offset"], r["cand_offset"]
+                for fl in range(len(co_a) - 1):
+                    xa = a["cand"][co_a[fl]:co_a[fl + 1]]
+                    xr = r["cand"][co_r[fl]:co_r[fl + 1]]
+                    if xa.shape != xr.shape or not all(np.array_equal(xa[m], xr[m]) for m in xa.dtype.names):
+                        print("stream", k, "batch", b, "frame", k * R + b * B + fl // 4, "list", fl % 4,
+                              "n", len(xa), len(xr))
+                        idx = [i for i in range(min(len(xa), len(xr))) if tuple(xa[i]) != tuple(xr[i])]
+                        print("   first diffs:", [(i, tuple(xa[i]), tuple(xr[i])) for i in idx[:5]])

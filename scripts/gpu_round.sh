@@ -20,6 +20,7 @@ cat gpurun_out/bench_$TAG.json
 rm -rf gpurun_out/prof_$TAG
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 20 --warmup 3 --no-cpu ${PROF_ARGS} > gpurun_out/prof_$TAG.out 2>&1 || { echo "rocprof failed"; tail -20 gpurun_out/prof_$TAG.out; exit 1; }
 find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \;
+python scripts/prof_union.py gpurun_out/prof_$TAG/run_kernel_trace.csv 4 ${PROF_SKIP:-6} > gpurun_out/prof_union_$TAG.txt && cat gpurun_out/prof_union_$TAG.txt
 [ -n "$NO_PMC" ] && exit 0
 for c in FETCH_SIZE WRITE_SIZE; do
   rm -rf gpurun_out/pmc_$TAG/$c

@@ -1,6 +1,8 @@
 """Several contexts on one GPU driven from several host threads (one HIP
 stream each, bench.py --streams): every batch must equal the same range run
-alone (no shared state between contexts)."""
+alone (no shared state between contexts).  Contexts beyond
+GPU_MAX_HW_QUEUES/2 per device are refused (lm_runtime.hip, live_ctx_acquire)."""
+import os
 import threading
 
 import numpy as np
@@ -26,7 +28,7 @@ def _run(ctx, frames_dev, k, R, NB, B, out):
 def test_threads_and_contexts_are_independent():
     torch = pytest.importorskip("torch")
     from locomouse_cpp_amd.runtime import Context, synth_frames_device
-    NS, NB, B = 3, 4, 64
+    NS, NB, B = 2, 12, 128
     R = NB * B
     cfg = S.SyntheticConfig()
     fr = torch.empty((NS, R + 1, 256, 1024), dtype=torch.uint8, device="cuda")
@@ -36,7 +38,9 @@ def test_threads_and_contexts_are_independent():
     ref = []
     for k in range(NS):
         o = []
-        _run(Context(cfg, max_batch=B), fr, k, R, NB, B, o)
+        c = Context(cfg, max_batch=B)
+        _run(c, fr, k, R, NB, B, o)
+        c.close()
         ref.append(o)
     ctxs = [Context(cfg, max_batch=B) for _ in range(NS)]
     outs = [[] for _ in range(NS)]
@@ -56,3 +60,22 @@ def test_threads_and_contexts_are_independent():
                     assert x.shape == y.shape and all(np.array_equal(x[n], y[n]) for n in x.dtype.names), (k, b, key)
                 else:
                     assert np.array_equal(x, y), (k, b, key)
+    for c in ctxs:
+        c.close()
+
+
+def test_contexts_beyond_hw_queue_budget_are_refused():
+    pytest.importorskip("torch")
+    from locomouse_cpp_amd.runtime import Context, LMError
+    hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    if os.environ.get("LM_ALLOW_QUEUE_SHARING"):
+        pytest.skip("LM_ALLOW_QUEUE_SHARING set")
+    lim = max(1, hwq // 2)
+    cfg = S.SyntheticConfig()
+    ctxs = [Context(cfg, max_batch=4) for _ in range(lim)]
+    with pytest.raises(LMError, match="too many contexts"):
+        Context(cfg, max_batch=4)
+    ctxs[-1].close()
+    ctxs[-1] = Context(cfg, max_batch=4)  # a released slot can be reused
+    for c in ctxs:
+        c.close()
