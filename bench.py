@@ -21,7 +21,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "frames/sec whole-node + achieved HBM GB/s; 1024×256 gray, 6 templates"
-FRAME_BYTES = 1024 * 256
+CONFIGS = {  # BASELINE.json configs with a GPU bench line: (rows, cols, description)
+    "c3": (256, 1024, "C3: 1024x256 u8 synthetic stream, 6 detectors (paw/snout/tail x bottom/side), "
+                      "full per-frame path incl. D2H of results"),
+    "c5": (512, 1920, "C5: 1920x512 u8 synthetic stream, geometry and detectors x2 (fp32, bit-exact mode), "
+                      "full per-frame path incl. D2H of results"),
+}
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
 
@@ -85,6 +90,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--resident", type=int, default=6400, help="frames resident in HBM per stream (cycled)")
     ap.add_argument("--streams", type=int, default=2,
@@ -121,16 +127,18 @@ def main():
     # step of the video, not a jump.
     unit = B * 100 // math.gcd(B, 100)
     R = max(unit, args.resident // unit * unit)
-    cfg = S.SyntheticConfig()
+    rows, cols, workload = CONFIGS[args.config]
+    FRAME_BYTES = rows * cols
+    cfg = S.SyntheticConfig(rows=rows, cols=cols)
     # NS contexts per GPU, each with its own HIP stream and host thread, each
     # on its own contiguous range of the video (rank-major): like a shard, its
     # first batch gets the previous frame as a 1-frame halo.
     ctxs = [Context(cfg, max_batch=B, device=local) for _ in range(NS)]
-    frames = torch.empty((NS, R + 1, 256, 1024), dtype=torch.uint8, device=f"cuda:{local}")
+    frames = torch.empty((NS, R + 1, rows, cols), dtype=torch.uint8, device=f"cuda:{local}")
     vbase = [(rank * NS + k) * R for k in range(NS)]
     for k in range(NS):
         # index 0 holds frame vbase-1 (the halo), index i frame vbase+i-1
-        synth_frames_device(frames[k].data_ptr(), 256, 1024, vbase[k] - 1, R + 1, FRAME_BYTES, device=local)
+        synth_frames_device(frames[k].data_ptr(), rows, cols, vbase[k] - 1, R + 1, FRAME_BYTES, device=local)
     torch.cuda.synchronize()
 
     state = [{"frame": vbase[k]} for k in range(NS)]
@@ -227,8 +235,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (lm_synth.h scene, resident in HBM)",
-        "config": {"workload": "C3: 1024x256 u8 synthetic stream, 6 detectors (paw/snout/tail x bottom/side), "
-                               "full per-frame path incl. D2H of results",
+        "config": {"workload": workload,
                    "batch_frames": B, "streams_per_gpu": NS, "frames_per_rank": args.steps * B * NS,
                    "resident_frames_per_stream": R,
                    "parallelism": f"frame shards x{world} (no collective)"},

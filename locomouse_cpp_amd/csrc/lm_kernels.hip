@@ -707,17 +707,35 @@ static inline const void* corr_fn(int variant) {
   return (const void*)&k_corr_kw<n>;
 }
 
+// wide detectors (the 1920x512 geometry of config C5: 44, 48, 52, 60) get the
+// production variant only; other variants fall back to the generic kernel
+#define LM_KW_WIDE_LIST(X) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+
+template <int n>
+static inline const void* corr_fn_wide(int variant) {
+  return variant == CORR_PK_ASM ? (const void*)&k_corr_pk<n, false, true> : nullptr;
+}
+
 static inline const void* corr_kernel(int variant, int kw, int* threads) {
   *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2 || variant == CORR_DB) ? 192 : 256;
+  const void* fn = nullptr;
   if (variant != CORR_GENERIC) switch (kw) {
 #define LM_KW_CASE(n) \
   case n:             \
-    return corr_fn<n>(variant);
+    fn = corr_fn<n>(variant);  \
+    break;
       LM_KW_LIST(LM_KW_CASE)
+#undef LM_KW_CASE
+#define LM_KW_CASE(n)             \
+  case n:                         \
+    fn = corr_fn_wide<n>(variant); \
+    break;
+      LM_KW_WIDE_LIST(LM_KW_CASE)
 #undef LM_KW_CASE
       default:
         break;
     }
+  if (fn) return fn;
   *threads = 256;
   return (const void*)&k_corr;
 }

@@ -138,6 +138,7 @@ struct lm_ctx {
   size_t corr_lds = 0;
   int corr_variant = 2;
   std::vector<std::pair<int, LmDetGroup>> corr_groups;  // (detector width, detectors)
+  std::vector<size_t> corr_group_lds;                    // dynamic LDS bytes per group launch
   // device buffers
   DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin, tailmask;
   DevBuf<int32_t> cal, npos, err;
@@ -462,6 +463,24 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     G.tile_end[G.n] = prev + K.det[d].tiles_x * K.det[d].tiles_y;
     ++G.n;
   }
+  // LDS per group: the packed kernel needs only its own tile window
+  // (LM_TH+kh-1 rows at pk_stride), so narrow groups are not sized for the
+  // widest detector and keep more workgroups per CU; other variants use the
+  // common size.
+  c->corr_group_lds.clear();
+  for (const auto& grp : c->corr_groups) {
+    size_t need = c->corr_lds;
+    int th = 0;
+    (void)corr_kernel(c->corr_variant, grp.first, &th);  // th == 256: generic fallback kernel
+    if (c->corr_variant == CORR_PK_ASM && th == 192) {
+      need = 0;
+      for (int k = 0; k < grp.second.n; ++k) {
+        const LmDet& D = K.det[grp.second.ids[k]];
+        need = std::max(need, (size_t)(LM_TH + D.kh - 1) * pk_stride(LM_TW + grp.first - 1) * sizeof(float));
+      }
+    }
+    c->corr_group_lds.push_back(need);
+  }
 
   // weights (float, rows zero-padded to kwp) and TM imadjust LUT
   std::vector<float> wts((size_t)w_off, 0.f);
@@ -521,7 +540,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   cap[AR_PWJC] = ns * LM_NFEAT * (64 + g.ong_nx * g.ong_ny + 1);
   cap[AR_PWNZ] = ns * LM_NFEAT * 1024;
   for (int a = 0; a < 2; ++a) c->arena[a].alloc(cap, ns);
-  for (const auto& grp : c->corr_groups) HIPCHK(corr_set_lds(c->corr_variant, grp.first, c->corr_lds));
+  for (size_t g = 0; g < c->corr_groups.size(); ++g)
+    HIPCHK(corr_set_lds(c->corr_variant, c->corr_groups[g].first, c->corr_group_lds[g]));
   HIPCHK(hipFuncSetAttribute((const void*)k_corr_dbg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->corr_lds));
 }
 
@@ -772,9 +792,10 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
         K, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
     T.end();
     T.begin("k_corr");
-    for (const auto& grp : c->corr_groups) {
+    for (size_t gi = 0; gi < c->corr_groups.size(); ++gi) {
+      const auto& grp = c->corr_groups[gi];
       const LmDetGroup& G = grp.second;
-      HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_lds, st, K, G,
+      HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_lds[gi], st, K, G,
                          c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->keys.p, c->npos.p, c->tailbin.p,
                          c->tailbin_slot_bytes));
     }

@@ -169,3 +169,57 @@ def test_nms_large_lists_global_path():
     assert dups > 1000
     frames = c.frames(0, 4)
     assert_same(_ctx(c).detect(frames, 0), _oracle(c, frames).result, "large: ")
+
+
+def test_c5_highres_geometry_bit_exact():
+    """Config C5: 1920x512 frames, geometry and detectors x2 (widths 44-60:
+    the wide width-specialised correlation kernels)."""
+    c5 = S.SyntheticConfig(rows=512, cols=1920)
+    frames = c5.frames(0, 4)
+    ctx = _ctx(c5, max_batch=4)
+    ctx.set_debug(1)
+    got = ctx.detect(frames, 0)
+    from oracle import oracle as O
+    ref = _oracle(c5, frames, flags=O.KEEP_DEBUG)
+    assert_same(got, ref.result, "C5: ")
+    for det in range(6):
+        s = ctx.debug_scores(3, det)
+        assert np.array_equal(s.view(np.uint32), ref.scores(3, det, s.shape).view(np.uint32)), det
+    ctx.close()
+
+
+def test_c5_carry_and_halo():
+    c5 = S.SyntheticConfig(rows=512, cols=1920)
+    frames = c5.frames(37, 7)
+    ref = _oracle(c5, frames).result
+    ctx = _ctx(c5, max_batch=4)
+    a = ctx.detect(frames[:3], 0)
+    b = ctx.detect(frames[3:], 3)
+    assert_same(concat_results([a, b]), ref, "C5 carry: ")
+    ctx.close()
+
+
+def test_long_stream_device_frames():
+    """1024 consecutive frames (a shard start at frame 5000, halo frame 4999)
+    in batches of 256 from device memory, against the oracle run on the same
+    frames: the C3 path at bench batch size."""
+    torch = pytest.importorskip("torch")
+    from locomouse_cpp_amd.abi import result_to_numpy
+    from locomouse_cpp_amd.results import slice_results
+    from locomouse_cpp_amd.runtime import synth_frames_device
+    from oracle import oracle as O
+    cfg = S.SyntheticConfig()
+    n, B, f0 = 1024, 256, 5000
+    d = torch.empty((n + 1, 256, 1024), dtype=torch.uint8, device="cuda")
+    synth_frames_device(d.data_ptr(), 256, 1024, f0 - 1, n + 1, 262144)
+    torch.cuda.synchronize()
+    host = d.cpu().numpy()
+    ctx = _ctx(cfg, max_batch=B)
+    parts = []
+    for b in range(0, n, B):
+        r = ctx.detect_device(d.data_ptr() + (1 + b) * 262144, 262144, B, f0 + b,
+                              d_prev_ptr=d.data_ptr() if b == 0 else None)
+        parts.append(result_to_numpy(r))
+    ctx.close()
+    ref = slice_results(O.OracleRun(cfg, host).result, 1)
+    assert_same(concat_results(parts), ref, "long: ")
