@@ -1,0 +1,324 @@
+// LocoMouse.cpp — host C++ mirror of the reference's per-frame LocoMouse
+// surface over the MI355X C-ABI.  See LocoMouse.hpp for the contract; every
+// method cites the reference code whose observable behaviour it keeps.
+#include "LocoMouse.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <iostream>
+#include <stdexcept>
+
+namespace locomouse {
+
+// ------------------------------------------------------------- Candidates
+
+bool compareCandidate(Candidate a, Candidate b) { return a.score() > b.score(); }  // Candidates.cpp:33-36
+
+P22D::P22D() : CB(), yt{-1}, st{-1} {}
+P22D::P22D(int xc, int ybc, int ytc, double scr_b, double scr_t) : CB(xc, ybc, scr_b), yt{ytc}, st{scr_t} {}
+P22D::P22D(Point_<int> Pb, Point_<int> Pt, double scr_b, double scr_t) : CB(Pb, scr_b), yt{Pt.y}, st{scr_t} {}
+P22D::P22D(Candidate Cb, Candidate Ct) : CB(Cb.point(), Cb.score()), yt{Ct.point().y}, st{Ct.score()} {}
+
+Point_<int> P22D::point_bottom() const { return CB.point(); }
+Point_<int> P22D::point_side(unsigned index) const { return Point_<int>(CB.point().x, yt.at(index)); }
+double P22D::score_bottom() const { return CB.score(); }
+double P22D::score_side(unsigned index) const { return st.at(index); }
+int P22D::x_coord() const { return CB.point().x; }
+int P22D::y_bottom_coord() const { return CB.point().y; }
+int P22D::y_side_coord(unsigned index) const { return yt.at(index); }
+
+void P22D::add_side_candidate(Candidate C) { add_side_candidate_safe(C.point().x, C.point().y, C.score()); }
+void P22D::add_side_candidate(Point_<int> P, double s) { add_side_candidate_safe(P.x, P.y, s); }
+void P22D::add_side_candidate(int y, double s) { add_side_candidate_safe(CB.point().x, y, s); }
+
+// Candidates.cpp:106-115: an empty P22D takes the first side candidate in
+// slot 0; later ones are appended and must have S >= 0 (CV_Assert).
+void P22D::add_side_candidate_safe(int, int Y, double S) {
+  if (number_of_candidates() == 0) {
+    yt[0] = Y;
+    st[0] = S;
+    return;
+  }
+  if (!(S >= 0)) throw std::runtime_error("P22D::add_side_candidate_safe: CV_Assert(S >= 0) failed.");
+  yt.push_back(Y);
+  st.push_back(S);
+}
+
+int P22D::number_of_candidates() const { return st[0] < 0 ? 0 : (int)st.size(); }  // Candidates.cpp:148-156
+Candidate P22D::get_candidate_side(unsigned index) const { return Candidate(CB.point().x, yt.at(index), st.at(index)); }
+Candidate P22D::get_candidate_bottom() const { return CB; }
+
+void P22D::set_side_raw(const int* y, const double* s, int count) {
+  if (count < 1) throw std::invalid_argument("P22D::set_side_raw: a P22D holds at least one side entry.");
+  yt.assign(y, y + count);
+  st.assign(s, s + count);
+}
+
+bool P22D::operator==(const P22D& o) const {
+  return CB.p == o.CB.p && CB.s == o.CB.s && yt == o.yt && st == o.st;
+}
+
+std::ostream& operator<<(std::ostream& out, const Candidate& c) {
+  return out << "[(" << c.point().x << ", " << c.point().y << ") with score = " << c.s << "]";
+}
+
+std::ostream& operator<<(std::ostream& out, const P22D& c) {
+  out << "Bottom candidate: " << c.get_candidate_bottom() << "\n" << c.number_of_candidates() << " top candidate(s):\n";
+  for (int i = 0; i < c.number_of_candidates(); ++i)
+    out << "[" << c.y_side_coord(i) << " with score = " << c.score_side(i) << "]\n";
+  return out;
+}
+
+// ------------------------------------------------------------------ MyMat
+
+void MyMat::put(unsigned i, unsigned j, double val) {
+  if ((int)i >= nrows || (int)j >= ncols) throw std::out_of_range("MyMat::put index out of range");
+  values[(size_t)j * nrows + i] = val;  // column-major (MyMat.cpp:64-70)
+}
+
+double MyMat::get(unsigned i, unsigned j) const {
+  if ((int)i >= nrows || (int)j >= ncols) throw std::out_of_range("MyMat::get index out of range");
+  return values[(size_t)j * nrows + i];
+}
+
+MATSPARSE::MATSPARSE(const MyMat* M) : n_rows(M->Nrows()), n_cols(M->Ncols()) {
+  Jc.reserve((size_t)n_cols + 1);
+  Jc.push_back(0);
+  for (int j = 0; j < n_cols; ++j) {  // MyMat.cpp:141-178
+    for (int i = 0; i < n_rows; ++i) {
+      const double v = M->get(i, j);
+      if (v != 0) {
+        Ir.push_back(i);
+        Pr.push_back(v);
+      }
+    }
+    Jc.push_back((int)Ir.size());
+  }
+  nzel = (int)Ir.size();
+}
+
+MATSPARSE::MATSPARSE(int rows, int cols, const int* jc, const int* ir, const double* pr)
+    : Jc(jc, jc + cols + 1), nzel(jc[cols]), n_rows(rows), n_cols(cols) {
+  Ir.assign(ir, ir + nzel);
+  Pr.assign(pr, pr + nzel);
+}
+
+double MATSPARSE::get(int, int) const { return 0; }  // MyMat.cpp:371-374 returns before its lookup
+
+double MATSPARSE::at(int irow, int icol) const {
+  if (icol < 0 || icol >= n_cols || irow < 0 || irow >= n_rows) throw std::out_of_range("MATSPARSE::at");
+  double val = 0;
+  for (int k = Jc[icol]; k < Jc[icol + 1]; ++k)
+    if (Ir[k] == irow) val = Pr[k];
+  return val;
+}
+
+bool MATSPARSE::operator==(const MATSPARSE& o) const {
+  return n_rows == o.n_rows && n_cols == o.n_cols && Jc == o.Jc && Ir == o.Ir && Pr == o.Pr;
+}
+
+std::ostream& operator<<(std::ostream& out, const MyMat& M) {
+  if (M.Nrows() == 0 || M.Ncols() == 0) return out << "Matrix is empty!\n";
+  out << "[";
+  for (int i = 0; i < M.Nrows(); ++i) {
+    for (int j = 0; j < M.Ncols(); ++j) out << M.get(i, j) << (j + 1 < M.Ncols() ? ", " : "");
+    out << (i + 1 < M.Nrows() ? ";\n" : "]\n");
+  }
+  return out;
+}
+
+// -------------------------------------------------------------- LocoMouse
+
+void throw_on_error(lm_status s) {
+  if (s == LM_OK) return;
+  if (s == LM_ERR_INVALID_ARGUMENT) throw std::invalid_argument(lm_last_error());
+  throw std::runtime_error(lm_last_error());
+}
+
+LocoMouse::LocoMouse(const LocoMouse_Inputs& inputs) : IN(inputs), METHOD(0), N_FRAMES(inputs.n_frames) {
+  if (!IN.read_frame) throw std::invalid_argument("LocoMouse: no frame reader (V) given.");
+  if (IN.batch < 1) throw std::invalid_argument("LocoMouse: batch must be >= 1.");
+  if (IN.setup.video_rows <= 0 || IN.setup.video_cols <= 0)
+    throw std::invalid_argument("LocoMouse: video size must be positive.");
+  FRAME_BYTES = (size_t)IN.setup.video_rows * IN.setup.video_cols;
+  IN.setup.method = 0;
+}
+
+LocoMouse::~LocoMouse() {
+  if (CTX) lm_ctx_destroy(CTX);
+}
+
+// :543-569: with use_provided_bounding_box the bottom-right corners are the
+// provided boxes' for every frame; otherwise the whole-video pass runs.
+void LocoMouse::getBoundingBox() {
+  if (IN.params.use_provided_bounding_box) {
+    const lm_rect& b = IN.params.bounding_box_bottom;
+    const lm_rect& s = IN.params.bounding_box_side;
+    BB_X_POS.assign(N_FRAMES, (uint32_t)(b.x + b.width));
+    BB_Y_SIDE_POS.assign(N_FRAMES, (uint32_t)(s.y + s.height));
+    BB_Y_BOTTOM_POS.assign(N_FRAMES, (uint32_t)(b.y + b.height));
+    HAVE_BB = true;
+  } else {
+    computeBoundingBox();
+  }
+}
+
+void LocoMouse::computeBoundingBox() {
+  throw std::runtime_error(
+      "computeBoundingBox: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) is not on this path; "
+      "set use_provided_bounding_box = 1.");
+}
+
+// :655-769 derives the geometry; here the device context does (lm_ctx_create
+// validates the same inputs and raises the reference's errors).
+void LocoMouse::initializeFeatureLoop() {
+  if (!HAVE_BB) throw std::runtime_error("initializeFeatureLoop: getBoundingBox() has not been called.");
+  if (CTX) return;
+  IN.setup.method = METHOD;
+  throw_on_error(lm_ctx_create(IN.device, &IN.setup, &IN.params, &IN.model, IN.batch, &CTX));
+  PENDING.assign(FRAME_BYTES * (size_t)IN.batch, 0);
+  N_PENDING = 0;
+}
+
+// :1273-1333 reads the next frame (V >> F, channel 0).  The frame is queued;
+// background subtraction, normalisation, calibration and (TM) imadjust run on
+// the device when its batch is processed.
+void LocoMouse::readFrame() {
+  if (!CTX) throw std::runtime_error("readFrame: initializeFeatureLoop() has not been called.");
+  if (N_PENDING == IN.batch) flush();  // a caller that skips storePreviousImage
+  if ((unsigned)(CURRENT_FRAME + 1) >= N_FRAMES || !IN.read_frame(PENDING.data() + (size_t)N_PENDING * FRAME_BYTES))
+    throw std::runtime_error("Error: Failed to read image from video file.\n");  // :1284-1286
+  ++N_PENDING;
+  ++CURRENT_FRAME;
+}
+
+// The eight per-frame stages of main.cpp:60-80 run inside lm_detect_batch.
+void LocoMouse::cropBoundingBox() {}
+void LocoMouse::detectTail() {}
+void LocoMouse::detectBottomCandidates() {}
+void LocoMouse::computeUnaryCostsBottom() {}
+void LocoMouse::computePairwiseCostsBottom() {}
+void LocoMouse::detectSideCandidates() {}
+void LocoMouse::matchBottomSideCandidates() {}
+
+// :1508-1513 keeps I_PAD for the next frame; the device keeps the previous
+// frame across batches, so this is where a full batch (or the video's last
+// frame) is handed over.
+void LocoMouse::storePreviousImage() {
+  if (N_PENDING && (N_PENDING == IN.batch || (unsigned)(CURRENT_FRAME + 1) == N_FRAMES)) flush();
+}
+
+void LocoMouse::sync() {
+  if (N_PENDING) flush();
+}
+
+lm_geometry LocoMouse::geometry() const {
+  lm_geometry g{};
+  if (!CTX) throw std::runtime_error("geometry: initializeFeatureLoop() has not been called.");
+  throw_on_error(lm_get_geometry(CTX, &g));
+  return g;
+}
+
+void LocoMouse::flush() {
+  const int n = N_PENDING, first = CURRENT_FRAME + 1 - n;
+  std::vector<int32_t> bb((size_t)3 * n);
+  for (int i = 0; i < n; ++i) {
+    bb[3 * i] = (int32_t)BB_X_POS[first + i];
+    bb[3 * i + 1] = (int32_t)BB_Y_BOTTOM_POS[first + i];
+    bb[3 * i + 2] = (int32_t)BB_Y_SIDE_POS[first + i];
+  }
+  lm_batch_result r{};
+  throw_on_error(lm_detect_batch(CTX, PENDING.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data(), &r));
+  N_PENDING = 0;
+  append(r);
+}
+
+void LocoMouse::append(const lm_batch_result& r) {
+  auto list = [&](int f, int k) {
+    const lm_candidate* b = r.cand + r.cand_offset[4 * f + k];
+    const lm_candidate* e = r.cand + r.cand_offset[4 * f + k + 1];
+    return std::vector<Candidate>(reinterpret_cast<const Candidate*>(b), reinterpret_cast<const Candidate*>(e));
+  };
+  for (int f = 0; f < r.n_frames; ++f) {
+    CANDIDATES_BOTTOM_PAW.push_back(list(f, 0));
+    CANDIDATES_BOTTOM_SNOUT.push_back(list(f, 1));
+    CANDIDATES_SIDE_PAW.push_back(list(f, 2));
+    CANDIDATES_SIDE_SNOUT.push_back(list(f, 3));
+    for (int k = 0; k < LM_N_FEATURES; ++k) {
+      const int q = 2 * f + k;
+      std::vector<P22D> pv;
+      for (int64_t i = r.p22d_offset[q]; i < r.p22d_offset[q + 1]; ++i) {
+        const lm_p22d& p = r.p22d[i];
+        P22D v(Candidate(p.bottom.x, p.bottom.y, p.bottom.score), Candidate());
+        v.set_side_raw(r.side_y + p.side_offset, r.side_s + p.side_offset, p.side_count);
+        pv.push_back(std::move(v));
+      }
+      (k ? CANDIDATES_MATCHED_VIEWS_SNOUT : CANDIDATES_MATCHED_VIEWS_PAW).push_back(std::move(pv));
+      const int ncol = k ? 1 : LM_N_PAWS;  // N_cand x 4 (paw) / x 1 (snout), column-major
+      const int64_t u0 = r.unary_offset[q], nu = r.unary_offset[q + 1] - u0;
+      MyMat U((unsigned)(nu / ncol), (unsigned)ncol);
+      std::copy(r.unary + u0, r.unary + u0 + nu, U.getValues());
+      (k ? UNARY_BOTTOM_SNOUT : UNARY_BOTTOM_PAW).push_back(std::move(U));
+      const int32_t* d = r.pw_dims + 3 * q;
+      if (d[0] >= 0)  // frames > 0 only (:896-919)
+        (k ? PAIRWISE_BOTTOM_SNOUT : PAIRWISE_BOTTOM_PAW)
+            .emplace_back(d[0], d[1], r.pw_jc + r.pw_jc_offset[q], r.pw_ir + r.pw_nz_offset[q],
+                          r.pw_pr + r.pw_nz_offset[q]);
+    }
+    TailTrack t;
+    std::copy(r.tail + 45 * f, r.tail + 45 * (f + 1), t.begin());
+    TRACKS_TAIL.push_back(t);
+  }
+}
+
+#define LM_ACCESSOR(fn, member) \
+  const decltype(LocoMouse::member)& LocoMouse::fn() { \
+    sync();                                       \
+    return member;                                \
+  }
+LM_ACCESSOR(candidates_bottom_paw, CANDIDATES_BOTTOM_PAW)
+LM_ACCESSOR(candidates_bottom_snout, CANDIDATES_BOTTOM_SNOUT)
+LM_ACCESSOR(candidates_side_paw, CANDIDATES_SIDE_PAW)
+LM_ACCESSOR(candidates_side_snout, CANDIDATES_SIDE_SNOUT)
+LM_ACCESSOR(candidates_matched_views_paw, CANDIDATES_MATCHED_VIEWS_PAW)
+LM_ACCESSOR(candidates_matched_views_snout, CANDIDATES_MATCHED_VIEWS_SNOUT)
+LM_ACCESSOR(unary_bottom_paw, UNARY_BOTTOM_PAW)
+LM_ACCESSOR(unary_bottom_snout, UNARY_BOTTOM_SNOUT)
+LM_ACCESSOR(pairwise_bottom_paw, PAIRWISE_BOTTOM_PAW)
+LM_ACCESSOR(pairwise_bottom_snout, PAIRWISE_BOTTOM_SNOUT)
+LM_ACCESSOR(tracks_tail, TRACKS_TAIL)
+#undef LM_ACCESSOR
+
+// ------------------------------------------------------------ TM, TM_DE
+
+LocoMouse_TM::LocoMouse_TM(const LocoMouse_Inputs& inputs) : LocoMouse(inputs) { METHOD = 1; }
+void LocoMouse_TM::readFrame() { LocoMouse::readFrame(); }  // + imadjust (TM.cpp:243-249), on the device
+void LocoMouse_TM::computeBoundingBox() {
+  throw std::runtime_error(
+      "LocoMouse_TM::computeBoundingBox: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) is not on this "
+      "path; set use_provided_bounding_box = 1.");
+}
+
+LocoMouse_TM_DE::LocoMouse_TM_DE(const LocoMouse_Inputs& inputs) : LocoMouse(inputs) { METHOD = 2; }
+void LocoMouse_TM_DE::readFrame() { LocoMouse::readFrame(); }
+void LocoMouse_TM_DE::computeBoundingBox() {
+  throw std::runtime_error(
+      "LocoMouse_TM_DE::computeBoundingBox: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) is not on this "
+      "path; set use_provided_bounding_box = 1.");
+}
+
+std::unique_ptr<LocoMouse> LocoMouse_Initialize(const LocoMouse_Inputs& inputs) {
+  switch (inputs.setup.method) {
+    case 0:
+      return std::unique_ptr<LocoMouse>(new LocoMouse(inputs));
+    case 1:
+      return std::unique_ptr<LocoMouse>(new LocoMouse_TM(inputs));
+    case 2:
+      return std::unique_ptr<LocoMouse>(new LocoMouse_TM_DE(inputs));
+    default:
+      std::cout << "Unknown method option. Attempting to track with the default method." << std::endl;
+      return std::unique_ptr<LocoMouse>(new LocoMouse(inputs));
+  }
+}
+
+}  // namespace locomouse

@@ -1,0 +1,157 @@
+// LocoMouse.hpp — host C++ mirror of the reference's LocoMouse class surface
+// for the per-frame detection path, running on the MI355X C-ABI
+// (include/locomouse_hip.h).
+//
+// Reference surface kept (LocoMouse_Core/LocoMouse_class.hpp:169-350,
+// main.cpp:45-82): the factory LocoMouse_Initialize (LocoMouse_Methods.cpp:3-26)
+// choosing LocoMouse / LocoMouse_TM / LocoMouse_TM_DE by method, the virtual
+// readFrame / getBoundingBox / computeBoundingBox, and the per-frame methods
+// called in main.cpp's order:
+//
+//   L->getBoundingBox(); L->initializeFeatureLoop();
+//   for (i < L->N_frames()) { readFrame; cropBoundingBox; detectTail;
+//     detectBottomCandidates; computeUnaryCostsBottom; computePairwiseCostsBottom;
+//     detectSideCandidates; matchBottomSideCandidates; storePreviousImage; }
+//
+// The per-frame methods are thin shims: readFrame copies the raw frame into a
+// batch buffer and storePreviousImage hands full batches (or the video's last
+// frames) to lm_detect_batch; the results are appended in frame order to the
+// same containers the reference fills (LocoMouse_class.hpp:219-236), exposed
+// here through accessors that first flush any pending frames.  Errors are the
+// reference's: std::invalid_argument / std::runtime_error (main.cpp:94-101).
+//
+// Inputs are already-decoded data (lm_setup / lm_params / lm_model plus a
+// frame reader): the YAML/AVI/PNG readers behind LocoMouse_ParseInputs are the
+// on-disk formats of SURVEY.md §8(f) row 2, outside this path.
+#ifndef LOCOMOUSE_HOST_LOCOMOUSE_HPP
+#define LOCOMOUSE_HOST_LOCOMOUSE_HPP
+
+#include <array>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "Candidates.hpp"
+#include "MyMat.hpp"
+#include "locomouse_hip.h"
+
+namespace locomouse {
+
+// What LocoMouse_ParseInputs + the file loaders provide (ParseInputs.cpp:62-99,
+// LocoMouse_class.cpp:307-540, :3095-3162), already in memory.  The pointers
+// inside setup/params/model must stay valid until initializeFeatureLoop().
+struct LocoMouse_Inputs {
+  lm_setup setup{};    // setup.method: 0 LocoMouse, 1 LocoMouse_TM, 2 LocoMouse_TM_DE
+  lm_params params{};
+  lm_model model{};
+  uint32_t n_frames = 0;  // N_FRAMES (CV_CAP_PROP_FRAME_COUNT)
+  // V >> F; extractChannel(F, F, 0): writes the next frame (video_rows x
+  // video_cols u8, row-major) and returns false at the end of the video.
+  std::function<bool(uint8_t* dst)> read_frame;
+  int device = 0;      // HIP device of this instance (one per GPU / host thread)
+  int batch = 256;     // frames per lm_detect_batch call
+};
+
+using TailTrack = std::array<int32_t, 3 * LM_N_TAIL_POINTS>;  // TRACKS_TAIL entry: 3x15, row-major, -1 = missing
+
+class LocoMouse {
+ public:
+  explicit LocoMouse(const LocoMouse_Inputs& inputs);
+  virtual ~LocoMouse();
+  LocoMouse(const LocoMouse&) = delete;
+  LocoMouse& operator=(const LocoMouse&) = delete;
+
+  virtual void readFrame();           // LocoMouse_class.cpp:1273-1333
+  virtual void getBoundingBox();      // :543-653 (provided box: constant BR corners)
+  virtual void computeBoundingBox();  // :575-653 — whole-video pass, §8(f) row 1
+  void initializeFeatureLoop();       // :655-769 (creates the device context)
+  void cropBoundingBox();             // :1408-1478
+  void detectTail();                  // :2541-2555
+  void detectBottomCandidates();      // :771-807
+  void computeUnaryCostsBottom();     // :873-894
+  void computePairwiseCostsBottom();  // :896-919
+  void detectSideCandidates();        // :809-838
+  void matchBottomSideCandidates();   // :999-1021
+  void storePreviousImage();          // :1508-1513
+  unsigned int N_frames() const { return N_FRAMES; }
+
+  // The reference's protected result vectors (LocoMouse_class.hpp:219-236),
+  // one entry per processed frame, in frame order.
+  const std::vector<std::vector<Candidate>>& candidates_bottom_paw();
+  const std::vector<std::vector<Candidate>>& candidates_bottom_snout();
+  const std::vector<std::vector<Candidate>>& candidates_side_paw();
+  const std::vector<std::vector<Candidate>>& candidates_side_snout();
+  const std::vector<std::vector<P22D>>& candidates_matched_views_paw();
+  const std::vector<std::vector<P22D>>& candidates_matched_views_snout();
+  const std::vector<MyMat>& unary_bottom_paw();
+  const std::vector<MyMat>& unary_bottom_snout();
+  const std::vector<MATSPARSE>& pairwise_bottom_paw();  // frames >= 1 only (:896-919)
+  const std::vector<MATSPARSE>& pairwise_bottom_snout();
+  const std::vector<TailTrack>& tracks_tail();
+  int current_frame() const { return CURRENT_FRAME; }
+  lm_geometry geometry() const;
+
+  // Processes the frames read so far (called by every accessor above).
+  void sync();
+
+ protected:
+  LocoMouse_Inputs IN;
+  int METHOD = 0;
+  unsigned int N_FRAMES = 0;
+  int CURRENT_FRAME = -1;
+  std::vector<uint32_t> BB_X_POS, BB_Y_SIDE_POS, BB_Y_BOTTOM_POS;  // per-frame BR corners (:547-557)
+  bool HAVE_BB = false;
+
+  std::vector<std::vector<Candidate>> CANDIDATES_BOTTOM_PAW, CANDIDATES_BOTTOM_SNOUT;
+  std::vector<std::vector<Candidate>> CANDIDATES_SIDE_PAW, CANDIDATES_SIDE_SNOUT;
+  std::vector<std::vector<P22D>> CANDIDATES_MATCHED_VIEWS_PAW, CANDIDATES_MATCHED_VIEWS_SNOUT;
+  std::vector<MyMat> UNARY_BOTTOM_PAW, UNARY_BOTTOM_SNOUT;
+  std::vector<MATSPARSE> PAIRWISE_BOTTOM_PAW, PAIRWISE_BOTTOM_SNOUT;
+  std::vector<TailTrack> TRACKS_TAIL;
+
+ private:
+  lm_ctx* CTX = nullptr;
+  std::vector<uint8_t> PENDING;  // raw frames read but not yet processed
+  int N_PENDING = 0;
+  size_t FRAME_BYTES = 0;
+  void flush();
+  void append(const lm_batch_result& r);
+};
+
+// LocoMouse_TM (LocoMouse_TM.hpp:30-55): readFrame adds imadjust
+// (TM.cpp:243-249), applied on the device for method 1.
+class LocoMouse_TM : public LocoMouse {
+ public:
+  explicit LocoMouse_TM(const LocoMouse_Inputs& inputs);
+  void readFrame() override;
+  void computeBoundingBox() override;  // TM.cpp:115-241 — §8(f) row 1
+};
+
+// LocoMouse_TM_DE (LocoMouse_TM_DE.hpp:30-45): the same readFrame as TM.
+class LocoMouse_TM_DE : public LocoMouse {
+ public:
+  explicit LocoMouse_TM_DE(const LocoMouse_Inputs& inputs);
+  void readFrame() override;
+  void computeBoundingBox() override;  // TM_DE.cpp:8-113 — §8(f) row 1
+};
+
+// LocoMouse_Methods.cpp:3-26: 0 LocoMouse, 1 LocoMouse_TM, 2 LocoMouse_TM_DE,
+// anything else prints a notice and uses LocoMouse.
+std::unique_ptr<LocoMouse> LocoMouse_Initialize(const LocoMouse_Inputs& inputs);
+
+// lm_status -> the reference's exception types (main.cpp:94-101).
+void throw_on_error(lm_status s);
+
+}  // namespace locomouse
+
+#ifndef LOCOMOUSE_NO_GLOBAL_NAMES
+using locomouse::LocoMouse;
+using locomouse::LocoMouse_Initialize;
+using locomouse::LocoMouse_Inputs;
+using locomouse::LocoMouse_TM;
+using locomouse::LocoMouse_TM_DE;
+#endif
+
+#endif

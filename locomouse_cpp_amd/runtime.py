@@ -27,15 +27,32 @@ HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-fvisibility=hidden", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 
 
+HOST_DIR = os.path.join(PKG, "host")
+HOST_LIB_PATH = os.path.join(PKG, "liblocomouse_host.so")
+
+
 def build(verbose=False):
     """Compile liblocomouse_hip.so for gfx950 in-tree (hipcc cross-compiles
-    without a GPU)."""
+    without a GPU), then the host C++ LocoMouse mirror above it."""
     cmd = ["hipcc", *HIPCC_FLAGS, "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-o", LIB_PATH,
            os.path.join(CSRC, "lm_runtime.hip")]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
+    build_host(verbose)
     return LIB_PATH
+
+
+def build_host(verbose=False):
+    """liblocomouse_host.so: the LocoMouse / Candidate / P22D / MyMat C++
+    surface (locomouse_cpp_amd/host) linked against the C-ABI library."""
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-I" + os.path.join(ROOT, "include"),
+           "-I" + HOST_DIR, "-o", HOST_LIB_PATH, os.path.join(HOST_DIR, "LocoMouse.cpp"), "-L" + PKG,
+           "-llocomouse_hip", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return HOST_LIB_PATH
 
 
 _lib = None

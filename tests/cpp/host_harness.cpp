@@ -1,0 +1,177 @@
+// host_harness.cpp — test harness for the host C++ LocoMouse mirror
+// (locomouse_cpp_amd/host).  lmh_run() drives a LocoMouse exactly as the
+// reference's main.cpp:45-82 does (factory, getBoundingBox,
+// initializeFeatureLoop, the nine per-frame calls per frame) over frames held
+// in memory, then flattens the result containers into an lm_batch_result so
+// the Python tests compare them with the oracle field by field.
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "LocoMouse.hpp"
+
+namespace {
+
+struct Flat {
+  std::vector<int64_t> cand_off, p22d_off, unary_off, jc_off, nz_off;
+  std::vector<lm_candidate> cand;
+  std::vector<lm_p22d> p22d;
+  std::vector<int32_t> side_y, pw_dims, pw_jc, pw_ir, tail;
+  std::vector<double> side_s, unary, pw_pr;
+} g_flat;
+
+int fail(const std::exception& e, int code, char* err, int errlen) {
+  if (err && errlen > 0) {
+    std::strncpy(err, e.what(), (size_t)errlen - 1);
+    err[errlen - 1] = 0;
+  }
+  return code;
+}
+
+}  // namespace
+
+extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_model* model, const uint8_t* frames,
+                       int n_frames, int n_read, int batch, int device, int call_order, lm_batch_result* out, char* err,
+                       int errlen) {
+  try {
+    locomouse::LocoMouse_Inputs in;
+    in.setup = *setup;
+    in.params = *params;
+    in.model = *model;
+    in.n_frames = (uint32_t)n_frames;
+    in.device = device;
+    in.batch = batch;
+    const size_t fb = (size_t)setup->video_rows * setup->video_cols;
+    int next = 0;
+    in.read_frame = [&](uint8_t* dst) {  // V >> F over the frames given
+      if (next >= n_read) return false;
+      std::memcpy(dst, frames + (size_t)next++ * fb, fb);
+      return true;
+    };
+    std::unique_ptr<LocoMouse> L = LocoMouse_Initialize(in);
+    L->getBoundingBox();
+    L->initializeFeatureLoop();
+    for (unsigned i = 0; i < L->N_frames(); ++i) {  // main.cpp:54-82
+      L->readFrame();
+      L->cropBoundingBox();
+      L->detectTail();
+      L->detectBottomCandidates();
+      L->computeUnaryCostsBottom();
+      L->computePairwiseCostsBottom();
+      L->detectSideCandidates();
+      L->matchBottomSideCandidates();
+      if (call_order == 1 && i % 3 == 1) (void)L->candidates_bottom_paw();  // mid-batch reads flush early
+      L->storePreviousImage();
+    }
+    Flat& F = g_flat;
+    F = Flat();
+    const auto& cbp = L->candidates_bottom_paw();
+    const auto& cbs = L->candidates_bottom_snout();
+    const auto& csp = L->candidates_side_paw();
+    const auto& css = L->candidates_side_snout();
+    const auto& mp = L->candidates_matched_views_paw();
+    const auto& ms = L->candidates_matched_views_snout();
+    const auto& up = L->unary_bottom_paw();
+    const auto& us = L->unary_bottom_snout();
+    const auto& pp = L->pairwise_bottom_paw();
+    const auto& ps = L->pairwise_bottom_snout();
+    const auto& tt = L->tracks_tail();
+    const int n = (int)cbp.size();
+    F.cand_off.push_back(0);
+    F.p22d_off.push_back(0);
+    F.unary_off.push_back(0);
+    F.jc_off.push_back(0);
+    F.nz_off.push_back(0);
+    for (int f = 0; f < n; ++f) {
+      for (const auto* lst : {&cbp[f], &cbs[f], &csp[f], &css[f]}) {
+        for (const Candidate& c : *lst) F.cand.push_back(lm_candidate{c.p.x, c.p.y, c.s});
+        F.cand_off.push_back((int64_t)F.cand.size());
+      }
+      for (int k = 0; k < 2; ++k) {
+        for (const P22D& p : (k ? ms : mp)[f]) {
+          lm_p22d q;
+          q.bottom = lm_candidate{p.x_coord(), p.y_bottom_coord(), p.score_bottom()};
+          q.side_offset = (int32_t)F.side_y.size();
+          q.side_count = (int32_t)p.raw_side_y().size();
+          F.side_y.insert(F.side_y.end(), p.raw_side_y().begin(), p.raw_side_y().end());
+          F.side_s.insert(F.side_s.end(), p.raw_side_s().begin(), p.raw_side_s().end());
+          F.p22d.push_back(q);
+        }
+        F.p22d_off.push_back((int64_t)F.p22d.size());
+        const MyMat& U = (k ? us : up)[f];
+        F.unary.insert(F.unary.end(), U.getValues(), U.getValues() + U.Numel());
+        F.unary_off.push_back((int64_t)F.unary.size());
+        // pairwise entries exist for frames >= 1 only
+        if (f >= 1) {
+          const MATSPARSE& P = (k ? ps : pp)[f - 1];
+          F.pw_dims.insert(F.pw_dims.end(), {P.Nrows(), P.Ncols(), P.nz()});
+          F.pw_jc.insert(F.pw_jc.end(), P.getJc(), P.getJc() + P.Ncols() + 1);
+          F.pw_ir.insert(F.pw_ir.end(), P.getIr(), P.getIr() + P.nz());
+          F.pw_pr.insert(F.pw_pr.end(), P.getPr(), P.getPr() + P.nz());
+        } else {
+          F.pw_dims.insert(F.pw_dims.end(), {-1, -1, 0});
+        }
+        F.jc_off.push_back((int64_t)F.pw_jc.size());
+        F.nz_off.push_back((int64_t)F.pw_ir.size());
+      }
+      F.tail.insert(F.tail.end(), tt[f].begin(), tt[f].end());
+    }
+    out->n_frames = n;
+    out->first_frame = 0;
+    out->cand_offset = F.cand_off.data();
+    out->cand = F.cand.data();
+    out->p22d_offset = F.p22d_off.data();
+    out->p22d = F.p22d.data();
+    out->side_y = F.side_y.data();
+    out->side_s = F.side_s.data();
+    out->unary_offset = F.unary_off.data();
+    out->unary = F.unary.data();
+    out->pw_dims = F.pw_dims.data();
+    out->pw_jc_offset = F.jc_off.data();
+    out->pw_jc = F.pw_jc.data();
+    out->pw_nz_offset = F.nz_off.data();
+    out->pw_ir = F.pw_ir.data();
+    out->pw_pr = F.pw_pr.data();
+    out->tail = F.tail.data();
+    return 0;
+  } catch (const std::invalid_argument& e) {
+    return fail(e, 1, err, errlen);
+  } catch (const std::runtime_error& e) {
+    return fail(e, 2, err, errlen);
+  } catch (const std::exception& e) {
+    return fail(e, 3, err, errlen);
+  }
+}
+
+// Container semantics that need no GPU (P22D slot-0 rule, MATSPARSE CSC).
+extern "C" int lmh_selftest(char* err, int errlen) {
+  try {
+    P22D p(Candidate(5, 7, 2.0), Candidate());
+    if (p.number_of_candidates() != 0) throw std::runtime_error("empty P22D must have 0 side candidates");
+    p.add_side_candidate(11, 0.5);  // fills slot 0
+    p.add_side_candidate(12, 0.25);
+    if (p.number_of_candidates() != 2 || p.y_side_coord(0) != 11 || p.score_side(1) != 0.25)
+      throw std::runtime_error("add_side_candidate order");
+    bool threw = false;
+    try {
+      p.add_side_candidate(13, -1.0);
+    } catch (const std::runtime_error&) {
+      threw = true;
+    }
+    if (!threw) throw std::runtime_error("CV_Assert(S >= 0) not enforced");
+    MyMat M(3, 2);
+    M.put(0, 0, 1.5);
+    M.put(2, 0, -2);
+    M.put(1, 1, 4);
+    MATSPARSE S(&M);
+    const int jc[] = {0, 2, 3}, ir[] = {0, 2, 1};
+    const double pr[] = {1.5, -2, 4};
+    if (!(S == MATSPARSE(3, 2, jc, ir, pr))) throw std::runtime_error("MATSPARSE CSC layout");
+    if (S.at(2, 0) != -2 || S.get(2, 0) != 0) throw std::runtime_error("MATSPARSE get/at");
+    if (!compareCandidate(Candidate(0, 0, 2), Candidate(0, 0, 1))) throw std::runtime_error("compareCandidate");
+    return 0;
+  } catch (const std::exception& e) {
+    return fail(e, 2, err, errlen);
+  }
+}

@@ -1,0 +1,70 @@
+"""ctypes access to tests/cpp/host_harness.cpp, which drives the host C++
+LocoMouse mirror (locomouse_cpp_amd/host) in main.cpp's call order."""
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG = os.path.join(ROOT, "locomouse_cpp_amd")
+SO = os.path.join(HERE, "cpp", "_build", "libhost_harness.so")
+
+
+def build(verbose=False):
+    os.makedirs(os.path.dirname(SO), exist_ok=True)
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I" + os.path.join(ROOT, "include"),
+           "-I" + os.path.join(PKG, "host"), "-o", SO, os.path.join(HERE, "cpp", "host_harness.cpp"), "-L" + PKG,
+           "-llocomouse_host", "-llocomouse_hip", "-Wl,-rpath,$ORIGIN/../../../locomouse_cpp_amd"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return SO
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        from locomouse_cpp_amd import runtime
+        runtime.lib()  # torch's HIP runtime first, then the C-ABI library
+        if not os.path.exists(SO):
+            raise RuntimeError(f"{SO} is missing: run tests/host_harness.build()")
+        L = C.CDLL(SO)
+        L.lmh_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                              C.c_int, C.c_void_p, C.c_char_p, C.c_int]
+        L.lmh_run.restype = C.c_int
+        L.lmh_selftest.argtypes = [C.c_char_p, C.c_int]
+        L.lmh_selftest.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+class HostError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{'invalid_argument' if code == 1 else 'runtime_error'}: {msg}")
+        self.code = code
+
+
+def run_video(cfg, frames, batch=8, device=0, n_frames=None, call_order=0):
+    """LocoMouse_Initialize + main.cpp's loop over `frames`; returns the
+    result containers as a result dict (abi.result_to_numpy layout)."""
+    import numpy as np
+    from locomouse_cpp_amd.abi import lm_batch_result, result_to_numpy
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    out = lm_batch_result()
+    err = C.create_string_buffer(512)
+    n = frames.shape[0] if n_frames is None else n_frames
+    rc = lib().lmh_run(C.byref(cfg.setup), C.byref(cfg.params), C.byref(cfg.model), frames.ctypes.data, n,
+                       frames.shape[0], batch, device, call_order, C.byref(out), err, 512)
+    if rc:
+        raise HostError(rc, err.value.decode())
+    return result_to_numpy(out)
+
+
+def selftest():
+    err = C.create_string_buffer(512)
+    rc = lib().lmh_selftest(err, 512)
+    if rc:
+        raise HostError(rc, err.value.decode())
