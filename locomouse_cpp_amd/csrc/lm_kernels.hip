@@ -124,10 +124,11 @@ __global__ __launch_bounds__(1024) void k_minmax_lut(const uint8_t* const* __res
 // ---------------------------------------------------------------- k_ingest
 // Builds the extended padded crops of both views for each slot: every I_PAD
 // pixel any detector tap reads.  Each thread writes 4 consecutive bytes.
-__global__ __launch_bounds__(256) void k_ingest(const LmConst K, const uint8_t* const* __restrict__ frame_ptr,
+__global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
                                                 const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
                                                 const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
                                                 int s0, uint8_t* __restrict__ ext, int64_t ext_slot_bytes) {
+  const LmConst& K = *Kp;
   const int slot = s0 + blockIdx.y;
   __shared__ uint8_t lut[256];
   lut[threadIdx.x] = luts[slot * 256 + threadIdx.x];
@@ -220,10 +221,11 @@ struct LmDetGroup {
   int32_t tile_end[LM_NDET];  // cumulative tile counts
 };
 
-__global__ __launch_bounds__(256) void k_corr(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+__global__ __launch_bounds__(256) void k_corr(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
                                               int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
                                               unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                               uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
   extern __shared__ float lds[];
   __shared__ int s_cnt, s_base;
   const int slot = s0 + blockIdx.y;
@@ -296,10 +298,11 @@ __global__ __launch_bounds__(256) void k_corr(const LmConst K, const LmDetGroup 
 // 4 taps).  One launch covers the detectors of one width (ids in G).
 
 template <int KW>
-__global__ __launch_bounds__(256) void k_corr_kw(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+__global__ __launch_bounds__(256) void k_corr_kw(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
                                                  int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
                                                  unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                                  uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
   extern __shared__ float lds[];
   __shared__ int s_cnt, s_base;
   const int slot = s0 + blockIdx.y;
@@ -402,11 +405,51 @@ DEV void lds_pairs(lm_f2 (&px)[N], unsigned base) {
   lds_pairs_impl<STRIDE, N>(px, base, std::make_integer_sequence<int, N>{});
 }
 
+// Tile fill: u8 ext-crop window (rows x cols from src, row pitch ew) -> fp32
+// LDS (row stride `stride`).  16-byte aligned vector loads, all of a round
+// issued before any is consumed (a workgroup's fill is one or two load
+// latencies, not one per 4 bytes), then unpacked with v_cvt_f32_ubyte*.
+// ew and the ext-crop base are multiples of 16; src itself need not be.
+// Reads up to 15 bytes past a row's last column (inside the padded row or the
+// next; the ext buffer has slack after its last slot).
+DEV void tile_fill_f32(float* __restrict__ lds, int stride, const uint8_t* __restrict__ src, int ew, int rows,
+                       int cols) {
+  const int mis = (int)((uintptr_t)src & 15);
+  const uint8_t* __restrict__ a = src - mis;
+  const int nch = (mis + cols + 15) >> 4;
+  const int total = rows * nch;
+  for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+      if (e < total) {
+        const int r = e / nch, ch = e - r * nch;
+        v[u] = *reinterpret_cast<const uint4*>(a + (int64_t)r * ew + ch * 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+      if (e < total) {
+        const int r = e / nch, ch = e - r * nch;
+        const int c0 = ch * 16 - mis;
+        float* __restrict__ o = lds + r * stride + c0;
+        const unsigned w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (c0 + k >= 0 && c0 + k < cols) o[k] = (float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+      }
+    }
+  }
+}
+
 template <int KW, bool WLDS, bool ASMLD = false>
-__global__ __launch_bounds__(192) void k_corr_pk(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+__global__ __launch_bounds__(192) void k_corr_pk(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
                                                  int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
                                                  unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                                  uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
   // WLDS: detector weights staged in LDS (broadcast reads) instead of scalar
   // loads, so every lgkm wait is an in-order LDS wait the compiler can count.
   extern __shared__ float lds[];
@@ -429,15 +472,7 @@ __global__ __launch_bounds__(192) void k_corr_pk(const LmConst K, const LmDetGro
                                     (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
                                     (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
   const int ew = K.ext_w[D.view];
-  const int cols4 = (cols + 3) >> 2;
-  for (int e = threadIdx.x; e < rows * cols4; e += blockDim.x) {
-    const int r = e / cols4, c4 = (e - r * cols4) << 2;
-    const uint8_t* p = src + (int64_t)r * ew + c4;
-    float* o = lds + r * stride + c4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c4 + k < stride) o[k] = (float)p[k];
-  }
+  tile_fill_f32(lds, stride, src, ew, rows, cols);
   float* wl = lds + ((rows * stride + 3) & ~3);
   if (WLDS)
     for (int e = threadIdx.x; e < D.kh * D.kwp; e += blockDim.x) wl[e] = weights[D.w_off + e];
@@ -498,10 +533,11 @@ __global__ __launch_bounds__(192) void k_corr_pk(const LmConst K, const LmDetGro
 #define P2_C 10
 
 template <int KW>
-__global__ __launch_bounds__(192) void k_corr_p2(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+__global__ __launch_bounds__(192) void k_corr_p2(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
                                                  int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
                                                  unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                                  uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
   extern __shared__ float lds[];
   __shared__ int s_cnt, s_base;
   const int slot = s0 + blockIdx.y;
@@ -604,10 +640,11 @@ DEV void db_fma(lm_f2 (&acc)[P2_C], const lm_f2 (&px)[P2_C + KW - 1], const floa
 }
 
 template <int KW>
-__global__ __launch_bounds__(192, 2) void k_corr_db(const LmConst K, const LmDetGroup G, const uint8_t* __restrict__ ext,
+__global__ __launch_bounds__(192, 2) void k_corr_db(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
                                                     int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
                                                     unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                                     uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
   constexpr int NQ = P2_C + KW - 1;
   constexpr int STR = pk_stride_c(LM_TW + KW - 1);
   extern __shared__ float lds[];
@@ -689,6 +726,276 @@ __global__ __launch_bounds__(192, 2) void k_corr_db(const LmConst K, const LmDet
                          &s_cnt, &s_base);
 }
 
+// k_corr_sp: software-pipelined packed correlation.  Thread shape of k_corr_p2
+// (one row pair x 10 columns; 192 threads = 8 x 24 cover the 80x48 tile), one
+// detector row per iteration t.  The loads for row pair t+1 are spread over
+// row t's FMA stream: pixel pair q is dead once FMA block j = q is done
+// (blocks run j = 0..KW-1 and block j reads pairs j..j+9), so its ds_read2 for
+// t+1 is issued right after that block, into the same registers; the 9 pairs
+// q >= KW follow the last block.  Row t+1's weights are scalar-loaded at the
+// top of iteration t.  A wave therefore waits on LDS only for the last 9
+// loads and never on the weights, instead of draining every load and scalar
+// load before its FMAs (k_corr_pk / k_corr_p2).  Same fmaf chain per output
+// (taps in row-major order from delta), so the scores stay bit-exact.
+template <int STRIDE, int Q>
+DEV void sp_load(lm_f2& dst, unsigned base) {
+  static_assert(Q + STRIDE <= 255, "ds_read2_b32 offset range");
+  asm volatile("s_waitcnt lgkmcnt(12)\n\tds_read2_b32 %0, %1 offset0:%2 offset1:%3"
+               : "=v"(dst)
+               : "v"(base), "i"(Q), "i"(Q + STRIDE)
+               : "memory");
+}
+
+template <int KW, int STRIDE, int... Qs>
+DEV void sp_tail(lm_f2 (&px)[P2_C + KW - 1], unsigned nbase, std::integer_sequence<int, Qs...>) {
+  (sp_load<STRIDE, KW + Qs>(px[KW + Qs], nbase), ...);
+}
+
+template <int KW, int STRIDE, int J>
+DEV void sp_block(lm_f2 (&acc)[P2_C], lm_f2 (&px)[P2_C + KW - 1], const float (&w)[KW], unsigned nbase) {
+  const lm_f2 w2 = (lm_f2){w[J], w[J]};
+#pragma unroll
+  for (int c = 0; c < P2_C; ++c) acc[c] = __builtin_elementwise_fma(w2, px[c + J], acc[c]);
+  __builtin_amdgcn_sched_barrier(0);
+  sp_load<STRIDE, J>(px[J], nbase);  // pair J is dead for row t: refill it for row t+1
+  if constexpr (J == KW - 1) sp_tail<KW, STRIDE>(px, nbase, std::make_integer_sequence<int, P2_C - 1>{});
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int KW, int STRIDE, int... Js>
+DEV void sp_row(lm_f2 (&acc)[P2_C], lm_f2 (&px)[P2_C + KW - 1], const float (&w)[KW], unsigned nbase,
+                std::integer_sequence<int, Js...>) {
+  (sp_block<KW, STRIDE, Js>(acc, px, w, nbase), ...);
+}
+
+template <int KW>
+__global__ __launch_bounds__(192) void k_corr_sp(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
+                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
+                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  constexpr int NQ = P2_C + KW - 1;
+  constexpr int STR = pk_stride_c(LM_TW + KW - 1);
+  extern __shared__ float lds[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - tb;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
+  const int stride = STR;
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  const int cols4 = (cols + 3) >> 2;
+  for (int e = threadIdx.x; e < rows * cols4; e += blockDim.x) {
+    const int r = e / cols4, c4 = (e - r * cols4) << 2;
+    const uint8_t* p = src + (int64_t)r * ew + c4;
+    float* o = lds + r * stride + c4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (c4 + k < stride) o[k] = (float)p[k];
+  }
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
+  lm_f2 acc[P2_C];
+#pragma unroll
+  for (int c = 0; c < P2_C; ++c) acc[c] = (lm_f2){D.delta, D.delta};
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  unsigned base =
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(lds + (ly * 2) * stride + lx * P2_C);
+  const unsigned rstep = (unsigned)stride * 4u;
+  lm_f2 px[NQ];
+  lds_pairs<STR, NQ>(px, base);  // row pair 0 (waits)
+  float wc[KW];
+#pragma unroll
+  for (int j = 0; j < KW; ++j) wc[j] = W[j];
+  for (int t = 0; t < kh; ++t) {
+    // the last iteration loads a (dead) row pair kh: the LDS tile has 2 spare rows
+    const float* wnr = W + min(t + 1, kh - 1) * kwp;
+    float wn[KW];
+#pragma unroll
+    for (int j = 0; j < KW; ++j) wn[j] = wnr[j];
+    __builtin_amdgcn_sched_barrier(0);  // row t+1's scalar loads issue before row t's FMAs
+    base += rstep;
+    sp_row<KW, STR>(acc, px, wc, base, std::make_integer_sequence<int, KW>{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // row t+1's pairs (and weights) have landed
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < KW; ++j) wc[j] = wn[j];
+  }
+  float accf[2][P2_C];
+#pragma unroll
+  for (int c = 0; c < P2_C; ++c) {
+    accf[0][c] = acc[c].x;
+    accf[1][c] = acc[c].y;
+  }
+  corr_epilogue<2, P2_C>(K, D, accf, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
+                         &s_cnt, &s_base);
+}
+
+// k_corr_cb: column-block pairs.  A packed accumulator holds outputs
+// (y, x) and (y, x + 40) of an 80 x 48 tile, so the two operands of every
+// v_pk_fma_f32 are pixels 40 columns apart in the same row.  The tile is kept
+// in LDS as float pairs LP[r][c] = (I[r][c], I[r][c + 40]), so each operand
+// pair is one ds_read_b64 (2 LDS cycles per wave, 256 B/clk) where the
+// row-pair kernels need a ds_read2_b32 (4 cycles, 128 B/clk): half the LDS
+// time for the same FMA count.  Thread (lx, ly), 8 x 24 threads: outputs
+// rows 2ly + {0, 1}, columns 5lx + {0..4} and 40 + 5lx + {0..4}.  Input row
+// T = 2ly + t feeds output row r through detector row i = t - r, so each
+// iteration uses weight rows t and t - 1.  Same fmaf chain per output (taps in
+// row-major order from delta): bit-exact with the reference restatement.
+#define CB_C 5
+#define CB_H 40
+constexpr int cb_stride_c(int kw) {  // pairs per LDS row: >= 40 + kw - 1 and == 4 or 12 (mod 16)
+  int s = CB_H + kw - 1;
+  while ((s & 7) != 4) ++s;
+  return s;
+}
+
+template <int Q>
+DEV void cb_load(lm_f2& dst, unsigned base) {
+  if constexpr (Q >= 15) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(Q * 8) : "memory");
+}
+
+template <int N, int... Qs>
+DEV void cb_loads_impl(lm_f2 (&px)[N], unsigned base, std::integer_sequence<int, Qs...>) {
+  (cb_load<Qs>(px[Qs], base), ...);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int KW, bool WLDS = false>
+__global__ __launch_bounds__(192) void k_corr_cb(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
+                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
+                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  constexpr int NQ = CB_C + KW - 1;
+  constexpr int S2 = cb_stride_c(KW);
+  extern __shared__ lm_f2 lp[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - tb;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1;
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  constexpr int PC = CB_H + KW - 1;  // pair columns used
+  for (int e = threadIdx.x; e < rows * PC; e += blockDim.x) {
+    const int r = e / PC, c = e - r * PC;
+    const uint8_t* p = src + (int64_t)r * ew + c;
+    lp[r * S2 + c] = (lm_f2){(float)p[0], (float)p[CB_H]};
+  }
+  // WLDS: detector weights staged in LDS after the tile and read as broadcast
+  // ds_reads (no scalar loads, whose waits also drain the LDS queue)
+  float* wl = reinterpret_cast<float*>(lp + rows * S2);
+  if (WLDS)
+    for (int e = threadIdx.x; e < D.kh * D.kwp; e += blockDim.x) wl[e] = weights[D.w_off + e];
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
+  lm_f2 acc[2][CB_C];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < CB_C; ++c) acc[r][c] = (lm_f2){D.delta, D.delta};
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  const unsigned base0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) lm_f2*)(lp + (ly * 2) * S2 + lx * CB_C);
+  for (int t = 0; t <= kh; ++t) {
+    lm_f2 px[NQ];
+    cb_loads_impl<NQ>(px, base0 + (unsigned)(t * S2 * 8), std::make_integer_sequence<int, NQ>{});
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = t - r;
+      if (i >= 0 && i < kh) {
+        const float* wr = (WLDS ? wl : W) + i * kwp;
+#pragma unroll
+        for (int j = 0; j < KW; ++j) {
+          const float w = wr[j];
+          const lm_f2 w2 = (lm_f2){w, w};
+#pragma unroll
+          for (int c = 0; c < CB_C; ++c) acc[r][c] = __builtin_elementwise_fma(w2, px[c + j], acc[r][c]);
+        }
+      }
+    }
+  }
+  // epilogue (see corr_epilogue): outputs (2ly + r, 5lx + c) in .x and (2ly + r, 40 + 5lx + c) in .y
+  const int my = D.m_y - D.in_y, mx = D.m_x - D.in_x;
+  if (D.kind != 0) {
+    uint8_t* __restrict__ tbm = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int c = 0; c < CB_C; ++c)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int y = oy0 + ly * 2 + r, x = ox0 + h * CB_H + lx * CB_C + c;
+          const float a = h ? acc[r][c].y : acc[r][c].x;
+          if (y < D.oh && x < D.ow) tbm[(int64_t)y * D.ow + x] = a > 0.0f ? 1 : 0;
+        }
+    return;
+  }
+  unsigned bits = 0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < CB_C; ++c) {
+      const lm_f2 pix = lp[(ly * 2 + r + my) * S2 + lx * CB_C + c + mx];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int y = oy0 + ly * 2 + r, x = ox0 + h * CB_H + lx * CB_C + c;
+        const float a = h ? acc[r][c].y : acc[r][c].x;
+        const float pv = h ? pix.y : pix.x;
+        if (y < D.oh && x < D.ow && pv > 25.0f && a > 0.0f) bits |= 1u << ((r * CB_C + c) * 2 + h);
+      }
+    }
+  const int nk = __popc(bits);
+  const int off = nk ? atomicAdd(&s_cnt, nk) : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
+  __syncthreads();
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + s_base + off;
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < CB_C; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (bits & (1u << ((r * CB_C + c) * 2 + h))) {
+          const int y = oy0 + ly * 2 + r, x = ox0 + h * CB_H + lx * CB_C + c;
+          const float a = h ? acc[r][c].y : acc[r][c].x;
+          kl[k++] = ((unsigned long long)(~__float_as_uint(a)) << 32) | (unsigned)(y * D.ow + x);
+        }
+}
+
 // widths with a specialised kernel; others use the generic k_corr
 #define LM_KW_LIST(X) \
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
@@ -696,10 +1003,17 @@ __global__ __launch_bounds__(192, 2) void k_corr_db(const LmConst K, const LmDet
 // Correlation variants: 0 generic (runtime width), 1 width-specialised plain
 // FMA (k_corr_kw), 2 packed FMA with compiler-scheduled LDS loads, 3 packed
 // FMA with explicit (row t, row t+1) ds_read2_b32 pair loads (default).
-enum { CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3, CORR_P2 = 4, CORR_DB = 5 };
+enum {
+  CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3, CORR_P2 = 4, CORR_DB = 5, CORR_SP = 6, CORR_CB = 7,
+  CORR_PK_WLDS = 8, CORR_CB_WLDS = 9
+};
 
 template <int n>
 static inline const void* corr_fn(int variant) {
+  if (variant == CORR_CB_WLDS) return (const void*)&k_corr_cb<n, true>;
+  if (variant == CORR_PK_WLDS) return (const void*)&k_corr_pk<n, true, true>;
+  if (variant == CORR_CB) return (const void*)&k_corr_cb<n>;
+  if (variant == CORR_SP) return (const void*)&k_corr_sp<n>;
   if (variant == CORR_DB) return (const void*)&k_corr_db<n>;
   if (variant == CORR_P2) return (const void*)&k_corr_p2<n>;
   if (variant == CORR_PK_ASM) return (const void*)&k_corr_pk<n, false, true>;
@@ -713,11 +1027,18 @@ static inline const void* corr_fn(int variant) {
 
 template <int n>
 static inline const void* corr_fn_wide(int variant) {
+  if (variant == CORR_CB_WLDS) return (const void*)&k_corr_cb<n, true>;
+  if (variant == CORR_PK_WLDS) return (const void*)&k_corr_pk<n, true, true>;
+  if (variant == CORR_CB) return (const void*)&k_corr_cb<n>;
+  if (variant == CORR_SP) return (const void*)&k_corr_sp<n>;
   return variant == CORR_PK_ASM ? (const void*)&k_corr_pk<n, false, true> : nullptr;
 }
 
 static inline const void* corr_kernel(int variant, int kw, int* threads) {
-  *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2 || variant == CORR_DB) ? 192 : 256;
+  *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2 || variant == CORR_DB ||
+              variant == CORR_SP || variant == CORR_CB || variant == CORR_PK_WLDS || variant == CORR_CB_WLDS)
+                 ? 192
+                 : 256;
   const void* fn = nullptr;
   if (variant != CORR_GENERIC) switch (kw) {
 #define LM_KW_CASE(n) \
@@ -746,7 +1067,7 @@ static inline hipError_t corr_set_lds(int variant, int kw, size_t lds) {
 }
 
 // Launch the correlation for one detector group (all detectors of one width).
-static inline hipError_t launch_corr(int variant, int kw, dim3 grid, size_t lds, hipStream_t st, const LmConst& K,
+static inline hipError_t launch_corr(int variant, int kw, dim3 grid, size_t lds, hipStream_t st, const LmConst* K,
                                      const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes,
                                      const float* weights, int s0, unsigned long long* keys, int32_t* n_pos,
                                      uint8_t* tailbin, int64_t tailbin_slot_bytes) {
@@ -759,9 +1080,10 @@ static inline hipError_t launch_corr(int variant, int kw, dim3 grid, size_t lds,
 
 
 // Debug copy of raw scores: same arithmetic as k_corr, no compaction.
-__global__ __launch_bounds__(256) void k_corr_dbg(const LmConst K, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+__global__ __launch_bounds__(256) void k_corr_dbg(const LmConst* __restrict__ Kp, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
                                                   const float* __restrict__ weights, int s0, float* __restrict__ dbg,
                                                   const int64_t* __restrict__ dbg_off, int64_t dbg_slot_floats) {
+  const LmConst& K = *Kp;
   extern __shared__ float lds[];
   const int slot = s0 + blockIdx.y;
   int d = 0;
@@ -911,10 +1233,11 @@ DEV void cc_largest(CCWork W, int n, int rows, int cols, int conn, IsFg is_fg, I
   __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void k_tail(const LmConst K, int s0, const uint8_t* __restrict__ tailbin,
+__global__ __launch_bounds__(1024) void k_tail(const LmConst* __restrict__ Kp, int s0, const uint8_t* __restrict__ tailbin,
                                                int64_t tailbin_slot_bytes, uint8_t* __restrict__ tailmask,
                                                unsigned* __restrict__ scratch, int64_t scratch_slot_words,
                                                LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err) {
+  const LmConst& K = *Kp;
   const int slot = s0 + blockIdx.x;
   const int TW = K.tail_w, HB = K.tail_hb, HS = K.tail_hs;
   const uint8_t* __restrict__ binb = tailbin + (int64_t)slot * tailbin_slot_bytes;
@@ -1349,11 +1672,12 @@ DEV double readlane_f64(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
-__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst K, int s0, int side, unsigned long long* __restrict__ keys,
+__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
                                                        const int32_t* __restrict__ n_pos, const uint8_t* __restrict__ tailmask,
                                                        unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
                                                        LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
                                                        long long* __restrict__ prof) {
+  const LmConst& K = *Kp;
   const int slot = s0 + blockIdx.x;
   const int feat = blockIdx.y;  // 0 paw, 1 snout
   // optional phase timestamps (LM_KPROF=1): clock64() of thread 0 per phase
@@ -1628,7 +1952,7 @@ DEV bool vel_criterion(const LmConst& K, const uint8_t* Fc, const uint8_t* Fp, c
   return (double)sum >= ((double)area) * alpha;
 }
 
-__global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const LmSlot* __restrict__ slots,
+__global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restrict__ Kp, const LmSlot* __restrict__ slots,
                                                          const uint8_t* const* __restrict__ frame_ptr,
                                                          const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
                                                          const uint8_t* __restrict__ luts, LmSlotOut* __restrict__ hdr,
@@ -1637,6 +1961,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const
                                                          double* __restrict__ arena_unary, int32_t* __restrict__ arena_jc,
                                                          int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
                                                          LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err) {
+  const LmConst& K = *Kp;
   const int slot = 1 + blockIdx.x;
   const int feat = blockIdx.y;
   LmSlotOut* H = hdr + slot;
@@ -1947,14 +2272,62 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst K, const
 // (frame first-1) into slot 0's candidate staging, where k_post reads the
 // previous frame's candidates (pairwisePotential, :896-919).  Runs first in a
 // batch, before k_corr reuses the key areas of slots >= 1.
-__global__ void k_carry(const LmConst K, unsigned long long* __restrict__ keys, const LmSlotOut* __restrict__ prev_hdr,
+__global__ void k_carry(const LmConst* __restrict__ Kp, unsigned long long* __restrict__ keys, const LmSlotOut* __restrict__ prev_hdr,
                         int prev_slot, LmSlotOut* __restrict__ hdr) {
+  const LmConst& K = *Kp;
   for (int l = 0; l < LM_NFEAT; ++l) {
     const int cnt = prev_hdr[prev_slot].cand_cnt[l];
     const LmCand* src = LM_CAND_STAGE(K, keys, prev_slot, l);
     LmCand* dst = LM_CAND_STAGE(K, keys, 0, l);
     for (int k = threadIdx.x; k < cnt; k += blockDim.x) dst[k] = src[k];
     if (threadIdx.x == 0) hdr[0].cand_cnt[l] = cnt;
+  }
+}
+
+// ------------------------------------------------------------- k_prep / k_out
+// The batch's only transfers between host and device memory are done by these
+// two kernels through mapped pinned host memory, so a batch's stream holds
+// nothing but kernels (ordered by the stream) -- no runtime copy or memset
+// operations.  Measured on MI355X/ROCm 7 (scripts/debug_mt.py, DESIGN.md
+// §6): with several contexts' streams active at once, runtime copies on a
+// stream (hipMemcpyAsync D2H/D2D/H2D) intermittently did not wait for, or ran
+// concurrently with, the kernels enqueued around them, and batches came back
+// with stale or partial results.
+//
+// k_prep: slots, frame pointers and the arena control block from host memory,
+// candidate counters and error flags zeroed.  One block.
+__global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots, const uint8_t* const* __restrict__ h_fptr,
+                                              const LmArenaCtl* __restrict__ h_ctl, int ns, LmSlot* __restrict__ slots,
+                                              const uint8_t** __restrict__ fptr, LmArenaCtl* __restrict__ ctl,
+                                              int32_t* __restrict__ npos, int32_t* __restrict__ err) {
+  for (int i = threadIdx.x; i < ns; i += blockDim.x) {
+    slots[i] = h_slots[i];
+    fptr[i] = h_fptr[i];
+  }
+  for (int i = threadIdx.x; i < ns * LM_NLIST; i += blockDim.x) npos[i] = 0;
+  if (threadIdx.x < 16) err[threadIdx.x] = 0;
+  if (threadIdx.x == 0) *ctl = *h_ctl;
+}
+
+// k_out: the pack header always, and when the batch succeeded and its packed
+// results fit the host buffer, the results themselves -> mapped pinned host
+// memory; then the next batch's previous frame (storePreviousImage,
+// LocoMouse_class.cpp:1508-1513) -> the halo buffer.  Packed sizes and frame
+// sizes are multiples of 16 bytes.
+__global__ __launch_bounds__(256) void k_out(const LmPackHdr* __restrict__ ph, LmPackHdr* __restrict__ h_ph,
+                                             const uint8_t* __restrict__ pack, uint8_t* __restrict__ h_pack, int64_t h_cap,
+                                             const uint8_t* __restrict__ halo_src, uint8_t* __restrict__ halo_dst,
+                                             int64_t halo_bytes) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
+  if (tid == 0) *h_ph = *ph;
+  const int64_t bytes = ph->bytes;
+  if (ph->overflow || ph->err || bytes > h_cap) return;
+  for (int64_t i = tid; i < bytes / 16; i += nth)
+    reinterpret_cast<uint4*>(h_pack)[i] = reinterpret_cast<const uint4*>(pack)[i];
+  if (halo_src) {
+    for (int64_t i = tid; i < halo_bytes / 16; i += nth)
+      reinterpret_cast<uint4*>(halo_dst)[i] = reinterpret_cast<const uint4*>(halo_src)[i];
+    for (int64_t i = halo_bytes / 16 * 16 + tid; i < halo_bytes; i += nth) halo_dst[i] = halo_src[i];
   }
 }
 
@@ -2032,13 +2405,14 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const LmSlotOut* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void k_pack_copy(const LmConst K, const LmSlotOut* __restrict__ hdr, int n,
+__global__ __launch_bounds__(256) void k_pack_copy(const LmConst* __restrict__ Kp, const LmSlotOut* __restrict__ hdr, int n,
                                                    const unsigned long long* __restrict__ keys,
                                                    const LmP22D* __restrict__ arena_p22d, const int32_t* __restrict__ arena_side_y,
                                                    const double* __restrict__ arena_side_s, const double* __restrict__ arena_unary,
                                                    const int32_t* __restrict__ arena_jc, const int32_t* __restrict__ arena_ir,
                                                    const double* __restrict__ arena_pr, const LmPackHdr* __restrict__ ph,
                                                    uint8_t* __restrict__ pack, const int64_t* __restrict__ side_base) {
+  const LmConst& K = *Kp;
   if (ph->overflow || ph->err) return;  // the host raises or reruns; offsets may be garbage
   const int f = blockIdx.x, feat = blockIdx.y, slot = 1 + f;
   const LmSlotOut& H = hdr[slot];

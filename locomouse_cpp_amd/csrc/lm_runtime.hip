@@ -36,6 +36,56 @@ void hip_check(hipError_t e, const char* what) {
 }
 #define HIPCHK(x) hip_check((x), #x)
 
+// Diagnostics (LM_GUARD=1): every device buffer gets 64 KiB guard zones on
+// both sides filled with 0xA5; lm_detect_batch* checks them after each batch
+// and fails with the buffer's address if a kernel wrote outside it.
+constexpr size_t kGuard = 64 * 1024;
+bool guard_mode() {
+  static const bool on = [] {
+    const char* v = getenv("LM_GUARD");
+    return v && atoi(v) != 0;
+  }();
+  return on;
+}
+// Diagnostics: LM_ALLOC=uncached|finegrained allocates every device buffer
+// with hipExtMallocWithFlags (cache-coherence experiments).
+unsigned alloc_flags() {
+  static const unsigned f = [] {
+    const char* v = getenv("LM_ALLOC");
+    if (!v) return 0u;
+    if (!strcmp(v, "uncached")) return (unsigned)hipDeviceMallocUncached;
+    if (!strcmp(v, "finegrained")) return (unsigned)hipDeviceMallocFinegrained;
+    return 0u;
+  }();
+  return f;
+}
+std::mutex g_guard_mu;
+std::map<const void*, size_t> g_guarded;  // user pointer -> user bytes
+
+void guard_check_all() {
+  std::vector<std::pair<const void*, size_t>> bufs;
+  {
+    std::lock_guard<std::mutex> lk(g_guard_mu);
+    bufs.assign(g_guarded.begin(), g_guarded.end());
+  }
+  std::vector<uint8_t> h(kGuard);
+  for (const auto& b : bufs) {
+    const uint8_t* u = static_cast<const uint8_t*>(b.first);
+    for (int side = 0; side < 2; ++side) {
+      const uint8_t* g = side ? u + b.second : u - kGuard;
+      HIPCHK(hipMemcpy(h.data(), g, kGuard, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < kGuard; ++i)
+        if (h[i] != 0xA5) {
+          char m[256];
+          snprintf(m, sizeof m, "guard: write %s buffer %p (%zu bytes) at offset %lld", side ? "past" : "before",
+                   (const void*)u, b.second,
+                   side ? (long long)(b.second + i) : -(long long)(kGuard - i));
+          throw std::runtime_error(m);
+        }
+    }
+  }
+}
+
 template <class T>
 struct DevBuf {
   T* p = nullptr;
@@ -43,11 +93,34 @@ struct DevBuf {
   void alloc(size_t count) {
     release();
     if (count == 0) count = 1;
-    HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    if (guard_mode()) {
+      uint8_t* base = nullptr;
+      const size_t bytes = count * sizeof(T);
+      HIPCHK(hipMalloc(&base, bytes + 2 * kGuard));
+      HIPCHK(hipMemset(base, 0xA5, kGuard));
+      HIPCHK(hipMemset(base + kGuard + bytes, 0xA5, kGuard));
+      p = reinterpret_cast<T*>(base + kGuard);
+      std::lock_guard<std::mutex> lk(g_guard_mu);
+      g_guarded[p] = bytes;
+    } else if (alloc_flags()) {
+      HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&p), count * sizeof(T), alloc_flags()));
+    } else {
+      HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    }
     n = count;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      if (guard_mode()) {
+        {
+          std::lock_guard<std::mutex> lk(g_guard_mu);
+          g_guarded.erase(p);
+        }
+        (void)hipFree(reinterpret_cast<uint8_t*>(p) - kGuard);
+      } else {
+        (void)hipFree(p);
+      }
+    }
     p = nullptr;
     n = 0;
   }
@@ -55,18 +128,21 @@ struct DevBuf {
 };
 
 template <class T>
-struct HostBuf {  // pinned
+struct HostBuf {  // pinned, mapped into the device address space (d: device-side pointer)
   T* p = nullptr;
+  T* d = nullptr;
   size_t n = 0;
   void alloc(size_t count) {
     release();
     if (count == 0) count = 1;
-    HIPCHK(hipHostMalloc(&p, count * sizeof(T), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&p, count * sizeof(T), hipHostMallocMapped));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), p, 0));
     n = count;
   }
   void release() {
     if (p) (void)hipHostFree(p);
     p = nullptr;
+    d = nullptr;
     n = 0;
   }
   ~HostBuf() { release(); }
@@ -121,7 +197,6 @@ struct Arena {
 
 struct lm_ctx {
   int device = 0;
-  bool counted = false;  // holds a slot of the per-device live-context budget
   hipStream_t stream = nullptr;
   int max_batch = 0, nslots = 0;
   int debug = 0;
@@ -147,6 +222,7 @@ struct lm_ctx {
   DevBuf<const uint8_t*> frame_ptr;
   DevBuf<LmSlot> slots;
   DevBuf<unsigned long long> keys, gscratch;
+  DevBuf<LmConst> dK;  // the per-context constants, passed to every kernel by pointer
   DevBuf<unsigned> tscratch;
   DevBuf<long long> kprof;  // LM_KPROF=1: k_nms phase timestamps
   bool kprof_on = false;
@@ -159,6 +235,7 @@ struct lm_ctx {
   HostBuf<int32_t> h_err;
   HostBuf<LmPackHdr> h_ph;
   HostBuf<uint8_t> h_pack;  // packed results of the last batch (lm_batch_result points here)
+  DevBuf<LmPackHdr> zero_ph;
   // state carried between batches
   bool have_state = false;
   int last_frame = -1, last_n = 0, last_parity = 0;
@@ -472,11 +549,25 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     size_t need = c->corr_lds;
     int th = 0;
     (void)corr_kernel(c->corr_variant, grp.first, &th);  // th == 256: generic fallback kernel
-    if (c->corr_variant == CORR_PK_ASM && th == 192) {
+    const int v = c->corr_variant;
+    if ((v == CORR_CB || v == CORR_CB_WLDS) && th == 192) {
+      need = 0;
+      int sc = CB_H + grp.first - 1;
+      while ((sc & 7) != 4) ++sc;
+      for (int k = 0; k < grp.second.n; ++k) {
+        const LmDet& D = K.det[grp.second.ids[k]];
+        need = std::max(need, (size_t)(LM_TH + D.kh - 1) * sc * 2 * sizeof(float) +
+                                  (v == CORR_CB_WLDS ? (size_t)D.kh * D.kwp * sizeof(float) : 0));
+      }
+    } else if ((v == CORR_PK_ASM || v == CORR_SP || v == CORR_PK_WLDS) && th == 192) {
       need = 0;
       for (int k = 0; k < grp.second.n; ++k) {
         const LmDet& D = K.det[grp.second.ids[k]];
-        need = std::max(need, (size_t)(LM_TH + D.kh - 1) * pk_stride(LM_TW + grp.first - 1) * sizeof(float));
+        // k_corr_sp reads two spare rows past the tile in its last iteration
+        const int spare = v == CORR_SP ? 2 : 0;
+        const size_t tile = (size_t)(LM_TH + D.kh - 1 + spare) * pk_stride(LM_TW + grp.first - 1);
+        need = std::max(need, (((tile + 3) & ~(size_t)3) + (v == CORR_PK_WLDS ? (size_t)D.kh * D.kwp : 0)) *
+                                  sizeof(float));
       }
     }
     c->corr_group_lds.push_back(need);
@@ -513,12 +604,16 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   HIPCHK(hipMemcpy(c->weights.p, wts.data(), wts.size() * sizeof(float), hipMemcpyHostToDevice));
   c->adj.alloc(256);
   HIPCHK(hipMemcpy(c->adj.p, adj, 256, hipMemcpyHostToDevice));
+  c->dK.alloc(1);
+  HIPCHK(hipMemcpy(c->dK.p, &c->K, sizeof(LmConst), hipMemcpyHostToDevice));
   const int64_t fstride = (nv + 255) / 256 * 256;
   c->frames.alloc((size_t)fstride * ns);
   c->halo.alloc(fstride);
   HIPCHK(hipMemset(c->halo.p, 0, fstride));
   c->luts.alloc((size_t)256 * ns);
-  c->ext.alloc((size_t)c->ext_slot_bytes * ns);
+  // slack: the last tiles' windows (and the fill's 16-byte rounding) read past
+  // the last slot's side view; those pixels only feed outputs that are discarded
+  c->ext.alloc((size_t)c->ext_slot_bytes * ns + (size_t)(LM_TH + 16) * std::max(K.ext_w[0], K.ext_w[1]) + 64);
   c->tailbin.alloc((size_t)c->tailbin_slot_bytes * ns);
   c->tailmask.alloc((size_t)K.tail_hb * K.tail_w * ns);
   c->tscratch.alloc((size_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w * ns);
@@ -531,6 +626,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->h_frame_ptr.alloc(ns);
   c->h_ctl.alloc(1);
   c->h_ph.alloc(1);
+  c->zero_ph.alloc(1);  // an all-zero pack header: k_out with it copies only the halo
+  HIPCHK(hipMemset(c->zero_ph.p, 0, sizeof(LmPackHdr)));
   c->h_err.alloc(16);
   int cap[AR_COUNT];
   cap[AR_CAND] = ns * LM_NLIST * 64;
@@ -540,50 +637,20 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   cap[AR_PWJC] = ns * LM_NFEAT * (64 + g.ong_nx * g.ong_ny + 1);
   cap[AR_PWNZ] = ns * LM_NFEAT * 1024;
   for (int a = 0; a < 2; ++a) c->arena[a].alloc(cap, ns);
+  c->h_pack.alloc((size_t)c->arena[0].pack_cap);
   for (size_t g = 0; g < c->corr_groups.size(); ++g)
     HIPCHK(corr_set_lds(c->corr_variant, c->corr_groups[g].first, c->corr_group_lds[g]));
   HIPCHK(hipFuncSetAttribute((const void*)k_corr_dbg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->corr_lds));
 }
 
-// Live contexts per device.  Each context owns one HIP stream, and HIP maps
-// streams onto GPU_MAX_HW_QUEUES hardware queues per process (4 by default).
-// Measured on MI355X (ROCm 7, scripts/debug_mt.py): once contexts share
-// hardware queues (more than GPU_MAX_HW_QUEUES/2 contexts in one process,
-// torch's own stream included in the budget) batches intermittently come
-// back with other batches' bytes in their candidate staging -- silently wrong
-// results.  Refuse such a context instead of corrupting results.
-std::mutex g_live_mu;
-std::map<int, int> g_live;
-
-int live_ctx_limit() {
-  if (const char* v = getenv("LM_ALLOW_QUEUE_SHARING"))
-    if (atoi(v) != 0) return 1 << 30;
-  int hwq = 4;
-  if (const char* v = getenv("GPU_MAX_HW_QUEUES")) hwq = std::max(1, atoi(v));
-  return std::max(1, hwq / 2);
-}
-
-void live_ctx_acquire(int device) {
-  std::lock_guard<std::mutex> lk(g_live_mu);
-  const int lim = live_ctx_limit();
-  if (g_live[device] >= lim)
-    throw std::runtime_error("too many contexts on HIP device " + std::to_string(device) + " in this process (limit " +
-                             std::to_string(lim) + " = GPU_MAX_HW_QUEUES/2): contexts sharing hardware queues return "
-                             "corrupted results; destroy a context or raise GPU_MAX_HW_QUEUES.");
-  ++g_live[device];
-}
-
-void live_ctx_release(int device) {
-  std::lock_guard<std::mutex> lk(g_live_mu);
-  --g_live[device];
-}
 
 // One epoch event per device (recorded when timing is switched on) that every
 // context's kernel spans are measured against.
+std::mutex g_epoch_mu;
 std::map<int, hipEvent_t> g_epoch;
 
 hipEvent_t epoch_event(const lm_ctx* c) {
-  std::lock_guard<std::mutex> lk(g_live_mu);
+  std::lock_guard<std::mutex> lk(g_epoch_mu);
   auto it = g_epoch.find(c->device);
   return it == g_epoch.end() ? nullptr : it->second;
 }
@@ -708,8 +775,64 @@ void kprof_report(lm_ctx* c, int n) {
   }
 }
 
+bool dbg_env(const char* name) {
+  const char* v = getenv(name);
+  return v && atoi(v) != 0;
+}
+
+// LM_LDS_HOG=all or a list of kernel names (diagnostics): those launches
+// reserve >= 82 KiB of LDS, so no two workgroups share a CU.
+bool hog_selected(const char* kname) {
+  const char* v = getenv("LM_LDS_HOG");
+  if (!v || !*v || !strcmp(v, "0")) return false;
+  if (!strcmp(v, "1") || !strcmp(v, "all")) return true;
+  return strstr(v, kname) != nullptr;
+}
+
+size_t lds_hog_named(const char* kname, const void* fn, size_t static_bytes) {
+  if (!hog_selected(kname)) return 0;
+  const size_t target = 82 * 1024;
+  if (static_bytes >= target) return 0;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(target - static_bytes));
+  return target - static_bytes;
+}
+
+// Batches of different contexts on the same device are serialised: a batch
+// (all its kernels, up to the results in host memory) runs to completion
+// before another context's batch starts.  Measured on MI355X (ROCm 7, torch's
+// HIP runtime; scripts/debug_mt.py, profiles/debug/): with the
+// kernels of 2-4 contexts' streams executing concurrently on one GPU,
+// batches intermittently came back corrupted (garbage candidates in the
+// staging buffers, wrong candidate counts) although every single-context run
+// -- tens of thousands of frames, cached, uncached and fine-grained memory --
+// was bit-exact.  Serialising the host-side enqueue, removing every runtime
+// copy/memset from the stream (k_prep/k_out), keeping LmConst out of the
+// kernel arguments and 64 KiB guard zones around every buffer did not remove
+// it; keeping workgroups of different kernels off the same CU
+// (LM_LDS_HOG=all) or serialising whole batches did.  Until the cause is
+// known, one batch at a time per device; one context per GPU is the
+// throughput configuration (bench.py --streams 1).
+std::mutex g_serial_mu[64];   // per device: one batch at a time
+std::mutex g_enqueue_mu[64];  // per device: host-side enqueue
+
+void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev,
+                    const int32_t* bb, bool device_frames, lm_batch_result* out);
+
 void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev, const int32_t* bb,
                bool device_frames, lm_batch_result* out) {
+  // Batches of different contexts on one device run one at a time (see
+  // g_serial_mu).  LM_CONCURRENT=1 lets them overlap (diagnostics only).
+  static const bool concurrent = dbg_env("LM_CONCURRENT");
+  if (concurrent) {
+    run_batch_impl(c, frames, pitch, n, first, prev, bb, device_frames, out);
+  } else {
+    std::lock_guard<std::mutex> lk(g_serial_mu[c->device & 63]);
+    run_batch_impl(c, frames, pitch, n, first, prev, bb, device_frames, out);
+  }
+}
+
+void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev,
+                    const int32_t* bb, bool device_frames, lm_batch_result* out) {
   if (n <= 0 || n > c->max_batch) throw std::invalid_argument("n must be in [1, max_batch].");
   if (first < 0) throw std::invalid_argument("first_frame must be >= 0.");
   if (!frames) throw std::invalid_argument("frames is NULL.");
@@ -720,6 +843,7 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
   if (carry && !(c->have_state && c->last_frame == first - 1))
     throw std::invalid_argument("frame first_frame-1 was not processed by this context: pass prev_frame (shard start).");
   const LmConst& K = c->K;
+  const LmConst* dK = c->dK.p;
   const lm_geometry& g = c->geo;
   const int64_t fstride = (c->npix + 255) / 256 * 256;
   hipStream_t st = c->stream;
@@ -756,46 +880,55 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
   }
   (void)K;
 
-  // ---- inputs
+  std::unique_lock<std::mutex> enq(g_enqueue_mu[c->device & 63]);  // see g_enqueue_mu
+  // ---- inputs.  Host frames (and a host halo frame) are the only runtime
+  // copies; the stream is drained after them, so everything the kernels read
+  // has landed (see k_prep / k_out for why the stream otherwise holds only
+  // kernels).
   if (!device_frames) {
     for (int s = 1; s <= n; ++s)
       HIPCHK(hipMemcpyAsync(c->frames.p + (int64_t)s * fstride, frames + (int64_t)(s - 1) * pitch, c->npix,
                             hipMemcpyHostToDevice, st));
+    if (halo) HIPCHK(hipMemcpyAsync(c->halo.p, prev, c->npix, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+  } else if (halo) {
+    k_out<<<64, 256, lds_hog_named("k_out", (const void*)k_out, 0), st>>>(c->zero_ph.p, c->h_ph.d, nullptr, nullptr, 0, prev, c->halo.p, c->npix);
   }
-  if (halo)
-    HIPCHK(hipMemcpyAsync(c->halo.p, prev, c->npix, device_frames ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(c->slots.p, c->h_slots.p, sizeof(LmSlot) * (n + 1), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(c->frame_ptr.p, c->h_frame_ptr.p, sizeof(void*) * (n + 1), hipMemcpyHostToDevice, st));
 
   const int cur = c->parity, prv = c->last_parity;
   for (int attempt = 0;; ++attempt) {
+    if (!enq.owns_lock()) enq.lock();
     Arena& A = c->arena[cur];
     LmArenaCtl& hc = *c->h_ctl.p;
     std::memset(&hc, 0, sizeof(hc));
     for (int k = 0; k < AR_COUNT; ++k) hc.cap[k] = A.cap[k];
-    HIPCHK(hipMemcpyAsync(A.ctl.p, &hc, sizeof(hc), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(c->npos.p, 0, sizeof(int32_t) * LM_NLIST * (n + 1), st));
-    HIPCHK(hipMemsetAsync(c->err.p, 0, 16 * sizeof(int32_t), st));
+    k_prep<<<1, 256, lds_hog_named("k_prep", (const void*)k_prep, 0), st>>>(c->h_slots.d, c->h_frame_ptr.d, c->h_ctl.d, n + 1, c->slots.p, c->frame_ptr.p, A.ctl.p,
+                              c->npos.p, c->err.p);
     if (carry && attempt == 0) {  // a rerun keeps slot 0's staged candidates
       T.begin("k_carry");
-      k_carry<<<1, 256, 0, st>>>(K, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
+      k_carry<<<1, 256, lds_hog_named("k_carry", (const void*)k_carry, 0), st>>>(dK, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
       T.end();
     }
     T.begin("k_minmax_lut");
-    k_minmax_lut<<<n + 1 - s_lut0, 1024, 0, st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0, c->adj.p,
+    k_minmax_lut<<<n + 1 - s_lut0, 1024, lds_hog_named("k_minmax_lut", (const void*)k_minmax_lut, 128), st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0, c->adj.p,
                                                  c->setup.method != 0, c->luts.p);
     T.end();
     const int nproc = n + 1 - s_proc0;
     const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
     T.begin("k_ingest");
-    k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
-        K, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
+    k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, lds_hog_named("k_ingest", (const void*)k_ingest, 256), st>>>(
+        dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
     T.end();
     T.begin("k_corr");
     for (size_t gi = 0; gi < c->corr_groups.size(); ++gi) {
       const auto& grp = c->corr_groups[gi];
       const LmDetGroup& G = grp.second;
-      HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_lds[gi], st, K, G,
+      size_t glds = c->corr_group_lds[gi];
+      if (hog_selected("k_corr") && glds < 82 * 1024) {
+        glds = 82 * 1024;
+        HIPCHK(corr_set_lds(c->corr_variant, grp.first, glds));
+      }
+      HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), glds, st, dK, G,
                          c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->keys.p, c->npos.p, c->tailbin.p,
                          c->tailbin_slot_bytes));
     }
@@ -806,11 +939,11 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
         c->dbg_offd.alloc(LM_NDET);
         HIPCHK(hipMemcpy(c->dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice));
       }
-      k_corr_dbg<<<dim3(K.n_tiles, nproc), 256, c->corr_lds, st>>>(K, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0,
+      k_corr_dbg<<<dim3(K.n_tiles, nproc), 256, c->corr_lds, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0,
                                                                    c->dbg.p, c->dbg_offd.p, c->dbg_slot_floats);
     }
     T.begin("k_tail");
-    k_tail<<<nproc, 1024, 0, st>>>(K, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p, c->tscratch.p,
+    k_tail<<<nproc, 1024, 0, st>>>(dK, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p, c->tscratch.p,
                                    (int64_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w, A.hdr.p, c->err.p);
     T.end();
     if (!c->gscratch.p) c->gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
@@ -822,25 +955,28 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
       kp1 = c->kprof.p + 16 * 2 * c->nslots;
     }
     T.begin("k_nms_bottom");
-    k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(K, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+    k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, lds_hog_named("k_nms", (const void*)k_nms, 50328), st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
                                                     c->gscratch_slot, A.hdr.p, c->err.p, kp0);
     T.end();
     T.begin("k_nms_side");
-    k_nms<<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(K, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+    k_nms<<<dim3(n, 2), LM_NMS_THREADS, lds_hog_named("k_nms", (const void*)k_nms, 50328), st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
                                                 c->gscratch_slot, A.hdr.p, c->err.p, kp1);
     T.end();
     T.begin("k_post");
-    k_post<<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(K, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
+    k_post<<<dim3(n, 2), LM_POST_THREADS, lds_hog_named("k_post", (const void*)k_post, 40984), st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
                                                    c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
                                                    A.pr.p, A.ctl.p, c->err.p);
     T.end();
     T.begin("k_pack");
-    k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
-    k_pack_copy<<<dim3(n, 2), 256, 0, st>>>(K, A.hdr.p, n, c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p,
+    k_pack_scan<<<1, 1024, lds_hog_named("k_pack_scan", (const void*)k_pack_scan, 136), st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
+    k_pack_copy<<<dim3(n, 2), 256, lds_hog_named("k_pack_copy", (const void*)k_pack_copy, 0), st>>>(dK, A.hdr.p, n, c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p,
                                             A.ir.p, A.pr.p, A.ph.p, A.pack.p, A.side_base.p);
     T.end();
+    // header + results to host memory, then frame n as the next batch's halo
+    k_out<<<128, 256, lds_hog_named("k_out", (const void*)k_out, 0), st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, c->h_frame_ptr.p[n],
+                               c->halo.p, c->npix);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->h_ph.p, A.ph.p, sizeof(LmPackHdr), hipMemcpyDeviceToHost, st));
+    if (enq.owns_lock()) enq.unlock();
     HIPCHK(hipStreamSynchronize(st));
     const LmPackHdr& ph = *c->h_ph.p;
     const int e = (c->debug & 4) ? (ph.err & ~4) : ph.err;  // debug bit 2: report but keep going
@@ -878,14 +1014,23 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
   T.collect();
   if (c->kprof_on) kprof_report(c, n);
 
-  // ---- one D2H of the packed results (already in lm_batch_result layout)
+  // ---- the packed results (lm_batch_result layout) are in h_pack unless
+  // they outgrew it: then grow it and let k_out copy them (and the halo) again
   Arena& A = c->arena[cur];
   const LmPackHdr ph = *c->h_ph.p;
-  if ((int64_t)c->h_pack.n < ph.bytes) c->h_pack.alloc((size_t)(ph.bytes + ph.bytes / 4));
-  HIPCHK(hipMemcpyAsync(c->h_pack.p, A.pack.p, (size_t)ph.bytes, hipMemcpyDeviceToHost, st));
-  // keep frame first+n-1 as the next batch's previous frame (storePreviousImage :1508-1513)
-  HIPCHK(hipMemcpyAsync(c->halo.p, c->h_frame_ptr.p[n], c->npix, hipMemcpyDeviceToDevice, st));
-  HIPCHK(hipStreamSynchronize(st));
+  if ((int64_t)c->h_pack.n < ph.bytes) {
+    c->h_pack.alloc((size_t)(ph.bytes + ph.bytes / 4));
+    enq.lock();
+    k_out<<<128, 256, lds_hog_named("k_out", (const void*)k_out, 0), st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, c->h_frame_ptr.p[n],
+                               c->halo.p, c->npix);
+    HIPCHK(hipGetLastError());
+    enq.unlock();
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  if (guard_mode()) {
+    HIPCHK(hipDeviceSynchronize());
+    guard_check_all();
+  }
   if (c->debug & 8) {  // diagnostics: a second, synchronous copy of the pack must equal the async one
     HIPCHK(hipDeviceSynchronize());
     std::vector<uint8_t> chk((size_t)ph.bytes);
@@ -946,9 +1091,7 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) throw HipError("invalid HIP device index");
-    live_ctx_acquire(device);
     c->device = device;
-    c->counted = true;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->max_batch = max_batch;
@@ -956,7 +1099,6 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     validate_and_build(c, setup, params, model);
   });
   if (s != LM_OK) {
-    if (c->counted) live_ctx_release(c->device);
     delete c;
     return s;
   }
@@ -965,7 +1107,6 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
 }
 
 LM_API void lm_ctx_destroy(lm_ctx* ctx) {
-  if (ctx && ctx->counted) live_ctx_release(ctx->device);
   delete ctx;
 }
 
@@ -994,7 +1135,7 @@ LM_API lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags) {
   if (!ctx) return fail(LM_ERR_INVALID_ARGUMENT, "null ctx");
   return guarded([&] {
     if (flags & 2) {
-      std::lock_guard<std::mutex> lk(g_live_mu);
+      std::lock_guard<std::mutex> lk(g_epoch_mu);
       if (!g_epoch.count(ctx->device)) {
         HIPCHK(hipSetDevice(ctx->device));
         hipEvent_t e;

@@ -1,8 +1,7 @@
 """Several contexts on one GPU driven from several host threads (one HIP
 stream each, bench.py --streams): every batch must equal the same range run
-alone (no shared state between contexts).  Contexts beyond
-GPU_MAX_HW_QUEUES/2 per device are refused (lm_runtime.hip, live_ctx_acquire)."""
-import os
+alone (no shared state between contexts; the host-side enqueue is
+serialised per device, lm_runtime.hip g_enqueue_mu)."""
 import threading
 
 import numpy as np
@@ -28,7 +27,7 @@ def _run(ctx, frames_dev, k, R, NB, B, out):
 def test_threads_and_contexts_are_independent():
     torch = pytest.importorskip("torch")
     from locomouse_cpp_amd.runtime import Context, synth_frames_device
-    NS, NB, B = 2, 12, 128
+    NS, NB, B = 3, 12, 128
     R = NB * B
     cfg = S.SyntheticConfig()
     fr = torch.empty((NS, R + 1, 256, 1024), dtype=torch.uint8, device="cuda")
@@ -63,19 +62,3 @@ def test_threads_and_contexts_are_independent():
     for c in ctxs:
         c.close()
 
-
-def test_contexts_beyond_hw_queue_budget_are_refused():
-    pytest.importorskip("torch")
-    from locomouse_cpp_amd.runtime import Context, LMError
-    hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
-    if os.environ.get("LM_ALLOW_QUEUE_SHARING"):
-        pytest.skip("LM_ALLOW_QUEUE_SHARING set")
-    lim = max(1, hwq // 2)
-    cfg = S.SyntheticConfig()
-    ctxs = [Context(cfg, max_batch=4) for _ in range(lim)]
-    with pytest.raises(LMError, match="too many contexts"):
-        Context(cfg, max_batch=4)
-    ctxs[-1].close()
-    ctxs[-1] = Context(cfg, max_batch=4)  # a released slot can be reused
-    for c in ctxs:
-        c.close()
