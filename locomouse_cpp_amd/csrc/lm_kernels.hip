@@ -219,6 +219,7 @@ struct LmDetGroup {
   int32_t n;
   int32_t ids[LM_NDET];
   int32_t tile_end[LM_NDET];  // cumulative tile counts
+  int32_t skip_taps;          // diagnostics (LM_CORR_SKIP=1): no FMAs, fill + epilogue only
 };
 
 __global__ __launch_bounds__(256) void k_corr(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
@@ -487,10 +488,13 @@ __global__ __launch_bounds__(192) void k_corr_pk(const LmConst* __restrict__ Kp,
     for (int c = 0; c < PK_C; ++c) acc[p][c] = (lm_f2){D.delta, D.delta};
   const float* __restrict__ W = weights + D.w_off;
   const int kh = D.kh, kwp = D.kwp;
-  for (int t = 0; t < kh + PK_R - 2; ++t) {
+  const int tend = (G.skip_taps & 1) ? 0 : kh + PK_R - 2;
+  lm_f2 px[PK_C + KW - 1];
+  for (int t = 0; t < tend; ++t) {
     const float* p0 = lds + (ly * PK_R + t) * stride + lx * PK_C;
-    lm_f2 px[PK_C + KW - 1];
-    if constexpr (ASMLD) {
+    if ((G.skip_taps & 4) && t > 0) {
+      // diagnostics: pixel pairs of row 0 reused (no LDS traffic in the loop)
+    } else if constexpr (ASMLD) {
       constexpr int STR = pk_stride_c(LM_TW + KW - 1);
       const unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p0;
       lds_pairs<STR, PK_C + KW - 1>(px, base);
@@ -502,7 +506,7 @@ __global__ __launch_bounds__(192) void k_corr_pk(const LmConst* __restrict__ Kp,
     for (int p = 0; p < PK_R / 2; ++p) {
       const int i = t - 2 * p;
       if (i >= 0 && i < kh) {
-        const float* wr = (WLDS ? wl : W) + i * kwp;
+        const float* wr = (WLDS ? wl : W) + ((G.skip_taps & 2) ? 0 : i * kwp);
 #pragma unroll
         for (int j = 0; j < KW; ++j) {
           const float w = wr[j];
@@ -935,7 +939,7 @@ __global__ __launch_bounds__(192) void k_corr_cb(const LmConst* __restrict__ Kp,
     for (int r = 0; r < 2; ++r) {
       const int i = t - r;
       if (i >= 0 && i < kh) {
-        const float* wr = (WLDS ? wl : W) + i * kwp;
+        const float* wr = (WLDS ? wl : W) + ((G.skip_taps & 2) ? 0 : i * kwp);
 #pragma unroll
         for (int j = 0; j < KW; ++j) {
           const float w = wr[j];
@@ -996,6 +1000,148 @@ __global__ __launch_bounds__(192) void k_corr_cb(const LmConst* __restrict__ Kp,
         }
 }
 
+// k_corr_c1: column-block pairs (as k_corr_cb) with one output row per
+// thread: 384 threads = 8 x 48 cover the 80 x 48 tile, each owning columns
+// 5lx+{0..4} and 40+5lx+{0..4} of row ly.  Twice the waves of the row-pair
+// kernels for the same LDS (up to 6 waves/SIMD), one detector row per
+// iteration, so row t+1's weights are scalar-loaded during row t, and row
+// t+1's pixel pairs (ds_read_b64) are loaded into each register as soon as
+// row t's FMA block j = q no longer needs pair q (as k_corr_sp).
+template <int Q>
+DEV void c1_load(lm_f2& dst, unsigned base) {
+  asm volatile("s_waitcnt lgkmcnt(10)\n\tds_read_b64 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(Q * 8) : "memory");
+}
+
+template <int KW, int... Qs>
+DEV void c1_tail(lm_f2 (&px)[CB_C + KW - 1], unsigned nbase, std::integer_sequence<int, Qs...>) {
+  (c1_load<KW + Qs>(px[KW + Qs], nbase), ...);
+}
+
+template <int KW, int J>
+DEV void c1_block(lm_f2 (&acc)[CB_C], lm_f2 (&px)[CB_C + KW - 1], const float (&w)[KW], unsigned nbase) {
+  const lm_f2 w2 = (lm_f2){w[J], w[J]};
+#pragma unroll
+  for (int c = 0; c < CB_C; ++c) acc[c] = __builtin_elementwise_fma(w2, px[c + J], acc[c]);
+  __builtin_amdgcn_sched_barrier(0);
+  c1_load<J>(px[J], nbase);  // pair J is dead for row t: refill it for row t+1
+  if constexpr (J == KW - 1) c1_tail<KW>(px, nbase, std::make_integer_sequence<int, CB_C - 1>{});
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int KW, int... Js>
+DEV void c1_row(lm_f2 (&acc)[CB_C], lm_f2 (&px)[CB_C + KW - 1], const float (&w)[KW], unsigned nbase,
+                std::integer_sequence<int, Js...>) {
+  (c1_block<KW, Js>(acc, px, w, nbase), ...);
+}
+
+template <int KW>
+__global__ __launch_bounds__(384) void k_corr_c1(const LmConst* __restrict__ Kp, const LmDetGroup G,
+                                                 const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                 const float* __restrict__ weights, int s0,
+                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  constexpr int NQ = CB_C + KW - 1;
+  constexpr int S2 = cb_stride_c(KW);
+  extern __shared__ lm_f2 lp[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  const LmDet D = K.det[d];
+  const int lt = blockIdx.x - tb;
+  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
+  const int rows = LM_TH + D.kh - 1;
+  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+  const int ew = K.ext_w[D.view];
+  constexpr int PC = CB_H + KW - 1;
+  for (int e = threadIdx.x; e < rows * PC; e += blockDim.x) {
+    const int r = e / PC, c = e - r * PC;
+    const uint8_t* p = src + (int64_t)r * ew + c;
+    lp[r * S2 + c] = (lm_f2){(float)p[0], (float)p[CB_H]};
+  }
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
+  lm_f2 acc[CB_C];
+#pragma unroll
+  for (int c = 0; c < CB_C; ++c) acc[c] = (lm_f2){D.delta, D.delta};
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) lm_f2*)(lp + ly * S2 + lx * CB_C);
+  const unsigned rstep = (unsigned)S2 * 8u;
+  lm_f2 px[NQ];
+  cb_loads_impl<NQ>(px, base, std::make_integer_sequence<int, NQ>{});  // row 0 (waits)
+  float wc[KW];
+#pragma unroll
+  for (int j = 0; j < KW; ++j) wc[j] = W[j];
+  for (int t = 0; t < kh; ++t) {
+    // the last iteration loads a (dead) row kh: the LDS tile has a spare row
+    const float* wnr = W + min(t + 1, kh - 1) * kwp;
+    float wn[KW];
+#pragma unroll
+    for (int j = 0; j < KW; ++j) wn[j] = wnr[j];
+    __builtin_amdgcn_sched_barrier(0);  // row t+1's scalar loads issue before row t's FMAs
+    base += rstep;
+    c1_row<KW>(acc, px, wc, base, std::make_integer_sequence<int, KW>{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // row t+1's pairs (and weights) have landed
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < KW; ++j) wc[j] = wn[j];
+  }
+  // epilogue: outputs (ly, 5lx + c) in .x and (ly, 40 + 5lx + c) in .y
+  const int my = D.m_y - D.in_y, mx = D.m_x - D.in_x;
+  if (D.kind != 0) {
+    uint8_t* __restrict__ tbm = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
+#pragma unroll
+    for (int c = 0; c < CB_C; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int y = oy0 + ly, x = ox0 + h * CB_H + lx * CB_C + c;
+        const float a = h ? acc[c].y : acc[c].x;
+        if (y < D.oh && x < D.ow) tbm[(int64_t)y * D.ow + x] = a > 0.0f ? 1 : 0;
+      }
+    return;
+  }
+  unsigned bits = 0;
+#pragma unroll
+  for (int c = 0; c < CB_C; ++c) {
+    const lm_f2 pix = lp[(ly + my) * S2 + lx * CB_C + c + mx];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int y = oy0 + ly, x = ox0 + h * CB_H + lx * CB_C + c;
+      const float a = h ? acc[c].y : acc[c].x;
+      const float pv = h ? pix.y : pix.x;
+      if (y < D.oh && x < D.ow && pv > 25.0f && a > 0.0f) bits |= 1u << (c * 2 + h);
+    }
+  }
+  const int nk = __popc(bits);
+  const int off = nk ? atomicAdd(&s_cnt, nk) : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
+  __syncthreads();
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + s_base + off;
+  int k = 0;
+#pragma unroll
+  for (int c = 0; c < CB_C; ++c)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (bits & (1u << (c * 2 + h))) {
+        const int y = oy0 + ly, x = ox0 + h * CB_H + lx * CB_C + c;
+        const float a = h ? acc[c].y : acc[c].x;
+        kl[k++] = ((unsigned long long)(~__float_as_uint(a)) << 32) | (unsigned)(y * D.ow + x);
+      }
+}
+
 // widths with a specialised kernel; others use the generic k_corr
 #define LM_KW_LIST(X) \
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
@@ -1005,11 +1151,12 @@ __global__ __launch_bounds__(192) void k_corr_cb(const LmConst* __restrict__ Kp,
 // FMA with explicit (row t, row t+1) ds_read2_b32 pair loads (default).
 enum {
   CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3, CORR_P2 = 4, CORR_DB = 5, CORR_SP = 6, CORR_CB = 7,
-  CORR_PK_WLDS = 8, CORR_CB_WLDS = 9
+  CORR_PK_WLDS = 8, CORR_CB_WLDS = 9, CORR_C1 = 10
 };
 
 template <int n>
 static inline const void* corr_fn(int variant) {
+  if (variant == CORR_C1) return (const void*)&k_corr_c1<n>;
   if (variant == CORR_CB_WLDS) return (const void*)&k_corr_cb<n, true>;
   if (variant == CORR_PK_WLDS) return (const void*)&k_corr_pk<n, true, true>;
   if (variant == CORR_CB) return (const void*)&k_corr_cb<n>;
@@ -1027,6 +1174,7 @@ static inline const void* corr_fn(int variant) {
 
 template <int n>
 static inline const void* corr_fn_wide(int variant) {
+  if (variant == CORR_C1) return (const void*)&k_corr_c1<n>;
   if (variant == CORR_CB_WLDS) return (const void*)&k_corr_cb<n, true>;
   if (variant == CORR_PK_WLDS) return (const void*)&k_corr_pk<n, true, true>;
   if (variant == CORR_CB) return (const void*)&k_corr_cb<n>;
@@ -1035,7 +1183,8 @@ static inline const void* corr_fn_wide(int variant) {
 }
 
 static inline const void* corr_kernel(int variant, int kw, int* threads) {
-  *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2 || variant == CORR_DB ||
+  if (variant == CORR_C1) *threads = 384;
+  else *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2 || variant == CORR_DB ||
               variant == CORR_SP || variant == CORR_CB || variant == CORR_PK_WLDS || variant == CORR_CB_WLDS)
                  ? 192
                  : 256;
@@ -1505,8 +1654,17 @@ DEV bool overlaps_xy(unsigned a, unsigned b, int bw, int bh) {
 //  * leaves (<= 16 elements): the final insertion sort is a stable sort of
 //    each leaf, done in registers by one thread per leaf.
 // q: two queues of qcap (first, last, depth); leaf: n flags; tf, tr: n ints.
+// Lanes of one wave exchanging data through memory.  k_nms reaches its
+// arrays through generic pointers (LDS, or global scratch for long lists), so
+// the accesses are FLAT instructions, which complete out of order: a
+// wavefront-scope fence alone emits no wait, and a lane could read a value
+// another lane had stored but whose store had not landed (measured: rare
+// wrong leaders in the tie sort and in peakClustering, more often when other
+// kernels load the memory system).  Drain both counters, then a workgroup
+// fence for the global-scratch case, then the wave barrier.
 DEV void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -1760,6 +1918,11 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
       const unsigned long long v = a[k];
       a[k] = ((unsigned long long)key_lo(v) << 32) | (unsigned)(~(unsigned)(v >> 32));
     }
+    // every key must be re-keyed before any thread ranks them (rank_sort reads
+    // all n keys); without this barrier a lagging wave's old-format keys were
+    // ranked among new-format ones -- duplicate ranks, unwritten slots, and
+    // garbage candidates in rare tie blocks
+    __syncthreads();
     if (!glob) {
       if (n <= LM_NMS_RANKSORT) {  // back to row-major order
         rank_sort(a, reinterpret_cast<unsigned long long*>(s_assign), n);
@@ -1835,6 +1998,7 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
     // assign[j] = leader, -1 undecided.
     const int lane = threadIdx.x;
     for (int j = lane; j < n; j += 64) assign[j] = -1;
+    wave_sync();
     int lead = 0;
     while (lead < n) {
       const unsigned xl = xy[lead];
@@ -1850,6 +2014,7 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
         const unsigned long long m = __ballot(und);
         if (m && next == n) next = b + __ffsll((long long)m) - 1;
       }
+      wave_sync();  // the next leader's sweep reads assign[] entries other lanes just wrote
       lead = next;
     }
   }
@@ -2287,12 +2452,9 @@ __global__ void k_carry(const LmConst* __restrict__ Kp, unsigned long long* __re
 // ------------------------------------------------------------- k_prep / k_out
 // The batch's only transfers between host and device memory are done by these
 // two kernels through mapped pinned host memory, so a batch's stream holds
-// nothing but kernels (ordered by the stream) -- no runtime copy or memset
-// operations.  Measured on MI355X/ROCm 7 (scripts/debug_mt.py, DESIGN.md
-// §6): with several contexts' streams active at once, runtime copies on a
-// stream (hipMemcpyAsync D2H/D2D/H2D) intermittently did not wait for, or ran
-// concurrently with, the kernels enqueued around them, and batches came back
-// with stale or partial results.
+// nothing but kernels: 5 runtime copies/memsets and a second stream sync per
+// batch are gone (the header and the packed results land in host memory in
+// the same pass, the host reads them after one hipStreamSynchronize).
 //
 // k_prep: slots, frame pointers and the arena control block from host memory,
 // candidate counters and error flags zeroed.  One block.

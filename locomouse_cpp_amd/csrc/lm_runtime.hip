@@ -36,6 +36,11 @@ void hip_check(hipError_t e, const char* what) {
 }
 #define HIPCHK(x) hip_check((x), #x)
 
+bool dbg_env(const char* name) {  // diagnostics switches (LM_* environment variables)
+  const char* v = getenv(name);
+  return v && atoi(v) != 0;
+}
+
 // Diagnostics (LM_GUARD=1): every device buffer gets 64 KiB guard zones on
 // both sides filled with 0xA5; lm_detect_batch* checks them after each batch
 // and fails with the buffer's address if a kernel wrote outside it.
@@ -46,18 +51,6 @@ bool guard_mode() {
     return v && atoi(v) != 0;
   }();
   return on;
-}
-// Diagnostics: LM_ALLOC=uncached|finegrained allocates every device buffer
-// with hipExtMallocWithFlags (cache-coherence experiments).
-unsigned alloc_flags() {
-  static const unsigned f = [] {
-    const char* v = getenv("LM_ALLOC");
-    if (!v) return 0u;
-    if (!strcmp(v, "uncached")) return (unsigned)hipDeviceMallocUncached;
-    if (!strcmp(v, "finegrained")) return (unsigned)hipDeviceMallocFinegrained;
-    return 0u;
-  }();
-  return f;
 }
 std::mutex g_guard_mu;
 std::map<const void*, size_t> g_guarded;  // user pointer -> user bytes
@@ -102,8 +95,6 @@ struct DevBuf {
       p = reinterpret_cast<T*>(base + kGuard);
       std::lock_guard<std::mutex> lk(g_guard_mu);
       g_guarded[p] = bytes;
-    } else if (alloc_flags()) {
-      HIPCHK(hipExtMallocWithFlags(reinterpret_cast<void**>(&p), count * sizeof(T), alloc_flags()));
     } else {
       HIPCHK(hipMalloc(&p, count * sizeof(T)));
     }
@@ -531,6 +522,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     if (it == c->corr_groups.end()) {
       LmDetGroup G;
       std::memset(&G, 0, sizeof(G));
+      if (const char* v = getenv("LM_CORR_SKIP")) G.skip_taps = atoi(v);  // diagnostics
       c->corr_groups.push_back({kw, G});
       it = c->corr_groups.end() - 1;
     }
@@ -550,13 +542,14 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     int th = 0;
     (void)corr_kernel(c->corr_variant, grp.first, &th);  // th == 256: generic fallback kernel
     const int v = c->corr_variant;
-    if ((v == CORR_CB || v == CORR_CB_WLDS) && th == 192) {
+    if ((v == CORR_CB || v == CORR_CB_WLDS || v == CORR_C1) && th != 256) {
       need = 0;
       int sc = CB_H + grp.first - 1;
       while ((sc & 7) != 4) ++sc;
       for (int k = 0; k < grp.second.n; ++k) {
         const LmDet& D = K.det[grp.second.ids[k]];
-        need = std::max(need, (size_t)(LM_TH + D.kh - 1) * sc * 2 * sizeof(float) +
+        const int spare = v == CORR_C1 ? 1 : 0;  // k_corr_c1 reads a spare row in its last iteration
+        need = std::max(need, (size_t)(LM_TH + D.kh - 1 + spare) * sc * 2 * sizeof(float) +
                                   (v == CORR_CB_WLDS ? (size_t)D.kh * D.kwp * sizeof(float) : 0));
       }
     } else if ((v == CORR_PK_ASM || v == CORR_SP || v == CORR_PK_WLDS) && th == 192) {
@@ -775,60 +768,42 @@ void kprof_report(lm_ctx* c, int n) {
   }
 }
 
-bool dbg_env(const char* name) {
-  const char* v = getenv(name);
-  return v && atoi(v) != 0;
-}
-
-// LM_LDS_HOG=all or a list of kernel names (diagnostics): those launches
-// reserve >= 82 KiB of LDS, so no two workgroups share a CU.
-bool hog_selected(const char* kname) {
-  const char* v = getenv("LM_LDS_HOG");
-  if (!v || !*v || !strcmp(v, "0")) return false;
-  if (!strcmp(v, "1") || !strcmp(v, "all")) return true;
-  return strstr(v, kname) != nullptr;
-}
-
-size_t lds_hog_named(const char* kname, const void* fn, size_t static_bytes) {
-  if (!hog_selected(kname)) return 0;
-  const size_t target = 82 * 1024;
-  if (static_bytes >= target) return 0;
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(target - static_bytes));
-  return target - static_bytes;
-}
-
-// Batches of different contexts on the same device are serialised: a batch
-// (all its kernels, up to the results in host memory) runs to completion
-// before another context's batch starts.  Measured on MI355X (ROCm 7, torch's
-// HIP runtime; scripts/debug_mt.py, profiles/debug/): with the
-// kernels of 2-4 contexts' streams executing concurrently on one GPU,
-// batches intermittently came back corrupted (garbage candidates in the
-// staging buffers, wrong candidate counts) although every single-context run
-// -- tens of thousands of frames, cached, uncached and fine-grained memory --
-// was bit-exact.  Serialising the host-side enqueue, removing every runtime
-// copy/memset from the stream (k_prep/k_out), keeping LmConst out of the
-// kernel arguments and 64 KiB guard zones around every buffer did not remove
-// it; keeping workgroups of different kernels off the same CU
-// (LM_LDS_HOG=all) or serialising whole batches did.  Until the cause is
-// known, one batch at a time per device; one context per GPU is the
-// throughput configuration (bench.py --streams 1).
-std::mutex g_serial_mu[64];   // per device: one batch at a time
-std::mutex g_enqueue_mu[64];  // per device: host-side enqueue
-
 void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev,
                     const int32_t* bb, bool device_frames, lm_batch_result* out);
 
 void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev, const int32_t* bb,
                bool device_frames, lm_batch_result* out) {
-  // Batches of different contexts on one device run one at a time (see
-  // g_serial_mu).  LM_CONCURRENT=1 lets them overlap (diagnostics only).
-  static const bool concurrent = dbg_env("LM_CONCURRENT");
-  if (concurrent) {
-    run_batch_impl(c, frames, pitch, n, first, prev, bb, device_frames, out);
-  } else {
-    std::lock_guard<std::mutex> lk(g_serial_mu[c->device & 63]);
-    run_batch_impl(c, frames, pitch, n, first, prev, bb, device_frames, out);
+  run_batch_impl(c, frames, pitch, n, first, prev, bb, device_frames, out);
+}
+
+// Diagnostics (LM_DUMP_DIR): one slot's candidate-path state after a failed
+// batch -> <dir>/dump_<frame>.bin: int32 [frame, slot, feat, npos_b, npos_s,
+// hdr.n_pos[4], hdr.cand_cnt[4], hdr.ties[4]] then, per list 0..3, the list's
+// whole key area (u64 x list_cap).
+void dump_slot(lm_ctx* c, const char* dir, int frame, int slot, int feat) {
+  const LmConst& K = c->K;
+  std::vector<int32_t> np(LM_NLIST);
+  HIPCHK(hipMemcpy(np.data(), c->npos.p + (int64_t)slot * LM_NLIST, LM_NLIST * sizeof(int32_t), hipMemcpyDeviceToHost));
+  LmSlotOut h;
+  HIPCHK(hipMemcpy(&h, c->arena[c->parity].hdr.p + slot, sizeof(h), hipMemcpyDeviceToHost));
+  std::string path = std::string(dir) + "/dump_" + std::to_string(frame) + ".bin";
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) return;
+  int32_t hd[5 + 12] = {frame, slot, feat, np[0], np[1]};
+  for (int l = 0; l < 4; ++l) {
+    hd[5 + l] = h.n_pos[l];
+    hd[9 + l] = h.cand_cnt[l];
+    hd[13 + l] = h.ties[l];
   }
+  fwrite(hd, sizeof(hd), 1, f);
+  fwrite(np.data(), sizeof(int32_t), LM_NLIST, f);
+  for (int l = 0; l < LM_NLIST; ++l) {
+    std::vector<unsigned long long> kv((size_t)K.list_cap[l]);
+    HIPCHK(hipMemcpy(kv.data(), c->keys.p + (int64_t)slot * K.keys_per_slot + K.list_off[l],
+                     kv.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    fwrite(kv.data(), sizeof(unsigned long long), kv.size(), f);
+  }
+  fclose(f);
 }
 
 void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev,
@@ -880,7 +855,6 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   }
   (void)K;
 
-  std::unique_lock<std::mutex> enq(g_enqueue_mu[c->device & 63]);  // see g_enqueue_mu
   // ---- inputs.  Host frames (and a host halo frame) are the only runtime
   // copies; the stream is drained after them, so everything the kernels read
   // has landed (see k_prep / k_out for why the stream otherwise holds only
@@ -892,43 +866,37 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
     if (halo) HIPCHK(hipMemcpyAsync(c->halo.p, prev, c->npix, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
   } else if (halo) {
-    k_out<<<64, 256, lds_hog_named("k_out", (const void*)k_out, 0), st>>>(c->zero_ph.p, c->h_ph.d, nullptr, nullptr, 0, prev, c->halo.p, c->npix);
+    k_out<<<64, 256, 0, st>>>(c->zero_ph.p, c->h_ph.d, nullptr, nullptr, 0, prev, c->halo.p, c->npix);
   }
 
   const int cur = c->parity, prv = c->last_parity;
   for (int attempt = 0;; ++attempt) {
-    if (!enq.owns_lock()) enq.lock();
     Arena& A = c->arena[cur];
     LmArenaCtl& hc = *c->h_ctl.p;
     std::memset(&hc, 0, sizeof(hc));
     for (int k = 0; k < AR_COUNT; ++k) hc.cap[k] = A.cap[k];
-    k_prep<<<1, 256, lds_hog_named("k_prep", (const void*)k_prep, 0), st>>>(c->h_slots.d, c->h_frame_ptr.d, c->h_ctl.d, n + 1, c->slots.p, c->frame_ptr.p, A.ctl.p,
+    k_prep<<<1, 256, 0, st>>>(c->h_slots.d, c->h_frame_ptr.d, c->h_ctl.d, n + 1, c->slots.p, c->frame_ptr.p, A.ctl.p,
                               c->npos.p, c->err.p);
     if (carry && attempt == 0) {  // a rerun keeps slot 0's staged candidates
       T.begin("k_carry");
-      k_carry<<<1, 256, lds_hog_named("k_carry", (const void*)k_carry, 0), st>>>(dK, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
+      k_carry<<<1, 256, 0, st>>>(dK, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
       T.end();
     }
     T.begin("k_minmax_lut");
-    k_minmax_lut<<<n + 1 - s_lut0, 1024, lds_hog_named("k_minmax_lut", (const void*)k_minmax_lut, 128), st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0, c->adj.p,
+    k_minmax_lut<<<n + 1 - s_lut0, 1024, 0, st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0, c->adj.p,
                                                  c->setup.method != 0, c->luts.p);
     T.end();
     const int nproc = n + 1 - s_proc0;
     const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
     T.begin("k_ingest");
-    k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, lds_hog_named("k_ingest", (const void*)k_ingest, 256), st>>>(
+    k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
         dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
     T.end();
     T.begin("k_corr");
     for (size_t gi = 0; gi < c->corr_groups.size(); ++gi) {
       const auto& grp = c->corr_groups[gi];
       const LmDetGroup& G = grp.second;
-      size_t glds = c->corr_group_lds[gi];
-      if (hog_selected("k_corr") && glds < 82 * 1024) {
-        glds = 82 * 1024;
-        HIPCHK(corr_set_lds(c->corr_variant, grp.first, glds));
-      }
-      HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), glds, st, dK, G,
+      HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_lds[gi], st, dK, G,
                          c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->keys.p, c->npos.p, c->tailbin.p,
                          c->tailbin_slot_bytes));
     }
@@ -955,28 +923,27 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       kp1 = c->kprof.p + 16 * 2 * c->nslots;
     }
     T.begin("k_nms_bottom");
-    k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, lds_hog_named("k_nms", (const void*)k_nms, 50328), st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+    k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
                                                     c->gscratch_slot, A.hdr.p, c->err.p, kp0);
     T.end();
     T.begin("k_nms_side");
-    k_nms<<<dim3(n, 2), LM_NMS_THREADS, lds_hog_named("k_nms", (const void*)k_nms, 50328), st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+    k_nms<<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
                                                 c->gscratch_slot, A.hdr.p, c->err.p, kp1);
     T.end();
     T.begin("k_post");
-    k_post<<<dim3(n, 2), LM_POST_THREADS, lds_hog_named("k_post", (const void*)k_post, 40984), st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
+    k_post<<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
                                                    c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
                                                    A.pr.p, A.ctl.p, c->err.p);
     T.end();
     T.begin("k_pack");
-    k_pack_scan<<<1, 1024, lds_hog_named("k_pack_scan", (const void*)k_pack_scan, 136), st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
-    k_pack_copy<<<dim3(n, 2), 256, lds_hog_named("k_pack_copy", (const void*)k_pack_copy, 0), st>>>(dK, A.hdr.p, n, c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p,
+    k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
+    k_pack_copy<<<dim3(n, 2), 256, 0, st>>>(dK, A.hdr.p, n, c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p,
                                             A.ir.p, A.pr.p, A.ph.p, A.pack.p, A.side_base.p);
     T.end();
     // header + results to host memory, then frame n as the next batch's halo
-    k_out<<<128, 256, lds_hog_named("k_out", (const void*)k_out, 0), st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, c->h_frame_ptr.p[n],
+    k_out<<<128, 256, 0, st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, c->h_frame_ptr.p[n],
                                c->halo.p, c->npix);
     HIPCHK(hipGetLastError());
-    if (enq.owns_lock()) enq.unlock();
     HIPCHK(hipStreamSynchronize(st));
     const LmPackHdr& ph = *c->h_ph.p;
     const int e = (c->debug & 4) ? (ph.err & ~4) : ph.err;  // debug bit 2: report but keep going
@@ -990,6 +957,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       HIPCHK(hipMemcpy(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost));
       const int32_t* d = c->h_err.p;
       const int tag = d[2], slot = tag >> 16;
+      if (const char* dir = getenv("LM_DUMP_DIR")) dump_slot(c, dir, first - 1 + slot, slot, (tag >> 12) & 1);
       char buf[256];
       snprintf(buf, sizeof buf, " [frame %d, %s %s candidate %d: box (%d,%d,%d,%d) in crop %dx%d]",
                first - 1 + slot, (tag >> 12 & 1) ? "snout" : "paw", (tag & 0x800) ? "side" : "bottom", tag & 0x7FF,
@@ -1020,11 +988,9 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   const LmPackHdr ph = *c->h_ph.p;
   if ((int64_t)c->h_pack.n < ph.bytes) {
     c->h_pack.alloc((size_t)(ph.bytes + ph.bytes / 4));
-    enq.lock();
-    k_out<<<128, 256, lds_hog_named("k_out", (const void*)k_out, 0), st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, c->h_frame_ptr.p[n],
+    k_out<<<128, 256, 0, st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, c->h_frame_ptr.p[n],
                                c->halo.p, c->npix);
     HIPCHK(hipGetLastError());
-    enq.unlock();
     HIPCHK(hipStreamSynchronize(st));
   }
   if (guard_mode()) {
