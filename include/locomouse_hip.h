@@ -245,6 +245,77 @@ int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32
  * that device), so the spans of several contexts' streams can be merged. */
 int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, double* t1, int32_t cap);
 
+/* ---- whole-video bounding-box pass, method 0 ----
+ *
+ * Replaces LocoMouse::computeBoundingBox (LocoMouse_class.cpp:579-653) with
+ * computeMouseBox (:948-997), largestBWAreaObject (:921-946),
+ * firstLastOverT (LocoMouse_class.hpp:411-440), computeMouseBoxSize
+ * (:1481-1506), medianvec / stdvec / vecmovingaverage (:1516-1608).  Frames
+ * are pushed in video order (the median filter's zero-padded border carries
+ * state from frame to frame, :585-603 + :952); lm_bb_finish runs the
+ * whole-video post-processing.  The results feed the detection path as
+ * lm_params.bounding_box_* sizes plus the per-frame `bb` corners of
+ * lm_detect_batch. */
+
+/* firstLastOverT reads the CV_32S row/column sums through ptr<float>
+ * (LocoMouse_class.hpp:419), i.e. it compares the sums' bit patterns as
+ * floats against min_pixel_visible.  AS_EXECUTED reproduces that (the
+ * drop-in default); INTEGER compares the integer sums, as the comment at
+ * :967-970 intends. */
+#define LM_BB_FIRSTLAST_AS_EXECUTED 0
+#define LM_BB_FIRSTLAST_INTEGER 1
+
+typedef struct {
+  int32_t median_filter_size;     /* odd, 1..63 (config.yml, :41-45) */
+  int32_t min_pixel_visible;      /* >= 0 (:47-50) */
+  int32_t moving_average_window;  /* odd, >= 1 (:120-123) */
+  int32_t conn_comp_connectivity; /* 4 or 8 (:33-39) */
+  int32_t firstlast_semantics;    /* LM_BB_FIRSTLAST_* */
+  int32_t reserved0;
+} lm_bb_params;
+
+/* The six per-frame values of computeMouseBox, after :636
+ * (bb_y_bottom += BB_BOTTOM_VIEW.y). */
+typedef struct {
+  double x, y_bottom, y_side, width, height_bottom, height_side;
+} lm_bb_frame;
+
+typedef struct {
+  int32_t n_frames;
+  int32_t reserved0;
+  lm_rect bb_side_mouse, bb_bottom_mouse; /* computeMouseBoxSize (x = y = 0) */
+  const uint32_t* x_pos;                  /* BB_X_POS[n_frames] (vecmovingaverage) */
+  const uint32_t* y_bottom_pos;           /* BB_Y_BOTTOM_POS */
+  const uint32_t* y_side_pos;             /* BB_Y_SIDE_POS */
+  const lm_bb_frame* frames;              /* per-frame values [n_frames] */
+} lm_bb_result;
+
+typedef struct lm_bb_ctx lm_bb_ctx;
+
+/* setup: as for lm_ctx_create (setup->method must be 0; the view boxes must
+ * span the full corrected width, as firstLastOverT reads I.cols sums, and
+ * must not overlap).  max_batch bounds n of lm_bb_push*. */
+lm_status lm_bb_create(int32_t device, const lm_setup* setup, const lm_bb_params* params, int32_t max_batch,
+                       lm_bb_ctx** out);
+void lm_bb_destroy(lm_bb_ctx* ctx);
+
+/* Push the next n frames of the video (host memory / device memory).  out
+ * (may be NULL) receives their lm_bb_frame values. */
+lm_status lm_bb_push(lm_bb_ctx* ctx, const uint8_t* frames, int64_t frame_pitch, int32_t n, lm_bb_frame* out);
+lm_status lm_bb_push_device(lm_bb_ctx* ctx, const uint8_t* d_frames, int64_t frame_pitch, int32_t n,
+                            lm_bb_frame* out);
+
+/* Post-processing over every frame pushed so far; arrays are owned by ctx and
+ * valid until the next call on it.  Fails when no frame was pushed. */
+lm_status lm_bb_finish(lm_bb_ctx* ctx, lm_bb_result* out);
+
+/* Diagnostics: the thresholded median image (0/1, N_ROWS x N_COLS, before the
+ * connected-component step) of frame f of the last push. */
+lm_status lm_bb_debug_binary(lm_bb_ctx* ctx, int32_t f, uint8_t* out, int32_t rows, int32_t cols);
+
+/* The ctx's HIP stream (hipStream_t as void*). */
+void* lm_bb_stream(lm_bb_ctx* ctx);
+
 /* Benchmark/test input utility (not a reference interface): writes frames
  * [first_frame, first_frame + n) of the synthetic scene of include/lm_synth.h
  * (rows x cols u8, frame_pitch bytes apart) into device memory of `device`. */

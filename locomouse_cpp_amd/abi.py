@@ -121,6 +121,46 @@ class lm_batch_result(C.Structure):
     ]
 
 
+LM_BB_FIRSTLAST_AS_EXECUTED, LM_BB_FIRSTLAST_INTEGER = 0, 1
+
+
+class lm_bb_params(C.Structure):
+    _fields_ = [
+        ("median_filter_size", C.c_int32),
+        ("min_pixel_visible", C.c_int32),
+        ("moving_average_window", C.c_int32),
+        ("conn_comp_connectivity", C.c_int32),
+        ("firstlast_semantics", C.c_int32),
+        ("reserved0", C.c_int32),
+    ]
+
+
+class lm_bb_frame(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("x", "y_bottom", "y_side", "width", "height_bottom", "height_side")]
+
+
+class lm_bb_result(C.Structure):
+    _fields_ = [
+        ("n_frames", C.c_int32),
+        ("reserved0", C.c_int32),
+        ("bb_side_mouse", lm_rect),
+        ("bb_bottom_mouse", lm_rect),
+        ("x_pos", C.POINTER(C.c_uint32)),
+        ("y_bottom_pos", C.POINTER(C.c_uint32)),
+        ("y_side_pos", C.POINTER(C.c_uint32)),
+        ("frames", C.POINTER(lm_bb_frame)),
+    ]
+
+
+BB_FRAME_DTYPE = np.dtype([(n, "<f8") for n in ("x", "y_bottom", "y_side", "width", "height_bottom", "height_side")])
+
+
+def bb_params(median_filter_size=11, min_pixel_visible=1, moving_average_window=5, connectivity=8,
+              semantics=LM_BB_FIRSTLAST_AS_EXECUTED):
+    """lm_bb_params with the reference defaults (LocoMouse_class.hpp:53-69)."""
+    return lm_bb_params(median_filter_size, min_pixel_visible, moving_average_window, connectivity, semantics, 0)
+
+
 CAND_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("score", "<f8")])
 P22D_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("score", "<f8"), ("side_offset", "<i4"), ("side_count", "<i4")])
 

@@ -1,0 +1,661 @@
+// lm_bbox.hip — whole-video bounding-box pass, method 0, on gfx950
+// (SURVEY.md §8(f) row 1): LocoMouse::computeBoundingBox
+// (LocoMouse_class.cpp:579-653) with computeMouseBox (:948-997),
+// largestBWAreaObject (:921-946), firstLastOverT (LocoMouse_class.hpp:411-440),
+// computeMouseBoxSize (:1481-1506), medianvec / stdvec / vecmovingaverage
+// (:1516-1608).  Included by lm_runtime.hip (one translation unit).
+//
+// Exact reformulation on 0/1 images.  medianBlur is a rank filter and the
+// threshold after it (:955, v > 2.55 <=> v >= 3) is monotone, so
+//     median(window) >= 3  <=>  #{x in window : x >= 3} >= (n + 1) / 2,  n = k^2.
+// The zero-initialised border ring of I_median (:585-603) is rewritten by the
+// in-place medianBlur every frame (:952) and read back by the next frame's
+// filter; only its indicator [v >= 3] ever reaches a later threshold, so the
+// ring is carried as 0/1 too.  The per-frame work becomes box counts over
+// bytes (k_bb_center) plus a small sequential recurrence over the ring
+// (k_bb_ring, one workgroup walking the batch's frames in order).
+//
+// Per batch of n frames:
+//   k_minmax_lut  normalize LUT per frame (shared with the detection path)
+//   k_bb_ingest   I_median centre indicator  M[f] = [corrected frame >= 3]
+//   k_bb_ring     ring state recurrence; writes ring_{f-1} into M[f]
+//   k_bb_center   11x11 (k x k) majority over M[f] -> thresholded image bin[f]
+//   k_bb_cc       per (frame, view): largest component (union-find in global
+//                 memory), row/column counts, firstLastOverT -> 4 limits
+// The host turns the limits into computeMouseBox's six values and runs the
+// whole-video post-processing in lm_bb_finish.
+
+struct LmBBConst {
+  int32_t n_rows, n_cols;  // corrected image
+  int32_t p, hp, wp;       // median half-size; I_median rows / cols
+  int32_t thr;             // ones needed in a window: (k*k + 1) / 2
+  int32_t flip;
+  int32_t view_y[2], view_h[2];  // 0 side, 1 bottom (x = 0, width = n_cols)
+  int32_t conn, semantics, min_pixel_visible;
+  int32_t ring_n;          // ring state bytes: top [p][wp] | bottom [p][wp] | left [n_rows][p] | right [n_rows][p]
+  int32_t pad_;
+  int64_t m_bytes;         // per-frame I_median indicator image (hp x wp)
+  int64_t bin_bytes;       // per-frame thresholded image (n_rows x n_cols)
+  int64_t cc_words;        // per-frame union-find scratch (3 words per view pixel)
+};
+
+// ---------------------------------------------------------------- k_bb_ingest
+// readFrame(I_center) (:615, :1273-1333) fused with the indicator: 4 centre
+// pixels per thread.
+__global__ __launch_bounds__(256) void k_bb_ingest(const LmBBConst K, const uint8_t* const* __restrict__ frame_ptr,
+                                                   const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+                                                   const uint8_t* __restrict__ luts, uint8_t* __restrict__ M) {
+  const int f = blockIdx.y;
+  __shared__ uint8_t lut[256];
+  lut[threadIdx.x] = luts[f * 256 + threadIdx.x];
+  __syncthreads();
+  const uint8_t* __restrict__ F = frame_ptr[f];
+  uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
+  const int64_t np = (int64_t)K.n_rows * K.n_cols;
+  const int64_t q0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t q = q0 + k;
+    if (q >= np) break;
+    const int r = (int)(q / K.n_cols), c = (int)(q % K.n_cols);
+    const int cs = K.flip ? K.n_cols - 1 - c : c;
+    const int idx = cal[(int64_t)r * K.n_cols + cs];
+    const int fv = F[idx], bv = bkg[idx];
+    Mf[(int64_t)(r + K.p) * K.wp + c + K.p] = lut[fv > bv ? fv - bv : 0] >= 3 ? 1 : 0;
+  }
+}
+
+// ------------------------------------------------------------------ k_bb_ring
+// One 1024-thread workgroup; the ring state lives in LDS across the batch.
+// For frame f: (1) gather the 2p-wide bands of M[f] around the border (ring
+// from the state, centre from global) and publish the state (= ring_{f-1})
+// into M[f]'s ring for k_bb_center; (2) horizontal clamped window counts;
+// (3) vertical clamped counts at the ring pixels -> ring_f.  Clamping is
+// medianBlur's BORDER_REPLICATE at the edges of I_median.
+__global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __restrict__ M, int n,
+                                                  uint8_t* __restrict__ ring) {
+  extern __shared__ uint8_t sm[];
+  const int p = K.p, p2 = 2 * p, hp = K.hp, wp = K.wp, nr = K.n_rows, thr = K.thr;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  uint8_t* sT = sm;                 // [p][wp]
+  uint8_t* sB = sT + p * wp;        // [p][wp]
+  uint8_t* sL = sB + p * wp;        // [nr][p]
+  uint8_t* sR = sL + nr * p;        // [nr][p]
+  uint8_t* bT = sm + K.ring_n;      // [2p][wp]  rows 0 .. 2p-1
+  uint8_t* bB = bT + p2 * wp;       // [2p][wp]  rows hp-2p .. hp-1
+  uint8_t* bL = bB + p2 * wp;       // [hp][2p]  cols 0 .. 2p-1
+  uint8_t* bR = bL + hp * p2;       // [hp][2p]  cols wp-2p .. wp-1
+  uint8_t* hT = bR + hp * p2;       // [2p][wp]
+  uint8_t* hB = hT + p2 * wp;       // [2p][wp]
+  uint8_t* hL = hB + p2 * wp;       // [hp][p]
+  uint8_t* hR = hL + hp * p;        // [hp][p]
+  for (int i = tid; i < K.ring_n; i += nt) sm[i] = ring[i];
+  __syncthreads();
+  for (int f = 0; f < n; ++f) {
+    uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
+    auto mget = [&](int r, int c) -> uint8_t {
+      if (r < p) return sT[r * wp + c];
+      if (r >= hp - p) return sB[(r - (hp - p)) * wp + c];
+      if (c < p) return sL[(r - p) * p + c];
+      if (c >= wp - p) return sR[(r - p) * p + c - (wp - p)];
+      return Mf[(int64_t)r * wp + c];
+    };
+    for (int i = tid; i < p2 * wp; i += nt) {
+      const int r = i / wp, c = i - r * wp;
+      bT[i] = mget(r, c);
+      bB[i] = mget(hp - p2 + r, c);
+    }
+    for (int i = tid; i < hp * p2; i += nt) {
+      const int r = i / p2, j = i - r * p2;
+      bL[i] = mget(r, j);
+      bR[i] = mget(r, wp - p2 + j);
+    }
+    for (int i = tid; i < p * wp; i += nt) {
+      const int r = i / wp, c = i - r * wp;
+      Mf[(int64_t)r * wp + c] = sT[i];
+      Mf[(int64_t)(hp - p + r) * wp + c] = sB[i];
+    }
+    for (int i = tid; i < nr * p; i += nt) {
+      const int r = i / p, j = i - r * p;
+      Mf[(int64_t)(r + p) * wp + j] = sL[i];
+      Mf[(int64_t)(r + p) * wp + wp - p + j] = sR[i];
+    }
+    __syncthreads();
+    for (int i = tid; i < p2 * wp; i += nt) {
+      const int r = i / wp, c = i - r * wp;
+      int a = 0, b = 0;
+      for (int dc = -p; dc <= p; ++dc) {
+        const int cc = min(max(c + dc, 0), wp - 1);
+        a += bT[r * wp + cc];
+        b += bB[r * wp + cc];
+      }
+      hT[i] = (uint8_t)a;
+      hB[i] = (uint8_t)b;
+    }
+    for (int i = tid; i < hp * p; i += nt) {
+      const int r = i / p, j = i - r * p;
+      int a = 0, b = 0;
+      for (int dc = -p; dc <= p; ++dc) {
+        a += bL[r * p2 + max(j + dc, 0)];
+        b += bR[r * p2 + min(p + j + dc, p2 - 1)];
+      }
+      hL[i] = (uint8_t)a;
+      hR[i] = (uint8_t)b;
+    }
+    __syncthreads();
+    for (int i = tid; i < p * wp; i += nt) {
+      const int r = i / wp, c = i - r * wp;
+      int a = 0, b = 0;
+      for (int dr = -p; dr <= p; ++dr) {
+        a += hT[max(r + dr, 0) * wp + c];
+        b += hB[min(p + r + dr, p2 - 1) * wp + c];
+      }
+      sT[i] = a >= thr ? 1 : 0;
+      sB[i] = b >= thr ? 1 : 0;
+    }
+    for (int i = tid; i < nr * p; i += nt) {
+      const int r = i / p, j = i - r * p;
+      int a = 0, b = 0;
+      for (int dr = -p; dr <= p; ++dr) {
+        a += hL[(r + p + dr) * p + j];
+        b += hR[(r + p + dr) * p + j];
+      }
+      sL[i] = a >= thr ? 1 : 0;
+      sR[i] = b >= thr ? 1 : 0;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < K.ring_n; i += nt) ring[i] = sm[i];
+}
+
+// ---------------------------------------------------------------- k_bb_center
+// Majority filter over the centre: one 64 x 32 output tile per 256 threads;
+// the (32+2p) x (64+2p) input window is staged in LDS, column counts run down
+// the tile, row sums of 2p+1 column counts give the window count.
+#define LM_BB_TW 64
+#define LM_BB_TH 32
+__global__ __launch_bounds__(256) void k_bb_center(const LmBBConst K, const uint8_t* __restrict__ M,
+                                                   uint8_t* __restrict__ bin) {
+  extern __shared__ uint8_t sm[];
+  const int p2 = 2 * K.p, IW = LM_BB_TW + p2, IH = LM_BB_TH + p2;
+  uint8_t* in = sm;                                           // [IH][IW]
+  uint16_t* vs = reinterpret_cast<uint16_t*>(sm + ((IH * IW + 15) & ~15));  // [TH][IW]
+  const int c0 = blockIdx.x * LM_BB_TW, r0 = blockIdx.y * LM_BB_TH, f = blockIdx.z;
+  const uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
+  for (int i = threadIdx.x; i < IH * IW; i += blockDim.x) {
+    const int rr = r0 + i / IW, cc = c0 + i % IW;
+    in[i] = (rr < K.hp && cc < K.wp) ? Mf[(int64_t)rr * K.wp + cc] : 0;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < IW; j += blockDim.x) {
+    int s = 0;
+    for (int k = 0; k < p2; ++k) s += in[k * IW + j];
+    for (int i = 0; i < LM_BB_TH; ++i) {
+      s += in[(i + p2) * IW + j];
+      vs[i * IW + j] = (uint16_t)s;
+      s -= in[i * IW + j];
+    }
+  }
+  __syncthreads();
+  uint8_t* __restrict__ B = bin + (int64_t)f * K.bin_bytes;
+  for (int o = threadIdx.x; o < LM_BB_TH * LM_BB_TW; o += blockDim.x) {
+    const int i = o / LM_BB_TW, c = o % LM_BB_TW;
+    const int r = r0 + i, cc = c0 + c;
+    if (r >= K.n_rows || cc >= K.n_cols) continue;
+    int s = 0;
+    for (int k = 0; k <= p2; ++k) s += vs[i * IW + c + k];
+    B[(int64_t)r * K.n_cols + cc] = s >= K.thr ? 1 : 0;
+  }
+}
+
+// -------------------------------------------------------------------- k_bb_cc
+// largestBWAreaObject + reduce + firstLastOverT for one (view, frame).
+// Union-find over the view's pixels in global memory (atomicMin hooking of the
+// larger root under the smaller); loads bypass the vector L1 so every wave
+// sees the hooks of the others.  Largest area wins; equal areas go to the
+// component OpenCV labels first (8-connectivity: Grana BBDT 2x2-block raster
+// order of its first block; 4-connectivity: Wu pixel raster order).
+DEV unsigned bb_ld(const unsigned* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+DEV void bb_st(unsigned* a, unsigned v) { __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+DEV unsigned bb_find(const unsigned* par, unsigned a) {
+  unsigned q = bb_ld(&par[a]);
+  while (q != a) {
+    a = q;
+    q = bb_ld(&par[a]);
+  }
+  return a;
+}
+
+DEV void bb_union(unsigned* par, unsigned a, unsigned b) {
+  while (true) {
+    a = bb_find(par, a);
+    b = bb_find(par, b);
+    if (a == b) return;
+    if (a < b) {
+      const unsigned t = a;
+      a = b;
+      b = t;
+    }
+    const unsigned old = atomicMin(&par[a], b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+// firstLastOverT's pass test on one row/column sum (LocoMouse_class.hpp:419-421).
+DEV bool bb_pass(const LmBBConst& K, int count) {
+  const int v = 255 * count;  // the mask is 0/255 (cv::compare, :945)
+  if (K.semantics == LM_BB_FIRSTLAST_INTEGER) return v >= K.min_pixel_visible;
+  return __int_as_float(v) >= (float)K.min_pixel_visible;  // CV_32S read through ptr<float>
+}
+
+__global__ __launch_bounds__(1024) void k_bb_cc(const LmBBConst K, const uint8_t* __restrict__ bin,
+                                                unsigned* __restrict__ scratch, int32_t* __restrict__ lims) {
+  extern __shared__ int cnt[];
+  const int v = blockIdx.x, f = blockIdx.y;
+  const int W = K.n_cols, H = K.view_h[v], NP = W * H;
+  const uint8_t* __restrict__ Bv = bin + (int64_t)f * K.bin_bytes + (int64_t)K.view_y[v] * W;
+  unsigned* par = scratch + (int64_t)f * K.cc_words + (v ? 3 * (int64_t)W * K.view_h[0] : 0);
+  unsigned* area = par + NP;
+  unsigned* key = area + NP;
+  int* colc = cnt;      // [W]  Row_* (reduce over rows)
+  int* rowc = cnt + W;  // [H]  Col_*
+  __shared__ unsigned long long s_red[16];
+  __shared__ unsigned s_best;
+  __shared__ int s_lim[2][3];  // (first, last, count) for Row, Col
+  const int tid = threadIdx.x, nt = blockDim.x;
+
+  for (int q = tid; q < NP; q += nt) {
+    bb_st(&par[q], Bv[q] ? (unsigned)q : 0xFFFFFFFFu);
+    bb_st(&area[q], 0u);
+    bb_st(&key[q], 0xFFFFFFFFu);
+  }
+  for (int i = tid; i < W + H; i += nt) cnt[i] = 0;
+  if (tid < 2) {
+    s_lim[tid][0] = 0x7FFFFFFF;
+    s_lim[tid][1] = -1;
+    s_lim[tid][2] = 0;
+  }
+  if (tid == 0) s_best = 0xFFFFFFFFu;
+  __syncthreads();
+  const bool c8 = K.conn == 8;
+  for (int q = tid; q < NP; q += nt) {
+    if (!Bv[q]) continue;
+    const int y = q / W, x = q - y * W;
+    if (x > 0 && Bv[q - 1]) bb_union(par, q, q - 1);
+    if (y > 0) {
+      if (Bv[q - W]) bb_union(par, q, q - W);
+      if (c8) {
+        if (x > 0 && Bv[q - W - 1]) bb_union(par, q, q - W - 1);
+        if (x + 1 < W && Bv[q - W + 1]) bb_union(par, q, q - W + 1);
+      }
+    }
+  }
+  __syncthreads();
+  const unsigned nbx = (unsigned)(W + 1) / 2;
+  for (int q = tid; q < NP; q += nt) {
+    if (!Bv[q]) continue;
+    const unsigned root = bb_find(par, q);
+    const int y = q / W, x = q - y * W;
+    const unsigned k = c8 ? (unsigned)(y >> 1) * nbx + (unsigned)(x >> 1) : (unsigned)q;
+    atomicAdd(&area[root], 1u);
+    atomicMin(&key[root], k);
+    bb_st(&par[q], root);
+  }
+  __syncthreads();
+  unsigned long long best = 0;
+  for (int q = tid; q < NP; q += nt) {
+    if (!Bv[q] || bb_ld(&par[q]) != (unsigned)q) continue;
+    const unsigned long long val = ((unsigned long long)bb_ld(&area[q]) << 32) | (0xFFFFFFFFu - bb_ld(&key[q]));
+    best = val > best ? val : best;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long other = __shfl_xor(best, o);
+    best = other > best ? other : best;
+  }
+  if ((tid & 63) == 0) s_red[tid >> 6] = best;
+  __syncthreads();
+  best = 0;
+  for (int w = 0; w < (nt >> 6); ++w) best = s_red[w] > best ? s_red[w] : best;
+  if (best) {
+    const unsigned barea = (unsigned)(best >> 32), bkey = 0xFFFFFFFFu - (unsigned)best;
+    for (int q = tid; q < NP; q += nt)
+      if (Bv[q] && bb_ld(&par[q]) == (unsigned)q && bb_ld(&area[q]) == barea && bb_ld(&key[q]) == bkey) s_best = q;
+  }
+  __syncthreads();
+  const unsigned broot = s_best;
+  if (broot != 0xFFFFFFFFu) {
+    for (int q = tid; q < NP; q += nt) {
+      if (!Bv[q] || bb_ld(&par[q]) != broot) continue;
+      const int y = q / W, x = q - y * W;
+      atomicAdd(&colc[x], 1);
+      atomicAdd(&rowc[y], 1);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < W + H; i += nt) {
+    const int d = i < W ? 0 : 1, idx = i < W ? i : i - W;
+    if (bb_pass(K, cnt[i])) {
+      atomicMin(&s_lim[d][0], idx);
+      atomicMax(&s_lim[d][1], idx);
+      atomicAdd(&s_lim[d][2], 1);
+    }
+  }
+  __syncthreads();
+  if (tid < 2) {
+    // first_last = {first, last}; {first, 0} when one entry passes; {-1, -1} when none.
+    const int n = s_lim[tid][2];
+    int32_t* o = lims + ((int64_t)f * 2 + v) * 4 + 2 * tid;
+    o[0] = n ? s_lim[tid][0] : -1;
+    o[1] = n == 0 ? -1 : (n == 1 ? 0 : s_lim[tid][1]);
+  }
+}
+
+// ================================================================ host side
+
+struct lm_bb_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int max_batch = 0;
+  int64_t npix = 0, frame_stride = 0;
+  int view_y[2] = {0, 0};
+  lm_bb_params P{};
+  LmBBConst K{};
+  size_t ring_lds = 0, center_lds = 0, cc_lds = 0;
+  DevBuf<uint8_t> bkg, frames, luts, M, ring, bin;
+  DevBuf<int32_t> cal;
+  DevBuf<unsigned> cc;
+  HostBuf<const uint8_t*> fptr;
+  HostBuf<int32_t> lims;
+  int last_n = 0;
+  std::vector<lm_bb_frame> per;
+  std::vector<uint32_t> x_pos, yb_pos, ys_pos;
+  ~lm_bb_ctx() {
+    if (stream) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(stream);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+};
+
+namespace {
+
+void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params* bp) {
+  if (!su || !bp) throw std::invalid_argument("null setup / params");
+  if (su->method != 0)
+    throw std::invalid_argument("lm_bb_*: only method 0 (LocoMouse::computeBoundingBox) is on this path.");
+  const lm_bb_params& P = *bp;
+  if (P.conn_comp_connectivity != 4 && P.conn_comp_connectivity != 8)
+    throw std::invalid_argument("Invalid configuration parameter: conn_comp_connectivity must be either 4 or 8.");
+  if (P.median_filter_size % 2 == 0 || P.median_filter_size < 1 || P.median_filter_size > 63)
+    throw std::invalid_argument("Invalid configuration parameter: median_filter_size must be odd (1..63 here).");
+  if (P.min_pixel_visible < 0)
+    throw std::invalid_argument("Invalid configuration parameter: min_pixel_visible must be non-negative.");
+  if (P.moving_average_window % 2 == 0 || P.moving_average_window < 1)
+    throw std::invalid_argument("Invalid configuration parameter: moving_average_window must be odd.");
+  if (P.firstlast_semantics != LM_BB_FIRSTLAST_AS_EXECUTED && P.firstlast_semantics != LM_BB_FIRSTLAST_INTEGER)
+    throw std::invalid_argument("firstlast_semantics must be LM_BB_FIRSTLAST_AS_EXECUTED or LM_BB_FIRSTLAST_INTEGER.");
+  if (!su->background || !su->ind_warp_mapping) throw std::invalid_argument("background / calibration missing.");
+  const int VR = su->video_rows, VC = su->video_cols, NR = su->calib_rows, NC = su->calib_cols;
+  if (VR <= 0 || VC <= 0 || NR <= 0 || NC <= 0) throw std::invalid_argument("empty video or calibration.");
+  const int64_t npix = (int64_t)VR * VC;
+  for (int64_t i = 0; i < (int64_t)NR * NC; ++i)
+    if (su->ind_warp_mapping[i] < 0 || su->ind_warp_mapping[i] >= npix)
+      throw std::runtime_error("Calibration mapping indices out of range.");
+  const lm_rect vw[2] = {su->view_box_side, su->view_box_bottom};
+  for (int v = 0; v < 2; ++v) {
+    if (vw[v].x != 0 || vw[v].width != NC)
+      throw std::invalid_argument("BB pass: view boxes must span the corrected width (firstLastOverT reads I.cols sums, :975-976).");
+    if (vw[v].y < 0 || vw[v].height <= 0 || vw[v].y + vw[v].height > NR)
+      throw std::runtime_error("BB pass: view box outside the corrected image.");
+  }
+  if (vw[0].y < vw[1].y + vw[1].height && vw[1].y < vw[0].y + vw[0].height)
+    throw std::invalid_argument("BB pass: overlapping side and bottom view boxes are not supported.");
+  c->P = P;
+  c->npix = npix;
+  c->frame_stride = (npix + 255) / 256 * 256;
+  LmBBConst& K = c->K;
+  K.n_rows = NR;
+  K.n_cols = NC;
+  K.p = P.median_filter_size / 2;
+  K.hp = NR + 2 * K.p;
+  K.wp = NC + 2 * K.p;
+  K.thr = (P.median_filter_size * P.median_filter_size + 1) / 2;
+  K.flip = su->flip ? 1 : 0;
+  for (int v = 0; v < 2; ++v) {
+    K.view_y[v] = vw[v].y;
+    K.view_h[v] = vw[v].height;
+    c->view_y[v] = vw[v].y;
+  }
+  K.conn = P.conn_comp_connectivity;
+  K.semantics = P.firstlast_semantics;
+  K.min_pixel_visible = P.min_pixel_visible;
+  K.ring_n = 2 * K.p * K.wp + 2 * NR * K.p;
+  K.m_bytes = ((int64_t)K.hp * K.wp + 255) / 256 * 256;
+  K.bin_bytes = ((int64_t)NR * NC + 255) / 256 * 256;
+  K.cc_words = 3 * (int64_t)NC * (vw[0].height + vw[1].height);
+  const int p = K.p, p2 = 2 * p;
+  c->ring_lds = (size_t)K.ring_n + 4 * (size_t)p2 * K.wp + 2 * (size_t)K.hp * p2 + 2 * (size_t)K.hp * p;
+  const int IW = LM_BB_TW + p2, IH = LM_BB_TH + p2;
+  c->center_lds = (size_t)((IH * IW + 15) & ~15) + 2 * (size_t)LM_BB_TH * IW;
+  c->cc_lds = 4 * (size_t)(NC + std::max(vw[0].height, vw[1].height));
+  const size_t lds_max = 160 * 1024;
+  if (c->ring_lds > lds_max || c->center_lds > lds_max || c->cc_lds > lds_max)
+    throw std::invalid_argument("BB pass: frame size / median_filter_size exceed the 160 KiB LDS of one workgroup.");
+  if ((int64_t)NC * std::max(vw[0].height, vw[1].height) >= (1ll << 31))
+    throw std::invalid_argument("BB pass: view too large.");
+
+  HIPCHK(hipFuncSetAttribute((const void*)k_bb_ring, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->ring_lds));
+  HIPCHK(hipFuncSetAttribute((const void*)k_bb_center, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->center_lds));
+  HIPCHK(hipFuncSetAttribute((const void*)k_bb_cc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->cc_lds));
+
+  const int B = c->max_batch;
+  c->bkg.alloc((size_t)c->frame_stride);
+  HIPCHK(hipMemset(c->bkg.p, 0, c->bkg.n));
+  HIPCHK(hipMemcpy(c->bkg.p, su->background, (size_t)npix, hipMemcpyHostToDevice));
+  c->cal.alloc((size_t)NR * NC);
+  HIPCHK(hipMemcpy(c->cal.p, su->ind_warp_mapping, sizeof(int32_t) * NR * NC, hipMemcpyHostToDevice));
+  c->frames.alloc((size_t)c->frame_stride * B);
+  c->luts.alloc((size_t)256 * B);
+  c->M.alloc((size_t)K.m_bytes * B);
+  HIPCHK(hipMemset(c->M.p, 0, c->M.n));
+  c->ring.alloc((size_t)std::max(K.ring_n, 1));
+  HIPCHK(hipMemset(c->ring.p, 0, c->ring.n));  // I_median = zeros (:588)
+  c->bin.alloc((size_t)K.bin_bytes * B);
+  c->cc.alloc((size_t)K.cc_words * B);
+  c->fptr.alloc((size_t)B);
+  c->lims.alloc((size_t)8 * B);
+}
+
+// computeMouseBox's six values from the four limits of each view (:983-993)
+// plus the bottom-view offset (:636).
+lm_bb_frame bb_frame_values(const int32_t* l, int bottom_view_y) {
+  const int32_t *ls = l, *lb = l + 4;  // {row first, row last, col first, col last}
+  lm_bb_frame o;
+  o.x = (lb[1] > ls[1]) ? (double)lb[1] : (double)ls[1];
+  o.y_bottom = (double)lb[3];
+  o.y_side = (double)ls[3];
+  const unsigned wt = (unsigned)(ls[1] - ls[0]), wb = (unsigned)(lb[1] - lb[0]);
+  o.width = wt > wb ? (double)wt : (double)wb;
+  o.height_bottom = (double)(lb[3] - lb[2]);
+  o.height_side = (double)(ls[3] - ls[2]);
+  o.y_bottom += bottom_view_y;
+  return o;
+}
+
+void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool device_frames, lm_bb_frame* out) {
+  if (!frames) throw std::invalid_argument("frames is NULL");
+  if (n < 1 || n > c->max_batch) throw std::invalid_argument("n must be in [1, max_batch]");
+  if (pitch < c->npix) throw std::invalid_argument("frame_pitch smaller than one frame.");
+  HIPCHK(hipSetDevice(c->device));
+  const LmBBConst& K = c->K;
+  hipStream_t s = c->stream;
+  for (int i = 0; i < n; ++i) {
+    if (device_frames) {
+      c->fptr.p[i] = frames + (int64_t)i * pitch;
+    } else {
+      uint8_t* dst = c->frames.p + (int64_t)i * c->frame_stride;
+      HIPCHK(hipMemcpyAsync(dst, frames + (int64_t)i * pitch, (size_t)c->npix, hipMemcpyHostToDevice, s));
+      c->fptr.p[i] = dst;
+    }
+  }
+  const int64_t np = (int64_t)K.n_rows * K.n_cols;
+  k_minmax_lut<<<n, 1024, 0, s>>>(c->fptr.d, c->bkg.p, (int)c->npix, 0, nullptr, 0, c->luts.p);
+  k_bb_ingest<<<dim3((unsigned)((np + 1023) / 1024), n), 256, 0, s>>>(K, c->fptr.d, c->bkg.p, c->cal.p, c->luts.p,
+                                                                       c->M.p);
+  if (K.p > 0) k_bb_ring<<<1, 1024, c->ring_lds, s>>>(K, c->M.p, n, c->ring.p);
+  k_bb_center<<<dim3((unsigned)((K.n_cols + LM_BB_TW - 1) / LM_BB_TW), (unsigned)((K.n_rows + LM_BB_TH - 1) / LM_BB_TH),
+                     n),
+                256, c->center_lds, s>>>(K, c->M.p, c->bin.p);
+  k_bb_cc<<<dim3(2, n), 1024, c->cc_lds, s>>>(K, c->bin.p, c->cc.p, c->lims.d);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  c->last_n = n;
+  for (int i = 0; i < n; ++i) {
+    const lm_bb_frame o = bb_frame_values(c->lims.p + 8 * i, c->view_y[1]);
+    c->per.push_back(o);
+    if (out) out[i] = o;
+  }
+}
+
+// (uint32_t)double as the reference's x86-64 build evaluates it (cvttsd2si to
+// 64 bits, low 32 bits kept): negative values wrap (-1.0 -> 4294967295).
+uint32_t bb_u32(double d) {
+  if (!(d > -9.2e18 && d < 9.2e18)) return 0;
+  return (uint32_t)(uint64_t)(int64_t)d;
+}
+
+// medianvec (:1516-1533): sorts in place; the odd case returns v[N/2 - 1].
+double bb_medianvec(std::vector<double>& v) {
+  const int N = (int)v.size();
+  if (N == 1) return v[0];
+  std::sort(v.begin(), v.end());
+  const int h = N / 2;
+  return N % 2 == 0 ? (v[h - 1] + v[h]) / 2 : v[h - 1];
+}
+
+// stdvec (:1535-1556): sample standard deviation, accumulated in order.
+double bb_stdvec(const std::vector<double>& v) {
+  const int N = (int)v.size();
+  if (N == 1) return 0.0;
+  double sum = 0.0;
+  for (double x : v) sum += x;
+  const double mean = sum / N;
+  double sq = 0.0;
+  for (double x : v) {
+    const double d = x - mean;
+    sq = sq + d * d;
+  }
+  return std::sqrt(sq / (N - 1));
+}
+
+// vecmovingaverage (:1558-1608): centred window average, floor-rounded; the
+// first N/2 and last N/2 + 1 samples are copied.
+void bb_movavg(const std::vector<double>& v, std::vector<uint32_t>& out, int N) {
+  const size_t n = v.size();
+  out.assign(n, 0);
+  if ((size_t)N >= n) {
+    for (size_t i = 0; i < n; ++i) out[i] = bb_u32(v[i]);
+    return;
+  }
+  const int h = N / 2;
+  double cur = 0;
+  for (int i = 0; i < h; ++i) out[i] = bb_u32(v[i]);
+  for (int i = 0; i < N; ++i) cur += v[i];
+  out[h] = bb_u32(std::floor(cur / N));
+  for (size_t i = 0; i + N < n; ++i) {
+    cur = cur - v[i] + v[i + N];
+    out[h + 1 + i] = bb_u32(std::floor(cur / N));
+  }
+  for (size_t i = n - h - 1; i < n; ++i) out[i] = bb_u32(v[i]);
+}
+
+void bb_finish(lm_bb_ctx* c, lm_bb_result* out) {
+  const size_t N = c->per.size();
+  if (N == 0) throw std::invalid_argument("lm_bb_finish: no frame was pushed.");
+  std::vector<double> x(N), yb(N), ys(N), w(N), hb(N), ht(N);
+  for (size_t i = 0; i < N; ++i) {
+    x[i] = c->per[i].x;
+    yb[i] = c->per[i].y_bottom;
+    ys[i] = c->per[i].y_side;
+    w[i] = c->per[i].width;
+    hb[i] = c->per[i].height_bottom;
+    ht[i] = c->per[i].height_side;
+  }
+  // computeMouseBoxSize (:1481-1506)
+  const double mw = bb_medianvec(w), mhb = bb_medianvec(hb), mht = bb_medianvec(ht);
+  const double sw = bb_stdvec(w), shb = bb_stdvec(hb), sht = bb_stdvec(ht);
+  const uint32_t w3 = bb_u32(mw + 3 * sw), hb3 = bb_u32(mhb + 3 * shb), ht3 = bb_u32(mht + 3 * sht);
+  const uint32_t fw = ((double)w3 < w[N - 1]) ? w3 : bb_u32(w[N - 1]);
+  const uint32_t fhb = ((double)hb3 < hb[N - 1]) ? hb3 : bb_u32(hb[N - 1]);
+  const uint32_t fht = ((double)ht3 < ht[N - 1]) ? ht3 : bb_u32(ht[N - 1]);
+  bb_movavg(x, c->x_pos, c->P.moving_average_window);
+  bb_movavg(yb, c->yb_pos, c->P.moving_average_window);
+  bb_movavg(ys, c->ys_pos, c->P.moving_average_window);
+  out->n_frames = (int32_t)N;
+  out->reserved0 = 0;
+  out->bb_side_mouse = lm_rect{0, 0, (int32_t)fw, (int32_t)fht};
+  out->bb_bottom_mouse = lm_rect{0, 0, (int32_t)fw, (int32_t)fhb};
+  out->x_pos = c->x_pos.data();
+  out->y_bottom_pos = c->yb_pos.data();
+  out->y_side_pos = c->ys_pos.data();
+  out->frames = c->per.data();
+}
+
+}  // namespace
+
+LM_API lm_status lm_bb_create(int32_t device, const lm_setup* setup, const lm_bb_params* params, int32_t max_batch,
+                              lm_bb_ctx** out) {
+  if (!out) return fail(LM_ERR_INVALID_ARGUMENT, "out is NULL");
+  *out = nullptr;
+  if (max_batch <= 0) return fail(LM_ERR_INVALID_ARGUMENT, "max_batch must be > 0");
+  lm_bb_ctx* c = new lm_bb_ctx();
+  lm_status s = guarded([&] {
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) throw HipError("invalid HIP device index");
+    c->device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->max_batch = max_batch;
+    bb_validate_and_build(c, setup, params);
+  });
+  if (s != LM_OK) {
+    delete c;
+    return s;
+  }
+  *out = c;
+  return LM_OK;
+}
+
+LM_API void lm_bb_destroy(lm_bb_ctx* ctx) { delete ctx; }
+
+LM_API lm_status lm_bb_push(lm_bb_ctx* ctx, const uint8_t* frames, int64_t frame_pitch, int32_t n, lm_bb_frame* out) {
+  if (!ctx) return fail(LM_ERR_INVALID_ARGUMENT, "null ctx");
+  return guarded([&] { bb_push(ctx, frames, frame_pitch, n, false, out); });
+}
+
+LM_API lm_status lm_bb_push_device(lm_bb_ctx* ctx, const uint8_t* d_frames, int64_t frame_pitch, int32_t n,
+                                   lm_bb_frame* out) {
+  if (!ctx) return fail(LM_ERR_INVALID_ARGUMENT, "null ctx");
+  return guarded([&] { bb_push(ctx, d_frames, frame_pitch, n, true, out); });
+}
+
+LM_API lm_status lm_bb_finish(lm_bb_ctx* ctx, lm_bb_result* out) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  return guarded([&] { bb_finish(ctx, out); });
+}
+
+LM_API lm_status lm_bb_debug_binary(lm_bb_ctx* ctx, int32_t f, uint8_t* out, int32_t rows, int32_t cols) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  if (f < 0 || f >= ctx->last_n) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
+  if (rows != ctx->K.n_rows || cols != ctx->K.n_cols) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
+  return guarded([&] {
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipMemcpy(out, ctx->bin.p + (int64_t)f * ctx->K.bin_bytes, (size_t)rows * cols, hipMemcpyDeviceToHost));
+  });
+}
+
+LM_API void* lm_bb_stream(lm_bb_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }

@@ -1193,3 +1193,6 @@ LM_API lm_status lm_synth_frames_device(int32_t device, uint8_t* d_out, int32_t 
     HIPCHK(hipDeviceSynchronize());
   });
 }
+
+// ------------------------------------------------ whole-video BB pass (method 0)
+#include "lm_bbox.hip"

@@ -10,7 +10,7 @@ import subprocess
 
 import numpy as np
 
-from .abi import LM_OK, lm_batch_result, lm_geometry, result_to_numpy
+from .abi import BB_FRAME_DTYPE, LM_OK, lm_batch_result, lm_bb_result, lm_geometry, result_to_numpy
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -21,6 +21,8 @@ EXPORTED = (
     "lm_abi_version", "lm_last_error", "lm_ctx_create", "lm_ctx_destroy", "lm_get_geometry", "lm_ctx_stream",
     "lm_detect_batch", "lm_detect_batch_device", "lm_ctx_set_debug", "lm_debug_scores", "lm_debug_tail_mask",
     "lm_debug_kernel_times", "lm_debug_kernel_spans", "lm_synth_frames_device",
+    "lm_bb_create", "lm_bb_destroy", "lm_bb_push", "lm_bb_push_device", "lm_bb_finish", "lm_bb_debug_binary",
+    "lm_bb_stream",
 )
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -90,6 +92,14 @@ def lib():
         L.lm_debug_kernel_spans.restype = C.c_int32
         L.lm_synth_frames_device.argtypes = [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32,
                                              C.c_int64]
+        L.lm_bb_create.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
+        L.lm_bb_destroy.argtypes = [C.c_void_p]
+        for fn in (L.lm_bb_push, L.lm_bb_push_device):
+            fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]
+        L.lm_bb_finish.argtypes = [C.c_void_p, C.POINTER(lm_bb_result)]
+        L.lm_bb_debug_binary.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
+        L.lm_bb_stream.argtypes = [C.c_void_p]
+        L.lm_bb_stream.restype = C.c_void_p
         _lib = L
     return _lib
 
@@ -191,6 +201,65 @@ class Context:
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
             lib().lm_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BBContext:
+    """One lm_bb_ctx: the whole-video bounding-box pass (method 0,
+    LocoMouse::computeBoundingBox, LocoMouse_class.cpp:579-653) on one HIP
+    device.  Frames are pushed in video order; finish() post-processes."""
+
+    def __init__(self, setup, bb_params, max_batch=64, device=0):
+        self._setup, self._params = setup, bb_params  # keep the structs alive
+        self._h = C.c_void_p()
+        _check(lib().lm_bb_create(device, C.byref(setup), C.byref(bb_params), max_batch, C.byref(self._h)))
+        self.max_batch = max_batch
+        self.rows, self.cols = setup.calib_rows, setup.calib_cols
+
+    def push(self, frames):
+        """Host frames [n, rows, cols] u8 -> per-frame values (BB_FRAME_DTYPE)."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        out = np.zeros(frames.shape[0], dtype=BB_FRAME_DTYPE)
+        _check(lib().lm_bb_push(self._h, frames.ctypes.data, frames.shape[1] * frames.shape[2], frames.shape[0],
+                                out.ctypes.data))
+        return out
+
+    def push_device(self, d_frames_ptr, pitch, n, values=True):
+        out = np.zeros(n, dtype=BB_FRAME_DTYPE) if values else None
+        _check(lib().lm_bb_push_device(self._h, C.c_void_p(d_frames_ptr), pitch, n,
+                                       out.ctypes.data if values else None))
+        return out
+
+    def finish(self):
+        r = lm_bb_result()
+        _check(lib().lm_bb_finish(self._h, C.byref(r)))
+        n = r.n_frames
+
+        def arr(ptr, dtype):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype).copy()
+        per = np.frombuffer(C.cast(r.frames, C.POINTER(C.c_uint8 * (n * BB_FRAME_DTYPE.itemsize))).contents,
+                            dtype=BB_FRAME_DTYPE, count=n).copy()
+        return {"frames": per, "x_pos": arr(r.x_pos, np.uint32), "y_bottom_pos": arr(r.y_bottom_pos, np.uint32),
+                "y_side_pos": arr(r.y_side_pos, np.uint32), "bb_side_mouse": r.bb_side_mouse.tuple(),
+                "bb_bottom_mouse": r.bb_bottom_mouse.tuple()}
+
+    def debug_binary(self, f):
+        out = np.zeros((self.rows, self.cols), dtype=np.uint8)
+        _check(lib().lm_bb_debug_binary(self._h, f, out.ctypes.data, self.rows, self.cols))
+        return out
+
+    def stream(self):
+        return lib().lm_bb_stream(self._h)
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            lib().lm_bb_destroy(self._h)
             self._h = C.c_void_p()
 
     def __del__(self):

@@ -608,6 +608,14 @@ class LocoMouseOracle {
   // LocoMouse::readFrame(Mat&), :1273-1333 (+ LocoMouse_TM::readFrame, TM.cpp:243-249)
   void readFrame(const uint8_t* F_raw) {
     CURRENT_FRAME += 1;
+    correct_frame(F_raw, BKG.data(), CAL.data(), VR, VC, N_ROWS, N_COLS, IMAGE_FLIP, METHOD == 1 || METHOD == 2,
+                  I_PAD.row(I_UNPAD.y) + I_UNPAD.x, I_PAD.cols);
+  }
+
+  // The image work of readFrame(Mat& I) (:1302-1327): subtract, normalize,
+  // correctImage, flip, written into rows of I at dst (row stride dst_stride).
+  static void correct_frame(const uint8_t* F_raw, const uint8_t* BKG, const int32_t* CAL, int VR, int VC, int N_ROWS,
+                            int N_COLS, bool flip, bool tm_adjust, uint8_t* dst0, int dst_stride) {
     const size_t NP = (size_t)VR * VC;
     std::vector<uint8_t> F(NP);
     for (size_t i = 0; i < NP; ++i) F[i] = F_raw[i] > BKG[i] ? (uint8_t)(F_raw[i] - BKG[i]) : 0;  // subtract (:1304)
@@ -633,12 +641,12 @@ class LocoMouseOracle {
     // TM imadjust(I, I, 0, 0.6, 0, 1) (LocoMouse_class.cpp:3204-3242)
     uint8_t adj[256];
     for (int p = 0; p < 256; ++p) adj[p] = (uint8_t)p;
-    if (METHOD == 1 || METHOD == 2) imadjust_lut(0, 0.6, 0, 1, adj);
-    // correctImage (:1337-1406) + flip(I, I, 1) (:1323-1327), writing into I_PAD(I_UNPAD)
+    if (tm_adjust) imadjust_lut(0, 0.6, 0, 1, adj);
+    // correctImage (:1337-1406) + flip(I, I, 1) (:1323-1327)
     for (int r = 0; r < N_ROWS; ++r) {
-      uint8_t* dst = I_PAD.row(I_UNPAD.y + r) + I_UNPAD.x;
+      uint8_t* dst = dst0 + (size_t)r * dst_stride;
       for (int c = 0; c < N_COLS; ++c) {
-        int cs = IMAGE_FLIP ? (N_COLS - 1 - c) : c;
+        int cs = flip ? (N_COLS - 1 - c) : c;
         dst[c] = adj[lut[F[CAL[(size_t)r * N_COLS + cs]]]];
       }
     }
@@ -1032,6 +1040,232 @@ class LocoMouseOracle {
   std::vector<Matf> dbg_scores;
 };
 
+// ------------------------------------------------ whole-video BB pass (method 0)
+// LocoMouse::computeBoundingBox (LocoMouse_class.cpp:579-653).
+
+// medianBlur(src, dst, ksize), CV_8UC1 (imgproc median_blur.cpp): the exact
+// median (rank n/2 of the n = ksize^2 window values) with BORDER_REPLICATE;
+// src is the whole matrix (no ROI parent).  Huang's running histogram per row.
+static Mat8 medianBlur8u(const Mat8& src, int ksize) {
+  if (ksize == 1) return src;
+  const int p = ksize / 2, R = src.rows, C = src.cols, half = ksize * ksize / 2;
+  auto cl = [](int v, int n) { return v < 0 ? 0 : (v >= n ? n - 1 : v); };
+  Mat8 out(R, C, 0);
+  for (int r = 0; r < R; ++r) {
+    int hist[256] = {0};
+    for (int dr = -p; dr <= p; ++dr)
+      for (int dc = -p; dc <= p; ++dc) hist[src.at(cl(r + dr, R), cl(dc, C))]++;
+    for (int c = 0; c < C; ++c) {
+      if (c > 0)
+        for (int dr = -p; dr <= p; ++dr) {
+          hist[src.at(cl(r + dr, R), cl(c - 1 - p, C))]--;
+          hist[src.at(cl(r + dr, R), cl(c + p, C))]++;
+        }
+      int s = 0, v = 0;
+      while ((s += hist[v]) <= half) ++v;
+      out.at(r, c) = (uint8_t)v;
+    }
+  }
+  return out;
+}
+
+// firstLastOverT<int> (LocoMouse_class.hpp:411-440).  The sums are CV_32S but
+// are read through values.ptr<float>(0) (:419): as executed, each int32 sum's
+// bit pattern is compared as a float with (float)th.  integer = 1 compares the
+// int32 values instead.  Note first_last[1] stays 0 when exactly one entry
+// passes (the index bookkeeping of :424-433).
+static void firstLastOverT(const int32_t* v, unsigned L, int first_last[2], int th, bool integer) {
+  bool has_first = false;
+  first_last[0] = 0;
+  first_last[1] = 0;
+  int index = 0;
+  for (unsigned i = 0; i < L; ++i) {
+    bool pass;
+    if (integer) {
+      pass = v[i] >= th;
+    } else {
+      float f;
+      std::memcpy(&f, &v[i], 4);
+      pass = f >= (float)th;
+    }
+    if (pass) {
+      first_last[index] = (int)i;
+      if (!has_first) {
+        index = 1;
+        has_first = true;
+      }
+    }
+  }
+  if (!has_first) {
+    first_last[0] = -1;
+    first_last[1] = -1;
+  }
+}
+
+// (uint32_t)double as the reference's x86-64 build evaluates it (cvttsd2si to
+// 64 bits, low 32 bits kept): negative values wrap (e.g. -1.0 -> 4294967295).
+static uint32_t x86_u32(double d) {
+  if (!(d > -9.2e18 && d < 9.2e18)) return 0;
+  return (uint32_t)(uint64_t)(int64_t)d;
+}
+
+// medianvec (:1516-1533): sorts v in place; odd N returns v[N/2 - 1].
+static double medianvec(std::vector<double>& v, int N) {
+  if (N == 1) return v[0];
+  std::sort(v.begin(), v.end());
+  int half = N / 2;
+  if (N % 2 == 0) return (v[half - 1] + v[half]) / 2;
+  return v[half - 1];
+}
+
+// stdvec (:1535-1556): sample standard deviation, summed in vector order.
+static double stdvec(const std::vector<double>& v, int N) {
+  if (N == 1) return 0.0;
+  double sum = 0.0;
+  for (int i = 0; i < N; ++i) sum += v[i];
+  double mean = sum / N;
+  double sq = 0.0;
+  for (int i = 0; i < N; ++i) {
+    double d = v[i] - mean;
+    sq = sq + d * d;
+  }
+  return std::sqrt(sq / (N - 1));
+}
+
+// vecmovingaverage (:1558-1608).
+static void vecmovingaverage(const std::vector<double>& v, std::vector<uint32_t>& vout, int N_window) {
+  const size_t n = v.size();
+  vout.assign(n, 0);
+  if ((size_t)N_window >= n) {
+    for (size_t i = 0; i < n; ++i) vout[i] = x86_u32(v[i]);
+    return;
+  }
+  double cur = 0;
+  int h = N_window / 2;
+  for (int i = 0; i < h; ++i) vout[i] = x86_u32(v[i]);
+  for (int i = 0; i < N_window; ++i) cur += v[i];
+  vout[h] = x86_u32(std::floor(cur / N_window));
+  for (size_t i = 0; i < n - N_window; ++i) {
+    cur = cur - v[i] + v[i + N_window];
+    vout[h + 1 + i] = x86_u32(std::floor(cur / N_window));
+  }
+  for (size_t i = n - h - 1; i < n; ++i) vout[i] = x86_u32(v[i]);
+}
+
+class BBOracle {
+ public:
+  BBOracle(const lm_setup& su, const lm_bb_params& bp) : P(bp) {
+    if (su.method != 0) throw std::invalid_argument("BB pass: only method 0 (LocoMouse::computeBoundingBox) is restated.");
+    if (P.median_filter_size % 2 == 0 || P.median_filter_size < 1 || P.median_filter_size > 63)
+      throw std::invalid_argument("Invalid configuration parameter: median_filter_size must be odd.");
+    if (P.min_pixel_visible < 0)
+      throw std::invalid_argument("Invalid configuration parameter: min_pixel_visible must be non-negative.");
+    if (P.moving_average_window % 2 == 0 || P.moving_average_window < 1)
+      throw std::invalid_argument("Invalid configuration parameter: moving_average_window must be odd.");
+    if (P.conn_comp_connectivity != 4 && P.conn_comp_connectivity != 8)
+      throw std::invalid_argument("Invalid configuration parameter: conn_comp_connectivity must be either 4 or 8.");
+    VR = su.video_rows;
+    VC = su.video_cols;
+    N_ROWS = su.calib_rows;
+    N_COLS = su.calib_cols;
+    BKG.assign(su.background, su.background + (size_t)VR * VC);
+    CAL.assign(su.ind_warp_mapping, su.ind_warp_mapping + (size_t)N_ROWS * N_COLS);
+    flip = su.flip != 0;
+    side = Rect(su.view_box_side.x, su.view_box_side.y, su.view_box_side.width, su.view_box_side.height);
+    bottom = Rect(su.view_box_bottom.x, su.view_box_bottom.y, su.view_box_bottom.width, su.view_box_bottom.height);
+    // :585-591
+    pad = P.median_filter_size / 2;
+    I_median = Mat8(N_ROWS + 2 * pad, N_COLS + 2 * pad, 0);
+  }
+
+  // One iteration of the frame loop :614-626.
+  void frame(const uint8_t* F) {
+    // readFrame(I_center): writes the central ROI of I_median only.
+    LocoMouseOracle::correct_frame(F, BKG.data(), CAL.data(), VR, VC, N_ROWS, N_COLS, flip, false,
+                                   I_median.row(pad) + pad, I_median.cols);
+    // computeMouseBox :948-997
+    I_median = medianBlur8u(I_median, P.median_filter_size);  // in place (:952), border ring kept
+    Mat8 I(N_ROWS, N_COLS, 0);
+    for (int r = 0; r < N_ROWS; ++r)
+      for (int c = 0; c < N_COLS; ++c) {
+        uint8_t& v = I_median.at(pad + r, pad + c);
+        v = v > 2.55 ? 1 : 0;  // threshold(I, I, 2.55, 1, THRESH_BINARY) (:955)
+        I.at(r, c) = v;
+      }
+    binary.push_back(I);
+    int lrs[2], lcs[2], lrb[2], lcb[2];
+    view_lims(I, side, lrs, lcs);
+    view_lims(I, bottom, lrb, lcb);
+    lm_bb_frame o;
+    o.x = (lrb[1] > lrs[1]) ? (double)lrb[1] : (double)lrs[1];  // :983
+    o.y_bottom = (double)lcb[1];
+    o.y_side = (double)lcs[1];
+    unsigned wt = (unsigned)(lrs[1] - lrs[0]), wb = (unsigned)(lrb[1] - lrb[0]);  // :988-991
+    o.width = wt > wb ? (double)wt : (double)wb;
+    o.height_bottom = (double)(lcb[1] - lcb[0]);
+    o.height_side = (double)(lcs[1] - lcs[0]);
+    o.y_bottom += bottom.y;  // :636
+    frames.push_back(o);
+  }
+
+  // largestBWAreaObject (:921-946) on the view, then reduce + firstLastOverT
+  // (:961-978).  The view's pixels of I_median become the 0/255 mask.
+  void view_lims(const Mat8& I, const Rect& v, int lr[2], int lc[2]) {
+    Mat8 bin(v.height, v.width, 0);
+    for (int r = 0; r < v.height; ++r)
+      for (int c = 0; c < v.width; ++c) bin.at(r, c) = I.at(v.y + r, v.x + c);
+    Mat8 m = selectLargestRegion(bin, P.conn_comp_connectivity);
+    std::vector<int32_t> rowsum(v.width, 0), colsum(v.height, 0);
+    for (int r = 0; r < v.height; ++r)
+      for (int c = 0; c < v.width; ++c) {
+        rowsum[c] += m.at(r, c);
+        colsum[r] += m.at(r, c);
+        I_median.at(pad + v.y + r, pad + v.x + c) = m.at(r, c);
+      }
+    const bool integer = P.firstlast_semantics == LM_BB_FIRSTLAST_INTEGER;
+    firstLastOverT(rowsum.data(), (unsigned)N_COLS, lr, P.min_pixel_visible, integer);  // L = I.cols (:975)
+    firstLastOverT(colsum.data(), (unsigned)v.height, lc, P.min_pixel_visible, integer);
+  }
+
+  // :628-646
+  void finish() {
+    const int N = (int)frames.size();
+    std::vector<double> bb_x(N), bb_yb(N), bb_ys(N), bw(N), bhb(N), bht(N);
+    for (int i = 0; i < N; ++i) {
+      bb_x[i] = frames[i].x;
+      bb_yb[i] = frames[i].y_bottom;
+      bb_ys[i] = frames[i].y_side;
+      bw[i] = frames[i].width;
+      bhb[i] = frames[i].height_bottom;
+      bht[i] = frames[i].height_side;
+    }
+    // computeMouseBoxSize (:1481-1506): the medians sort the vectors first.
+    double mw = medianvec(bw, N), mhb = medianvec(bhb, N), mht = medianvec(bht, N);
+    double sw = stdvec(bw, N), shb = stdvec(bhb, N), sht = stdvec(bht, N);
+    uint32_t w3 = x86_u32(mw + 3 * sw), hb3 = x86_u32(mhb + 3 * shb), ht3 = x86_u32(mht + 3 * sht);
+    uint32_t fw = ((double)w3 < bw[N - 1]) ? w3 : x86_u32(bw[N - 1]);
+    uint32_t fhb = ((double)hb3 < bhb[N - 1]) ? hb3 : x86_u32(bhb[N - 1]);
+    uint32_t fht = ((double)ht3 < bht[N - 1]) ? ht3 : x86_u32(bht[N - 1]);
+    bb_side = lm_rect{0, 0, (int32_t)fw, (int32_t)fht};
+    bb_bottom = lm_rect{0, 0, (int32_t)fw, (int32_t)fhb};
+    vecmovingaverage(bb_x, x_pos, P.moving_average_window);
+    vecmovingaverage(bb_yb, yb_pos, P.moving_average_window);
+    vecmovingaverage(bb_ys, ys_pos, P.moving_average_window);
+  }
+
+  lm_bb_params P;
+  int VR = 0, VC = 0, N_ROWS = 0, N_COLS = 0, pad = 0;
+  bool flip = false;
+  std::vector<uint8_t> BKG;
+  std::vector<int32_t> CAL;
+  Rect side, bottom;
+  Mat8 I_median;
+  std::vector<lm_bb_frame> frames;
+  std::vector<Mat8> binary;
+  lm_rect bb_side{}, bb_bottom{};
+  std::vector<uint32_t> x_pos, yb_pos, ys_pos;
+};
+
 }  // namespace lmo
 
 // ------------------------------------------------------------------ C API
@@ -1157,4 +1391,54 @@ LMO_API void lmo_synth_frames(int32_t rows, int32_t cols, int64_t first, int32_t
 
 LMO_API void lmo_synth_background(int32_t rows, int32_t cols, uint8_t* out) {
   for (int64_t i = 0; i < (int64_t)rows * cols; ++i) out[i] = lm_synth_background(i);
+}
+
+/* Whole-video BB pass (method 0) over frames 0..n-1: per-frame values, the
+ * final box sizes and BR corner tracks; binary (optional) receives the
+ * thresholded median images [n][N_ROWS][N_COLS]. */
+LMO_API int lmo_bb_run(const lm_setup* su, const lm_bb_params* bp, const uint8_t* frames, int64_t pitch, int32_t n,
+                       lm_bb_frame* per_frame, lm_rect* bb_side, lm_rect* bb_bottom, uint32_t* x_pos,
+                       uint32_t* yb_pos, uint32_t* ys_pos, uint8_t* binary) {
+  try {
+    if (n < 1) throw std::invalid_argument("BB pass needs at least one frame.");
+    lmo::BBOracle B(*su, *bp);
+    for (int32_t f = 0; f < n; ++f) B.frame(frames + (size_t)f * pitch);
+    B.finish();
+    for (int32_t f = 0; f < n; ++f) {
+      per_frame[f] = B.frames[f];
+      x_pos[f] = B.x_pos[f];
+      yb_pos[f] = B.yb_pos[f];
+      ys_pos[f] = B.ys_pos[f];
+      if (binary) std::memcpy(binary + (size_t)f * B.N_ROWS * B.N_COLS, B.binary[f].d.data(), B.binary[f].d.size());
+    }
+    *bb_side = B.bb_side;
+    *bb_bottom = B.bb_bottom;
+    return LM_OK;
+  } catch (const std::invalid_argument& e) {
+    return map_exc(e, LM_ERR_INVALID_ARGUMENT);
+  } catch (const std::exception& e) {
+    return map_exc(e, LM_ERR_RUNTIME);
+  }
+}
+
+/* Pieces of the BB pass, for the oracle's own unit tests. */
+LMO_API void lmo_median_blur(const uint8_t* src, int32_t rows, int32_t cols, int32_t ksize, uint8_t* dst) {
+  lmo::Mat8 m(rows, cols, 0);
+  std::memcpy(m.d.data(), src, (size_t)rows * cols);
+  lmo::Mat8 o = lmo::medianBlur8u(m, ksize);
+  std::memcpy(dst, o.d.data(), (size_t)rows * cols);
+}
+
+LMO_API void lmo_first_last(const int32_t* v, uint32_t L, int32_t th, int32_t integer, int32_t* out2) {
+  int fl[2];
+  lmo::firstLastOverT(v, L, fl, th, integer != 0);
+  out2[0] = fl[0];
+  out2[1] = fl[1];
+}
+
+LMO_API void lmo_movavg(const double* v, int32_t n, int32_t window, uint32_t* out) {
+  std::vector<double> in(v, v + n);
+  std::vector<uint32_t> o;
+  lmo::vecmovingaverage(in, o, window);
+  std::memcpy(out, o.data(), sizeof(uint32_t) * n);
 }

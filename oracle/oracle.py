@@ -9,7 +9,7 @@ import subprocess
 
 import numpy as np
 
-from locomouse_cpp_amd.abi import lm_batch_result, lm_geometry, result_to_numpy
+from locomouse_cpp_amd.abi import BB_FRAME_DTYPE, lm_batch_result, lm_geometry, lm_rect, result_to_numpy
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liblm_oracle.so")
@@ -43,6 +43,12 @@ def lib():
         L.lmo_std_sort_perm.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
         L.lmo_synth_frames.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_void_p]
         L.lmo_synth_background.argtypes = [C.c_int32, C.c_int32, C.c_void_p]
+        L.lmo_median_blur.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
+        L.lmo_first_last.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_void_p]
+        L.lmo_movavg.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
+        L.lmo_bb_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p,
+                                 C.POINTER(lm_rect), C.POINTER(lm_rect), C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_void_p]
         _lib = L
     return _lib
 
@@ -128,4 +134,46 @@ def synth_frames_c(rows, cols, first, n):
 def synth_background_c(rows, cols):
     out = np.zeros((rows, cols), dtype=np.uint8)
     lib().lmo_synth_background(rows, cols, out.ctypes.data)
+    return out
+
+
+def bb_run(setup, bb_params, frames, binary=False):
+    """Whole-video BB pass, method 0 (LocoMouse::computeBoundingBox,
+    LocoMouse_class.cpp:579-653) over frames [n, rows, cols] u8."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    n = frames.shape[0]
+    per = np.zeros(n, dtype=BB_FRAME_DTYPE)
+    xs, yb, ys = (np.zeros(n, dtype=np.uint32) for _ in range(3))
+    side, bottom = lm_rect(), lm_rect()
+    binimg = np.zeros((n, setup.calib_rows, setup.calib_cols), dtype=np.uint8) if binary else None
+    rc = lib().lmo_bb_run(C.byref(setup), C.byref(bb_params), frames.ctypes.data, frames.shape[1] * frames.shape[2], n,
+                          per.ctypes.data, C.byref(side), C.byref(bottom), xs.ctypes.data, yb.ctypes.data,
+                          ys.ctypes.data, binimg.ctypes.data if binary else None)
+    if rc:
+        raise OracleError(rc, lib().lmo_last_error().decode())
+    out = {"frames": per, "x_pos": xs, "y_bottom_pos": yb, "y_side_pos": ys, "bb_side_mouse": side.tuple(),
+           "bb_bottom_mouse": bottom.tuple()}
+    if binary:
+        out["binary"] = binimg
+    return out
+
+
+def median_blur(img, ksize):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = np.zeros_like(img)
+    lib().lmo_median_blur(img.ctypes.data, img.shape[0], img.shape[1], ksize, out.ctypes.data)
+    return out
+
+
+def first_last(values, th, integer=False, length=None):
+    v = np.ascontiguousarray(values, dtype=np.int32)
+    out = np.zeros(2, dtype=np.int32)
+    lib().lmo_first_last(v.ctypes.data, len(v) if length is None else length, th, 1 if integer else 0, out.ctypes.data)
+    return tuple(int(x) for x in out)
+
+
+def moving_average(values, window):
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    out = np.zeros(len(v), dtype=np.uint32)
+    lib().lmo_movavg(v.ctypes.data, len(v), window, out.ctypes.data)
     return out

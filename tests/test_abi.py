@@ -42,7 +42,8 @@ def test_last_error_and_null_arguments_without_gpu():
 
 
 @pytest.mark.parametrize("name", ["lm_rect", "lm_location_prior", "lm_params", "lm_detector", "lm_model", "lm_setup",
-                                  "lm_geometry", "lm_candidate", "lm_p22d", "lm_batch_result"])
+                                  "lm_geometry", "lm_candidate", "lm_p22d", "lm_batch_result",
+                                  "lm_bb_params", "lm_bb_frame", "lm_bb_result"])
 def test_struct_layout_matches_header(tmp_path, name):
     src = tmp_path / "sz.c"
     src.write_text(f'#include <stdio.h>\n#include "locomouse_hip.h"\nint main(void){{printf("%zu", sizeof({name}));}}\n')
