@@ -18,10 +18,12 @@
 // Per batch of n frames:
 //   k_minmax_lut  normalize LUT per frame (shared with the detection path)
 //   k_bb_ingest   I_median centre indicator  M[f] = [corrected frame >= 3]
+//   k_bb_bands    the border bands of M[f] in k_bb_ring's LDS layout
 //   k_bb_ring     ring state recurrence; writes ring_{f-1} into M[f]
 //   k_bb_center   11x11 (k x k) majority over M[f] -> thresholded image bin[f]
-//   k_bb_cc       per (frame, view): largest component (union-find in global
-//                 memory), row/column counts, firstLastOverT -> 4 limits
+//   k_bb_cc       per (frame, view): largest component (row runs + union-find
+//                 in LDS; per-pixel union-find in global memory when a view
+//                 has too many runs), row/column counts, firstLastOverT
 // The host turns the limits into computeMouseBox's six values and runs the
 // whole-video post-processing in lm_bb_finish.
 
@@ -33,10 +35,10 @@ struct LmBBConst {
   int32_t view_y[2], view_h[2];  // 0 side, 1 bottom (x = 0, width = n_cols)
   int32_t conn, semantics, min_pixel_visible;
   int32_t ring_n;          // ring state bytes: top [p][wp] | bottom [p][wp] | left [n_rows][p] | right [n_rows][p]
-  int32_t pad_;
+  int32_t band_n;          // per-frame band bytes (k_bb_bands), multiple of 16
   int64_t m_bytes;         // per-frame I_median indicator image (hp x wp)
   int64_t bin_bytes;       // per-frame thresholded image (n_rows x n_cols)
-  int64_t cc_words;        // per-frame union-find scratch (3 words per view pixel)
+  int64_t cc_words;        // per-frame run tables for views with many runs (6 words per possible run)
 };
 
 // ---------------------------------------------------------------- k_bb_ingest
@@ -65,105 +67,220 @@ __global__ __launch_bounds__(256) void k_bb_ingest(const LmBBConst K, const uint
   }
 }
 
+// ----------------------------------------------------------------- k_bb_bands
+// Per frame, the 2p-wide bands of M[f] along the border in exactly the LDS
+// layout k_bb_ring uses (top [2p][wp] | bottom [2p][wp] | left [hp][2p] |
+// right [hp][2p]), so the sequential kernel fetches a frame with contiguous
+// dword loads issued one frame ahead.  Ring positions are placeholders (the
+// ring kernel overwrites them from its state).
+__global__ __launch_bounds__(256) void k_bb_bands(const LmBBConst K, const uint8_t* __restrict__ M,
+                                                  uint8_t* __restrict__ bands) {
+  const int f = blockIdx.y, p2 = 2 * K.p, wp = K.wp, hp = K.hp;
+  const uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
+  const int q0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int tb = p2 * wp, lb = hp * p2;
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int q = q0 + k;
+    if (q >= 2 * tb + 2 * lb) break;
+    int r, c;
+    if (q < 2 * tb) {
+      const int qq = q < tb ? q : q - tb;
+      r = qq / wp;
+      c = qq - r * wp;
+      if (q >= tb) r += hp - p2;
+    } else {
+      const int qq = q - 2 * tb, side = qq >= lb, q2 = side ? qq - lb : qq;
+      r = q2 / p2;
+      c = q2 - r * p2 + (side ? wp - p2 : 0);
+    }
+    w |= (uint32_t)Mf[(int64_t)r * wp + c] << (8 * k);
+  }
+  if (q0 < K.band_n) *reinterpret_cast<uint32_t*>(bands + (int64_t)f * K.band_n + q0) = w;
+}
+
 // ------------------------------------------------------------------ k_bb_ring
 // One 1024-thread workgroup; the ring state lives in LDS across the batch.
-// For frame f: (1) gather the 2p-wide bands of M[f] around the border (ring
-// from the state, centre from global) and publish the state (= ring_{f-1})
-// into M[f]'s ring for k_bb_center; (2) horizontal clamped window counts;
-// (3) vertical clamped counts at the ring pixels -> ring_f.  Clamping is
-// medianBlur's BORDER_REPLICATE at the edges of I_median.
-__global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __restrict__ M, int n,
-                                                  uint8_t* __restrict__ ring) {
+// For frame f: (1) copy the frame's bands (prefetched into registers during
+// frame f-1) into LDS, put the ring state (= ring_{f-1}) over their ring
+// positions and publish it into M[f]'s ring for k_bb_center; (2) horizontal
+// clamped window counts; (3) vertical clamped counts at the ring pixels ->
+// ring_f.  Clamping is medianBlur's BORDER_REPLICATE at the edges of
+// I_median.  Counts run as sliding sums along rows / columns (segments per
+// thread), so a frame costs O(band area) LDS byte operations.
+#define LM_BB_SEG 24   // horizontal segment per thread
+#define LM_BB_VCH 16   // left/right ring rows per thread
+#define LM_BB_BDW 16   // band dwords per thread (band_n <= 64 KiB)
+__global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __restrict__ M,
+                                                  const uint8_t* __restrict__ bands, int n,
+                                                  uint8_t* __restrict__ ring, unsigned long long* __restrict__ prof) {
+  unsigned long long t_last = prof ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto tick = [&](int ph) {  // diagnostics (LM_BB_PROF=1): shader clocks per phase, thread 0
+    if (prof && threadIdx.x == 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      prof[ph] += t - t_last;
+      t_last = t;
+    }
+  };
   extern __shared__ uint8_t sm[];
   const int p = K.p, p2 = 2 * p, hp = K.hp, wp = K.wp, nr = K.n_rows, thr = K.thr;
   const int tid = threadIdx.x, nt = blockDim.x;
-  uint8_t* sT = sm;                 // [p][wp]
-  uint8_t* sB = sT + p * wp;        // [p][wp]
-  uint8_t* sL = sB + p * wp;        // [nr][p]
-  uint8_t* sR = sL + nr * p;        // [nr][p]
-  uint8_t* bT = sm + K.ring_n;      // [2p][wp]  rows 0 .. 2p-1
-  uint8_t* bB = bT + p2 * wp;       // [2p][wp]  rows hp-2p .. hp-1
-  uint8_t* bL = bB + p2 * wp;       // [hp][2p]  cols 0 .. 2p-1
-  uint8_t* bR = bL + hp * p2;       // [hp][2p]  cols wp-2p .. wp-1
-  uint8_t* hT = bR + hp * p2;       // [2p][wp]
-  uint8_t* hB = hT + p2 * wp;       // [2p][wp]
-  uint8_t* hL = hB + p2 * wp;       // [hp][p]
-  uint8_t* hR = hL + hp * p;        // [hp][p]
+  uint8_t* sT = sm;                          // [p][wp]
+  uint8_t* sB = sT + p * wp;                 // [p][wp]
+  uint8_t* sL = sB + p * wp;                 // [nr][p]
+  uint8_t* sR = sL + nr * p;                 // [nr][p]
+  uint8_t* bT = sm + ((K.ring_n + 15) & ~15);  // [2p][wp]  rows 0 .. 2p-1
+  uint8_t* bB = bT + p2 * wp;                // [2p][wp]  rows hp-2p .. hp-1
+  uint8_t* bL = bB + p2 * wp;                // [hp][2p]  cols 0 .. 2p-1
+  uint8_t* bR = bL + hp * p2;                // [hp][2p]  cols wp-2p .. wp-1
+  uint8_t* hT = bT + ((K.band_n + 15) & ~15);  // [2p][wp]
+  uint8_t* hB = hT + p2 * wp;                // [2p][wp]
+  uint8_t* hL = hB + p2 * wp;                // [hp][p]
+  uint8_t* hR = hL + hp * p;                 // [hp][p]
+  uint32_t* bT32 = reinterpret_cast<uint32_t*>(bT);
+  const int nd = K.band_n >> 2;
+  uint32_t cur[LM_BB_BDW], nxt[LM_BB_BDW];
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(bands);
+#pragma unroll
+    for (int k = 0; k < LM_BB_BDW; ++k) cur[k] = tid + k * nt < nd ? src[tid + k * nt] : 0u;
+  }
   for (int i = tid; i < K.ring_n; i += nt) sm[i] = ring[i];
   __syncthreads();
+  const int nseg = (wp + LM_BB_SEG - 1) / LM_BB_SEG;
+  const int nhT = 2 * p2 * nseg;  // horizontal tasks, top + bottom bands
+  const int nch = (nr + LM_BB_VCH - 1) / LM_BB_VCH;
   for (int f = 0; f < n; ++f) {
     uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
-    auto mget = [&](int r, int c) -> uint8_t {
-      if (r < p) return sT[r * wp + c];
-      if (r >= hp - p) return sB[(r - (hp - p)) * wp + c];
-      if (c < p) return sL[(r - p) * p + c];
-      if (c >= wp - p) return sR[(r - p) * p + c - (wp - p)];
-      return Mf[(int64_t)r * wp + c];
-    };
-    for (int i = tid; i < p2 * wp; i += nt) {
-      const int r = i / wp, c = i - r * wp;
-      bT[i] = mget(r, c);
-      bB[i] = mget(hp - p2 + r, c);
+    if (f + 1 < n) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(bands + (int64_t)(f + 1) * K.band_n);
+#pragma unroll
+      for (int k = 0; k < LM_BB_BDW; ++k) nxt[k] = tid + k * nt < nd ? src[tid + k * nt] : 0u;
     }
-    for (int i = tid; i < hp * p2; i += nt) {
-      const int r = i / p2, j = i - r * p2;
-      bL[i] = mget(r, j);
-      bR[i] = mget(r, wp - p2 + j);
-    }
-    for (int i = tid; i < p * wp; i += nt) {
-      const int r = i / wp, c = i - r * wp;
-      Mf[(int64_t)r * wp + c] = sT[i];
-      Mf[(int64_t)(hp - p + r) * wp + c] = sB[i];
-    }
+#pragma unroll
+    for (int k = 0; k < LM_BB_BDW; ++k)
+      if (tid + k * nt < nd) bT32[tid + k * nt] = cur[k];
+    // publish ring_{f-1} into M[f]
+    for (int c = tid; c < wp; c += nt)
+      for (int r = 0; r < p; ++r) {
+        Mf[(int64_t)r * wp + c] = sT[r * wp + c];
+        Mf[(int64_t)(hp - p + r) * wp + c] = sB[r * wp + c];
+      }
     for (int i = tid; i < nr * p; i += nt) {
       const int r = i / p, j = i - r * p;
       Mf[(int64_t)(r + p) * wp + j] = sL[i];
       Mf[(int64_t)(r + p) * wp + wp - p + j] = sR[i];
     }
     __syncthreads();
-    for (int i = tid; i < p2 * wp; i += nt) {
-      const int r = i / wp, c = i - r * wp;
-      int a = 0, b = 0;
-      for (int dc = -p; dc <= p; ++dc) {
-        const int cc = min(max(c + dc, 0), wp - 1);
-        a += bT[r * wp + cc];
-        b += bB[r * wp + cc];
+    tick(0);
+    // ring positions of the bands from the state
+    for (int c = tid; c < wp; c += nt) {
+      for (int r = 0; r < p; ++r) {
+        bT[r * wp + c] = sT[r * wp + c];
+        bB[(p + r) * wp + c] = sB[r * wp + c];
       }
-      hT[i] = (uint8_t)a;
-      hB[i] = (uint8_t)b;
+      if (c < p || c >= wp - p) {
+        const uint8_t* side = c < p ? sL + c : sR + c - (wp - p);
+        for (int r = p; r < p2; ++r) {
+          bT[r * wp + c] = side[(r - p) * p];                  // M row r
+          bB[(r - p) * wp + c] = side[(hp - p2 + r - p - p) * p];  // M row hp-2p+(r-p)
+        }
+      }
     }
-    for (int i = tid; i < hp * p; i += nt) {
-      const int r = i / p, j = i - r * p;
-      int a = 0, b = 0;
-      for (int dc = -p; dc <= p; ++dc) {
-        a += bL[r * p2 + max(j + dc, 0)];
-        b += bR[r * p2 + min(p + j + dc, p2 - 1)];
+    for (int r = tid; r < hp; r += nt) {
+      if (r < p || r >= hp - p) {
+        const uint8_t* src = r < p ? sT + r * wp : sB + (r - (hp - p)) * wp;
+        for (int j = 0; j < p2; ++j) {
+          bL[r * p2 + j] = src[j];
+          bR[r * p2 + j] = src[wp - p2 + j];
+        }
+      } else {
+        for (int j = 0; j < p; ++j) {
+          bL[r * p2 + j] = sL[(r - p) * p + j];
+          bR[r * p2 + p + j] = sR[(r - p) * p + j];
+        }
       }
-      hL[i] = (uint8_t)a;
-      hR[i] = (uint8_t)b;
-    }
-    __syncthreads();
-    for (int i = tid; i < p * wp; i += nt) {
-      const int r = i / wp, c = i - r * wp;
-      int a = 0, b = 0;
-      for (int dr = -p; dr <= p; ++dr) {
-        a += hT[max(r + dr, 0) * wp + c];
-        b += hB[min(p + r + dr, p2 - 1) * wp + c];
-      }
-      sT[i] = a >= thr ? 1 : 0;
-      sB[i] = b >= thr ? 1 : 0;
-    }
-    for (int i = tid; i < nr * p; i += nt) {
-      const int r = i / p, j = i - r * p;
-      int a = 0, b = 0;
-      for (int dr = -p; dr <= p; ++dr) {
-        a += hL[(r + p + dr) * p + j];
-        b += hR[(r + p + dr) * p + j];
-      }
-      sL[i] = a >= thr ? 1 : 0;
-      sR[i] = b >= thr ? 1 : 0;
     }
     __syncthreads();
+    tick(1);
+    // (2) horizontal counts: sliding sums over row segments
+    for (int t = tid; t < nhT + 2 * hp; t += nt) {
+      if (t < nhT) {
+        const int band = t / (p2 * nseg), rem = t - band * (p2 * nseg);
+        const int r = rem / nseg, c0 = (rem - r * nseg) * LM_BB_SEG, c1 = min(c0 + LM_BB_SEG, wp);
+        const uint8_t* src = (band ? bB : bT) + r * wp;
+        uint8_t* dst = (band ? hB : hT) + r * wp;
+        int s = 0;
+        for (int dc = -p; dc <= p; ++dc) s += src[min(max(c0 + dc, 0), wp - 1)];
+        dst[c0] = (uint8_t)s;
+        for (int c = c0 + 1; c < c1; ++c) {
+          s += src[min(c + p, wp - 1)] - src[max(c - 1 - p, 0)];
+          dst[c] = (uint8_t)s;
+        }
+      } else {
+        const int q = t - nhT, side = q / hp, r = q - side * hp;
+        if (side == 0) {  // ring cols 0..p-1: band cols [j-p, j+p] clamped at 0
+          const uint8_t* src = bL + r * p2;
+          int s = 0;
+          for (int dc = -p; dc <= p; ++dc) s += src[max(dc, 0)];
+          hL[r * p] = (uint8_t)s;
+          for (int j = 1; j < p; ++j) {
+            s += src[j + p] - src[max(j - 1 - p, 0)];
+            hL[r * p + j] = (uint8_t)s;
+          }
+        } else {  // ring cols wp-p+j: band cols [j, 2p+j] clamped at 2p-1
+          const uint8_t* src = bR + r * p2;
+          int s = 0;
+          for (int k = 0; k <= p2; ++k) s += src[min(k, p2 - 1)];
+          hR[r * p] = (uint8_t)s;
+          for (int j = 1; j < p; ++j) {
+            s += src[p2 - 1] - src[j - 1];
+            hR[r * p + j] = (uint8_t)s;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    tick(2);
+    // (3) vertical counts -> ring_f
+    for (int t = tid; t < 2 * wp + 2 * p * nch; t += nt) {
+      if (t < wp) {  // top ring column: rows [r-p, r+p] clamped at 0
+        const int c = t;
+        int s = (p + 1) * hT[c];
+        for (int k = 1; k <= p; ++k) s += hT[k * wp + c];
+        sT[c] = s >= thr ? 1 : 0;
+        for (int r = 1; r < p; ++r) {
+          s += hT[(r + p) * wp + c] - hT[max(r - 1 - p, 0) * wp + c];
+          sT[r * wp + c] = s >= thr ? 1 : 0;
+        }
+      } else if (t < 2 * wp) {  // bottom ring column: band rows [i, 2p+i] clamped at 2p-1
+        const int c = t - wp;
+        int s = 0;
+        for (int k = 0; k <= p2; ++k) s += hB[min(k, p2 - 1) * wp + c];
+        sB[c] = s >= thr ? 1 : 0;
+        for (int i = 1; i < p; ++i) {
+          s += hB[(p2 - 1) * wp + c] - hB[(i - 1) * wp + c];
+          sB[i * wp + c] = s >= thr ? 1 : 0;
+        }
+      } else {  // left / right ring: (side, column j, chunk of rows)
+        const int q = t - 2 * wp, side = q / (p * nch), rem = q - side * (p * nch);
+        const int j = rem / nch, r0 = (rem - j * nch) * LM_BB_VCH, r1 = min(r0 + LM_BB_VCH, nr);
+        const uint8_t* h = side ? hR : hL;
+        uint8_t* st = side ? sR : sL;
+        int s = 0;
+        for (int dr = -p; dr <= p; ++dr) s += h[(r0 + p + dr) * p + j];
+        st[r0 * p + j] = s >= thr ? 1 : 0;
+        for (int r = r0 + 1; r < r1; ++r) {
+          s += h[(r + p + p) * p + j] - h[(r - 1) * p + j];
+          st[r * p + j] = s >= thr ? 1 : 0;
+        }
+      }
+    }
+    __syncthreads();
+    tick(3);
+#pragma unroll
+    for (int k = 0; k < LM_BB_BDW; ++k) cur[k] = nxt[k];
   }
   for (int i = tid; i < K.ring_n; i += nt) ring[i] = sm[i];
 }
@@ -209,28 +326,58 @@ __global__ __launch_bounds__(256) void k_bb_center(const LmBBConst K, const uint
 }
 
 // -------------------------------------------------------------------- k_bb_cc
-// largestBWAreaObject + reduce + firstLastOverT for one (view, frame).
-// Union-find over the view's pixels in global memory (atomicMin hooking of the
-// larger root under the smaller); loads bypass the vector L1 so every wave
-// sees the hooks of the others.  Largest area wins; equal areas go to the
-// component OpenCV labels first (8-connectivity: Grana BBDT 2x2-block raster
-// order of its first block; 4-connectivity: Wu pixel raster order).
+// largestBWAreaObject + reduce + firstLastOverT for one (view, frame).  The
+// largest area wins; equal areas go to the component OpenCV labels first
+// (8-connectivity: Grana BBDT 2x2-block raster order of its first block;
+// 4-connectivity: Wu pixel raster order).  Global-memory union-find tables
+// are read with L1-bypassing loads so every wave sees the others' hooks.
 DEV unsigned bb_ld(const unsigned* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 DEV void bb_st(unsigned* a, unsigned v) { __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-DEV unsigned bb_find(const unsigned* par, unsigned a) {
-  unsigned q = bb_ld(&par[a]);
+// firstLastOverT's pass test on one row/column sum (LocoMouse_class.hpp:419-421).
+DEV bool bb_pass(const LmBBConst& K, int count) {
+  const int v = 255 * count;  // the mask is 0/255 (cv::compare, :945)
+  if (K.semantics == LM_BB_FIRSTLAST_INTEGER) return v >= K.min_pixel_visible;
+  return __int_as_float(v) >= (float)K.min_pixel_visible;  // CV_32S read through ptr<float>
+}
+
+// Row-run labelling.  Runs are found with wave ballots, linked to the
+// overlapping runs of the row above (8-connectivity: columns within +-1), and
+// a union-find forest over runs (atomicMin hooking of the larger root under
+// the smaller, so a component's root is its first run in raster order) gives
+// areas and first-label keys.  The run table lives in LDS when a view has at
+// most LM_BB_RUN_CAP runs (clean masks: a few per row), else in the global
+// scratch with L1-bypassing loads (noisy masks: thousands per view).
+#define LM_BB_RUN_CAP 2048
+
+struct BBRuns {
+  unsigned *rs, *re, *ry, *par, *area, *key;
+};
+
+template <bool G>
+DEV unsigned rld(const unsigned* a) {
+  if constexpr (G) return bb_ld(a);
+  else return *a;
+}
+template <bool G>
+DEV void rst(unsigned* a, unsigned v) {
+  if constexpr (G) bb_st(a, v);
+  else *a = v;
+}
+template <bool G>
+DEV unsigned rfind(const unsigned* par, unsigned a) {
+  unsigned q = rld<G>(&par[a]);
   while (q != a) {
     a = q;
-    q = bb_ld(&par[a]);
+    q = rld<G>(&par[a]);
   }
   return a;
 }
-
-DEV void bb_union(unsigned* par, unsigned a, unsigned b) {
+template <bool G>
+DEV void runion(unsigned* par, unsigned a, unsigned b) {
   while (true) {
-    a = bb_find(par, a);
-    b = bb_find(par, b);
+    a = rfind<G>(par, a);
+    b = rfind<G>(par, b);
     if (a == b) return;
     if (a < b) {
       const unsigned t = a;
@@ -243,35 +390,151 @@ DEV void bb_union(unsigned* par, unsigned a, unsigned b) {
   }
 }
 
-// firstLastOverT's pass test on one row/column sum (LocoMouse_class.hpp:419-421).
-DEV bool bb_pass(const LmBBConst& K, int count) {
-  const int v = 255 * count;  // the mask is 0/255 (cv::compare, :945)
-  if (K.semantics == LM_BB_FIRSTLAST_INTEGER) return v >= K.min_pixel_visible;
-  return __int_as_float(v) >= (float)K.min_pixel_visible;  // CV_32S read through ptr<float>
+// Exclusive scan of v[0..n) in place by wave 0; the total goes to *total.
+// Block-wide call.
+DEV void bb_wave0_scan(int* v, int n, int* total) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int carry = 0;
+    for (int b = 0; b < n; b += 64) {
+      const int i = b + lane;
+      const int x = i < n ? v[i] : 0;
+      int inc = x;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      if (i < n) v[i] = carry + inc - x;
+      carry += __shfl(inc, 63);
+    }
+    if (lane == 0) *total = carry;
+  }
+  __syncthreads();
 }
 
+// Labels the runs of one view, picks the largest component (ties: first
+// OpenCV label) and accumulates its per-column (difference array) and per-row
+// pixel counts.  Returns the chosen root or 0xFFFFFFFF.  Block-wide call.
+template <bool G>
+DEV unsigned bb_cc_runs(const BBRuns S, const uint8_t* __restrict__ Bv, int W, int H, int R, const int* rowoff,
+                        bool c8, int* colc, int* rowc, unsigned long long* s_red, unsigned* s_best) {
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+  const unsigned long long lt = (1ull << lane) - 1;
+  const unsigned nbx = (unsigned)(W + 1) / 2;
+  for (int y = wave; y < H; y += nw) {
+    const uint8_t* row = Bv + (int64_t)y * W;
+    int ns = rowoff[y], ne = rowoff[y];
+    unsigned long long carry = 0;
+    for (int x0 = 0; x0 < W; x0 += 64) {
+      const int x = x0 + lane;
+      const unsigned long long bits = __ballot(x < W && row[x] != 0);
+      const bool nxt = x0 + 64 < W && row[x0 + 64] != 0;  // wave-uniform
+      const unsigned long long st = bits & ~((bits << 1) | carry);
+      const unsigned long long en = bits & ~((bits >> 1) | (nxt ? 1ull << 63 : 0ull));
+      if ((st >> lane) & 1) {
+        const int k = ns + __popcll(st & lt);
+        rst<G>(&S.rs[k], (unsigned)x);
+        rst<G>(&S.ry[k], (unsigned)y);
+      }
+      if ((en >> lane) & 1) rst<G>(&S.re[ne + __popcll(en & lt)], (unsigned)x);
+      ns += __popcll(st);
+      ne += __popcll(en);
+      carry = bits >> 63;
+    }
+  }
+  for (int i = tid; i < R; i += nt) {
+    rst<G>(&S.par[i], (unsigned)i);
+    rst<G>(&S.area[i], 0u);
+    rst<G>(&S.key[i], 0xFFFFFFFFu);
+  }
+  __syncthreads();
+  const int d = c8 ? 1 : 0;
+  for (int i = tid; i < R; i += nt) {
+    const int y = (int)rld<G>(&S.ry[i]);
+    if (y == 0) continue;
+    const int a0 = (int)rld<G>(&S.rs[i]) - d, a1 = (int)rld<G>(&S.re[i]) + d;
+    int lo = rowoff[y - 1], hi = rowoff[y];
+    while (lo < hi) {  // first run of row y-1 ending at or after a0
+      const int mid = (lo + hi) >> 1;
+      if ((int)rld<G>(&S.re[mid]) < a0) lo = mid + 1; else hi = mid;
+    }
+    for (int j = lo; j < rowoff[y] && (int)rld<G>(&S.rs[j]) <= a1; ++j) runion<G>(S.par, i, j);
+  }
+  __syncthreads();
+  for (int i = tid; i < R; i += nt) {
+    const unsigned root = rfind<G>(S.par, i);
+    const unsigned y = rld<G>(&S.ry[i]), x = rld<G>(&S.rs[i]);
+    atomicAdd(&S.area[root], rld<G>(&S.re[i]) - x + 1);
+    atomicMin(&S.key[root], c8 ? (y >> 1) * nbx + (x >> 1) : y * (unsigned)W + x);
+    rst<G>(&S.par[i], root);
+  }
+  __syncthreads();
+  unsigned long long best = 0;
+  for (int i = tid; i < R; i += nt) {
+    if (rld<G>(&S.par[i]) != (unsigned)i) continue;
+    const unsigned long long val = ((unsigned long long)rld<G>(&S.area[i]) << 32) | (0xFFFFFFFFu - rld<G>(&S.key[i]));
+    best = val > best ? val : best;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long other = __shfl_xor(best, o);
+    best = other > best ? other : best;
+  }
+  if (lane == 0) s_red[wave] = best;
+  __syncthreads();
+  best = 0;
+  for (int w = 0; w < nw; ++w) best = s_red[w] > best ? s_red[w] : best;
+  if (best) {
+    const unsigned barea = (unsigned)(best >> 32), bkey = 0xFFFFFFFFu - (unsigned)best;
+    for (int i = tid; i < R; i += nt)
+      if (rld<G>(&S.par[i]) == (unsigned)i && rld<G>(&S.area[i]) == barea && rld<G>(&S.key[i]) == bkey) *s_best = i;
+  }
+  __syncthreads();
+  const unsigned broot = *s_best;
+  if (broot != 0xFFFFFFFFu)
+    for (int i = tid; i < R; i += nt) {
+      if (rld<G>(&S.par[i]) != broot) continue;
+      const int x0 = (int)rld<G>(&S.rs[i]), x1 = (int)rld<G>(&S.re[i]);
+      atomicAdd(&rowc[rld<G>(&S.ry[i])], x1 - x0 + 1);
+      atomicAdd(&colc[x0], 1);
+      atomicSub(&colc[x1 + 1], 1);
+    }
+  __syncthreads();
+  // difference array -> per-column counts (inclusive scan by wave 0)
+  if (tid < 64) {
+    int carry = 0;
+    for (int b = 0; b < W; b += 64) {
+      const int i = b + lane;
+      int inc = i < W ? colc[i] : 0;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      if (i < W) colc[i] = carry + inc;
+      carry += __shfl(inc, 63);
+    }
+  }
+  __syncthreads();
+  return broot;
+}
+
+// largestBWAreaObject + reduce + firstLastOverT for one (view, frame).
 __global__ __launch_bounds__(1024) void k_bb_cc(const LmBBConst K, const uint8_t* __restrict__ bin,
                                                 unsigned* __restrict__ scratch, int32_t* __restrict__ lims) {
   extern __shared__ int cnt[];
   const int v = blockIdx.x, f = blockIdx.y;
-  const int W = K.n_cols, H = K.view_h[v], NP = W * H;
+  const int W = K.n_cols, H = K.view_h[v];
   const uint8_t* __restrict__ Bv = bin + (int64_t)f * K.bin_bytes + (int64_t)K.view_y[v] * W;
-  unsigned* par = scratch + (int64_t)f * K.cc_words + (v ? 3 * (int64_t)W * K.view_h[0] : 0);
-  unsigned* area = par + NP;
-  unsigned* key = area + NP;
-  int* colc = cnt;      // [W]  Row_* (reduce over rows)
-  int* rowc = cnt + W;  // [H]  Col_*
+  int* colc = cnt;            // [W + 1]  Row_* (reduce over rows), via a difference array
+  int* rowc = cnt + W + 1;    // [H]      Col_*
+  int* rowoff = rowc + H;     // [H + 1]  run offsets per row
+  unsigned* lds_runs = reinterpret_cast<unsigned*>(rowoff + H + 1);  // 6 x [LM_BB_RUN_CAP]
   __shared__ unsigned long long s_red[16];
   __shared__ unsigned s_best;
+  __shared__ int s_total;
   __shared__ int s_lim[2][3];  // (first, last, count) for Row, Col
-  const int tid = threadIdx.x, nt = blockDim.x;
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
 
-  for (int q = tid; q < NP; q += nt) {
-    bb_st(&par[q], Bv[q] ? (unsigned)q : 0xFFFFFFFFu);
-    bb_st(&area[q], 0u);
-    bb_st(&key[q], 0xFFFFFFFFu);
-  }
-  for (int i = tid; i < W + H; i += nt) cnt[i] = 0;
+  for (int i = tid; i < W + 2 * H + 2; i += nt) cnt[i] = 0;
   if (tid < 2) {
     s_lim[tid][0] = 0x7FFFFFFF;
     s_lim[tid][1] = -1;
@@ -279,67 +542,41 @@ __global__ __launch_bounds__(1024) void k_bb_cc(const LmBBConst K, const uint8_t
   }
   if (tid == 0) s_best = 0xFFFFFFFFu;
   __syncthreads();
+  // runs per row: a run starts at a foreground pixel whose left neighbour is background
+  for (int y = wave; y < H; y += nw) {
+    const uint8_t* row = Bv + (int64_t)y * W;
+    int n = 0;
+    unsigned long long carry = 0;
+    for (int x0 = 0; x0 < W; x0 += 64) {
+      const int x = x0 + lane;
+      const unsigned long long bits = __ballot(x < W && row[x] != 0);
+      n += __popcll(bits & ~((bits << 1) | carry));
+      carry = bits >> 63;
+    }
+    if (lane == 0) rowoff[y] = n;
+  }
+  __syncthreads();
+  bb_wave0_scan(rowoff, H, &s_total);
+  const int R = s_total;
   const bool c8 = K.conn == 8;
-  for (int q = tid; q < NP; q += nt) {
-    if (!Bv[q]) continue;
-    const int y = q / W, x = q - y * W;
-    if (x > 0 && Bv[q - 1]) bb_union(par, q, q - 1);
-    if (y > 0) {
-      if (Bv[q - W]) bb_union(par, q, q - W);
-      if (c8) {
-        if (x > 0 && Bv[q - W - 1]) bb_union(par, q, q - W - 1);
-        if (x + 1 < W && Bv[q - W + 1]) bb_union(par, q, q - W + 1);
-      }
-    }
+  if (R <= LM_BB_RUN_CAP) {
+    unsigned* b = lds_runs;
+    const BBRuns S{b, b + LM_BB_RUN_CAP, b + 2 * LM_BB_RUN_CAP, b + 3 * LM_BB_RUN_CAP, b + 4 * LM_BB_RUN_CAP,
+                   b + 5 * LM_BB_RUN_CAP};
+    bb_cc_runs<false>(S, Bv, W, H, R, rowoff, c8, colc, rowc, s_red, &s_best);
+  } else {
+    const int64_t cap = (int64_t)H * ((W + 1) / 2);  // at most ceil(W/2) runs per row
+    unsigned* b = scratch + (int64_t)f * K.cc_words + (v ? 6 * (int64_t)K.view_h[0] * ((W + 1) / 2) : 0);
+    const BBRuns S{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap, b + 5 * cap};
+    bb_cc_runs<true>(S, Bv, W, H, R, rowoff, c8, colc, rowc, s_red, &s_best);
   }
-  __syncthreads();
-  const unsigned nbx = (unsigned)(W + 1) / 2;
-  for (int q = tid; q < NP; q += nt) {
-    if (!Bv[q]) continue;
-    const unsigned root = bb_find(par, q);
-    const int y = q / W, x = q - y * W;
-    const unsigned k = c8 ? (unsigned)(y >> 1) * nbx + (unsigned)(x >> 1) : (unsigned)q;
-    atomicAdd(&area[root], 1u);
-    atomicMin(&key[root], k);
-    bb_st(&par[q], root);
-  }
-  __syncthreads();
-  unsigned long long best = 0;
-  for (int q = tid; q < NP; q += nt) {
-    if (!Bv[q] || bb_ld(&par[q]) != (unsigned)q) continue;
-    const unsigned long long val = ((unsigned long long)bb_ld(&area[q]) << 32) | (0xFFFFFFFFu - bb_ld(&key[q]));
-    best = val > best ? val : best;
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long other = __shfl_xor(best, o);
-    best = other > best ? other : best;
-  }
-  if ((tid & 63) == 0) s_red[tid >> 6] = best;
-  __syncthreads();
-  best = 0;
-  for (int w = 0; w < (nt >> 6); ++w) best = s_red[w] > best ? s_red[w] : best;
-  if (best) {
-    const unsigned barea = (unsigned)(best >> 32), bkey = 0xFFFFFFFFu - (unsigned)best;
-    for (int q = tid; q < NP; q += nt)
-      if (Bv[q] && bb_ld(&par[q]) == (unsigned)q && bb_ld(&area[q]) == barea && bb_ld(&key[q]) == bkey) s_best = q;
-  }
-  __syncthreads();
-  const unsigned broot = s_best;
-  if (broot != 0xFFFFFFFFu) {
-    for (int q = tid; q < NP; q += nt) {
-      if (!Bv[q] || bb_ld(&par[q]) != broot) continue;
-      const int y = q / W, x = q - y * W;
-      atomicAdd(&colc[x], 1);
-      atomicAdd(&rowc[y], 1);
-    }
-  }
-  __syncthreads();
+  (void)lane;
   for (int i = tid; i < W + H; i += nt) {
-    const int d = i < W ? 0 : 1, idx = i < W ? i : i - W;
-    if (bb_pass(K, cnt[i])) {
-      atomicMin(&s_lim[d][0], idx);
-      atomicMax(&s_lim[d][1], idx);
-      atomicAdd(&s_lim[d][2], 1);
+    const int dd = i < W ? 0 : 1, idx = i < W ? i : i - W;
+    if (bb_pass(K, i < W ? colc[i] : rowc[idx])) {
+      atomicMin(&s_lim[dd][0], idx);
+      atomicMax(&s_lim[dd][1], idx);
+      atomicAdd(&s_lim[dd][2], 1);
     }
   }
   __syncthreads();
@@ -363,7 +600,8 @@ struct lm_bb_ctx {
   lm_bb_params P{};
   LmBBConst K{};
   size_t ring_lds = 0, center_lds = 0, cc_lds = 0;
-  DevBuf<uint8_t> bkg, frames, luts, M, ring, bin;
+  DevBuf<uint8_t> bkg, frames, luts, M, ring, bin, bands;
+  DevBuf<unsigned long long> prof;  // LM_BB_PROF=1: k_bb_ring phase clocks
   DevBuf<int32_t> cal;
   DevBuf<unsigned> cc;
   HostBuf<const uint8_t*> fptr;
@@ -372,6 +610,12 @@ struct lm_bb_ctx {
   std::vector<lm_bb_frame> per;
   std::vector<uint32_t> x_pos, yb_pos, ys_pos;
   ~lm_bb_ctx() {
+    if (prof.p) {
+      unsigned long long h[8];
+      if (hipMemcpy(h, prof.p, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
+        fprintf(stderr, "k_bb_ring phase clocks: copy+publish %llu  ring-fill %llu  horizontal %llu  vertical %llu\n",
+                h[0], h[1], h[2], h[3]);
+    }
     if (stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
@@ -411,6 +655,8 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
     if (vw[v].y < 0 || vw[v].height <= 0 || vw[v].y + vw[v].height > NR)
       throw std::runtime_error("BB pass: view box outside the corrected image.");
   }
+  if (NR < P.median_filter_size / 2 || NC < P.median_filter_size / 2)
+    throw std::invalid_argument("BB pass: corrected image smaller than the median filter's half size.");
   if (vw[0].y < vw[1].y + vw[1].height && vw[1].y < vw[0].y + vw[0].height)
     throw std::invalid_argument("BB pass: overlapping side and bottom view boxes are not supported.");
   c->P = P;
@@ -435,12 +681,16 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
   K.ring_n = 2 * K.p * K.wp + 2 * NR * K.p;
   K.m_bytes = ((int64_t)K.hp * K.wp + 255) / 256 * 256;
   K.bin_bytes = ((int64_t)NR * NC + 255) / 256 * 256;
-  K.cc_words = 3 * (int64_t)NC * (vw[0].height + vw[1].height);
+  K.cc_words = 6 * (int64_t)((NC + 1) / 2) * (vw[0].height + vw[1].height);  // run tables of both views
   const int p = K.p, p2 = 2 * p;
-  c->ring_lds = (size_t)K.ring_n + 4 * (size_t)p2 * K.wp + 2 * (size_t)K.hp * p2 + 2 * (size_t)K.hp * p;
+  K.band_n = (2 * p2 * K.wp + 2 * K.hp * p2 + 15) & ~15;
+  c->ring_lds = (size_t)((K.ring_n + 15) & ~15) + (size_t)K.band_n + 2 * (size_t)p2 * K.wp + 2 * (size_t)K.hp * p;
+  if (K.band_n > 4 * 1024 * LM_BB_BDW)
+    throw std::invalid_argument("BB pass: frame size / median_filter_size exceed the ring kernel's band registers.");
   const int IW = LM_BB_TW + p2, IH = LM_BB_TH + p2;
   c->center_lds = (size_t)((IH * IW + 15) & ~15) + 2 * (size_t)LM_BB_TH * IW;
-  c->cc_lds = 4 * (size_t)(NC + std::max(vw[0].height, vw[1].height));
+  const int hmax = std::max(vw[0].height, vw[1].height);
+  c->cc_lds = 4 * (size_t)(NC + 1 + 2 * hmax + 1) + (size_t)LM_BB_RUN_CAP * 6 * 4;
   const size_t lds_max = 160 * 1024;
   if (c->ring_lds > lds_max || c->center_lds > lds_max || c->cc_lds > lds_max)
     throw std::invalid_argument("BB pass: frame size / median_filter_size exceed the 160 KiB LDS of one workgroup.");
@@ -464,6 +714,11 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
   c->ring.alloc((size_t)std::max(K.ring_n, 1));
   HIPCHK(hipMemset(c->ring.p, 0, c->ring.n));  // I_median = zeros (:588)
   c->bin.alloc((size_t)K.bin_bytes * B);
+  c->bands.alloc((size_t)std::max(K.band_n, 16) * B);
+  if (dbg_env("LM_BB_PROF")) {
+    c->prof.alloc(8);
+    HIPCHK(hipMemset(c->prof.p, 0, 8 * sizeof(unsigned long long)));
+  }
   c->cc.alloc((size_t)K.cc_words * B);
   c->fptr.alloc((size_t)B);
   c->lims.alloc((size_t)8 * B);
@@ -505,7 +760,10 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
   k_minmax_lut<<<n, 1024, 0, s>>>(c->fptr.d, c->bkg.p, (int)c->npix, 0, nullptr, 0, c->luts.p);
   k_bb_ingest<<<dim3((unsigned)((np + 1023) / 1024), n), 256, 0, s>>>(K, c->fptr.d, c->bkg.p, c->cal.p, c->luts.p,
                                                                        c->M.p);
-  if (K.p > 0) k_bb_ring<<<1, 1024, c->ring_lds, s>>>(K, c->M.p, n, c->ring.p);
+  if (K.p > 0) {
+    k_bb_bands<<<dim3((unsigned)((K.band_n / 4 + 255) / 256), n), 256, 0, s>>>(K, c->M.p, c->bands.p);
+    k_bb_ring<<<1, 1024, c->ring_lds, s>>>(K, c->M.p, c->bands.p, n, c->ring.p, c->prof.p);
+  }
   k_bb_center<<<dim3((unsigned)((K.n_cols + LM_BB_TW - 1) / LM_BB_TW), (unsigned)((K.n_rows + LM_BB_TH - 1) / LM_BB_TH),
                      n),
                 256, c->center_lds, s>>>(K, c->M.p, c->bin.p);

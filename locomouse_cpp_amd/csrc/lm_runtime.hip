@@ -293,6 +293,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     throw std::runtime_error("Provided bounding box for the bottom view exceeds the image dimensions.");
   if (us.x < 0 || us.y < 0 || us.x + us.width >= NC || us.y + us.height >= NR)
     throw std::runtime_error("Provided bounding box for the side view exceeds the image dimensions.");
+  if (ub.width <= 0 || ub.height <= 0 || us.width <= 0 || us.height <= 0)
+    throw std::runtime_error("Empty mouse bounding box: cropBoundingBox / filter2D would work on an empty image.");
   // model (:3095-3162)
   const lm_detector* dets[6] = {&M->paw_bottom, &M->snout_bottom, &M->tail_bottom, &M->paw_side, &M->snout_side, &M->tail_side};
   const char* names[6] = {"modelPaw_bottom", "modelSnout_bottom", "modelTail_bottom", "modelPaw_side", "modelSnout_side", "modelTail_side"};

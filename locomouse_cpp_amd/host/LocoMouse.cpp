@@ -157,16 +157,51 @@ void LocoMouse::getBoundingBox() {
     BB_X_POS.assign(N_FRAMES, (uint32_t)(b.x + b.width));
     BB_Y_SIDE_POS.assign(N_FRAMES, (uint32_t)(s.y + s.height));
     BB_Y_BOTTOM_POS.assign(N_FRAMES, (uint32_t)(b.y + b.height));
+    BB_BOTTOM_MOUSE = lm_rect{0, 0, b.width, b.height};
+    BB_SIDE_MOUSE = lm_rect{0, 0, s.width, s.height};
     HAVE_BB = true;
   } else {
     computeBoundingBox();
   }
 }
 
+// :579-653: every frame of the video through computeMouseBox (readFrame into
+// the padded median image, :615), then computeMouseBoxSize and the moving
+// averages — all in lm_bb_push / lm_bb_finish.  The video is re-read from
+// frame 0 afterwards, as initializeFeatureLoop's V.set(POS_FRAMES, 0)
+// (:761-762) does in the reference.
 void LocoMouse::computeBoundingBox() {
-  throw std::runtime_error(
-      "computeBoundingBox: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) is not on this path; "
-      "set use_provided_bounding_box = 1.");
+  if (!IN.rewind)
+    throw std::invalid_argument("computeBoundingBox: the frame reader cannot rewind (V.set(CV_CAP_PROP_POS_FRAMES, 0)).");
+  if (N_FRAMES == 0) throw std::runtime_error("computeBoundingBox: the video has no frames.");
+  lm_setup su = IN.setup;
+  su.method = 0;
+  lm_bb_ctx* raw = nullptr;
+  throw_on_error(lm_bb_create(IN.device, &su, &IN.bb_params, IN.batch, &raw));
+  std::unique_ptr<lm_bb_ctx, void (*)(lm_bb_ctx*)> bb(raw, lm_bb_destroy);
+  std::vector<uint8_t> buf(FRAME_BYTES * (size_t)IN.batch);
+  for (unsigned done = 0; done < N_FRAMES;) {
+    const int n = (int)std::min<unsigned>((unsigned)IN.batch, N_FRAMES - done);
+    for (int i = 0; i < n; ++i)
+      if (!IN.read_frame(buf.data() + (size_t)i * FRAME_BYTES))
+        throw std::runtime_error("Error: Failed to read image from video file.\n");  // :1284-1286
+    throw_on_error(lm_bb_push(bb.get(), buf.data(), (int64_t)FRAME_BYTES, n, nullptr));
+    done += (unsigned)n;
+  }
+  lm_bb_result r{};
+  throw_on_error(lm_bb_finish(bb.get(), &r));
+  BB_X_POS.assign(r.x_pos, r.x_pos + r.n_frames);
+  BB_Y_BOTTOM_POS.assign(r.y_bottom_pos, r.y_bottom_pos + r.n_frames);
+  BB_Y_SIDE_POS.assign(r.y_side_pos, r.y_side_pos + r.n_frames);
+  BB_SIDE_MOUSE = r.bb_side_mouse;
+  BB_BOTTOM_MOUSE = r.bb_bottom_mouse;
+  // The detection context derives its geometry from these sizes (:655-700);
+  // the per-frame corners go to lm_detect_batch.
+  IN.params.bounding_box_side = BB_SIDE_MOUSE;
+  IN.params.bounding_box_bottom = BB_BOTTOM_MOUSE;
+  IN.params.use_provided_bounding_box = 1;
+  HAVE_BB = true;
+  IN.rewind();
 }
 
 // :655-769 derives the geometry; here the device context does (lm_ctx_create

@@ -51,7 +51,13 @@ struct LocoMouse_Inputs {
   // video_cols u8, row-major) and returns false at the end of the video.
   std::function<bool(uint8_t* dst)> read_frame;
   int device = 0;      // HIP device of this instance (one per GPU / host thread)
-  int batch = 256;     // frames per lm_detect_batch call
+  int batch = 256;     // frames per lm_detect_batch / lm_bb_push call
+  // Whole-video BB pass (use_provided_bounding_box = 0): config.yml's
+  // median_filter_size / min_pixel_visible / moving_average_window /
+  // conn_comp_connectivity, and V.set(CV_CAP_PROP_POS_FRAMES, 0) (:761-762)
+  // to re-read the video from frame 0 after the pass.
+  lm_bb_params bb_params{11, 1, 5, 8, LM_BB_FIRSTLAST_AS_EXECUTED, 0};
+  std::function<void()> rewind;
 };
 
 using TailTrack = std::array<int32_t, 3 * LM_N_TAIL_POINTS>;  // TRACKS_TAIL entry: 3x15, row-major, -1 = missing
@@ -65,7 +71,7 @@ class LocoMouse {
 
   virtual void readFrame();           // LocoMouse_class.cpp:1273-1333
   virtual void getBoundingBox();      // :543-653 (provided box: constant BR corners)
-  virtual void computeBoundingBox();  // :575-653 — whole-video pass, §8(f) row 1
+  virtual void computeBoundingBox();  // :575-653 — whole-video pass (lm_bb_*), §8(f) row 1
   void initializeFeatureLoop();       // :655-769 (creates the device context)
   void cropBoundingBox();             // :1408-1478
   void detectTail();                  // :2541-2555
@@ -102,7 +108,17 @@ class LocoMouse {
   unsigned int N_FRAMES = 0;
   int CURRENT_FRAME = -1;
   std::vector<uint32_t> BB_X_POS, BB_Y_SIDE_POS, BB_Y_BOTTOM_POS;  // per-frame BR corners (:547-557)
+  lm_rect BB_SIDE_MOUSE{}, BB_BOTTOM_MOUSE{};                       // box sizes (x = y = 0)
   bool HAVE_BB = false;
+
+ public:
+  const std::vector<uint32_t>& bb_x_pos() const { return BB_X_POS; }
+  const std::vector<uint32_t>& bb_y_side_pos() const { return BB_Y_SIDE_POS; }
+  const std::vector<uint32_t>& bb_y_bottom_pos() const { return BB_Y_BOTTOM_POS; }
+  lm_rect bb_side_mouse() const { return BB_SIDE_MOUSE; }
+  lm_rect bb_bottom_mouse() const { return BB_BOTTOM_MOUSE; }
+
+ protected:
 
   std::vector<std::vector<Candidate>> CANDIDATES_BOTTOM_PAW, CANDIDATES_BOTTOM_SNOUT;
   std::vector<std::vector<Candidate>> CANDIDATES_SIDE_PAW, CANDIDATES_SIDE_SNOUT;

@@ -31,9 +31,10 @@ int fail(const std::exception& e, int code, char* err, int errlen) {
 
 }  // namespace
 
-extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_model* model, const uint8_t* frames,
-                       int n_frames, int n_read, int batch, int device, int call_order, lm_batch_result* out, char* err,
-                       int errlen) {
+extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_model* model,
+                       const lm_bb_params* bb_params, const uint8_t* frames, int n_frames, int n_read, int batch,
+                       int device, int call_order, lm_batch_result* out, uint32_t* bb_corners, lm_rect* bb_sizes,
+                       char* err, int errlen) {
   try {
     locomouse::LocoMouse_Inputs in;
     in.setup = *setup;
@@ -49,9 +50,23 @@ extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_
       std::memcpy(dst, frames + (size_t)next++ * fb, fb);
       return true;
     };
+    if (bb_params) {
+      in.bb_params = *bb_params;
+      in.rewind = [&] { next = 0; };  // V.set(CV_CAP_PROP_POS_FRAMES, 0)
+    }
     std::unique_ptr<LocoMouse> L = LocoMouse_Initialize(in);
     L->getBoundingBox();
     L->initializeFeatureLoop();
+    if (bb_corners)
+      for (unsigned i = 0; i < L->N_frames(); ++i) {
+        bb_corners[3 * i] = L->bb_x_pos()[i];
+        bb_corners[3 * i + 1] = L->bb_y_bottom_pos()[i];
+        bb_corners[3 * i + 2] = L->bb_y_side_pos()[i];
+      }
+    if (bb_sizes) {
+      bb_sizes[0] = L->bb_side_mouse();
+      bb_sizes[1] = L->bb_bottom_mouse();
+    }
     for (unsigned i = 0; i < L->N_frames(); ++i) {  // main.cpp:54-82
       L->readFrame();
       L->cropBoundingBox();

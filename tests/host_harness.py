@@ -32,8 +32,8 @@ def lib():
         if not os.path.exists(SO):
             raise RuntimeError(f"{SO} is missing: run tests/host_harness.build()")
         L = C.CDLL(SO)
-        L.lmh_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
-                              C.c_int, C.c_void_p, C.c_char_p, C.c_int]
+        L.lmh_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                              C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_int]
         L.lmh_run.restype = C.c_int
         L.lmh_selftest.argtypes = [C.c_char_p, C.c_int]
         L.lmh_selftest.restype = C.c_int
@@ -47,20 +47,29 @@ class HostError(RuntimeError):
         self.code = code
 
 
-def run_video(cfg, frames, batch=8, device=0, n_frames=None, call_order=0):
+def run_video(cfg, frames, batch=8, device=0, n_frames=None, call_order=0, bb_params=None, with_bb=False):
     """LocoMouse_Initialize + main.cpp's loop over `frames`; returns the
-    result containers as a result dict (abi.result_to_numpy layout)."""
+    result containers as a result dict (abi.result_to_numpy layout).
+    bb_params: lm_bb_params for the whole-video BB pass (used when
+    cfg.params.use_provided_bounding_box == 0); with_bb also returns the
+    corners [n][3] (x, y_bottom, y_side) and the (side, bottom) box sizes."""
     import numpy as np
-    from locomouse_cpp_amd.abi import lm_batch_result, result_to_numpy
+    from locomouse_cpp_amd.abi import lm_batch_result, lm_rect, result_to_numpy
     frames = np.ascontiguousarray(frames, dtype=np.uint8)
     out = lm_batch_result()
     err = C.create_string_buffer(512)
     n = frames.shape[0] if n_frames is None else n_frames
-    rc = lib().lmh_run(C.byref(cfg.setup), C.byref(cfg.params), C.byref(cfg.model), frames.ctypes.data, n,
-                       frames.shape[0], batch, device, call_order, C.byref(out), err, 512)
+    corners = np.zeros((n, 3), dtype=np.uint32)
+    sizes = (lm_rect * 2)()
+    rc = lib().lmh_run(C.byref(cfg.setup), C.byref(cfg.params), C.byref(cfg.model),
+                       C.byref(bb_params) if bb_params is not None else None, frames.ctypes.data, n,
+                       frames.shape[0], batch, device, call_order, C.byref(out), corners.ctypes.data, sizes, err, 512)
     if rc:
         raise HostError(rc, err.value.decode())
-    return result_to_numpy(out)
+    res = result_to_numpy(out)
+    if with_bb:
+        return res, corners, (sizes[0].tuple(), sizes[1].tuple())
+    return res
 
 
 def selftest():

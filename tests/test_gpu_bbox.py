@@ -146,3 +146,12 @@ def test_bb_argument_errors():
     with pytest.raises(LMError):
         ctx.push(cfg.frames(0, 3))  # n > max_batch
     ctx.close()
+
+
+@pytest.mark.parametrize("k,conn", [(1, 8), (3, 4)])
+def test_bb_many_runs_global_fallback(k, conn):
+    """Noisy masks with more row runs per view than the LDS run table holds
+    (LM_BB_RUN_CAP) keep their run tables in global memory."""
+    cfg = SyntheticConfig()
+    frames = bb_frames(cfg, 4, seed=17, noise=60)
+    check(cfg, abi.bb_params(median_filter_size=k, connectivity=conn, semantics=INTEGER), frames, batch=4)

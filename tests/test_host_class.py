@@ -18,12 +18,41 @@ def test_container_semantics():
     H.selftest()
 
 
-def test_whole_video_bb_pass_is_reported_not_on_path():
+def test_whole_video_bb_pass_needs_a_rewindable_reader_and_method_0():
     cfg = S.SyntheticConfig()
     cfg.params.use_provided_bounding_box = 0
+    with pytest.raises(H.HostError, match="rewind") as e:
+        H.run_video(cfg, cfg.frames(0, 2))  # no bb_params -> no rewind callback
+    assert e.value.code == 1
+    cfg = S.SyntheticConfig(method=1)
+    cfg.params.use_provided_bounding_box = 0
     with pytest.raises(H.HostError, match="computeBoundingBox") as e:
-        H.run_video(cfg, cfg.frames(0, 2))
+        H.run_video(cfg, cfg.frames(0, 2))  # LocoMouse_TM's pass is a later row
     assert e.value.code == 2  # std::runtime_error, caught by main.cpp:98-101
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [5, 16])
+def test_computed_bounding_box_then_main_loop_matches_oracle(batch):
+    """use_provided_bounding_box = 0: getBoundingBox -> computeBoundingBox
+    (lm_bb_*), rewind, then the per-frame loop on the computed boxes; against
+    oracle.bb_run followed by the oracle loop on the same boxes."""
+    import numpy as np
+    from locomouse_cpp_amd import abi
+    from oracle import oracle as O
+    from test_gpu_parity import assert_same
+    from bb_scenes import bb_frames
+    cfg = S.SyntheticConfig()
+    cfg.params.use_provided_bounding_box = 0
+    frames = bb_frames(cfg, 12, seed=4)
+    bbp = abi.bb_params(semantics=abi.LM_BB_FIRSTLAST_INTEGER)
+    got, corners, sizes = H.run_video(cfg, frames, batch=batch, bb_params=bbp, with_bb=True)
+    r = O.bb_run(cfg.setup, bbp, frames)
+    ref_corners = np.stack([r["x_pos"], r["y_bottom_pos"], r["y_side_pos"]], 1)
+    assert np.array_equal(corners, ref_corners)
+    assert sizes == (r["bb_side_mouse"], r["bb_bottom_mouse"])
+    cfg2 = S.SyntheticConfig(bounding_boxes={"side": r["bb_side_mouse"], "bottom": r["bb_bottom_mouse"]})
+    assert_same(got, O.OracleRun(cfg2, frames, bb=ref_corners.astype(np.int32)).result, f"host bb b{batch}: ")
 
 
 @pytest.mark.gpu
