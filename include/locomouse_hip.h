@@ -69,14 +69,15 @@ typedef struct {
 /* config.yml keys the per-frame path reads (LocoMouse_class.cpp:18-249;
  * defaults LocoMouse_class.hpp:53-74).  Keys that only feed the whole-video
  * bounding-box pass (median_filter_size, min_pixel_visible,
- * moving_average_window) are not part of this path. */
+ * moving_average_window, the TM zero_* / bb_* keys) are in lm_bb_params. */
 typedef struct {
   int32_t conn_comp_connectivity;               /* 4 or 8 */
   int32_t max_displacement_bottom;
   int32_t max_displacement_side;
   int32_t occlusion_grid_spacing_pixels_side;
   int32_t occlusion_grid_spacing_pixels_bottom;
-  int32_t use_provided_bounding_box;            /* must be 1 (BB pre-pass not on this path) */
+  int32_t use_provided_bounding_box;            /* must be 1: a computed box (lm_bb_*) is passed as
+                                                   its sizes here + per-frame corners (bb) */
   int32_t transform_gray_values;                /* LUT on the bottom crop mask, :1445-1454 */
   int32_t reserved0;
   double side_bottom_min_overlap;
@@ -245,37 +246,47 @@ int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32
  * that device), so the spans of several contexts' streams can be merged. */
 int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, double* t1, int32_t cap);
 
-/* ---- whole-video bounding-box pass, method 0 ----
+/* ---- whole-video bounding-box pass ----
  *
- * Replaces LocoMouse::computeBoundingBox (LocoMouse_class.cpp:579-653) with
- * computeMouseBox (:948-997), largestBWAreaObject (:921-946),
- * firstLastOverT (LocoMouse_class.hpp:411-440), computeMouseBoxSize
- * (:1481-1506), medianvec / stdvec / vecmovingaverage (:1516-1608).  Frames
- * are pushed in video order (the median filter's zero-padded border carries
- * state from frame to frame, :585-603 + :952); lm_bb_finish runs the
- * whole-video post-processing.  The results feed the detection path as
- * lm_params.bounding_box_* sizes plus the per-frame `bb` corners of
+ * Replaces the virtual computeBoundingBox of the three methods:
+ *   method 0  LocoMouse::computeBoundingBox (LocoMouse_class.cpp:579-653) with
+ *             computeMouseBox (:948-997), largestBWAreaObject (:921-946),
+ *             firstLastOverT (LocoMouse_class.hpp:411-440), computeMouseBoxSize
+ *             (:1481-1506), medianvec / stdvec / vecmovingaverage (:1516-1608);
+ *   method 1  LocoMouse_TM::computeBoundingBox (LocoMouse_TM.cpp:115-157,
+ *             computeMouseBox_DD :192-241);
+ *   method 2  LocoMouse_TM_DE::computeBoundingBox (LocoMouse_TM_DE.cpp:8-113)
+ *             with imadjust_default (LocoMouse_class.cpp:3244-3311).
+ * Frames are pushed in video order (method 0's median filter carries its
+ * zero-padded border from frame to frame, :585-603 + :952); lm_bb_finish
+ * runs the whole-video post-processing.  The results feed the detection path
+ * as lm_params.bounding_box_* sizes plus the per-frame `bb` corners of
  * lm_detect_batch. */
 
-/* firstLastOverT reads the CV_32S row/column sums through ptr<float>
- * (LocoMouse_class.hpp:419), i.e. it compares the sums' bit patterns as
- * floats against min_pixel_visible.  AS_EXECUTED reproduces that (the
- * drop-in default); INTEGER compares the integer sums, as the comment at
- * :967-970 intends. */
+/* firstLastOverT reads the CV_32S row/column sums of methods 0 and 1 through
+ * ptr<float> (LocoMouse_class.hpp:419), i.e. it compares the sums' bit
+ * patterns as floats against min_pixel_visible.  AS_EXECUTED reproduces that
+ * (the drop-in default); INTEGER compares the integer sums, as the comment at
+ * :967-970 intends (method 0 only).  Method 2 sums in CV_32F and is unaffected. */
 #define LM_BB_FIRSTLAST_AS_EXECUTED 0
 #define LM_BB_FIRSTLAST_INTEGER 1
 
 typedef struct {
-  int32_t median_filter_size;     /* odd, 1..63 (config.yml, :41-45) */
-  int32_t min_pixel_visible;      /* >= 0 (:47-50) */
+  int32_t median_filter_size;     /* odd, 1..63 (config.yml, :41-45) — method 0 */
+  int32_t min_pixel_visible;      /* >= 0 (:47-50) — methods 0, 1 */
   int32_t moving_average_window;  /* odd, >= 1 (:120-123) */
-  int32_t conn_comp_connectivity; /* 4 or 8 (:33-39) */
+  int32_t conn_comp_connectivity; /* 4 or 8 (:33-39) — method 0 */
   int32_t firstlast_semantics;    /* LM_BB_FIRSTLAST_* */
+  /* LocoMouse_TM config keys (TM.cpp:44-113, defaults TM.hpp:19-31) — method 1 */
+  int32_t zero_col_pre, zero_col_post, zero_row_pre, zero_row_post;
+  int32_t bb_width, bb_height_side;
   int32_t reserved0;
 } lm_bb_params;
 
 /* The six per-frame values of computeMouseBox, after :636
- * (bb_y_bottom += BB_BOTTOM_VIEW.y). */
+ * (bb_y_bottom += BB_BOTTOM_VIEW.y).  Methods 1 and 2 compute x only; their
+ * y values are the fixed corners they assign (TM.cpp:140-141,
+ * TM_DE.cpp:36-37) and the sizes are 0. */
 typedef struct {
   double x, y_bottom, y_side, width, height_bottom, height_side;
 } lm_bb_frame;
@@ -292,9 +303,11 @@ typedef struct {
 
 typedef struct lm_bb_ctx lm_bb_ctx;
 
-/* setup: as for lm_ctx_create (setup->method must be 0; the view boxes must
- * span the full corrected width, as firstLastOverT reads I.cols sums, and
- * must not overlap).  max_batch bounds n of lm_bb_push*. */
+/* setup: as for lm_ctx_create; setup->method selects the pass.  The view
+ * boxes must span the full corrected width (firstLastOverT reads N_COLS
+ * sums) and, for method 0, must not overlap.  max_batch bounds n of
+ * lm_bb_push*.  Method 1 supports LM_BB_FIRSTLAST_AS_EXECUTED only: its
+ * result then depends on min_pixel_visible alone. */
 lm_status lm_bb_create(int32_t device, const lm_setup* setup, const lm_bb_params* params, int32_t max_batch,
                        lm_bb_ctx** out);
 void lm_bb_destroy(lm_bb_ctx* ctx);

@@ -131,6 +131,12 @@ class lm_bb_params(C.Structure):
         ("moving_average_window", C.c_int32),
         ("conn_comp_connectivity", C.c_int32),
         ("firstlast_semantics", C.c_int32),
+        ("zero_col_pre", C.c_int32),
+        ("zero_col_post", C.c_int32),
+        ("zero_row_pre", C.c_int32),
+        ("zero_row_post", C.c_int32),
+        ("bb_width", C.c_int32),
+        ("bb_height_side", C.c_int32),
         ("reserved0", C.c_int32),
     ]
 
@@ -156,9 +162,12 @@ BB_FRAME_DTYPE = np.dtype([(n, "<f8") for n in ("x", "y_bottom", "y_side", "widt
 
 
 def bb_params(median_filter_size=11, min_pixel_visible=1, moving_average_window=5, connectivity=8,
-              semantics=LM_BB_FIRSTLAST_AS_EXECUTED):
-    """lm_bb_params with the reference defaults (LocoMouse_class.hpp:53-69)."""
-    return lm_bb_params(median_filter_size, min_pixel_visible, moving_average_window, connectivity, semantics, 0)
+              semantics=LM_BB_FIRSTLAST_AS_EXECUTED, zero_cols=(46, 760), zero_rows=(100, 149), bb_width=400,
+              bb_height_side=150):
+    """lm_bb_params with the reference defaults (LocoMouse_class.hpp:53-69,
+    LocoMouse_TM.hpp:19-31)."""
+    return lm_bb_params(median_filter_size, min_pixel_visible, moving_average_window, connectivity, semantics,
+                        zero_cols[0], zero_cols[1], zero_rows[0], zero_rows[1], bb_width, bb_height_side, 0)
 
 
 CAND_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("score", "<f8")])

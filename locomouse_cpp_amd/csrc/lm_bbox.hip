@@ -589,6 +589,112 @@ __global__ __launch_bounds__(1024) void k_bb_cc(const LmBBConst K, const uint8_t
   }
 }
 
+// ------------------------------------------------------------------- k_bb_de
+// LocoMouse_TM_DE::computeMouseBox_DE (TM_DE.cpp:56-113), one workgroup per
+// frame: histogram of the corrected side view -> imadjust_default LUT
+// (LocoMouse_class.cpp:3244-3311, float cumulative sums, convertTo with float
+// scale / shift), the hard-coded zero bands (only rows [100, 149) and columns
+// [46, 760) survive), threshold(12.75) and CV_32F column sums, then
+// firstLastOverT(th = 10) and bb_x = min(width - 1, last * 1.1).
+__global__ __launch_bounds__(1024) void k_bb_de(const LmBBConst K, const uint8_t* const* __restrict__ frame_ptr,
+                                                const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+                                                const uint8_t* __restrict__ luts, double* __restrict__ bbx) {
+  extern __shared__ int colc[];  // [n_cols]
+  __shared__ unsigned hist[16][256];
+  __shared__ uint8_t lut[256], lut2[256];
+  __shared__ float s_sf, s_hf;
+  __shared__ int s_noscale, s_last, s_cnt;
+  const int f = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, wave = tid >> 6;
+  const int NC = K.n_cols, vy = K.view_y[0], vh = K.view_h[0];
+  const uint8_t* __restrict__ F = frame_ptr[f];
+  if (tid < 256) lut[tid] = luts[f * 256 + tid];
+  for (int i = tid; i < 16 * 256; i += nt) (&hist[0][0])[i] = 0;
+  for (int i = tid; i < NC; i += nt) colc[i] = 0;
+  if (tid == 0) {
+    s_last = -1;
+    s_cnt = 0;
+  }
+  __syncthreads();
+  auto pix = [&](int r, int c) -> int {  // corrected image I(r, c) (readFrame, :1302-1327)
+    const int cs = K.flip ? NC - 1 - c : c;
+    const int idx = cal[(int64_t)r * NC + cs];
+    const int fv = F[idx], bv = bkg[idx];
+    return lut[fv > bv ? fv - bv : 0];
+  };
+  const int np = vh * NC;
+  for (int q = tid; q < np; q += nt) {
+    const int r = q / NC, c = q - r * NC;
+    atomicAdd(&hist[wave][pix(vy + r, c)], 1u);
+  }
+  __syncthreads();
+  if (tid < 256) {
+    unsigned h = 0;
+    for (int w = 1; w < 16; ++w) h += hist[w][tid];
+    hist[0][tid] += h;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double sd = 0;
+    for (int i = 0; i < 256; ++i) sd += (float)hist[0][i];
+    const float sum_histf = (float)sd, min_tol = 0.01f, max_tol = 0.99f;
+    float cum = 0;
+    int idx0 = 0, idx1 = 0, imin = 0, imax = 0;
+    bool cmin = true, cmax = true;
+    for (int i = 0; i < 256; ++i) {
+      cum = __fadd_rn(cum, (float)hist[0][i]);
+      const float cn = __fdiv_rn(cum, sum_histf);
+      if ((cn > min_tol) & cmin) {
+        idx0 = i;
+        cmin = false;
+        imin = i;
+      }
+      if ((cn >= max_tol) & cmax) {
+        idx1 = i;
+        cmax = false;
+        imax = i;
+      }
+      if (!(cmin || cmax)) break;
+    }
+    if (imin == imax) idx1 = 256;
+    const float r0 = __fdiv_rn((float)idx0, 255.0f), r1 = __fdiv_rn((float)idx1, 255.0f);
+    const double d = (double)__fsub_rn(r1, r0);
+    const double inv = 1. / d;
+    const double alpha = inv, beta = -(double)r0 * inv;
+    s_noscale = fabs(alpha - 1) < 2.220446049250313e-16 && fabs(beta) < 2.220446049250313e-16;
+    s_sf = (float)alpha;
+    s_hf = (float)beta;
+  }
+  __syncthreads();
+  if (tid < 256) {
+    int v = tid;
+    if (!s_noscale) {
+      const float t = __fadd_rn(__fmul_rn((float)tid, s_sf), s_hf);
+      const int iv = (int)rintf(t);
+      v = iv < 0 ? 0 : (iv > 255 ? 255 : iv);
+    }
+    lut2[tid] = (uint8_t)v;
+  }
+  __syncthreads();
+  const int r0 = 100, r1 = min(149, vh), c0 = 46, c1 = min(760, NC);
+  const int bw = c1 - c0;
+  for (int q = tid; q < (r1 - r0) * bw; q += nt) {
+    const int r = r0 + q / bw, c = c0 + q % bw;
+    if (lut2[pix(vy + r, c)] > 12) atomicAdd(&colc[c], 1);
+  }
+  __syncthreads();
+  for (int i = tid; i < NC; i += nt)
+    if ((float)colc[i] >= (float)10) {  // firstLastOverT(Row_side, N_COLS, lims, MIN_PIXEL_COUNT = 10)
+      atomicMax(&s_last, i);
+      atomicAdd(&s_cnt, 1);
+    }
+  __syncthreads();
+  if (tid == 0) {
+    const int last = s_cnt == 0 ? -1 : (s_cnt == 1 ? 0 : s_last);
+    const double a = (double)(K.n_cols - 1), b = (double)last * 1.1;  // std::min(width - 1, last * WIDTH_MARGIN)
+    bbx[f] = b < a ? b : a;
+  }
+}
+
 // ================================================================ host side
 
 struct lm_bb_ctx {
@@ -606,6 +712,8 @@ struct lm_bb_ctx {
   DevBuf<unsigned> cc;
   HostBuf<const uint8_t*> fptr;
   HostBuf<int32_t> lims;
+  HostBuf<double> bbx;  // method 2: per-frame bb_x
+  int method = 0, side_h = 0, bottom_h = 0;
   int last_n = 0;
   std::vector<lm_bb_frame> per;
   std::vector<uint32_t> x_pos, yb_pos, ys_pos;
@@ -628,9 +736,12 @@ namespace {
 
 void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params* bp) {
   if (!su || !bp) throw std::invalid_argument("null setup / params");
-  if (su->method != 0)
-    throw std::invalid_argument("lm_bb_*: only method 0 (LocoMouse::computeBoundingBox) is on this path.");
   const lm_bb_params& P = *bp;
+  const int method = su->method;
+  if (method < 0 || method > 2) throw std::invalid_argument("method must be 0, 1 or 2.");
+  if (method == 1 && P.firstlast_semantics != LM_BB_FIRSTLAST_AS_EXECUTED)
+    throw std::invalid_argument("lm_bb_*, method 1: only LM_BB_FIRSTLAST_AS_EXECUTED (the result then depends on "
+                                "min_pixel_visible alone; bwAreaOpen / disk filter / imfill are not run).");
   if (P.conn_comp_connectivity != 4 && P.conn_comp_connectivity != 8)
     throw std::invalid_argument("Invalid configuration parameter: conn_comp_connectivity must be either 4 or 8.");
   if (P.median_filter_size % 2 == 0 || P.median_filter_size < 1 || P.median_filter_size > 63)
@@ -650,15 +761,31 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
       throw std::runtime_error("Calibration mapping indices out of range.");
   const lm_rect vw[2] = {su->view_box_side, su->view_box_bottom};
   for (int v = 0; v < 2; ++v) {
-    if (vw[v].x != 0 || vw[v].width != NC)
-      throw std::invalid_argument("BB pass: view boxes must span the corrected width (firstLastOverT reads I.cols sums, :975-976).");
-    if (vw[v].y < 0 || vw[v].height <= 0 || vw[v].y + vw[v].height > NR)
+    if ((v == 0 || method == 0) && (vw[v].x != 0 || vw[v].width != NC))
+      throw std::invalid_argument("BB pass: view boxes must span the corrected width (firstLastOverT reads N_COLS sums, :975-976).");
+    if (vw[v].x < 0 || vw[v].y < 0 || vw[v].height <= 0 || vw[v].width <= 0 || vw[v].y + vw[v].height > NR ||
+        vw[v].x + vw[v].width > NC)
       throw std::runtime_error("BB pass: view box outside the corrected image.");
   }
-  if (NR < P.median_filter_size / 2 || NC < P.median_filter_size / 2)
-    throw std::invalid_argument("BB pass: corrected image smaller than the median filter's half size.");
-  if (vw[0].y < vw[1].y + vw[1].height && vw[1].y < vw[0].y + vw[0].height)
-    throw std::invalid_argument("BB pass: overlapping side and bottom view boxes are not supported.");
+  if (method == 0) {
+    if (NR < P.median_filter_size / 2 || NC < P.median_filter_size / 2)
+      throw std::invalid_argument("BB pass: corrected image smaller than the median filter's half size.");
+    if (vw[0].y < vw[1].y + vw[1].height && vw[1].y < vw[0].y + vw[0].height)
+      throw std::invalid_argument("BB pass: overlapping side and bottom view boxes are not supported.");
+  } else if (method == 1) {  // computeMouseBox_DD's colRange / rowRange bounds (TM.cpp:205-208)
+    if (P.zero_col_pre < 0 || P.zero_col_post < 0 || P.zero_row_pre < 0 || P.zero_row_post < 0)
+      throw std::invalid_argument("Invalid configuration parameter: zero_*_* parameters range from 0 to the relevant size of the image.");
+    if (P.bb_width < 1 || P.bb_height_side < 1)
+      throw std::invalid_argument("Invalid configuration parameter: bb_width / bb_height_side must be at least 1 pixel.");
+    if (P.zero_col_pre > NC || P.zero_col_post > NC || P.zero_row_pre > vw[0].height || P.zero_row_post > vw[0].height)
+      throw std::runtime_error("BB pass, method 1: zero_* ranges exceed the side view (cv::Mat::colRange/rowRange assert).");
+  } else {  // computeMouseBox_DE's hard-coded ranges (TM_DE.cpp:69-72)
+    if (760 > NC || 149 > vw[0].height)
+      throw std::runtime_error("BB pass, method 2: the hard-coded zero ranges exceed the side view (cv::Mat::colRange/rowRange assert).");
+  }
+  c->method = method;
+  c->side_h = vw[0].height;
+  c->bottom_h = vw[1].height;
   c->P = P;
   c->npix = npix;
   c->frame_stride = (npix + 255) / 256 * 256;
@@ -697,6 +824,21 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
   if ((int64_t)NC * std::max(vw[0].height, vw[1].height) >= (1ll << 31))
     throw std::invalid_argument("BB pass: view too large.");
 
+  if (method != 0) {
+    c->bkg.alloc((size_t)c->frame_stride);
+    HIPCHK(hipMemset(c->bkg.p, 0, c->bkg.n));
+    HIPCHK(hipMemcpy(c->bkg.p, su->background, (size_t)npix, hipMemcpyHostToDevice));
+    c->cal.alloc((size_t)NR * NC);
+    HIPCHK(hipMemcpy(c->cal.p, su->ind_warp_mapping, sizeof(int32_t) * NR * NC, hipMemcpyHostToDevice));
+    if (method == 2) {
+      c->frames.alloc((size_t)c->frame_stride * c->max_batch);
+      c->luts.alloc((size_t)256 * c->max_batch);
+      c->fptr.alloc((size_t)c->max_batch);
+      c->bbx.alloc((size_t)c->max_batch);
+      HIPCHK(hipFuncSetAttribute((const void*)k_bb_de, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * NC));
+    }
+    return;
+  }
   HIPCHK(hipFuncSetAttribute((const void*)k_bb_ring, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->ring_lds));
   HIPCHK(hipFuncSetAttribute((const void*)k_bb_center, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->center_lds));
   HIPCHK(hipFuncSetAttribute((const void*)k_bb_cc, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->cc_lds));
@@ -747,6 +889,20 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
   HIPCHK(hipSetDevice(c->device));
   const LmBBConst& K = c->K;
   hipStream_t s = c->stream;
+  if (c->method == 1) {
+    // computeMouseBox_DD: the as-executed result depends on min_pixel_visible
+    // only (see lm_bb_create); the frames themselves are not read.
+    lm_bb_frame o{};
+    o.x = c->P.min_pixel_visible <= 0 ? (double)(K.n_cols - 1) : -1.0;  // firstLastOverT -> lims[1]
+    o.y_bottom = (double)(K.n_rows - 1);
+    o.y_side = 164.0;  // 165 - 1 (TM.cpp:141)
+    c->last_n = n;
+    for (int i = 0; i < n; ++i) {
+      c->per.push_back(o);
+      if (out) out[i] = o;
+    }
+    return;
+  }
   for (int i = 0; i < n; ++i) {
     if (device_frames) {
       c->fptr.p[i] = frames + (int64_t)i * pitch;
@@ -758,6 +914,21 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
   }
   const int64_t np = (int64_t)K.n_rows * K.n_cols;
   k_minmax_lut<<<n, 1024, 0, s>>>(c->fptr.d, c->bkg.p, (int)c->npix, 0, nullptr, 0, c->luts.p);
+  if (c->method == 2) {
+    k_bb_de<<<n, 1024, 4 * K.n_cols, s>>>(K, c->fptr.d, c->bkg.p, c->cal.p, c->luts.p, c->bbx.d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    c->last_n = n;
+    for (int i = 0; i < n; ++i) {
+      lm_bb_frame o{};
+      o.x = c->bbx.p[i];
+      o.y_bottom = (double)(K.n_rows - 1);
+      o.y_side = (double)(c->side_h - 1);
+      c->per.push_back(o);
+      if (out) out[i] = o;
+    }
+    return;
+  }
   k_bb_ingest<<<dim3((unsigned)((np + 1023) / 1024), n), 256, 0, s>>>(K, c->fptr.d, c->bkg.p, c->cal.p, c->luts.p,
                                                                        c->M.p);
   if (K.p > 0) {
@@ -833,6 +1004,23 @@ void bb_movavg(const std::vector<double>& v, std::vector<uint32_t>& out, int N) 
 void bb_finish(lm_bb_ctx* c, lm_bb_result* out) {
   const size_t N = c->per.size();
   if (N == 0) throw std::invalid_argument("lm_bb_finish: no frame was pushed.");
+  out->n_frames = (int32_t)N;
+  out->reserved0 = 0;
+  out->frames = c->per.data();
+  if (c->method != 0) {  // TM.cpp:145-155, TM_DE.cpp:41-52
+    std::vector<double> x(N);
+    for (size_t i = 0; i < N; ++i) x[i] = c->per[i].x;
+    bb_movavg(x, c->x_pos, c->P.moving_average_window);
+    c->yb_pos.assign(N, (uint32_t)(c->K.n_rows - 1));
+    c->ys_pos.assign(N, c->method == 1 ? 164u : (uint32_t)(c->side_h - 1));
+    const int w = c->method == 1 ? c->P.bb_width : 400;
+    out->bb_side_mouse = lm_rect{0, 0, w, c->method == 1 ? c->P.bb_height_side : c->side_h};
+    out->bb_bottom_mouse = lm_rect{0, 0, w, c->bottom_h};
+    out->x_pos = c->x_pos.data();
+    out->y_bottom_pos = c->yb_pos.data();
+    out->y_side_pos = c->ys_pos.data();
+    return;
+  }
   std::vector<double> x(N), yb(N), ys(N), w(N), hb(N), ht(N);
   for (size_t i = 0; i < N; ++i) {
     x[i] = c->per[i].x;
@@ -908,6 +1096,7 @@ LM_API lm_status lm_bb_finish(lm_bb_ctx* ctx, lm_bb_result* out) {
 
 LM_API lm_status lm_bb_debug_binary(lm_bb_ctx* ctx, int32_t f, uint8_t* out, int32_t rows, int32_t cols) {
   if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  if (ctx->method != 0) return fail(LM_ERR_INVALID_ARGUMENT, "debug binary images exist for method 0 only");
   if (f < 0 || f >= ctx->last_n) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
   if (rows != ctx->K.n_rows || cols != ctx->K.n_cols) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
   return guarded([&] {

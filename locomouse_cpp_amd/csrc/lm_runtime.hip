@@ -269,7 +269,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       throw std::invalid_argument("location_prior: CV_Assert(minx < maxx && miny < maxy)");
   }
   if (!P->use_provided_bounding_box)
-    throw std::invalid_argument("use_provided_bounding_box = 0 needs the whole-video BB pass (not on this path).");
+    throw std::invalid_argument("use_provided_bounding_box = 0: run the whole-video BB pass (lm_bb_*) first and pass its boxes and corners.");
   if (P->transform_gray_values)
     throw std::runtime_error(
         "transform_gray_values: LUT re-types the bottom mask to CV_32F and Mat::setTo asserts (LocoMouse_class.cpp:1448, :849).");

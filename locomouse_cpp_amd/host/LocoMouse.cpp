@@ -170,12 +170,15 @@ void LocoMouse::getBoundingBox() {
 // averages — all in lm_bb_push / lm_bb_finish.  The video is re-read from
 // frame 0 afterwards, as initializeFeatureLoop's V.set(POS_FRAMES, 0)
 // (:761-762) does in the reference.
-void LocoMouse::computeBoundingBox() {
+void LocoMouse::computeBoundingBox() { runBoundingBoxPass(0); }
+
+// The pass of LocoMouse (method 0), LocoMouse_TM (1) or LocoMouse_TM_DE (2).
+void LocoMouse::runBoundingBoxPass(int method) {
   if (!IN.rewind)
     throw std::invalid_argument("computeBoundingBox: the frame reader cannot rewind (V.set(CV_CAP_PROP_POS_FRAMES, 0)).");
   if (N_FRAMES == 0) throw std::runtime_error("computeBoundingBox: the video has no frames.");
   lm_setup su = IN.setup;
-  su.method = 0;
+  su.method = method;
   lm_bb_ctx* raw = nullptr;
   throw_on_error(lm_bb_create(IN.device, &su, &IN.bb_params, IN.batch, &raw));
   std::unique_ptr<lm_bb_ctx, void (*)(lm_bb_ctx*)> bb(raw, lm_bb_destroy);
@@ -328,19 +331,11 @@ LM_ACCESSOR(tracks_tail, TRACKS_TAIL)
 
 LocoMouse_TM::LocoMouse_TM(const LocoMouse_Inputs& inputs) : LocoMouse(inputs) { METHOD = 1; }
 void LocoMouse_TM::readFrame() { LocoMouse::readFrame(); }  // + imadjust (TM.cpp:243-249), on the device
-void LocoMouse_TM::computeBoundingBox() {
-  throw std::runtime_error(
-      "LocoMouse_TM::computeBoundingBox: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) is not on this "
-      "path; set use_provided_bounding_box = 1.");
-}
+void LocoMouse_TM::computeBoundingBox() { runBoundingBoxPass(1); }  // TM.cpp:115-157
 
 LocoMouse_TM_DE::LocoMouse_TM_DE(const LocoMouse_Inputs& inputs) : LocoMouse(inputs) { METHOD = 2; }
 void LocoMouse_TM_DE::readFrame() { LocoMouse::readFrame(); }
-void LocoMouse_TM_DE::computeBoundingBox() {
-  throw std::runtime_error(
-      "LocoMouse_TM_DE::computeBoundingBox: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) is not on this "
-      "path; set use_provided_bounding_box = 1.");
-}
+void LocoMouse_TM_DE::computeBoundingBox() { runBoundingBoxPass(2); }  // TM_DE.cpp:8-54
 
 std::unique_ptr<LocoMouse> LocoMouse_Initialize(const LocoMouse_Inputs& inputs) {
   switch (inputs.setup.method) {

@@ -56,7 +56,7 @@ struct LocoMouse_Inputs {
   // median_filter_size / min_pixel_visible / moving_average_window /
   // conn_comp_connectivity, and V.set(CV_CAP_PROP_POS_FRAMES, 0) (:761-762)
   // to re-read the video from frame 0 after the pass.
-  lm_bb_params bb_params{11, 1, 5, 8, LM_BB_FIRSTLAST_AS_EXECUTED, 0};
+  lm_bb_params bb_params{11, 1, 5, 8, LM_BB_FIRSTLAST_AS_EXECUTED, 46, 760, 100, 149, 400, 150, 0};
   std::function<void()> rewind;
 };
 
@@ -129,6 +129,9 @@ class LocoMouse {
 
  private:
   lm_ctx* CTX = nullptr;
+ protected:
+  void runBoundingBoxPass(int method);  // lm_bb_* over the whole video, then rewind
+ private:
   std::vector<uint8_t> PENDING;  // raw frames read but not yet processed
   int N_PENDING = 0;
   size_t FRAME_BYTES = 0;
@@ -142,7 +145,7 @@ class LocoMouse_TM : public LocoMouse {
  public:
   explicit LocoMouse_TM(const LocoMouse_Inputs& inputs);
   void readFrame() override;
-  void computeBoundingBox() override;  // TM.cpp:115-241 — §8(f) row 1
+  void computeBoundingBox() override;  // TM.cpp:115-241 — §8(f) row 1 (lm_bb_*, method 1)
 };
 
 // LocoMouse_TM_DE (LocoMouse_TM_DE.hpp:30-45): the same readFrame as TM.
@@ -150,7 +153,7 @@ class LocoMouse_TM_DE : public LocoMouse {
  public:
   explicit LocoMouse_TM_DE(const LocoMouse_Inputs& inputs);
   void readFrame() override;
-  void computeBoundingBox() override;  // TM_DE.cpp:8-113 — §8(f) row 1
+  void computeBoundingBox() override;  // TM_DE.cpp:8-113 — §8(f) row 1 (lm_bb_*, method 2)
 };
 
 // LocoMouse_Methods.cpp:3-26: 0 LocoMouse, 1 LocoMouse_TM, 2 LocoMouse_TM_DE,

@@ -1155,7 +1155,10 @@ static void vecmovingaverage(const std::vector<double>& v, std::vector<uint32_t>
 class BBOracle {
  public:
   BBOracle(const lm_setup& su, const lm_bb_params& bp) : P(bp) {
-    if (su.method != 0) throw std::invalid_argument("BB pass: only method 0 (LocoMouse::computeBoundingBox) is restated.");
+    METHOD = su.method;
+    if (METHOD < 0 || METHOD > 2) throw std::invalid_argument("BB pass: method must be 0, 1 or 2.");
+    if (METHOD == 1 && P.firstlast_semantics != LM_BB_FIRSTLAST_AS_EXECUTED)
+      throw std::invalid_argument("BB pass, method 1: only the as-executed firstLastOverT is restated.");
     if (P.median_filter_size % 2 == 0 || P.median_filter_size < 1 || P.median_filter_size > 63)
       throw std::invalid_argument("Invalid configuration parameter: median_filter_size must be odd.");
     if (P.min_pixel_visible < 0)
@@ -1176,10 +1179,124 @@ class BBOracle {
     // :585-591
     pad = P.median_filter_size / 2;
     I_median = Mat8(N_ROWS + 2 * pad, N_COLS + 2 * pad, 0);
+    if (METHOD == 1) {  // computeMouseBox_DD's colRange / rowRange bounds (TM.cpp:205-208)
+      if (P.zero_col_pre > side.width || P.zero_col_post > N_COLS || N_COLS > side.width ||
+          P.zero_row_pre > side.height || P.zero_row_post > side.height)
+        throw std::runtime_error("BB pass, method 1: zero_* ranges exceed the side view (cv::Mat::colRange/rowRange assert).");
+    }
+    if (METHOD == 2) {  // computeMouseBox_DE's hard-coded ranges (TM_DE.cpp:69-72)
+      if (46 > side.width || 760 > N_COLS || N_COLS > side.width || 100 > side.height || 149 > side.height)
+        throw std::runtime_error("BB pass, method 2: the hard-coded zero ranges exceed the side view (cv::Mat::colRange/rowRange assert).");
+    }
   }
 
-  // One iteration of the frame loop :614-626.
+  // imadjust_default (LocoMouse_class.cpp:3244-3311) as a LUT over the image's
+  // histogram: the 1% / 99% cumulative bins (float arithmetic), then the
+  // MatExpr (I - r0) / (r1 - r0) that OpenCV evaluates as
+  // convertTo(alpha = 1/(r1-r0), beta = -r0/(r1-r0)) with float scale/shift.
+  static void imadjust_default_lut(const std::vector<uint32_t>& hist, uint8_t lut[256]) {
+    float sum_histf = 0;
+    {
+      double s = 0;
+      for (int i = 0; i < 256; ++i) s += (float)hist[i];
+      sum_histf = (float)s;
+    }
+    const float min_tol = 0.01f, max_tol = 0.99f;
+    float cumsum_step = 0;
+    int idx0 = 0, idx1 = 0, imin = 0, imax = 0;
+    bool check_min = true, check_max = true;
+    for (int i = 0; i < 256; ++i) {
+      cumsum_step += (float)hist[i];
+      const float cn = cumsum_step / sum_histf;
+      if ((cn > min_tol) & check_min) {
+        idx0 = i;
+        check_min = false;
+        imin = i;
+      }
+      if ((cn >= max_tol) & check_max) {
+        idx1 = i;
+        check_max = false;
+        imax = i;
+      }
+      if (!(check_min || check_max)) break;
+    }
+    if (imin == imax) idx1 = 256;
+    const float r0 = (float)idx0 / (float)255, r1 = (float)idx1 / (float)255;
+    const double d = (double)(r1 - r0);
+    const double alpha = 1.0 * (1. / d), beta = -(double)r0 * (1. / d);
+    const bool noscale = std::fabs(alpha - 1) < DBL_EPSILON && std::fabs(beta) < DBL_EPSILON;
+    const float sf = (float)alpha, hf = (float)beta;
+    for (int p = 0; p < 256; ++p) {
+      if (noscale) {
+        lut[p] = (uint8_t)p;
+        continue;
+      }
+      float v = (float)p * sf;
+      v = v + hf;
+      long iv = std::lrint(v);
+      lut[p] = (uint8_t)(iv < 0 ? 0 : iv > 255 ? 255 : iv);
+    }
+  }
+
+  // LocoMouse_TM_DE::computeMouseBox_DE (TM_DE.cpp:56-113) on the frame's
+  // corrected image (base readFrame, :31).
+  double frame_de(const uint8_t* F) {
+    Mat8 I(N_ROWS, N_COLS, 0);
+    LocoMouseOracle::correct_frame(F, BKG.data(), CAL.data(), VR, VC, N_ROWS, N_COLS, flip, false, I.row(0), N_COLS);
+    std::vector<uint32_t> hist(256, 0);  // calcHist over I_SIDE
+    for (int r = 0; r < side.height; ++r)
+      for (int c = 0; c < side.width; ++c) hist[I.at(side.y + r, side.x + c)]++;
+    uint8_t lut[256];
+    imadjust_default_lut(hist, lut);
+    std::vector<float> colsum(side.width, 0.f);
+    for (int r = 0; r < side.height; ++r)
+      for (int c = 0; c < side.width; ++c) {
+        uint8_t v = lut[I.at(side.y + r, side.x + c)];
+        if (c < 46 || c >= 760 || r < 100 || r >= 149) v = 0;  // colRange/rowRange(...).setTo(0)
+        colsum[c] += v > 12 ? 1.f : 0.f;  // threshold(12.75) -> 1; reduce CV_32FC1
+      }
+    int fl[2];
+    bool has_first = false;  // firstLastOverT<int> on float sums, th = MIN_PIXEL_COUNT = 10
+    fl[0] = fl[1] = 0;
+    int index = 0;
+    for (int i = 0; i < N_COLS; ++i)
+      if (colsum[i] >= (float)10) {
+        fl[index] = i;
+        if (!has_first) {
+          index = 1;
+          has_first = true;
+        }
+      }
+    if (!has_first) fl[0] = fl[1] = -1;
+    return std::min((double)(side.width - 1), (double)fl[1] * 1.1);  // WIDTH_MARGIN (TM_DE.hpp:28)
+  }
+
+  // LocoMouse_TM::computeMouseBox_DD (TM.cpp:192-241): imadjust_default, zero
+  // bands, threshold, bwAreaOpen, disk filter2D, imfill, then reduce to CV_32S
+  // and firstLastOverT.  The CV_32S column sums are integers in
+  // [0, 255 * rows] < 2^23, so read as floats (ptr<float>, :419) they are +0
+  // or denormal: each passes (>= (float)min_pixel_visible) iff
+  // min_pixel_visible <= 0, whatever the image.  The restatement therefore
+  // evaluates firstLastOverT on an all-zero sum vector (tests/test_bbox_oracle.py
+  // checks the premise on random sums).
+  double frame_dd() {
+    std::vector<int32_t> zero(N_COLS, 0);
+    int fl[2];
+    firstLastOverT(zero.data(), (unsigned)N_COLS, fl, P.min_pixel_visible, false);
+    return (double)fl[1];
+  }
+
+  // One iteration of the frame loop :614-626 (method 0), TM.cpp:137-142
+  // (method 1), TM_DE.cpp:33-38 (method 2).
   void frame(const uint8_t* F) {
+    if (METHOD != 0) {
+      lm_bb_frame o{};
+      o.x = METHOD == 1 ? frame_dd() : frame_de(F);
+      o.y_bottom = (double)(N_ROWS - 1);
+      o.y_side = METHOD == 1 ? 164.0 : (double)(side.height - 1);  // 165 - 1 (TM.cpp:141)
+      frames.push_back(o);
+      return;
+    }
     // readFrame(I_center): writes the central ROI of I_median only.
     LocoMouseOracle::correct_frame(F, BKG.data(), CAL.data(), VR, VC, N_ROWS, N_COLS, flip, false,
                                    I_median.row(pad) + pad, I_median.cols);
@@ -1227,9 +1344,20 @@ class BBOracle {
     firstLastOverT(colsum.data(), (unsigned)v.height, lc, P.min_pixel_visible, integer);
   }
 
-  // :628-646
+  // :628-646 (method 0); TM.cpp:145-155; TM_DE.cpp:41-52
   void finish() {
     const int N = (int)frames.size();
+    if (METHOD != 0) {
+      std::vector<double> bb_x(N);
+      for (int i = 0; i < N; ++i) bb_x[i] = frames[i].x;
+      vecmovingaverage(bb_x, x_pos, P.moving_average_window);
+      yb_pos.assign(N, (uint32_t)(N_ROWS - 1));
+      ys_pos.assign(N, METHOD == 1 ? 164u : (uint32_t)(side.height - 1));
+      const int w = METHOD == 1 ? P.bb_width : 400;
+      bb_side = lm_rect{0, 0, w, METHOD == 1 ? P.bb_height_side : side.height};
+      bb_bottom = lm_rect{0, 0, w, bottom.height};
+      return;
+    }
     std::vector<double> bb_x(N), bb_yb(N), bb_ys(N), bw(N), bhb(N), bht(N);
     for (int i = 0; i < N; ++i) {
       bb_x[i] = frames[i].x;
@@ -1254,6 +1382,7 @@ class BBOracle {
   }
 
   lm_bb_params P;
+  int METHOD = 0;
   int VR = 0, VC = 0, N_ROWS = 0, N_COLS = 0, pad = 0;
   bool flip = false;
   std::vector<uint8_t> BKG;
@@ -1409,7 +1538,8 @@ LMO_API int lmo_bb_run(const lm_setup* su, const lm_bb_params* bp, const uint8_t
       x_pos[f] = B.x_pos[f];
       yb_pos[f] = B.yb_pos[f];
       ys_pos[f] = B.ys_pos[f];
-      if (binary) std::memcpy(binary + (size_t)f * B.N_ROWS * B.N_COLS, B.binary[f].d.data(), B.binary[f].d.size());
+      if (binary && B.METHOD == 0)
+        std::memcpy(binary + (size_t)f * B.N_ROWS * B.N_COLS, B.binary[f].d.data(), B.binary[f].d.size());
     }
     *bb_side = B.bb_side;
     *bb_bottom = B.bb_bottom;
@@ -1441,4 +1571,9 @@ LMO_API void lmo_movavg(const double* v, int32_t n, int32_t window, uint32_t* ou
   std::vector<uint32_t> o;
   lmo::vecmovingaverage(in, o, window);
   std::memcpy(out, o.data(), sizeof(uint32_t) * n);
+}
+
+LMO_API void lmo_imadjust_default_lut(const uint32_t* hist, uint8_t* lut) {
+  std::vector<uint32_t> h(hist, hist + 256);
+  lmo::BBOracle::imadjust_default_lut(h, lut);
 }

@@ -45,6 +45,7 @@ def lib():
         L.lmo_synth_background.argtypes = [C.c_int32, C.c_int32, C.c_void_p]
         L.lmo_median_blur.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]
         L.lmo_first_last.argtypes = [C.c_void_p, C.c_uint32, C.c_int32, C.c_int32, C.c_void_p]
+        L.lmo_imadjust_default_lut.argtypes = [C.c_void_p, C.c_void_p]
         L.lmo_movavg.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
         L.lmo_bb_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p,
                                  C.POINTER(lm_rect), C.POINTER(lm_rect), C.c_void_p, C.c_void_p, C.c_void_p,
@@ -176,4 +177,11 @@ def moving_average(values, window):
     v = np.ascontiguousarray(values, dtype=np.float64)
     out = np.zeros(len(v), dtype=np.uint32)
     lib().lmo_movavg(v.ctypes.data, len(v), window, out.ctypes.data)
+    return out
+
+
+def imadjust_default_lut(hist):
+    h = np.ascontiguousarray(hist, dtype=np.uint32)
+    out = np.zeros(256, dtype=np.uint8)
+    lib().lmo_imadjust_default_lut(h.ctypes.data, out.ctypes.data)
     return out

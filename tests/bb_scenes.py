@@ -18,11 +18,11 @@ def _ellipse(yy, xx, cy, cx, a, b):
     return ((xx - cx) / a) ** 2 + ((yy - cy) / b) ** 2 <= 1.0
 
 
-def bb_frames(cfg, n, first=0, noise=1, seed=0, border=False, empty_every=0, ties=False):
+def bb_frames(cfg, n, first=0, noise=1, seed=0, border=False, empty_every=0, ties=False, side_h=None):
     rows, cols, s = cfg.rows, cfg.cols, cfg.scale
     bkg = cfg.background.astype(np.int32)
     yy, xx = np.mgrid[0:rows, 0:cols]
-    side_h = 96 * s
+    side_h = 96 * s if side_h is None else side_h
     out = np.zeros((n, rows, cols), dtype=np.uint8)
     for i in range(n):
         f = first + i

@@ -131,3 +131,88 @@ def test_integer_semantics_tracks_the_mouse():
     assert np.all(per["height_side"] > 10)
     w, hs, hb = r["bb_side_mouse"][2], r["bb_side_mouse"][3], r["bb_bottom_mouse"][3]
     assert 100 < w <= per["width"].max() and 10 < hs <= per["height_side"].max() and 10 < hb
+
+
+def np_imadjust_default_lut(hist):
+    """numpy float32 model of imadjust_default (LocoMouse_class.cpp:3244-3311)."""
+    f32 = np.float32
+    total = f32(float(np.sum(hist.astype(np.float64))))
+    cum, idx0, idx1, imin, imax, cmin, cmax = f32(0), 0, 0, 0, 0, True, True
+    for i in range(256):
+        cum = f32(cum + f32(hist[i]))
+        cn = f32(cum / total)
+        if cn > f32(0.01) and cmin:
+            idx0 = imin = i
+            cmin = False
+        if cn >= f32(0.99) and cmax:
+            idx1 = imax = i
+            cmax = False
+        if not (cmin or cmax):
+            break
+    if imin == imax:
+        idx1 = 256
+    r0, r1 = f32(f32(idx0) / f32(255)), f32(f32(idx1) / f32(255))
+    d = float(f32(r1 - r0))
+    alpha, beta = 1.0 * (1.0 / d), -float(r0) * (1.0 / d)
+    if abs(alpha - 1) < np.finfo(np.float64).eps and abs(beta) < np.finfo(np.float64).eps:
+        return np.arange(256, dtype=np.uint8)
+    v = np.arange(256, dtype=np.float32) * f32(alpha) + f32(beta)
+    return np.clip(np.rint(v), 0, 255).astype(np.uint8)
+
+
+def test_imadjust_default_lut_restatement():
+    rng = np.random.default_rng(21)
+    for t in range(40):
+        h = np.zeros(256, dtype=np.uint32)
+        if t % 4 == 0:
+            h[rng.integers(0, 256)] = 5000  # single value: imin == imax
+        else:
+            lo, hi = sorted(rng.integers(0, 256, size=2))
+            h[lo:hi + 1] = rng.integers(0, 300, size=hi - lo + 1)
+            h[rng.integers(0, 256, size=5)] += rng.integers(0, 50, size=5).astype(np.uint32)
+        if h.sum() == 0:
+            h[0] = 1
+        assert np.array_equal(O.imadjust_default_lut(h), np_imadjust_default_lut(h)), t
+
+
+def test_tm_as_executed_sums_never_reach_float_threshold():
+    """Premise of the method-1 restatement: CV_32S sums in [0, 255*rows] read as
+    floats pass firstLastOverT iff min_pixel_visible <= 0."""
+    rng = np.random.default_rng(4)
+    for rows in (96, 512, 4096):
+        v = rng.integers(0, 255 * rows + 1, size=1024).astype(np.int32)
+        v[rng.random(1024) < 0.3] = 0
+        for th in (0, 1, 7, 255):
+            assert O.first_last(v, th) == O.first_last(np.zeros(1024, np.int32), th)
+
+
+def de_config():
+    """1024 x 320 frames with a 160-row side view: computeMouseBox_DE's
+    hard-coded rows [100, 149) lie inside it."""
+    cfg = SyntheticConfig(rows=320, cols=1024, method=2)
+    cfg.setup.view_box_side = abi.lm_rect(0, 0, 1024, 160)
+    cfg.setup.view_box_bottom = abi.lm_rect(0, 160, 1024, 160)
+    return cfg
+
+
+def test_tm_de_pass_tracks_the_side_view_body():
+    cfg = de_config()
+    frames = bb_frames(cfg, 6, seed=3, side_h=250)
+    r = O.bb_run(cfg.setup, abi.bb_params(), frames)
+    x = r["frames"]["x"]
+    assert np.all(x > 400) and np.all(x <= 1023)
+    assert np.all(r["y_bottom_pos"] == 319) and np.all(r["y_side_pos"] == 159)
+    assert r["bb_side_mouse"] == (0, 0, 400, 160) and r["bb_bottom_mouse"] == (0, 0, 400, 160)
+
+
+def test_tm_pass_as_executed_is_constant():
+    cfg = de_config()
+    cfg.setup.method = 1
+    frames = bb_frames(cfg, 4, seed=3, side_h=250)
+    r = O.bb_run(cfg.setup, abi.bb_params(), frames)
+    assert np.all(r["frames"]["x"] == -1) and np.all(r["x_pos"] == 0xFFFFFFFF)
+    assert np.all(r["y_side_pos"] == 164) and r["bb_side_mouse"] == (0, 0, 400, 150)
+    r0 = O.bb_run(cfg.setup, abi.bb_params(min_pixel_visible=0), frames)
+    assert np.all(r0["frames"]["x"] == 1023)
+    with pytest.raises(O.OracleError):
+        O.bb_run(cfg.setup, abi.bb_params(semantics=abi.LM_BB_FIRSTLAST_INTEGER), frames)

@@ -155,3 +155,31 @@ def test_bb_many_runs_global_fallback(k, conn):
     cfg = SyntheticConfig()
     frames = bb_frames(cfg, 4, seed=17, noise=60)
     check(cfg, abi.bb_params(median_filter_size=k, connectivity=conn, semantics=INTEGER), frames, batch=4)
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_bb_tm_de_bit_exact(flip):
+    """LocoMouse_TM_DE's pass (method 2): imadjust_default + fixed bands per frame."""
+    from tests.test_bbox_oracle import de_config
+    cfg = de_config()
+    cfg.setup.flip = 1 if flip else 0
+    frames = bb_frames(cfg, 24, seed=31, side_h=250, empty_every=7)
+    for w in (5, 1):
+        from oracle import oracle as O
+        params = abi.bb_params(moving_average_window=w)
+        ref = O.bb_run(cfg.setup, params, frames)
+        assert_bb_equal(run_gpu(cfg, params, frames, batch=10), ref)
+
+
+def test_bb_tm_as_executed():
+    from oracle import oracle as O
+    from locomouse_cpp_amd.runtime import BBContext, LMError
+    from tests.test_bbox_oracle import de_config
+    cfg = de_config()
+    cfg.setup.method = 1
+    frames = bb_frames(cfg, 9, seed=5, side_h=250)
+    for mpv in (1, 0):
+        params = abi.bb_params(min_pixel_visible=mpv, bb_width=380, bb_height_side=140)
+        assert_bb_equal(run_gpu(cfg, params, frames, batch=4), O.bb_run(cfg.setup, params, frames))
+    with pytest.raises(LMError):
+        BBContext(cfg.setup, abi.bb_params(semantics=INTEGER))

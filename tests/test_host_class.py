@@ -24,11 +24,11 @@ def test_whole_video_bb_pass_needs_a_rewindable_reader_and_method_0():
     with pytest.raises(H.HostError, match="rewind") as e:
         H.run_video(cfg, cfg.frames(0, 2))  # no bb_params -> no rewind callback
     assert e.value.code == 1
-    cfg = S.SyntheticConfig(method=1)
+    cfg = S.SyntheticConfig(method=2)
     cfg.params.use_provided_bounding_box = 0
-    with pytest.raises(H.HostError, match="computeBoundingBox") as e:
-        H.run_video(cfg, cfg.frames(0, 2))  # LocoMouse_TM's pass is a later row
-    assert e.value.code == 2  # std::runtime_error, caught by main.cpp:98-101
+    with pytest.raises(H.HostError, match="rewind") as e:
+        H.run_video(cfg, cfg.frames(0, 2))
+    assert e.value.code == 1
 
 
 @pytest.mark.gpu
@@ -83,3 +83,27 @@ def test_read_past_end_of_video_raises_runtime_error():
     with pytest.raises(H.HostError, match="Failed to read image") as e:
         H.run_video(cfg, frames, n_frames=5)
     assert e.value.code == 2
+
+
+@pytest.mark.gpu
+def test_tm_de_computed_bounding_box_then_main_loop_matches_oracle():
+    """LocoMouse_TM_DE with use_provided_bounding_box = 0 (method 2 pass)."""
+    import numpy as np
+    from locomouse_cpp_amd import abi
+    from oracle import oracle as O
+    from test_gpu_parity import assert_same
+    from bb_scenes import bb_frames
+    from test_bbox_oracle import de_config
+    cfg = de_config()
+    cfg.params.use_provided_bounding_box = 0
+    frames = bb_frames(cfg, 10, seed=8, side_h=250)
+    bbp = abi.bb_params()
+    got, corners, sizes = H.run_video(cfg, frames, batch=4, bb_params=bbp, with_bb=True)
+    r = O.bb_run(cfg.setup, bbp, frames)
+    ref_corners = np.stack([r["x_pos"], r["y_bottom_pos"], r["y_side_pos"]], 1)
+    assert np.array_equal(corners, ref_corners)
+    assert sizes == (r["bb_side_mouse"], r["bb_bottom_mouse"])
+    cfg2 = de_config()
+    cfg2.params.bounding_box_side = abi.lm_rect(*r["bb_side_mouse"])
+    cfg2.params.bounding_box_bottom = abi.lm_rect(*r["bb_bottom_mouse"])
+    assert_same(got, O.OracleRun(cfg2, frames, bb=ref_corners.astype(np.int32)).result, "host TM_DE bb: ")
