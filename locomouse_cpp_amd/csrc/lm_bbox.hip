@@ -36,6 +36,8 @@ struct LmBBConst {
   int32_t conn, semantics, min_pixel_visible;
   int32_t ring_n;          // ring state bytes: top [p][wp] | bottom [p][wp] | left [n_rows][p] | right [n_rows][p]
   int32_t band_n;          // per-frame band bytes (k_bb_bands), multiple of 16
+  int32_t bits_nw;         // bit-packed ring (p <= 15): words per band row; 0 = byte ring in M
+  int32_t pad2_;
   int64_t m_bytes;         // per-frame I_median indicator image (hp x wp)
   int64_t bin_bytes;       // per-frame thresholded image (n_rows x n_cols)
   int64_t cc_words;        // per-frame run tables for views with many runs (6 words per possible run)
@@ -109,6 +111,11 @@ __global__ __launch_bounds__(256) void k_bb_bands(const LmBBConst K, const uint8
 // ring_f.  Clamping is medianBlur's BORDER_REPLICATE at the edges of
 // I_median.  Counts run as sliding sums along rows / columns (segments per
 // thread), so a frame costs O(band area) LDS byte operations.
+// Workgroup barrier that waits for LDS traffic only: __syncthreads() would also
+// drain the global prefetch of the next frame and the ring publish stores
+// (s_waitcnt vmcnt(0)), exposing their latency at every barrier.
+DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 #define LM_BB_SEG 24   // horizontal segment per thread
 #define LM_BB_VCH 16   // left/right ring rows per thread
 #define LM_BB_BDW 16   // band dwords per thread (band_n <= 64 KiB)
@@ -147,7 +154,7 @@ __global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __
     for (int k = 0; k < LM_BB_BDW; ++k) cur[k] = tid + k * nt < nd ? src[tid + k * nt] : 0u;
   }
   for (int i = tid; i < K.ring_n; i += nt) sm[i] = ring[i];
-  __syncthreads();
+  lds_barrier();
   const int nseg = (wp + LM_BB_SEG - 1) / LM_BB_SEG;
   const int nhT = 2 * p2 * nseg;  // horizontal tasks, top + bottom bands
   const int nch = (nr + LM_BB_VCH - 1) / LM_BB_VCH;
@@ -172,7 +179,7 @@ __global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __
       Mf[(int64_t)(r + p) * wp + j] = sL[i];
       Mf[(int64_t)(r + p) * wp + wp - p + j] = sR[i];
     }
-    __syncthreads();
+    lds_barrier();
     tick(0);
     // ring positions of the bands from the state
     for (int c = tid; c < wp; c += nt) {
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     tick(1);
     // (2) horizontal counts: sliding sums over row segments
     for (int t = tid; t < nhT + 2 * hp; t += nt) {
@@ -241,7 +248,7 @@ __global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     tick(2);
     // (3) vertical counts -> ring_f
     for (int t = tid; t < 2 * wp + 2 * p * nch; t += nt) {
@@ -277,12 +284,268 @@ __global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     tick(3);
 #pragma unroll
     for (int k = 0; k < LM_BB_BDW; ++k) cur[k] = nxt[k];
   }
   for (int i = tid; i < K.ring_n; i += nt) ring[i] = sm[i];
+}
+
+// ------------------------------------------------- bit-packed ring (p <= 7)
+// The same recurrence on bitmaps: the 2p-row top/bottom bands as rows of
+// 32-bit words, the 2p-column left/right bands as one word per I_median row.
+// The ring state lives inside these bitmaps (ring positions), so a frame is:
+// merge the frame's centre bits (prefetched one frame ahead) -> window counts
+// by popcount of funnel-shifted words (top / bottom: one thread per column
+// keeps its 2p counts in registers and forms the vertical counts there) ->
+// new ring rows by wave ballots -> refresh corner duplicates and padding.
+// k_bb_center reads ring_{f-1} from the published band words (rbits).
+//
+// Band word layout (per frame; also the global band / rbits buffers):
+//   T  [2p][NW]  I_median rows 0 .. 2p-1, bit position = column + p; the p
+//                positions on either side replicate columns 0 / wp-1
+//                (BORDER_REPLICATE), so a window is one popcount
+//   Bt [2p][NW]  rows hp-2p .. hp-1, same columns
+//   L  [hp]      bit j = column j (j < 2p)
+//   R  [hp]      bit j = column wp-2p+j
+struct BBBits {
+  int P, NW, hp, wp, nw;  // nw: words per frame
+  DEV int t(int r) const { return r * NW; }
+  DEV int b(int r) const { return (2 * P + r) * NW; }
+  DEV int l(int r) const { return 4 * P * NW + r; }
+  DEV int rr(int r) const { return 4 * P * NW + hp + r; }
+};
+
+DEV BBBits bb_bits(const LmBBConst& K) {
+  BBBits B;
+  B.P = K.p;
+  B.NW = K.bits_nw;
+  B.hp = K.hp;
+  B.wp = K.wp;
+  B.nw = 4 * K.p * K.bits_nw + 2 * K.hp;
+  return B;
+}
+
+DEV bool bb_is_center(int P, int hp, int wp, int r, int c) { return r >= P && r < hp - P && c >= P && c < wp - P; }
+
+// Centre bits of M[f] in the band word layout (ring and padding positions 0).
+__global__ __launch_bounds__(256) void k_bb_bands_bits(const LmBBConst K, const uint8_t* __restrict__ M,
+                                                       uint32_t* __restrict__ bands) {
+  const BBBits B = bb_bits(K);
+  const int f = blockIdx.y, w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= B.nw) return;
+  const int P = B.P, hp = B.hp, wp = B.wp;
+  const uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
+  uint32_t v = 0;
+  if (w < 4 * P * B.NW) {
+    const int band = w / (2 * P * B.NW), q = w - band * 2 * P * B.NW;
+    const int i = q / B.NW, k = q - i * B.NW;
+    const int r = band ? hp - 2 * P + i : i;
+    for (int j = 0; j < 32; ++j) {
+      const int c = 32 * k + j - P;
+      if (c >= 0 && c < wp && bb_is_center(P, hp, wp, r, c) && Mf[(int64_t)r * wp + c]) v |= 1u << j;
+    }
+  } else {
+    const int q = w - 4 * P * B.NW, side = q >= hp, r = side ? q - hp : q;
+    for (int j = 0; j < 2 * P; ++j) {
+      const int c = side ? wp - 2 * P + j : j;
+      if (bb_is_center(P, hp, wp, r, c) && Mf[(int64_t)r * wp + c]) v |= 1u << j;
+    }
+  }
+  bands[(int64_t)f * B.nw + w] = v;
+}
+
+// Ones at positions [lo, lo + n) of a bitmap row (n <= 32).
+DEV int bb_popc_range(const uint32_t* row, int lo, int n) {
+  const int k = lo >> 5, s = lo & 31;
+  const unsigned long long x = (((unsigned long long)row[k + 1] << 32) | row[k]) >> s;
+  return __popcll(x & ((1ull << n) - 1));
+}
+DEV uint32_t bb_get_bits(const uint32_t* row, int lo, int n) {  // n <= 32
+  const int k = lo >> 5, s = lo & 31;
+  const unsigned long long x = (((unsigned long long)row[k + 1] << 32) | row[k]) >> s;
+  return (uint32_t)(x & ((1ull << n) - 1));
+}
+DEV void bb_set_bits(uint32_t* row, int lo, int n, uint32_t v) {  // n <= 32, single writer
+  const int k = lo >> 5, s = lo & 31;
+  const unsigned long long m = ((1ull << n) - 1) << s, x = (unsigned long long)v << s;
+  unsigned long long w = (((unsigned long long)row[k + 1] << 32) | row[k]);
+  w = (w & ~m) | (x & m);
+  row[k] = (uint32_t)w;
+  row[k + 1] = (uint32_t)(w >> 32);
+}
+// Padding positions of a T/Bt row replicate columns 0 and wp-1.
+DEV void bb_pad_row(uint32_t* row, int P, int wp) {
+  bb_set_bits(row, 0, P, ((row[P >> 5] >> (P & 31)) & 1u) ? 0xFFFFFFFFu : 0u);
+  const int q = wp - 1 + P;
+  bb_set_bits(row, wp + P, P, ((row[q >> 5] >> (q & 31)) & 1u) ? 0xFFFFFFFFu : 0u);
+}
+
+template <int P>
+__global__ __launch_bounds__(1024) void k_bb_ring_bits(const LmBBConst K, const uint32_t* __restrict__ bands, int n,
+                                                       uint32_t* __restrict__ state, uint32_t* __restrict__ rbits) {
+  extern __shared__ uint32_t smw[];
+  const BBBits B = bb_bits(K);
+  const int NW = B.NW, hp = B.hp, wp = B.wp, nw = B.nw, thr = K.thr;
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t* W = smw;                                  // [nw] band words
+  uint32_t* HL = smw + nw;                            // [2][hp][HLW] packed byte counts
+  constexpr int HLW = (P + 3) / 4;
+  constexpr uint32_t PM = (1u << P) - 1, P2M = (1u << (2 * P)) - 1;
+  const int npos = wp + P;  // column c sits at position c + P
+  // per-thread word slots and their frame-invariant keep masks (non-centre bits)
+  constexpr int SL = 4;
+  uint32_t keep[SL];
+  for (int k = 0; k < SL; ++k) {
+    const int w = tid + k * nt;
+    uint32_t m = 0xFFFFFFFFu;
+    if (w < 4 * P * NW) {
+      const int band = w / (2 * P * NW), q = w - band * 2 * P * NW;
+      const int i = q / NW, kk = q - i * NW;
+      const int r = band ? hp - 2 * P + i : i;
+      for (int j = 0; j < 32; ++j) {
+        const int c = 32 * kk + j - P;
+        if (c >= 0 && c < wp && bb_is_center(P, hp, wp, r, c)) m &= ~(1u << j);
+      }
+    } else if (w < nw) {
+      const int q = w - 4 * P * NW, side = q >= hp, r = side ? q - hp : q;
+      m = (r < P || r >= hp - P) ? 0xFFFFFFFFu : (side ? ~(PM << P) : ~PM);
+    }
+    keep[k] = m;
+  }
+  for (int w = tid; w < nw; w += nt) W[w] = state[w];
+  uint32_t cur[SL], nxt[SL];
+#pragma unroll
+  for (int k = 0; k < SL; ++k) cur[k] = tid + k * nt < nw ? bands[tid + k * nt] : 0u;
+  lds_barrier();
+  for (int f = 0; f < n; ++f) {
+    if (f + 1 < n) {
+#pragma unroll
+      for (int k = 0; k < SL; ++k) nxt[k] = tid + k * nt < nw ? bands[(int64_t)(f + 1) * nw + tid + k * nt] : 0u;
+    }
+    // (A) merge the centre bits; publish ring_{f-1} + centre for k_bb_center
+#pragma unroll
+    for (int k = 0; k < SL; ++k) {
+      const int w = tid + k * nt;
+      if (w < nw) {
+        const uint32_t v = (W[w] & keep[k]) | cur[k];
+        W[w] = v;
+        rbits[(int64_t)f * nw + w] = v;
+      }
+    }
+    lds_barrier();
+    // (B) top / bottom: thread per position, 2p window counts -> vertical counts in registers
+    uint32_t ntop[2] = {0, 0}, nbot[2] = {0, 0};
+    for (int cb = 0; cb < 2 && cb * nt < npos; ++cb) {
+      const int c = cb * nt + tid - P;
+      if (c >= 0 && c < wp) {
+        int h[2 * P];
+#pragma unroll
+        for (int i = 0; i < 2 * P; ++i) h[i] = bb_popc_range(W + B.t(i), c, 2 * P + 1);
+        int sacc = (P + 1) * h[0];
+#pragma unroll
+        for (int k = 1; k <= P; ++k) sacc += h[k];
+        uint32_t bits = sacc >= thr ? 1u : 0u;
+#pragma unroll
+        for (int r = 1; r < P; ++r) {
+          sacc += h[r + P] - h[r - 1 - P < 0 ? 0 : r - 1 - P];
+          bits |= (sacc >= thr ? 1u : 0u) << r;
+        }
+        ntop[cb] = bits;
+#pragma unroll
+        for (int i = 0; i < 2 * P; ++i) h[i] = bb_popc_range(W + B.b(i), c, 2 * P + 1);
+        sacc = 0;
+#pragma unroll
+        for (int k = 0; k <= 2 * P; ++k) sacc += h[k < 2 * P - 1 ? k : 2 * P - 1];
+        bits = sacc >= thr ? 1u : 0u;
+#pragma unroll
+        for (int i = 1; i < P; ++i) {
+          sacc += h[2 * P - 1] - h[i - 1];
+          bits |= (sacc >= thr ? 1u : 0u) << i;
+        }
+        nbot[cb] = bits;
+      }
+    }
+    // left / right: per row, p window counts (packed bytes) -> HL
+    for (int q = tid; q < 2 * hp; q += nt) {
+      const int side = q >= hp, r = side ? q - hp : q;
+      const uint32_t word = W[side ? B.rr(r) : B.l(r)];
+      uint32_t pk[HLW];
+#pragma unroll
+      for (int k = 0; k < HLW; ++k) pk[k] = 0;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        int cnt;
+        if (!side) {  // columns [j-p, j+p], clamped at 0
+          cnt = __popc(word & ((2u << (j + P)) - 1)) + (P - j) * (int)(word & 1u);
+        } else {      // band columns [j, 2p+j], clamped at 2p-1
+          cnt = __popc(word & P2M & ~((1u << j) - 1)) + (j + 1) * (int)((word >> (2 * P - 1)) & 1u);
+        }
+        pk[j >> 2] |= (uint32_t)cnt << (8 * (j & 3));
+      }
+#pragma unroll
+      for (int k = 0; k < HLW; ++k) HL[(side * hp + r) * HLW + k] = pk[k];
+    }
+    lds_barrier();
+    // (C) new top / bottom ring rows by ballot (padding positions 0 for now);
+    // left / right vertical counts -> new left / right ring bits
+    for (int cb = 0; cb < 2 && cb * nt < npos; ++cb) {
+      const int c = cb * nt + tid - P;
+      const bool valid = c >= 0 && c < wp;
+      const int wbase = (cb * nt + wave * 64) >> 5;
+      const bool wr = lane == 0 && cb * nt + wave * 64 < npos + P;
+#pragma unroll
+      for (int r = 0; r < P; ++r) {
+        const unsigned long long bt = __ballot(valid && ((ntop[cb] >> r) & 1u));
+        const unsigned long long bb = __ballot(valid && ((nbot[cb] >> r) & 1u));
+        if (wr) {
+          W[B.t(r) + wbase] = (uint32_t)bt;
+          W[B.t(r) + wbase + 1] = (uint32_t)(bt >> 32);
+          W[B.b(P + r) + wbase] = (uint32_t)bb;
+          W[B.b(P + r) + wbase + 1] = (uint32_t)(bb >> 32);
+        }
+      }
+    }
+    for (int q = tid; q < 2 * (hp - 2 * P); q += nt) {
+      const int side = q >= hp - 2 * P, R = P + (side ? q - (hp - 2 * P) : q);
+      uint32_t acc[HLW];
+#pragma unroll
+      for (int k = 0; k < HLW; ++k) acc[k] = 0;
+#pragma unroll
+      for (int d = -P; d <= P; ++d)
+#pragma unroll
+        for (int k = 0; k < HLW; ++k) acc[k] += HL[(side * hp + R + d) * HLW + k];  // bytes <= (2p+1)^2 <= 225
+      uint32_t bits = 0;
+#pragma unroll
+      for (int j = 0; j < P; ++j) bits |= (((acc[j >> 2] >> (8 * (j & 3))) & 255u) >= (uint32_t)thr ? 1u : 0u) << j;
+      if (!side) W[B.l(R)] = (W[B.l(R)] & ~PM) | bits;
+      else W[B.rr(R)] = (W[B.rr(R)] & ~(PM << P)) | (bits << P);
+    }
+    lds_barrier();
+    // (D) corner duplicates and padding: L/R rows of the top / bottom rings
+    // from T/Bt; ring columns of T rows p..2p-1 and Bt rows 0..p-1 from L/R
+    for (int q = tid; q < 4 * P; q += nt) {
+      const int grp = q / P, i = q - grp * P;
+      if (grp < 2) {  // top ring row i / bottom ring row hp-p+i (band row p+i)
+        uint32_t* row = W + (grp == 0 ? B.t(i) : B.b(P + i));
+        const int r = grp == 0 ? i : hp - P + i;
+        bb_pad_row(row, P, wp);
+        W[B.l(r)] = bb_get_bits(row, P, 2 * P);              // columns 0 .. 2p-1
+        W[B.rr(r)] = bb_get_bits(row, wp - 2 * P + P, 2 * P);  // columns wp-2p .. wp-1
+      } else {  // grp 2: T row p+i (I_median row p+i); grp 3: Bt row i (row hp-2p+i)
+        const int r = grp == 2 ? P + i : hp - 2 * P + i;
+        uint32_t* row = W + (grp == 2 ? B.t(P + i) : B.b(i));
+        bb_set_bits(row, P, P, W[B.l(r)] & PM);                 // columns 0 .. p-1
+        bb_set_bits(row, wp, P, (W[B.rr(r)] >> P) & PM);        // columns wp-p .. wp-1
+        bb_pad_row(row, P, wp);
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < SL; ++k) cur[k] = nxt[k];
+  }
+  for (int w = tid; w < nw; w += nt) state[w] = W[w];
 }
 
 // ---------------------------------------------------------------- k_bb_center
@@ -292,16 +555,42 @@ __global__ __launch_bounds__(1024) void k_bb_ring(const LmBBConst K, uint8_t* __
 #define LM_BB_TW 64
 #define LM_BB_TH 32
 __global__ __launch_bounds__(256) void k_bb_center(const LmBBConst K, const uint8_t* __restrict__ M,
-                                                   uint8_t* __restrict__ bin) {
+                                                   const uint32_t* __restrict__ rbits, uint8_t* __restrict__ bin) {
   extern __shared__ uint8_t sm[];
   const int p2 = 2 * K.p, IW = LM_BB_TW + p2, IH = LM_BB_TH + p2;
   uint8_t* in = sm;                                           // [IH][IW]
   uint16_t* vs = reinterpret_cast<uint16_t*>(sm + ((IH * IW + 15) & ~15));  // [TH][IW]
   const int c0 = blockIdx.x * LM_BB_TW, r0 = blockIdx.y * LM_BB_TH, f = blockIdx.z;
   const uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
+  const int P = K.p, hp = K.hp, wp = K.wp;
+  const BBBits Bb = bb_bits(K);
+  const uint32_t* __restrict__ Rb = rbits + (int64_t)f * Bb.nw;
   for (int i = threadIdx.x; i < IH * IW; i += blockDim.x) {
     const int rr = r0 + i / IW, cc = c0 + i % IW;
-    in[i] = (rr < K.hp && cc < K.wp) ? Mf[(int64_t)rr * K.wp + cc] : 0;
+    uint8_t v = 0;
+    if (rr < hp && cc < wp) {
+      if (K.bits_nw && (rr < P || rr >= hp - P || cc < P || cc >= wp - P)) {  // ring_{f-1} from the band bits
+        uint32_t w;
+        int bit;
+        if (rr < P) {
+          w = Rb[Bb.t(rr) + ((cc + P) >> 5)];
+          bit = (cc + P) & 31;
+        } else if (rr >= hp - P) {
+          w = Rb[Bb.b(rr - (hp - 2 * P)) + ((cc + P) >> 5)];
+          bit = (cc + P) & 31;
+        } else if (cc < P) {
+          w = Rb[Bb.l(rr)];
+          bit = cc;
+        } else {
+          w = Rb[Bb.rr(rr)];
+          bit = cc - (wp - 2 * P);
+        }
+        v = (uint8_t)((w >> bit) & 1u);
+      } else {
+        v = Mf[(int64_t)rr * wp + cc];
+      }
+    }
+    in[i] = v;
   }
   __syncthreads();
   for (int j = threadIdx.x; j < IW; j += blockDim.x) {
@@ -707,6 +996,8 @@ struct lm_bb_ctx {
   LmBBConst K{};
   size_t ring_lds = 0, center_lds = 0, cc_lds = 0;
   DevBuf<uint8_t> bkg, frames, luts, M, ring, bin, bands;
+  DevBuf<uint32_t> rbits;  // bit-packed ring: per-frame band words (published ring_{f-1})
+  size_t ring_bits_lds = 0;
   DevBuf<unsigned long long> prof;  // LM_BB_PROF=1: k_bb_ring phase clocks
   DevBuf<int32_t> cal;
   DevBuf<unsigned> cc;
@@ -721,7 +1012,7 @@ struct lm_bb_ctx {
     if (prof.p) {
       unsigned long long h[8];
       if (hipMemcpy(h, prof.p, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
-        fprintf(stderr, "k_bb_ring phase clocks: copy+publish %llu  ring-fill %llu  horizontal %llu  vertical %llu\n",
+        fprintf(stderr, "k_bb_ring phase clocks: %llu  %llu  %llu  %llu\n",
                 h[0], h[1], h[2], h[3]);
     }
     if (stream) {
@@ -811,6 +1102,16 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
   K.cc_words = 6 * (int64_t)((NC + 1) / 2) * (vw[0].height + vw[1].height);  // run tables of both views
   const int p = K.p, p2 = 2 * p;
   K.band_n = (2 * p2 * K.wp + 2 * K.hp * p2 + 15) & ~15;
+  // bit-packed ring for p <= 7 (packed byte sums of (2p+1)^2 <= 255 window counts)
+  K.bits_nw = 0;
+  if (p >= 1 && p <= 7 && NR >= 2 * p && NC >= 2 * p && K.wp + 2 * p <= 2048) {
+    const int nw_row = (K.wp + 2 * p + 63) / 64 * 2 + 1;  // ballot words up to the 64-aligned end, +1 for funnels
+    const int nw = 4 * p * nw_row + 2 * K.hp;
+    if (nw <= 4 * 1024) {
+      K.bits_nw = nw_row;
+      c->ring_bits_lds = 4 * ((size_t)nw + 2 * (size_t)K.hp * ((p + 3) / 4));
+    }
+  }
   c->ring_lds = (size_t)((K.ring_n + 15) & ~15) + (size_t)K.band_n + 2 * (size_t)p2 * K.wp + 2 * (size_t)K.hp * p;
   if (K.band_n > 4 * 1024 * LM_BB_BDW)
     throw std::invalid_argument("BB pass: frame size / median_filter_size exceed the ring kernel's band registers.");
@@ -856,7 +1157,16 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
   c->ring.alloc((size_t)std::max(K.ring_n, 1));
   HIPCHK(hipMemset(c->ring.p, 0, c->ring.n));  // I_median = zeros (:588)
   c->bin.alloc((size_t)K.bin_bytes * B);
-  c->bands.alloc((size_t)std::max(K.band_n, 16) * B);
+  if (K.bits_nw) {
+    const size_t nw = 4 * (size_t)K.p * K.bits_nw + 2 * (size_t)K.hp;
+    c->bands.alloc(nw * 4 * B);
+    c->rbits.alloc(nw * B);
+    c->ring.alloc(nw * 4);
+    HIPCHK(hipMemset(c->ring.p, 0, c->ring.n));  // I_median = zeros (:588)
+  } else {
+    c->bands.alloc((size_t)std::max(K.band_n, 16) * B);
+    c->rbits.alloc(1);
+  }
   if (dbg_env("LM_BB_PROF")) {
     c->prof.alloc(8);
     HIPCHK(hipMemset(c->prof.p, 0, 8 * sizeof(unsigned long long)));
@@ -931,13 +1241,25 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
   }
   k_bb_ingest<<<dim3((unsigned)((np + 1023) / 1024), n), 256, 0, s>>>(K, c->fptr.d, c->bkg.p, c->cal.p, c->luts.p,
                                                                        c->M.p);
-  if (K.p > 0) {
+  if (K.bits_nw) {
+    const int nw = 4 * K.p * K.bits_nw + 2 * K.hp;
+    uint32_t* bw = reinterpret_cast<uint32_t*>(c->bands.p);
+    uint32_t* st = reinterpret_cast<uint32_t*>(c->ring.p);
+    k_bb_bands_bits<<<dim3((unsigned)((nw + 255) / 256), n), 256, 0, s>>>(K, c->M.p, bw);
+    switch (K.p) {
+#define LM_BB_RING_CASE(PP) \
+  case PP: k_bb_ring_bits<PP><<<1, 1024, c->ring_bits_lds, s>>>(K, bw, n, st, c->rbits.p); break;
+      LM_BB_RING_CASE(1) LM_BB_RING_CASE(2) LM_BB_RING_CASE(3) LM_BB_RING_CASE(4) LM_BB_RING_CASE(5)
+      LM_BB_RING_CASE(6) LM_BB_RING_CASE(7)
+#undef LM_BB_RING_CASE
+    }
+  } else if (K.p > 0) {
     k_bb_bands<<<dim3((unsigned)((K.band_n / 4 + 255) / 256), n), 256, 0, s>>>(K, c->M.p, c->bands.p);
     k_bb_ring<<<1, 1024, c->ring_lds, s>>>(K, c->M.p, c->bands.p, n, c->ring.p, c->prof.p);
   }
   k_bb_center<<<dim3((unsigned)((K.n_cols + LM_BB_TW - 1) / LM_BB_TW), (unsigned)((K.n_rows + LM_BB_TH - 1) / LM_BB_TH),
                      n),
-                256, c->center_lds, s>>>(K, c->M.p, c->bin.p);
+                256, c->center_lds, s>>>(K, c->M.p, c->rbits.p, c->bin.p);
   k_bb_cc<<<dim3(2, n), 1024, c->cc_lds, s>>>(K, c->bin.p, c->cc.p, c->lims.d);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));

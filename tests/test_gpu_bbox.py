@@ -70,7 +70,7 @@ def test_bb_scene_bit_exact(semantics, conn):
         assert got["frames"]["width"].max() > 100
 
 
-@pytest.mark.parametrize("k", [1, 3, 5, 21])
+@pytest.mark.parametrize("k", [1, 3, 5, 15, 17, 21])
 def test_bb_median_sizes(k):
     cfg = SyntheticConfig()
     frames = bb_frames(cfg, 9, seed=k, border=True, noise=2)
