@@ -549,68 +549,91 @@ __global__ __launch_bounds__(1024) void k_bb_ring_bits(const LmBBConst K, const 
 }
 
 // ---------------------------------------------------------------- k_bb_center
-// Majority filter over the centre: one 64 x 32 output tile per 256 threads;
-// the (32+2p) x (64+2p) input window is staged in LDS, column counts run down
-// the tile, row sums of 2p+1 column counts give the window count.
-#define LM_BB_TW 64
-#define LM_BB_TH 32
+// Majority filter over the centre: one 128 x 64 output tile per 256 threads.
+// The (64+2p) x (128+2p) input window is staged in LDS; column counts run
+// down the tile (thread per column), window counts slide along row segments
+// (thread per 32 outputs), and the 0/1 tile leaves through coalesced dword
+// stores.
+#define LM_BB_TW 128
+#define LM_BB_TH 64
 __global__ __launch_bounds__(256) void k_bb_center(const LmBBConst K, const uint8_t* __restrict__ M,
                                                    const uint32_t* __restrict__ rbits, uint8_t* __restrict__ bin) {
   extern __shared__ uint8_t sm[];
-  const int p2 = 2 * K.p, IW = LM_BB_TW + p2, IH = LM_BB_TH + p2;
-  uint8_t* in = sm;                                           // [IH][IW]
-  uint16_t* vs = reinterpret_cast<uint16_t*>(sm + ((IH * IW + 15) & ~15));  // [TH][IW]
-  const int c0 = blockIdx.x * LM_BB_TW, r0 = blockIdx.y * LM_BB_TH, f = blockIdx.z;
+  const int P = K.p, p2 = 2 * P, hp = K.hp, wp = K.wp;
+  const int IW = LM_BB_TW + p2, IH = LM_BB_TH + p2;
+  uint8_t* in = sm;                                        // [IH][IW], later the output tile [TH][TW]
+  uint8_t* vs = sm + ((IH * IW + 15) & ~15);               // [TH][IW] column counts
+  const int c0 = blockIdx.x * LM_BB_TW, r0 = blockIdx.y * LM_BB_TH, f = blockIdx.z, tid = threadIdx.x;
   const uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
-  const int P = K.p, hp = K.hp, wp = K.wp;
   const BBBits Bb = bb_bits(K);
   const uint32_t* __restrict__ Rb = rbits + (int64_t)f * Bb.nw;
-  for (int i = threadIdx.x; i < IH * IW; i += blockDim.x) {
-    const int rr = r0 + i / IW, cc = c0 + i % IW;
-    uint8_t v = 0;
-    if (rr < hp && cc < wp) {
-      if (K.bits_nw && (rr < P || rr >= hp - P || cc < P || cc >= wp - P)) {  // ring_{f-1} from the band bits
-        uint32_t w;
-        int bit;
-        if (rr < P) {
-          w = Rb[Bb.t(rr) + ((cc + P) >> 5)];
-          bit = (cc + P) & 31;
-        } else if (rr >= hp - P) {
-          w = Rb[Bb.b(rr - (hp - 2 * P)) + ((cc + P) >> 5)];
-          bit = (cc + P) & 31;
-        } else if (cc < P) {
-          w = Rb[Bb.l(rr)];
-          bit = cc;
+  for (int i = 0; i < IH; ++i) {
+    const int rr = r0 + i;
+    for (int j = tid; j < IW; j += blockDim.x) {
+      const int cc = c0 + j;
+      uint8_t v = 0;
+      if (rr < hp && cc < wp) {
+        if (K.bits_nw && (rr < P || rr >= hp - P || cc < P || cc >= wp - P)) {  // ring_{f-1} from the band bits
+          uint32_t w;
+          int bit;
+          if (rr < P) {
+            w = Rb[Bb.t(rr) + ((cc + P) >> 5)];
+            bit = (cc + P) & 31;
+          } else if (rr >= hp - P) {
+            w = Rb[Bb.b(rr - (hp - 2 * P)) + ((cc + P) >> 5)];
+            bit = (cc + P) & 31;
+          } else if (cc < P) {
+            w = Rb[Bb.l(rr)];
+            bit = cc;
+          } else {
+            w = Rb[Bb.rr(rr)];
+            bit = cc - (wp - 2 * P);
+          }
+          v = (uint8_t)((w >> bit) & 1u);
         } else {
-          w = Rb[Bb.rr(rr)];
-          bit = cc - (wp - 2 * P);
+          v = Mf[(int64_t)rr * wp + cc];
         }
-        v = (uint8_t)((w >> bit) & 1u);
-      } else {
-        v = Mf[(int64_t)rr * wp + cc];
       }
+      in[i * IW + j] = v;
     }
-    in[i] = v;
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < IW; j += blockDim.x) {
+  for (int j = tid; j < IW; j += blockDim.x) {
     int s = 0;
     for (int k = 0; k < p2; ++k) s += in[k * IW + j];
     for (int i = 0; i < LM_BB_TH; ++i) {
       s += in[(i + p2) * IW + j];
-      vs[i * IW + j] = (uint16_t)s;
+      vs[i * IW + j] = (uint8_t)s;
       s -= in[i * IW + j];
     }
   }
   __syncthreads();
-  uint8_t* __restrict__ B = bin + (int64_t)f * K.bin_bytes;
-  for (int o = threadIdx.x; o < LM_BB_TH * LM_BB_TW; o += blockDim.x) {
-    const int i = o / LM_BB_TW, c = o % LM_BB_TW;
-    const int r = r0 + i, cc = c0 + c;
-    if (r >= K.n_rows || cc >= K.n_cols) continue;
+  {
+    constexpr int SEG = LM_BB_TW * LM_BB_TH / 256;  // 32 outputs per thread
+    const int i = tid / (LM_BB_TW / SEG), cs = (tid % (LM_BB_TW / SEG)) * SEG;
+    const uint8_t* v = vs + i * IW + cs;
     int s = 0;
-    for (int k = 0; k <= p2; ++k) s += vs[i * IW + c + k];
-    B[(int64_t)r * K.n_cols + cc] = s >= K.thr ? 1 : 0;
+    for (int k = 0; k <= p2; ++k) s += v[k];
+    uint8_t* o = in + i * LM_BB_TW + cs;
+    o[0] = s >= K.thr ? 1 : 0;
+    for (int c = 1; c < SEG; ++c) {
+      s += v[c + p2] - v[c - 1];
+      o[c] = s >= K.thr ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  uint8_t* __restrict__ B = bin + (int64_t)f * K.bin_bytes;
+  const bool full = c0 + LM_BB_TW <= K.n_cols && (K.n_cols & 3) == 0;
+  for (int q = tid; q < LM_BB_TH * (LM_BB_TW / 4); q += blockDim.x) {
+    const int i = q / (LM_BB_TW / 4), c4 = (q % (LM_BB_TW / 4)) * 4, r = r0 + i;
+    if (r >= K.n_rows) continue;
+    if (full) {
+      *reinterpret_cast<uint32_t*>(B + (int64_t)r * K.n_cols + c0 + c4) =
+          *reinterpret_cast<const uint32_t*>(in + i * LM_BB_TW + c4);
+    } else {
+      for (int k = 0; k < 4; ++k)
+        if (c0 + c4 + k < K.n_cols) B[(int64_t)r * K.n_cols + c0 + c4 + k] = in[i * LM_BB_TW + c4 + k];
+    }
   }
 }
 
@@ -1116,7 +1139,7 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
   if (K.band_n > 4 * 1024 * LM_BB_BDW)
     throw std::invalid_argument("BB pass: frame size / median_filter_size exceed the ring kernel's band registers.");
   const int IW = LM_BB_TW + p2, IH = LM_BB_TH + p2;
-  c->center_lds = (size_t)((IH * IW + 15) & ~15) + 2 * (size_t)LM_BB_TH * IW;
+  c->center_lds = (size_t)((IH * IW + 15) & ~15) + (size_t)LM_BB_TH * IW;
   const int hmax = std::max(vw[0].height, vw[1].height);
   c->cc_lds = 4 * (size_t)(NC + 1 + 2 * hmax + 1) + (size_t)LM_BB_RUN_CAP * 6 * 4;
   const size_t lds_max = 160 * 1024;
