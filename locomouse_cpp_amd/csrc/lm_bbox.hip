@@ -36,8 +36,8 @@ struct LmBBConst {
   int32_t conn, semantics, min_pixel_visible;
   int32_t ring_n;          // ring state bytes: top [p][wp] | bottom [p][wp] | left [n_rows][p] | right [n_rows][p]
   int32_t band_n;          // per-frame band bytes (k_bb_bands), multiple of 16
-  int32_t bits_nw;         // bit-packed ring (p <= 15): words per band row; 0 = byte ring in M
-  int32_t pad2_;
+  int32_t bits_nw;         // bit-packed ring (p <= 7): words per band row; 0 = byte ring in M
+  int32_t run_cap;         // k_bb_cc: runs per view held in LDS
   int64_t m_bytes;         // per-frame I_median indicator image (hp x wp)
   int64_t bin_bytes;       // per-frame thresholded image (n_rows x n_cols)
   int64_t cc_words;        // per-frame run tables for views with many runs (6 words per possible run)
@@ -653,28 +653,32 @@ DEV bool bb_pass(const LmBBConst& K, int count) {
   return __int_as_float(v) >= (float)K.min_pixel_visible;  // CV_32S read through ptr<float>
 }
 
-// Row-run labelling.  Runs are found with wave ballots, linked to the
+// Row-run labelling.  The view is staged as a bitmap in LDS (16 pixels per
+// lane from 16-byte loads); runs are read off 64-column words, linked to the
 // overlapping runs of the row above (8-connectivity: columns within +-1), and
 // a union-find forest over runs (atomicMin hooking of the larger root under
 // the smaller, so a component's root is its first run in raster order) gives
 // areas and first-label keys.  The run table lives in LDS when a view has at
-// most LM_BB_RUN_CAP runs (clean masks: a few per row), else in the global
+// most K.run_cap runs (clean masks: a few per row), else in the global
 // scratch with L1-bypassing loads (noisy masks: thousands per view).
-#define LM_BB_RUN_CAP 2048
-
+// Run table: start / end column (u16 in LDS, u32 in global memory),
+// union-find parent, area and first-label key per run; a run's row is found
+// by binary search in the per-row run offsets.
+template <class IX>
 struct BBRuns {
-  unsigned *rs, *re, *ry, *par, *area, *key;
+  IX *rs, *re;
+  unsigned *par, *area, *key;
 };
 
-template <bool G>
-DEV unsigned rld(const unsigned* a) {
-  if constexpr (G) return bb_ld(a);
-  else return *a;
+template <bool G, class T>
+DEV unsigned rld(const T* a) {
+  if constexpr (G) return bb_ld(reinterpret_cast<const unsigned*>(a));
+  else return (unsigned)*a;
 }
-template <bool G>
-DEV void rst(unsigned* a, unsigned v) {
-  if constexpr (G) bb_st(a, v);
-  else *a = v;
+template <bool G, class T>
+DEV void rst(T* a, unsigned v) {
+  if constexpr (G) bb_st(reinterpret_cast<unsigned*>(a), v);
+  else *a = (T)v;
 }
 template <bool G>
 DEV unsigned rfind(const unsigned* par, unsigned a) {
@@ -724,36 +728,43 @@ DEV void bb_wave0_scan(int* v, int n, int* total) {
   __syncthreads();
 }
 
-// Labels the runs of one view, picks the largest component (ties: first
-// OpenCV label) and accumulates its per-column (difference array) and per-row
-// pixel counts.  Returns the chosen root or 0xFFFFFFFF.  Block-wide call.
-template <bool G>
-DEV unsigned bb_cc_runs(const BBRuns S, const uint8_t* __restrict__ Bv, int W, int H, int R, const int* rowoff,
-                        bool c8, int* colc, int* rowc, unsigned long long* s_red, unsigned* s_best) {
+// Row of run i: the last y with rowoff[y] <= i (rowoff exclusive offsets).
+DEV int bb_row_of(const int* rowoff, int H, int i) {
+  int lo = 0, hi = H;  // first y with rowoff[y] > i, minus one
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (rowoff[mid] <= i) lo = mid + 1; else hi = mid;
+  }
+  return lo - 1;
+}
+
+// Labels the runs of one view (bitmap rows bm[y][0..nb64], 64 columns per
+// word), picks the largest component (ties: first OpenCV label) and
+// accumulates its per-column (difference array) and per-row pixel counts.
+// Block-wide call.
+template <bool G, class IX>
+DEV void bb_cc_runs(const BBRuns<IX> S, const unsigned long long* bm, int nb64, int W, int H, int R,
+                    const int* rowoff, bool c8, int* colc, int* rowc, unsigned long long* s_red, unsigned* s_best) {
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
   const unsigned long long lt = (1ull << lane) - 1;
   const unsigned nbx = (unsigned)(W + 1) / 2;
   for (int y = wave; y < H; y += nw) {
-    const uint8_t* row = Bv + (int64_t)y * W;
+    const unsigned long long* row = bm + (int64_t)y * (nb64 + 1);
     int ns = rowoff[y], ne = rowoff[y];
     unsigned long long carry = 0;
-    for (int x0 = 0; x0 < W; x0 += 64) {
-      const int x = x0 + lane;
-      const unsigned long long bits = __ballot(x < W && row[x] != 0);
-      const bool nxt = x0 + 64 < W && row[x0 + 64] != 0;  // wave-uniform
+    for (int k = 0; k < nb64; ++k) {
+      const unsigned long long bits = row[k], nxt = row[k + 1] & 1ull;  // wave-uniform
       const unsigned long long st = bits & ~((bits << 1) | carry);
-      const unsigned long long en = bits & ~((bits >> 1) | (nxt ? 1ull << 63 : 0ull));
-      if ((st >> lane) & 1) {
-        const int k = ns + __popcll(st & lt);
-        rst<G>(&S.rs[k], (unsigned)x);
-        rst<G>(&S.ry[k], (unsigned)y);
-      }
+      const unsigned long long en = bits & ~((bits >> 1) | (nxt << 63));
+      const int x = 64 * k + lane;
+      if ((st >> lane) & 1) rst<G>(&S.rs[ns + __popcll(st & lt)], (unsigned)x);
       if ((en >> lane) & 1) rst<G>(&S.re[ne + __popcll(en & lt)], (unsigned)x);
       ns += __popcll(st);
       ne += __popcll(en);
       carry = bits >> 63;
     }
   }
+  __syncthreads();  // the LDS union-find arrays overlay the bitmap
   for (int i = tid; i < R; i += nt) {
     rst<G>(&S.par[i], (unsigned)i);
     rst<G>(&S.area[i], 0u);
@@ -762,7 +773,7 @@ DEV unsigned bb_cc_runs(const BBRuns S, const uint8_t* __restrict__ Bv, int W, i
   __syncthreads();
   const int d = c8 ? 1 : 0;
   for (int i = tid; i < R; i += nt) {
-    const int y = (int)rld<G>(&S.ry[i]);
+    const int y = bb_row_of(rowoff, H, i);
     if (y == 0) continue;
     const int a0 = (int)rld<G>(&S.rs[i]) - d, a1 = (int)rld<G>(&S.re[i]) + d;
     int lo = rowoff[y - 1], hi = rowoff[y];
@@ -775,7 +786,7 @@ DEV unsigned bb_cc_runs(const BBRuns S, const uint8_t* __restrict__ Bv, int W, i
   __syncthreads();
   for (int i = tid; i < R; i += nt) {
     const unsigned root = rfind<G>(S.par, i);
-    const unsigned y = rld<G>(&S.ry[i]), x = rld<G>(&S.rs[i]);
+    const unsigned y = (unsigned)bb_row_of(rowoff, H, i), x = rld<G>(&S.rs[i]);
     atomicAdd(&S.area[root], rld<G>(&S.re[i]) - x + 1);
     atomicMin(&S.key[root], c8 ? (y >> 1) * nbx + (x >> 1) : y * (unsigned)W + x);
     rst<G>(&S.par[i], root);
@@ -806,7 +817,7 @@ DEV unsigned bb_cc_runs(const BBRuns S, const uint8_t* __restrict__ Bv, int W, i
     for (int i = tid; i < R; i += nt) {
       if (rld<G>(&S.par[i]) != broot) continue;
       const int x0 = (int)rld<G>(&S.rs[i]), x1 = (int)rld<G>(&S.re[i]);
-      atomicAdd(&rowc[rld<G>(&S.ry[i])], x1 - x0 + 1);
+      atomicAdd(&rowc[bb_row_of(rowoff, H, i)], x1 - x0 + 1);
       atomicAdd(&colc[x0], 1);
       atomicSub(&colc[x1 + 1], 1);
     }
@@ -826,63 +837,109 @@ DEV unsigned bb_cc_runs(const BBRuns S, const uint8_t* __restrict__ Bv, int W, i
     }
   }
   __syncthreads();
-  return broot;
+}
+
+// LDS of k_bb_cc: counts, run offsets, the view bitmap (dead once the runs
+// are extracted, so the union-find arrays reuse it), run columns.
+struct BBCCLayout {
+  int colc, rowc, rowoff, bm, par, area, key, rs, re, bytes;  // byte offsets
+};
+__host__ __device__ inline BBCCLayout bb_cc_layout(int W, int Hmax, int cap) {
+  BBCCLayout L;
+  int o = 0;
+  L.colc = o;
+  o += 4 * (W + 1);
+  L.rowc = o;
+  o += 4 * Hmax;
+  L.rowoff = o;
+  o += 4 * (Hmax + 1);
+  o = (o + 7) & ~7;
+  L.bm = o;
+  L.par = o;
+  L.area = o + 4 * cap;
+  L.key = o + 8 * cap;
+  const int bmb = 8 * Hmax * ((W + 63) / 64 + 1), ufb = 12 * cap;
+  o += bmb > ufb ? bmb : ufb;
+  L.rs = o;
+  o += 2 * cap;
+  L.re = o;
+  o += 2 * cap;
+  L.bytes = o;
+  return L;
 }
 
 // largestBWAreaObject + reduce + firstLastOverT for one (view, frame).
 __global__ __launch_bounds__(1024) void k_bb_cc(const LmBBConst K, const uint8_t* __restrict__ bin,
                                                 unsigned* __restrict__ scratch, int32_t* __restrict__ lims) {
-  extern __shared__ int cnt[];
+  extern __shared__ __attribute__((aligned(16))) uint8_t smc[];
   const int v = blockIdx.x, f = blockIdx.y;
-  const int W = K.n_cols, H = K.view_h[v];
+  const int W = K.n_cols, H = K.view_h[v], nb64 = (W + 63) / 64;
+  const BBCCLayout L = bb_cc_layout(W, max(K.view_h[0], K.view_h[1]), K.run_cap);
   const uint8_t* __restrict__ Bv = bin + (int64_t)f * K.bin_bytes + (int64_t)K.view_y[v] * W;
-  int* colc = cnt;            // [W + 1]  Row_* (reduce over rows), via a difference array
-  int* rowc = cnt + W + 1;    // [H]      Col_*
-  int* rowoff = rowc + H;     // [H + 1]  run offsets per row
-  unsigned* lds_runs = reinterpret_cast<unsigned*>(rowoff + H + 1);  // 6 x [LM_BB_RUN_CAP]
+  int* colc = reinterpret_cast<int*>(smc + L.colc);      // [W + 1]  Row_* (reduce over rows), difference array
+  int* rowc = reinterpret_cast<int*>(smc + L.rowc);      // [H]      Col_*
+  int* rowoff = reinterpret_cast<int*>(smc + L.rowoff);  // [H + 1]  run offsets per row
+  unsigned long long* bm = reinterpret_cast<unsigned long long*>(smc + L.bm);  // [H][nb64 + 1]
   __shared__ unsigned long long s_red[16];
   __shared__ unsigned s_best;
   __shared__ int s_total;
   __shared__ int s_lim[2][3];  // (first, last, count) for Row, Col
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
 
-  for (int i = tid; i < W + 2 * H + 2; i += nt) cnt[i] = 0;
+  for (int i = tid; i < W + 1 + H + H + 1; i += nt) {
+    if (i < W + 1) colc[i] = 0;
+    else if (i < W + 1 + H) rowc[i - W - 1] = 0;
+  }
   if (tid < 2) {
     s_lim[tid][0] = 0x7FFFFFFF;
     s_lim[tid][1] = -1;
     s_lim[tid][2] = 0;
   }
   if (tid == 0) s_best = 0xFFFFFFFFu;
-  __syncthreads();
-  // runs per row: a run starts at a foreground pixel whose left neighbour is background
+  // view bitmap (16 pixels per lane, wide loads) and run starts per row
+  const bool vec = (W & 15) == 0;
   for (int y = wave; y < H; y += nw) {
     const uint8_t* row = Bv + (int64_t)y * W;
+    uint16_t* brow = reinterpret_cast<uint16_t*>(bm + (int64_t)y * (nb64 + 1));
     int n = 0;
-    unsigned long long carry = 0;
-    for (int x0 = 0; x0 < W; x0 += 64) {
-      const int x = x0 + lane;
-      const unsigned long long bits = __ballot(x < W && row[x] != 0);
-      n += __popcll(bits & ~((bits << 1) | carry));
-      carry = bits >> 63;
+    unsigned carry = 0;
+    for (int x0 = 0; x0 < 64 * (nb64 + 1); x0 += 1024) {
+      const int x = x0 + 16 * lane;
+      unsigned m = 0;
+      if (x < W) {
+        if (vec) {
+          const uint4 q = *reinterpret_cast<const uint4*>(row + x);
+          const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int k = 0; k < 16; ++k) m |= (((w4[k >> 2] >> (8 * (k & 3))) & 255u) ? 1u : 0u) << k;
+        } else {
+          for (int k = 0; k < 16 && x + k < W; ++k) m |= (row[x + k] ? 1u : 0u) << k;
+        }
+      }
+      if (x < 64 * (nb64 + 1)) brow[x >> 4] = (uint16_t)m;
+      const unsigned prev = (unsigned)__shfl_up((int)(m >> 15), 1);
+      const unsigned cin = lane ? prev : carry;
+      n += __popc(m & ~((m << 1) | cin) & 0xFFFFu);
+      carry = (unsigned)__shfl((int)(m >> 15), 63);
     }
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
     if (lane == 0) rowoff[y] = n;
   }
   __syncthreads();
   bb_wave0_scan(rowoff, H, &s_total);
   const int R = s_total;
   const bool c8 = K.conn == 8;
-  if (R <= LM_BB_RUN_CAP) {
-    unsigned* b = lds_runs;
-    const BBRuns S{b, b + LM_BB_RUN_CAP, b + 2 * LM_BB_RUN_CAP, b + 3 * LM_BB_RUN_CAP, b + 4 * LM_BB_RUN_CAP,
-                   b + 5 * LM_BB_RUN_CAP};
-    bb_cc_runs<false>(S, Bv, W, H, R, rowoff, c8, colc, rowc, s_red, &s_best);
+  if (R <= K.run_cap && W <= 65536) {
+    const BBRuns<uint16_t> S{reinterpret_cast<uint16_t*>(smc + L.rs), reinterpret_cast<uint16_t*>(smc + L.re),
+                             reinterpret_cast<unsigned*>(smc + L.par), reinterpret_cast<unsigned*>(smc + L.area),
+                             reinterpret_cast<unsigned*>(smc + L.key)};
+    bb_cc_runs<false>(S, bm, nb64, W, H, R, rowoff, c8, colc, rowc, s_red, &s_best);
   } else {
     const int64_t cap = (int64_t)H * ((W + 1) / 2);  // at most ceil(W/2) runs per row
-    unsigned* b = scratch + (int64_t)f * K.cc_words + (v ? 6 * (int64_t)K.view_h[0] * ((W + 1) / 2) : 0);
-    const BBRuns S{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap, b + 5 * cap};
-    bb_cc_runs<true>(S, Bv, W, H, R, rowoff, c8, colc, rowc, s_red, &s_best);
+    unsigned* b = scratch + (int64_t)f * K.cc_words + (v ? 5 * (int64_t)K.view_h[0] * ((W + 1) / 2) : 0);
+    const BBRuns<unsigned> S{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap};
+    bb_cc_runs<true>(S, bm, nb64, W, H, R, rowoff, c8, colc, rowc, s_red, &s_best);
   }
-  (void)lane;
   for (int i = tid; i < W + H; i += nt) {
     const int dd = i < W ? 0 : 1, idx = i < W ? i : i - W;
     if (bb_pass(K, i < W ? colc[i] : rowc[idx])) {
@@ -1012,6 +1069,8 @@ __global__ __launch_bounds__(1024) void k_bb_de(const LmBBConst K, const uint8_t
 struct lm_bb_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t s2 = nullptr;  // majority filter + components, overlapping the ring on `stream`
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   int max_batch = 0;
   int64_t npix = 0, frame_stride = 0;
   int view_y[2] = {0, 0};
@@ -1041,6 +1100,10 @@ struct lm_bb_ctx {
     if (stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
+      if (s2) (void)hipStreamSynchronize(s2);
+      for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+      if (s2) (void)hipStreamDestroy(s2);
       (void)hipStreamDestroy(stream);
     }
   }
@@ -1122,7 +1185,7 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
   K.ring_n = 2 * K.p * K.wp + 2 * NR * K.p;
   K.m_bytes = ((int64_t)K.hp * K.wp + 255) / 256 * 256;
   K.bin_bytes = ((int64_t)NR * NC + 255) / 256 * 256;
-  K.cc_words = 6 * (int64_t)((NC + 1) / 2) * (vw[0].height + vw[1].height);  // run tables of both views
+  K.cc_words = 5 * (int64_t)((NC + 1) / 2) * (vw[0].height + vw[1].height);  // run tables of both views
   const int p = K.p, p2 = 2 * p;
   K.band_n = (2 * p2 * K.wp + 2 * K.hp * p2 + 15) & ~15;
   // bit-packed ring for p <= 7 (packed byte sums of (2p+1)^2 <= 255 window counts)
@@ -1141,7 +1204,12 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
   const int IW = LM_BB_TW + p2, IH = LM_BB_TH + p2;
   c->center_lds = (size_t)((IH * IW + 15) & ~15) + (size_t)LM_BB_TH * IW;
   const int hmax = std::max(vw[0].height, vw[1].height);
-  c->cc_lds = 4 * (size_t)(NC + 1 + 2 * hmax + 1) + (size_t)LM_BB_RUN_CAP * 6 * 4;
+  {
+    int cap = 16384;
+    while (cap > 64 && bb_cc_layout(NC, hmax, cap).bytes > 160 * 1024) cap -= 64;
+    K.run_cap = cap;
+    c->cc_lds = (size_t)bb_cc_layout(NC, hmax, K.run_cap).bytes;
+  }
   const size_t lds_max = 160 * 1024;
   if (c->ring_lds > lds_max || c->center_lds > lds_max || c->cc_lds > lds_max)
     throw std::invalid_argument("BB pass: frame size / median_filter_size exceed the 160 KiB LDS of one workgroup.");
@@ -1264,27 +1332,51 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
   }
   k_bb_ingest<<<dim3((unsigned)((np + 1023) / 1024), n), 256, 0, s>>>(K, c->fptr.d, c->bkg.p, c->cal.p, c->luts.p,
                                                                        c->M.p);
+  // The ring recurrence (one workgroup) runs chunk by chunk on stream s; the
+  // majority filter and components of chunk i follow on stream s2 as soon as
+  // its ring is done, overlapping the ring of chunk i+1.
+  static const int chunks = [] {
+    const char* e = getenv("LM_BB_CHUNKS");
+    return e ? std::max(1, std::min(4, atoi(e))) : 4;
+  }();
+  const int nch = K.p > 0 && n >= 16 ? chunks : 1;
+  const int csz = (n + nch - 1) / nch;
+  const dim3 cgrid((unsigned)((K.n_cols + LM_BB_TW - 1) / LM_BB_TW), (unsigned)((K.n_rows + LM_BB_TH - 1) / LM_BB_TH));
+  const int nw = K.bits_nw ? 4 * K.p * K.bits_nw + 2 * K.hp : 0;
+  uint32_t* bw = reinterpret_cast<uint32_t*>(c->bands.p);
+  uint32_t* st = reinterpret_cast<uint32_t*>(c->ring.p);
   if (K.bits_nw) {
-    const int nw = 4 * K.p * K.bits_nw + 2 * K.hp;
-    uint32_t* bw = reinterpret_cast<uint32_t*>(c->bands.p);
-    uint32_t* st = reinterpret_cast<uint32_t*>(c->ring.p);
     k_bb_bands_bits<<<dim3((unsigned)((nw + 255) / 256), n), 256, 0, s>>>(K, c->M.p, bw);
-    switch (K.p) {
-#define LM_BB_RING_CASE(PP) \
-  case PP: k_bb_ring_bits<PP><<<1, 1024, c->ring_bits_lds, s>>>(K, bw, n, st, c->rbits.p); break;
-      LM_BB_RING_CASE(1) LM_BB_RING_CASE(2) LM_BB_RING_CASE(3) LM_BB_RING_CASE(4) LM_BB_RING_CASE(5)
-      LM_BB_RING_CASE(6) LM_BB_RING_CASE(7)
-#undef LM_BB_RING_CASE
-    }
   } else if (K.p > 0) {
     k_bb_bands<<<dim3((unsigned)((K.band_n / 4 + 255) / 256), n), 256, 0, s>>>(K, c->M.p, c->bands.p);
-    k_bb_ring<<<1, 1024, c->ring_lds, s>>>(K, c->M.p, c->bands.p, n, c->ring.p, c->prof.p);
   }
-  k_bb_center<<<dim3((unsigned)((K.n_cols + LM_BB_TW - 1) / LM_BB_TW), (unsigned)((K.n_rows + LM_BB_TH - 1) / LM_BB_TH),
-                     n),
-                256, c->center_lds, s>>>(K, c->M.p, c->rbits.p, c->bin.p);
-  k_bb_cc<<<dim3(2, n), 1024, c->cc_lds, s>>>(K, c->bin.p, c->cc.p, c->lims.d);
+  for (int ch = 0; ch < nch; ++ch) {
+    const int f0 = ch * csz, m = std::min(csz, n - f0);
+    if (m <= 0) break;
+    if (K.bits_nw) {
+      const uint32_t* bwc = bw + (int64_t)f0 * nw;
+      uint32_t* rbc = c->rbits.p + (int64_t)f0 * nw;
+      switch (K.p) {
+#define LM_BB_RING_CASE(PP) \
+  case PP: k_bb_ring_bits<PP><<<1, 1024, c->ring_bits_lds, s>>>(K, bwc, m, st, rbc); break;
+        LM_BB_RING_CASE(1) LM_BB_RING_CASE(2) LM_BB_RING_CASE(3) LM_BB_RING_CASE(4) LM_BB_RING_CASE(5)
+        LM_BB_RING_CASE(6) LM_BB_RING_CASE(7)
+#undef LM_BB_RING_CASE
+      }
+    } else if (K.p > 0) {
+      k_bb_ring<<<1, 1024, c->ring_lds, s>>>(K, c->M.p + (int64_t)f0 * K.m_bytes, c->bands.p + (int64_t)f0 * K.band_n, m,
+                                             c->ring.p, c->prof.p);
+    }
+    HIPCHK(hipEventRecord(c->ev[ch], s));
+    HIPCHK(hipStreamWaitEvent(c->s2, c->ev[ch], 0));
+    k_bb_center<<<dim3(cgrid.x, cgrid.y, m), 256, c->center_lds, c->s2>>>(
+        K, c->M.p + (int64_t)f0 * K.m_bytes, K.bits_nw ? c->rbits.p + (int64_t)f0 * nw : c->rbits.p,
+        c->bin.p + (int64_t)f0 * K.bin_bytes);
+    k_bb_cc<<<dim3(2, m), 1024, c->cc_lds, c->s2>>>(K, c->bin.p + (int64_t)f0 * K.bin_bytes,
+                                                   c->cc.p + (int64_t)f0 * K.cc_words, c->lims.d + 8 * f0);
+  }
   HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->s2));
   HIPCHK(hipStreamSynchronize(s));
   c->last_n = n;
   for (int i = 0; i < n; ++i) {
@@ -1410,6 +1502,8 @@ LM_API lm_status lm_bb_create(int32_t device, const lm_setup* setup, const lm_bb
     c->device = device;
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->max_batch = max_batch;
     bb_validate_and_build(c, setup, params);
   });

@@ -148,13 +148,16 @@ def test_bb_argument_errors():
     ctx.close()
 
 
-@pytest.mark.parametrize("k,conn", [(1, 8), (3, 4)])
-def test_bb_many_runs_global_fallback(k, conn):
-    """Noisy masks with more row runs per view than the LDS run table holds
-    (LM_BB_RUN_CAP) keep their run tables in global memory."""
+@pytest.mark.parametrize("k,conn,density", [(1, 8, 0.5), (1, 4, 0.3), (3, 4, 0.5)])
+def test_bb_many_runs_global_fallback(k, conn, density):
+    """Salt-and-pepper masks: with k = 1 a view holds tens of thousands of
+    row runs, more than the LDS run table (LM_BB_RUN_CAP), so its run table
+    lives in global memory; k = 3 smooths them back under the cap."""
     cfg = SyntheticConfig()
-    frames = bb_frames(cfg, 4, seed=17, noise=60)
-    check(cfg, abi.bb_params(median_filter_size=k, connectivity=conn, semantics=INTEGER), frames, batch=4)
+    rng = np.random.default_rng(int(density * 100) + k)
+    frames = np.clip(cfg.background.astype(np.int32)[None] +
+                     (rng.random((3, cfg.rows, cfg.cols)) < density) * 100, 0, 255).astype(np.uint8)
+    check(cfg, abi.bb_params(median_filter_size=k, connectivity=conn, semantics=INTEGER), frames, batch=3)
 
 
 @pytest.mark.parametrize("flip", [False, True])
