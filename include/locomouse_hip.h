@@ -78,8 +78,8 @@ typedef struct {
   int32_t occlusion_grid_spacing_pixels_bottom;
   int32_t use_provided_bounding_box;            /* must be 1: a computed box (lm_bb_*) is passed as
                                                    its sizes here + per-frame corners (bb) */
-  int32_t transform_gray_values;                /* LUT on the bottom crop mask, :1445-1454 */
-  int32_t reserved0;
+  int32_t transform_gray_values;                /* LUT on the bottom crop, :1445-1454 (see below) */
+  int32_t use_reference_image_brightness;       /* histogram matching, :1437-1443 (see below) */
   double side_bottom_min_overlap;
   double occlusion_grid_max_width;
   double tail_sub_bounding_box;
@@ -91,6 +91,15 @@ typedef struct {
   lm_rect bounding_box_bottom;                  /* bounding_box_bottom (x y w h) */
   float gray_value_transformation[256];         /* used iff transform_gray_values */
 } lm_params;
+/* Grey-level options, as the reference executes them:
+ *  - use_reference_image_brightness: LocoMouse_Parameters computes the
+ *    reference CDF with computeNormalizedCDF into an unallocated cv::Mat
+ *    (:189, :3392-3405: ptr<float>(0) of an empty Mat), so the reference
+ *    cannot start with it set; lm_ctx_create fails with LM_ERR_RUNTIME.
+ *  - transform_gray_values: LUT(I_BOTTOM_MOUSE, table, I_BOTTOM_MOUSE) with a
+ *    floating-point table re-creates the crop as CV_32F and the later
+ *    Mat::setTo(0, mask) asserts (:1448, :849); lm_ctx_create fails with
+ *    LM_ERR_RUNTIME. */
 
 /* One linear detector (model.yml modelX_view / biasX_view, :3106-3148).
  * Weights are row-major doubles as read from the model file; they are rounded

@@ -32,7 +32,7 @@ class lm_params(C.Structure):
         ("occlusion_grid_spacing_pixels_bottom", C.c_int32),
         ("use_provided_bounding_box", C.c_int32),
         ("transform_gray_values", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("use_reference_image_brightness", C.c_int32),
         ("side_bottom_min_overlap", C.c_double),
         ("occlusion_grid_max_width", C.c_double),
         ("tail_sub_bounding_box", C.c_double),

@@ -270,6 +270,10 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   }
   if (!P->use_provided_bounding_box)
     throw std::invalid_argument("use_provided_bounding_box = 0: run the whole-video BB pass (lm_bb_*) first and pass its boxes and corners.");
+  if (P->use_reference_image_brightness)
+    throw std::runtime_error(
+        "use_reference_image_brightness: computeNormalizedCDF writes the reference CDF through an unallocated cv::Mat "
+        "(LocoMouse_class.cpp:189, :3392-3405); the reference cannot start with this option.");
   if (P->transform_gray_values)
     throw std::runtime_error(
         "transform_gray_values: LUT re-types the bottom mask to CV_32F and Mat::setTo asserts (LocoMouse_class.cpp:1448, :849).");

@@ -474,6 +474,8 @@ class LocoMouseOracle {
       throw std::invalid_argument("Invalid configuration parameter: must belong to [0,1].");
     if (!P.use_provided_bounding_box)
       throw std::invalid_argument("use_provided_bounding_box = 0 needs the whole-video BB pass (not on this path).");
+    if (P.use_reference_image_brightness)
+      throw std::runtime_error("use_reference_image_brightness: computeNormalizedCDF into an unallocated cv::Mat (LocoMouse_class.cpp:189, :3392-3405).");
     if (P.transform_gray_values)
       throw std::runtime_error("transform_gray_values: LUT re-types the bottom mask to CV_32F and Mat::setTo asserts (LocoMouse_class.cpp:1448, :849).");
     for (int k = 0; k < 4; ++k) prior_paw.emplace_back(P.location_prior[k]);

@@ -131,6 +131,12 @@ def test_error_mapping(cfg):
     with pytest.raises(LMError) as e:
         ctx.detect(cfg.frames(3, 2), 3)  # frame 2 never seen and no halo
     assert e.value.code == 1
+    for option in ("use_reference_image_brightness", "transform_gray_values"):  # §8(f) row 4, as executed
+        bad = S.SyntheticConfig()
+        setattr(bad.params, option, 1)
+        with pytest.raises(LMError) as e:
+            _ctx(bad)
+        assert e.value.code == 2
 
 
 def _quantized_config(rank):
