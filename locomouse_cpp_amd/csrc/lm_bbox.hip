@@ -1304,9 +1304,16 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
     }
     return;
   }
+  // device frames are read in place when 16-byte aligned (k_minmax_lut loads 16 B per lane)
+  const bool direct = device_frames && ((((uintptr_t)frames | (uintptr_t)pitch) & 15) == 0);
+  if (device_frames && !direct)
+    HIPCHK(hipMemcpy2DAsync(c->frames.p, (size_t)c->frame_stride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
+                            hipMemcpyDeviceToDevice, s));
   for (int i = 0; i < n; ++i) {
-    if (device_frames) {
+    if (direct) {
       c->fptr.p[i] = frames + (int64_t)i * pitch;
+    } else if (device_frames) {
+      c->fptr.p[i] = c->frames.p + (int64_t)i * c->frame_stride;
     } else {
       uint8_t* dst = c->frames.p + (int64_t)i * c->frame_stride;
       HIPCHK(hipMemcpyAsync(dst, frames + (int64_t)i * pitch, (size_t)c->npix, hipMemcpyHostToDevice, s));

@@ -830,6 +830,9 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   hipStream_t st = c->stream;
   Timer T(c);
 
+  // Device frames are read in place when 16-byte aligned (the kernels load
+  // 16 B per lane); otherwise they are first copied into the staging slots.
+  const bool direct = device_frames && ((((uintptr_t)frames | (uintptr_t)pitch) & 15) == 0);
   // ---- slots: frame pointers and crop rectangles (cropBoundingBox :1420-1470)
   const int s_lut0 = first > 0 ? 0 : 1, s_proc0 = halo ? 0 : 1;
   for (int s = 0; s <= n; ++s) {
@@ -839,7 +842,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
     S.frame = gframe;
     S.active = s >= s_lut0;
     if (s == 0) c->h_frame_ptr.p[0] = c->halo.p;
-    else c->h_frame_ptr.p[s] = device_frames ? frames + (int64_t)(s - 1) * pitch : c->frames.p + (int64_t)s * fstride;
+    else c->h_frame_ptr.p[s] = direct ? frames + (int64_t)(s - 1) * pitch : c->frames.p + (int64_t)s * fstride;
     if (s < s_lut0) continue;
     const int bi = halo ? s : s - 1;  // index into bb[]
     int bx = c->bb_x, byb = c->bb_yb, bys = c->bb_ys;
@@ -871,8 +874,14 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
                             hipMemcpyHostToDevice, st));
     if (halo) HIPCHK(hipMemcpyAsync(c->halo.p, prev, c->npix, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
-  } else if (halo) {
-    k_out<<<64, 256, 0, st>>>(c->zero_ph.p, c->h_ph.d, nullptr, nullptr, 0, prev, c->halo.p, c->npix);
+  } else {
+    if (!direct)
+      HIPCHK(hipMemcpy2DAsync(c->frames.p + fstride, (size_t)fstride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
+                              hipMemcpyDeviceToDevice, st));
+    if (halo && ((uintptr_t)prev & 15) == 0)
+      k_out<<<64, 256, 0, st>>>(c->zero_ph.p, c->h_ph.d, nullptr, nullptr, 0, prev, c->halo.p, c->npix);
+    else if (halo)
+      HIPCHK(hipMemcpyAsync(c->halo.p, prev, (size_t)c->npix, hipMemcpyDeviceToDevice, st));
   }
 
   const int cur = c->parity, prv = c->last_parity;

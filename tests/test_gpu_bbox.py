@@ -186,3 +186,26 @@ def test_bb_tm_as_executed():
         assert_bb_equal(run_gpu(cfg, params, frames, batch=4), O.bb_run(cfg.setup, params, frames))
     with pytest.raises(LMError):
         BBContext(cfg.setup, abi.bb_params(semantics=INTEGER))
+
+
+def test_bb_unaligned_device_frames():
+    """Device frames at an odd address / pitch are staged before the kernels."""
+    import torch
+    from locomouse_cpp_amd.runtime import BBContext
+    from oracle import oracle as O
+    cfg = SyntheticConfig()
+    frames = bb_frames(cfg, 6, seed=23)
+    npix = frames.shape[1] * frames.shape[2]
+    pitch = npix + 7
+    buf = torch.zeros(5 + pitch * 6, dtype=torch.uint8, device="cuda:0")
+    for i in range(6):
+        buf[5 + i * pitch: 5 + i * pitch + npix] = torch.from_numpy(frames[i].reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    params = abi.bb_params(semantics=INTEGER)
+    ctx = BBContext(cfg.setup, params, max_batch=6)
+    try:
+        ctx.push_device(buf.data_ptr() + 5, pitch, 6, values=False)
+        got = ctx.finish()
+    finally:
+        ctx.close()
+    assert_bb_equal(got, O.bb_run(cfg.setup, params, frames))

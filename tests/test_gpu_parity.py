@@ -122,6 +122,25 @@ def test_device_frames_api(cfg):
     assert_same(got, _oracle(cfg, frames).result, "device: ")
 
 
+def test_device_frames_unaligned(cfg):
+    """Device frames at an odd address and pitch (staged by a D2D copy), plus
+    an unaligned halo frame."""
+    torch = pytest.importorskip("torch")
+    frames = cfg.frames(40, 7)
+    npix = frames.shape[1] * frames.shape[2]
+    pitch = npix + 5
+    buf = torch.zeros(3 + pitch * 7, dtype=torch.uint8, device="cuda:0")
+    for i in range(7):
+        buf[3 + i * pitch: 3 + i * pitch + npix] = torch.from_numpy(frames[i].reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    from locomouse_cpp_amd.abi import result_to_numpy
+    ctx = _ctx(cfg)
+    base = buf.data_ptr() + 3
+    got = result_to_numpy(ctx.detect_device(base + pitch, pitch, 6, 41, d_prev_ptr=base))  # frame 40 as halo
+    from locomouse_cpp_amd.results import slice_results
+    assert_same(got, slice_results(_oracle(cfg, frames).result, 1), "unaligned device: ")
+
+
 def test_error_mapping(cfg):
     from locomouse_cpp_amd.runtime import LMError
     with pytest.raises(LMError) as e:
