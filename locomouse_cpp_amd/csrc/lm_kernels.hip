@@ -2478,8 +2478,11 @@ __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots
 // sizes are multiples of 16 bytes.
 __global__ __launch_bounds__(256) void k_out(const LmPackHdr* __restrict__ ph, LmPackHdr* __restrict__ h_ph,
                                              const uint8_t* __restrict__ pack, uint8_t* __restrict__ h_pack, int64_t h_cap,
-                                             const uint8_t* __restrict__ halo_src, uint8_t* __restrict__ halo_dst,
-                                             int64_t halo_bytes) {
+                                             const uint8_t* __restrict__ halo_arg, const uint8_t* const* __restrict__ fptr,
+                                             int fidx, uint8_t* __restrict__ halo_dst, int64_t halo_bytes) {
+  // halo source: halo_arg, else the batch's frame pointer fptr[fidx] (device
+  // array written by k_prep, so a captured graph replays with fresh frames)
+  const uint8_t* __restrict__ halo_src = halo_arg ? halo_arg : (fptr ? fptr[fidx] : nullptr);
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (int64_t)gridDim.x * blockDim.x;
   if (tid == 0) *h_ph = *ph;
   const int64_t bytes = ph->bytes;

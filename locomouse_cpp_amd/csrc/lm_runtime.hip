@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -236,8 +237,21 @@ struct lm_ctx {
   std::vector<const char*> t_names;  // static kernel names
   std::vector<double> t_ms, t_t0, t_t1;
   std::vector<hipEvent_t> ev_pool;
+  // captured per-batch kernel chains, keyed by (n, parity, carry, last n, s_lut0, s_proc0, 0)
+  struct GraphEntry {
+    hipGraphExec_t exec[3];  // kernels before k_corr, k_corr, after
+  };
+  std::map<std::array<int, 7>, GraphEntry> graphs;
+  bool use_graphs = true;
+  void drop_graphs() {
+    for (auto& g : graphs)
+      for (hipGraphExec_t x : g.second.exec)
+        if (x) (void)hipGraphExecDestroy(x);
+    graphs.clear();
+  }
 
   ~lm_ctx() {
+    drop_graphs();
     if (stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(stream);
@@ -686,15 +700,20 @@ struct Timer {
     }
     return c->ev_pool[i];
   }
+  bool capturing = false;  // inside a graph capture: a failed record aborts the capture, not the batch
+  void record(hipEvent_t e) {
+    const hipError_t r = hipEventRecord(e, c->stream);
+    if (r != hipSuccess && !capturing) hip_check(r, "hipEventRecord");
+  }
   void begin(const char* name) {
     if (!on) return;
     const int i = (int)ev.size() * 2;
-    HIPCHK(hipEventRecord(pool(i), c->stream));
+    record(pool(i));
     ev.push_back({name, i});
   }
   void end() {
     if (!on) return;
-    HIPCHK(hipEventRecord(pool(ev.back().second + 1), c->stream));
+    record(pool(ev.back().second + 1));
   }
   // Durations, plus start/end against the device's epoch event so callers can
   // take the union of one kernel's spans over several contexts' streams.
@@ -879,85 +898,149 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       HIPCHK(hipMemcpy2DAsync(c->frames.p + fstride, (size_t)fstride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
                               hipMemcpyDeviceToDevice, st));
     if (halo && ((uintptr_t)prev & 15) == 0)
-      k_out<<<64, 256, 0, st>>>(c->zero_ph.p, c->h_ph.d, nullptr, nullptr, 0, prev, c->halo.p, c->npix);
+      k_out<<<64, 256, 0, st>>>(c->zero_ph.p, c->h_ph.d, nullptr, nullptr, 0, prev, nullptr, 0, c->halo.p, c->npix);
     else if (halo)
       HIPCHK(hipMemcpyAsync(c->halo.p, prev, (size_t)c->npix, hipMemcpyDeviceToDevice, st));
   }
 
   const int cur = c->parity, prv = c->last_parity;
+  if (!c->gscratch.p) c->gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
+  static const bool graphs_env = [] {
+    const char* v = getenv("LM_GRAPH");
+    return !v || atoi(v) != 0;
+  }();
+  // The kernel chain of one batch attempt.  Kernel arguments depend only on
+  // the key of c->graphs (frame pointers and slots reach the kernels through
+  // k_prep's copies of mapped host arrays), so the chain is captured once per
+  // key into a hipGraph and replayed.
+  auto chain = [&](Arena& A, bool do_carry, int part) {  // part: 0 pre, 1 k_corr, 2 post, -1 all
+    const int nproc = n + 1 - s_proc0;
+    if (part <= 0) {
+      k_prep<<<1, 256, 0, st>>>(c->h_slots.d, c->h_frame_ptr.d, c->h_ctl.d, n + 1, c->slots.p, c->frame_ptr.p, A.ctl.p,
+                                c->npos.p, c->err.p);
+      if (do_carry) {  // a rerun keeps slot 0's staged candidates
+        T.begin("k_carry");
+        k_carry<<<1, 256, 0, st>>>(dK, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
+        T.end();
+      }
+      T.begin("k_minmax_lut");
+      k_minmax_lut<<<n + 1 - s_lut0, 1024, 0, st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0, c->adj.p,
+                                                   c->setup.method != 0, c->luts.p);
+      T.end();
+      const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
+      T.begin("k_ingest");
+      k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
+          dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
+      T.end();
+    }
+    if (part == 1 || part < 0) {
+      T.begin("k_corr");
+      for (size_t gi = 0; gi < c->corr_groups.size(); ++gi) {
+        const auto& grp = c->corr_groups[gi];
+        const LmDetGroup& G = grp.second;
+        HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_lds[gi], st, dK, G,
+                           c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->keys.p, c->npos.p, c->tailbin.p,
+                           c->tailbin_slot_bytes));
+      }
+      T.end();
+    }
+    if (part == 2 || part < 0) {
+      if (c->debug & 1) {
+        if (!c->dbg.p) {
+          c->dbg.alloc((size_t)c->dbg_slot_floats * c->nslots);
+          c->dbg_offd.alloc(LM_NDET);
+          HIPCHK(hipMemcpy(c->dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice));
+        }
+        k_corr_dbg<<<dim3(K.n_tiles, nproc), 256, c->corr_lds, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0,
+                                                                     c->dbg.p, c->dbg_offd.p, c->dbg_slot_floats);
+      }
+      T.begin("k_tail");
+      k_tail<<<nproc, 1024, 0, st>>>(dK, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p, c->tscratch.p,
+                                     (int64_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w, A.hdr.p, c->err.p);
+      T.end();
+      long long *kp0 = nullptr, *kp1 = nullptr;
+      if (c->kprof_on) {
+        if (!c->kprof.p) c->kprof.alloc((size_t)2 * 16 * 2 * c->nslots);
+        HIPCHK(hipMemsetAsync(c->kprof.p, 0, sizeof(long long) * 2 * 16 * 2 * c->nslots, st));
+        kp0 = c->kprof.p;
+        kp1 = c->kprof.p + 16 * 2 * c->nslots;
+      }
+      T.begin("k_nms_bottom");
+      k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+                                                      c->gscratch_slot, A.hdr.p, c->err.p, kp0);
+      T.end();
+      T.begin("k_nms_side");
+      k_nms<<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+                                                  c->gscratch_slot, A.hdr.p, c->err.p, kp1);
+      T.end();
+      T.begin("k_post");
+      k_post<<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
+                                                     c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
+                                                     A.pr.p, A.ctl.p, c->err.p);
+      T.end();
+      T.begin("k_pack");
+      k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
+      k_pack_copy<<<dim3(n, 2), 256, 0, st>>>(dK, A.hdr.p, n, c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p,
+                                              A.ir.p, A.pr.p, A.ph.p, A.pack.p, A.side_base.p);
+      T.end();
+      // header + results to host memory, then frame n as the next batch's halo
+      k_out<<<128, 256, 0, st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, nullptr,
+                                 c->frame_ptr.p, n, c->halo.p, c->npix);
+    }
+  };
   for (int attempt = 0;; ++attempt) {
     Arena& A = c->arena[cur];
     LmArenaCtl& hc = *c->h_ctl.p;
     std::memset(&hc, 0, sizeof(hc));
     for (int k = 0; k < AR_COUNT; ++k) hc.cap[k] = A.cap[k];
-    k_prep<<<1, 256, 0, st>>>(c->h_slots.d, c->h_frame_ptr.d, c->h_ctl.d, n + 1, c->slots.p, c->frame_ptr.p, A.ctl.p,
-                              c->npos.p, c->err.p);
-    if (carry && attempt == 0) {  // a rerun keeps slot 0's staged candidates
-      T.begin("k_carry");
-      k_carry<<<1, 256, 0, st>>>(dK, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
-      T.end();
-    }
-    T.begin("k_minmax_lut");
-    k_minmax_lut<<<n + 1 - s_lut0, 1024, 0, st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0, c->adj.p,
-                                                 c->setup.method != 0, c->luts.p);
-    T.end();
-    const int nproc = n + 1 - s_proc0;
-    const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
-    T.begin("k_ingest");
-    k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
-        dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
-    T.end();
-    T.begin("k_corr");
-    for (size_t gi = 0; gi < c->corr_groups.size(); ++gi) {
-      const auto& grp = c->corr_groups[gi];
-      const LmDetGroup& G = grp.second;
-      HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_lds[gi], st, dK, G,
-                         c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->keys.p, c->npos.p, c->tailbin.p,
-                         c->tailbin_slot_bytes));
-    }
-    T.end();
-    if (c->debug & 1) {
-      if (!c->dbg.p) {
-        c->dbg.alloc((size_t)c->dbg_slot_floats * c->nslots);
-        c->dbg_offd.alloc(LM_NDET);
-        HIPCHK(hipMemcpy(c->dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice));
+    const bool graph = graphs_env && c->use_graphs && attempt == 0 && !(c->debug & 1) && !c->kprof_on;
+    if (graph) {
+      // Three graphs per key (before / k_corr / after), so the timing events
+      // of k_corr (the roofline kernel) are recorded on the stream between
+      // graph launches; the other kernels are not timed on this path.
+      const std::array<int, 7> key{n, cur, carry ? 1 : 0, carry ? c->last_n : 0, s_lut0, s_proc0, 0};
+      auto it = c->graphs.find(key);
+      if (it == c->graphs.end()) {
+        lm_ctx::GraphEntry ent{};
+        bool ok = true;
+        const bool t_on = T.on;
+        T.on = false;
+        for (int part = 0; part < 3 && ok; ++part) {
+          hipGraph_t g = nullptr;
+          ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
+          if (!ok) break;
+          try {
+            chain(A, carry, part);
+          } catch (const std::exception&) {
+            ok = false;
+          }
+          const hipError_t e = hipStreamEndCapture(st, &g);
+          ok = ok && e == hipSuccess && g;
+          if (ok) ok = hipGraphInstantiate(&ent.exec[part], g, nullptr, nullptr, 0) == hipSuccess;
+          if (g) (void)hipGraphDestroy(g);
+        }
+        T.on = t_on;
+        (void)hipGetLastError();
+        if (ok) {
+          it = c->graphs.emplace(key, ent).first;
+        } else {  // capture unsupported here: run the chain directly from now on
+          for (hipGraphExec_t x : ent.exec)
+            if (x) (void)hipGraphExecDestroy(x);
+          c->use_graphs = false;
+        }
       }
-      k_corr_dbg<<<dim3(K.n_tiles, nproc), 256, c->corr_lds, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0,
-                                                                   c->dbg.p, c->dbg_offd.p, c->dbg_slot_floats);
+      if (it != c->graphs.end()) {
+        HIPCHK(hipGraphLaunch(it->second.exec[0], st));
+        T.begin("k_corr");
+        HIPCHK(hipGraphLaunch(it->second.exec[1], st));
+        T.end();
+        HIPCHK(hipGraphLaunch(it->second.exec[2], st));
+      } else {
+        chain(A, carry, -1);
+      }
+    } else {
+      chain(A, carry && attempt == 0, -1);
     }
-    T.begin("k_tail");
-    k_tail<<<nproc, 1024, 0, st>>>(dK, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p, c->tscratch.p,
-                                   (int64_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w, A.hdr.p, c->err.p);
-    T.end();
-    if (!c->gscratch.p) c->gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
-    long long *kp0 = nullptr, *kp1 = nullptr;
-    if (c->kprof_on) {
-      if (!c->kprof.p) c->kprof.alloc((size_t)2 * 16 * 2 * c->nslots);
-      HIPCHK(hipMemsetAsync(c->kprof.p, 0, sizeof(long long) * 2 * 16 * 2 * c->nslots, st));
-      kp0 = c->kprof.p;
-      kp1 = c->kprof.p + 16 * 2 * c->nslots;
-    }
-    T.begin("k_nms_bottom");
-    k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                    c->gscratch_slot, A.hdr.p, c->err.p, kp0);
-    T.end();
-    T.begin("k_nms_side");
-    k_nms<<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                c->gscratch_slot, A.hdr.p, c->err.p, kp1);
-    T.end();
-    T.begin("k_post");
-    k_post<<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
-                                                   c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
-                                                   A.pr.p, A.ctl.p, c->err.p);
-    T.end();
-    T.begin("k_pack");
-    k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
-    k_pack_copy<<<dim3(n, 2), 256, 0, st>>>(dK, A.hdr.p, n, c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p,
-                                            A.ir.p, A.pr.p, A.ph.p, A.pack.p, A.side_base.p);
-    T.end();
-    // header + results to host memory, then frame n as the next batch's halo
-    k_out<<<128, 256, 0, st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, c->h_frame_ptr.p[n],
-                               c->halo.p, c->npix);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
     const LmPackHdr& ph = *c->h_ph.p;
@@ -987,6 +1070,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
     if (e) throw std::runtime_error("device error flags " + std::to_string(e));
     if (!ph.overflow) break;
     if (attempt >= 3) throw std::runtime_error("result arena overflow persists.");
+    c->drop_graphs();  // arena / pack buffers are reallocated below
     if (ph.overflow & 2) {
       int ncap[AR_COUNT];
       for (int k = 0; k < AR_COUNT; ++k) ncap[k] = std::max(A.cap[k], (int)(ph.used[k] * 1.25) + 1024);
@@ -1002,9 +1086,10 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   Arena& A = c->arena[cur];
   const LmPackHdr ph = *c->h_ph.p;
   if ((int64_t)c->h_pack.n < ph.bytes) {
+    c->drop_graphs();
     c->h_pack.alloc((size_t)(ph.bytes + ph.bytes / 4));
-    k_out<<<128, 256, 0, st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, c->h_frame_ptr.p[n],
-                               c->halo.p, c->npix);
+    k_out<<<128, 256, 0, st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, nullptr,
+                               c->frame_ptr.p, n, c->halo.p, c->npix);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
   }
