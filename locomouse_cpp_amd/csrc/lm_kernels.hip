@@ -151,6 +151,65 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
   *reinterpret_cast<uint32_t*>(ext + (int64_t)slot * ext_slot_bytes + q) = word;
 }
 
+// ---------------------------------------------------------------- k_ingest_fb
+// k_ingest for LM_INGEST_FB consecutive slots per thread: the calibration
+// index and background byte of a crop pixel are loaded once and reused for
+// every slot whose crop sits at the same place (always, with a provided
+// bounding box); only the frame gather and the per-frame LUT are per slot.
+#define LM_INGEST_FB 8
+__global__ __launch_bounds__(256) void k_ingest_fb(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
+                                                   const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+                                                   const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
+                                                   int s0, int s_end, int fb, uint8_t* __restrict__ ext,
+                                                   int64_t ext_slot_bytes) {
+  const LmConst& K = *Kp;
+  const int sb = s0 + blockIdx.y * fb;
+  const int nf = min(fb, s_end - sb);
+  __shared__ uint8_t lut[LM_INGEST_FB][256];
+  for (int i = threadIdx.x; i < nf * 256; i += blockDim.x) lut[i >> 8][i & 255] = luts[(sb + (i >> 8)) * 256 + (i & 255)];
+  __syncthreads();
+  const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
+  const int64_t etot = e0 + (int64_t)K.ext_h[1] * K.ext_w[1];
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (q >= etot) return;
+  const int v = q < e0 ? 0 : 1;
+  const int64_t qq = v == 0 ? q : q - e0;
+  const int er = (int)(qq / K.ext_w[v]);
+  const int ec = (int)(qq % K.ext_w[v]);  // multiple of 4 (ext_w % 16 == 0)
+  int idx[4] = {-1, -1, -1, -1}, bv[4] = {0, 0, 0, 0};  // defined before the first crop test
+  int px = INT32_MIN, py = INT32_MIN;
+  for (int f = 0; f < nf; ++f) {
+    const int slot = sb + f;
+    const LmSlot sl = slots[slot];
+    if (sl.crop_x[v] != px || sl.crop_y[v] != py) {  // crop moved: recompute the gather indices
+      px = sl.crop_x[v];
+      py = sl.crop_y[v];
+      const int R = py + K.ext_oy[v] + er - K.pad_pre_rows;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int c = px + K.ext_ox[v] + ec + k - K.pad_pre_cols;
+        if (R < 0 || R >= K.n_rows || c < 0 || c >= K.n_cols) {
+          idx[k] = -1;
+        } else {
+          if (K.flip) c = K.n_cols - 1 - c;
+          idx[k] = cal[R * K.n_cols + c];
+          bv[k] = bkg[idx[k]];
+        }
+      }
+    }
+    const uint8_t* __restrict__ F = frame_ptr[slot];
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (idx[k] >= 0) {
+        const int fv = F[idx[k]];
+        word |= (uint32_t)lut[f][fv > bv[k] ? fv - bv[k] : 0] << (8 * k);
+      }
+    }
+    *reinterpret_cast<uint32_t*>(ext + (int64_t)slot * ext_slot_bytes + q) = word;
+  }
+}
+
 // ------------------------------------------------------------------ k_corr
 // One block = one 80x48 output tile of one detector of one slot; 256 threads
 // as 16x16, each LM_R rows x LM_C columns.  The input tile is staged in LDS as

@@ -905,6 +905,10 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
 
   const int cur = c->parity, prv = c->last_parity;
   if (!c->gscratch.p) c->gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
+  static const int ingest_fb = [] {  // slots per k_ingest_fb thread; LM_INGEST_FB=0: k_ingest
+    const char* v = getenv("LM_INGEST_FB");
+    return v ? std::max(0, std::min(LM_INGEST_FB, atoi(v))) : LM_INGEST_FB;
+  }();
   static const bool graphs_env = [] {
     const char* v = getenv("LM_GRAPH");
     return !v || atoi(v) != 0;
@@ -929,9 +933,36 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       T.end();
       const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
       T.begin("k_ingest");
-      k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
-          dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
+      if (ingest_fb)
+        k_ingest_fb<<<dim3((unsigned)((etot / 4 + 255) / 256), (unsigned)((nproc + ingest_fb - 1) / ingest_fb)), 256, 0,
+                      st>>>(dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, n + 1, ingest_fb,
+                            c->ext.p, c->ext_slot_bytes);
+      else
+        k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
+            dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
       T.end();
+      if (ingest_fb && dbg_env("LM_INGEST_CHECK")) {  // diagnostics: compare with k_ingest
+        DevBuf<uint8_t> e2;
+        e2.alloc((size_t)c->ext_slot_bytes * c->nslots);
+        k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
+            dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, e2.p, c->ext_slot_bytes);
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<uint8_t> a((size_t)c->ext_slot_bytes), b((size_t)c->ext_slot_bytes);
+        for (int sl = s_proc0; sl <= n; ++sl) {
+          HIPCHK(hipMemcpy(a.data(), c->ext.p + (int64_t)sl * c->ext_slot_bytes, a.size(), hipMemcpyDeviceToHost));
+          HIPCHK(hipMemcpy(b.data(), e2.p + (int64_t)sl * c->ext_slot_bytes, b.size(), hipMemcpyDeviceToHost));
+          int64_t bad = -1, nbad = 0;
+          for (int64_t q = 0; q < etot; ++q)
+            if (a[q] != b[q]) {
+              if (bad < 0) bad = q;
+              ++nbad;
+            }
+          if (bad >= 0)
+            fprintf(stderr, "[ingest check] slot %d: %ld bytes differ, first at %ld (fb %d vs ref %d), e0 %ld ext_w %d,%d\n",
+                    sl, (long)nbad, (long)bad, a[bad], b[bad], (long)((int64_t)K.ext_h[0] * K.ext_w[0]), K.ext_w[0],
+                    K.ext_w[1]);
+        }
+      }
     }
     if (part == 1 || part < 0) {
       T.begin("k_corr");
