@@ -85,6 +85,51 @@ def cpu_baseline(cfg, seconds=10.0, max_frames=2000):
             "cpu": cpu}
 
 
+def run_bb(args):
+    """The whole-video bounding-box pass (lm_bb_push_device, method 0) on one
+    GPU: frames resident in HBM, `--steps` pushes of `--batch` frames after
+    `--warmup`; the CPU baseline is the oracle restatement on a bounded
+    sample.  Prints one JSON line (not the headline metric)."""
+    import time
+
+    import torch
+
+    from locomouse_cpp_amd import abi
+    from locomouse_cpp_amd.runtime import BBContext, synth_frames_device
+    from locomouse_cpp_amd.synthetic import SyntheticConfig
+    rows, cols, workload = CONFIGS[args.config]
+    cfg = SyntheticConfig(rows=rows, cols=cols)
+    params = abi.bb_params(semantics=args.bb_semantics)
+    B, pitch, nbuf = args.batch, rows * cols, 4
+    d = torch.empty(nbuf * B * pitch, dtype=torch.uint8, device="cuda:0")
+    synth_frames_device(d.data_ptr(), rows, cols, 0, nbuf * B, pitch)
+    ctx = BBContext(cfg.setup, params, max_batch=B)
+    for i in range(args.warmup):
+        ctx.push_device(d.data_ptr() + (i % nbuf) * B * pitch, pitch, B, values=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ctx.push_device(d.data_ptr() + (i % nbuf) * B * pitch, pitch, B, values=False)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.close()
+    line = {"metric": "whole-video bounding-box pass frames/s (method 0)", "value": args.steps * B / dt,
+            "unit": "frames/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "replicas",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic (lm_synth.h scene, resident in HBM)",
+            "config": {"workload": workload + "; LocoMouse::computeBoundingBox over the stream", "batch_frames": B,
+                       "firstlast_semantics": "integer" if args.bb_semantics else "as executed"}}
+    if not args.no_cpu:
+        from oracle import oracle as O  # CPU baseline only
+        nf = 40 if rows <= 256 else 10
+        fr = cfg.frames(0, nf)
+        t1 = time.perf_counter()
+        O.bb_run(cfg.setup, params, fr)
+        line["cpu_baseline"] = {"value": nf / (time.perf_counter() - t1), "unit": "frames/s", "cores": 1,
+                                "kind": "port", "sample": f"{nf} frames, oracle/lm_oracle.cpp BBOracle, one thread"}
+    print(json.dumps(line))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,7 +143,12 @@ def main():
     ap.add_argument("--round-robin", action="store_true", help="one host thread drives all streams in turn")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", choices=["detect", "bb"], default="detect",
+                    help="bb: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) instead of the headline path")
+    ap.add_argument("--bb-semantics", type=int, default=0, help="firstLastOverT: 0 as executed, 1 integer sums")
     args = ap.parse_args()
+    if args.workload == "bb":
+        return run_bb(args)
 
     import torch
     import torch.distributed as dist
