@@ -244,3 +244,30 @@ def frame_views(res, f):
     out["pairwise"] = pw
     out["tail"] = res["tail"][f]
     return out
+
+
+class lm_tracks(C.Structure):  # include/locomouse_track.h
+    _fields_ = [
+        ("n_frames", C.c_int32),
+        ("paw_tracks", C.POINTER(C.c_int32)),
+        ("snout_tracks", C.POINTER(C.c_int32)),
+        ("tracks_tail", C.POINTER(C.c_int32)),
+        ("track_index_bottom", C.POINTER(C.c_int32)),
+        ("track_index_side", C.POINTER(C.c_int32)),
+    ]
+
+
+def numpy_to_result(res):
+    """An lm_batch_result pointing into a result dict's arrays (the dict must
+    outlive it; arrays are made contiguous in place)."""
+    r = lm_batch_result()
+    keep = {}
+    for k in ("cand_offset", "cand", "p22d_offset", "p22d", "side_y", "side_s", "unary_offset", "unary", "pw_dims",
+              "pw_jc_offset", "pw_jc", "pw_nz_offset", "pw_ir", "pw_pr", "tail"):
+        a = np.ascontiguousarray(res[k])
+        keep[k] = a
+        setattr(r, k, C.cast(a.ctypes.data, dict(lm_batch_result._fields_)[k]))
+    r.n_frames = int(res["n_frames"])
+    r.first_frame = int(res.get("first_frame", 0))
+    r._keep = keep
+    return r

@@ -271,42 +271,23 @@ void LocoMouse::flush() {
   append(r);
 }
 
-void LocoMouse::append(const lm_batch_result& r) {
-  auto list = [&](int f, int k) {
-    const lm_candidate* b = r.cand + r.cand_offset[4 * f + k];
-    const lm_candidate* e = r.cand + r.cand_offset[4 * f + k + 1];
-    return std::vector<Candidate>(reinterpret_cast<const Candidate*>(b), reinterpret_cast<const Candidate*>(e));
-  };
-  for (int f = 0; f < r.n_frames; ++f) {
-    CANDIDATES_BOTTOM_PAW.push_back(list(f, 0));
-    CANDIDATES_BOTTOM_SNOUT.push_back(list(f, 1));
-    CANDIDATES_SIDE_PAW.push_back(list(f, 2));
-    CANDIDATES_SIDE_SNOUT.push_back(list(f, 3));
-    for (int k = 0; k < LM_N_FEATURES; ++k) {
-      const int q = 2 * f + k;
-      std::vector<P22D> pv;
-      for (int64_t i = r.p22d_offset[q]; i < r.p22d_offset[q + 1]; ++i) {
-        const lm_p22d& p = r.p22d[i];
-        P22D v(Candidate(p.bottom.x, p.bottom.y, p.bottom.score), Candidate());
-        v.set_side_raw(r.side_y + p.side_offset, r.side_s + p.side_offset, p.side_count);
-        pv.push_back(std::move(v));
-      }
-      (k ? CANDIDATES_MATCHED_VIEWS_SNOUT : CANDIDATES_MATCHED_VIEWS_PAW).push_back(std::move(pv));
-      const int ncol = k ? 1 : LM_N_PAWS;  // N_cand x 4 (paw) / x 1 (snout), column-major
-      const int64_t u0 = r.unary_offset[q], nu = r.unary_offset[q + 1] - u0;
-      MyMat U((unsigned)(nu / ncol), (unsigned)ncol);
-      std::copy(r.unary + u0, r.unary + u0 + nu, U.getValues());
-      (k ? UNARY_BOTTOM_SNOUT : UNARY_BOTTOM_PAW).push_back(std::move(U));
-      const int32_t* d = r.pw_dims + 3 * q;
-      if (d[0] >= 0)  // frames > 0 only (:896-919)
-        (k ? PAIRWISE_BOTTOM_SNOUT : PAIRWISE_BOTTOM_PAW)
-            .emplace_back(d[0], d[1], r.pw_jc + r.pw_jc_offset[q], r.pw_ir + r.pw_nz_offset[q],
-                          r.pw_pr + r.pw_nz_offset[q]);
-    }
-    TailTrack t;
-    std::copy(r.tail + 45 * f, r.tail + 45 * (f + 1), t.begin());
-    TRACKS_TAIL.push_back(t);
-  }
+// After the loop (main.cpp:86-91): the tracker over the containers above.
+TrackSetup LocoMouse::track_setup() {
+  sync();
+  if (CURRENT_FRAME + 1 != (int)N_FRAMES)
+    throw std::runtime_error("computeBottomTracks: the per-frame loop has not read every frame.");
+  TrackSetup S = make_track_setup(geometry(), IN.params, N_FRAMES);
+  S.bb_x_pos = &BB_X_POS;
+  S.bb_y_bottom_pos = &BB_Y_BOTTOM_POS;
+  S.bb_y_side_pos = &BB_Y_SIDE_POS;
+  return S;
+}
+
+void LocoMouse::computeBottomTracks() { locomouse::computeBottomTracks(*this, track_setup(), TRACKS); }
+void LocoMouse::computeSideTracks() { locomouse::computeSideTracks(*this, track_setup(), TRACKS); }
+void LocoMouse::exportResults() {
+  exportTracks(*this, track_setup(), TRACKS);
+  if (!IN.output_file.empty()) writeOutputYaml(IN.output_file, TRACKS);
 }
 
 #define LM_ACCESSOR(fn, member) \

@@ -35,6 +35,7 @@
 
 #include "Candidates.hpp"
 #include "MyMat.hpp"
+#include "Tracks.hpp"
 #include "locomouse_hip.h"
 
 namespace locomouse {
@@ -58,11 +59,12 @@ struct LocoMouse_Inputs {
   // to re-read the video from frame 0 after the pass.
   lm_bb_params bb_params{11, 1, 5, 8, LM_BB_FIRSTLAST_AS_EXECUTED, 46, 760, 100, 149, 400, 150, 0};
   std::function<void()> rewind;
+  // exportResults writes <output_file> (the reference's
+  // <outdir>/output_<stem>.yml, :360) when non-empty.
+  std::string output_file;
 };
 
-using TailTrack = std::array<int32_t, 3 * LM_N_TAIL_POINTS>;  // TRACKS_TAIL entry: 3x15, row-major, -1 = missing
-
-class LocoMouse {
+class LocoMouse : protected FrameResults {
  public:
   explicit LocoMouse(const LocoMouse_Inputs& inputs);
   virtual ~LocoMouse();
@@ -81,6 +83,10 @@ class LocoMouse {
   void detectSideCandidates();        // :809-838
   void matchBottomSideCandidates();   // :999-1021
   void storePreviousImage();          // :1508-1513
+  // After the per-frame loop (main.cpp:86-91; SURVEY.md §8(f) row 3, host C++):
+  void computeBottomTracks();         // :2153-2200 (match2nd, 4 paw orders + snout)
+  void computeSideTracks();           // :2202-2214 (bestSideViewMatch)
+  void exportResults();               // :2348-2482 (track export; YAML when output_file is set)
   unsigned int N_frames() const { return N_FRAMES; }
 
   // The reference's protected result vectors (LocoMouse_class.hpp:219-236),
@@ -96,6 +102,7 @@ class LocoMouse {
   const std::vector<MATSPARSE>& pairwise_bottom_paw();  // frames >= 1 only (:896-919)
   const std::vector<MATSPARSE>& pairwise_bottom_snout();
   const std::vector<TailTrack>& tracks_tail();
+  const TrackResults& tracks() const { return TRACKS; }  // TRACK_INDEX_* and the exported matrices
   int current_frame() const { return CURRENT_FRAME; }
   lm_geometry geometry() const;
 
@@ -119,13 +126,10 @@ class LocoMouse {
   lm_rect bb_bottom_mouse() const { return BB_BOTTOM_MOUSE; }
 
  protected:
-
-  std::vector<std::vector<Candidate>> CANDIDATES_BOTTOM_PAW, CANDIDATES_BOTTOM_SNOUT;
-  std::vector<std::vector<Candidate>> CANDIDATES_SIDE_PAW, CANDIDATES_SIDE_SNOUT;
-  std::vector<std::vector<P22D>> CANDIDATES_MATCHED_VIEWS_PAW, CANDIDATES_MATCHED_VIEWS_SNOUT;
-  std::vector<MyMat> UNARY_BOTTOM_PAW, UNARY_BOTTOM_SNOUT;
-  std::vector<MATSPARSE> PAIRWISE_BOTTOM_PAW, PAIRWISE_BOTTOM_SNOUT;
-  std::vector<TailTrack> TRACKS_TAIL;
+  // The result vectors (CANDIDATES_*, UNARY_*, PAIRWISE_*, TRACKS_TAIL) are
+  // the FrameResults members; the tracks below are computed from them.
+  TrackResults TRACKS;
+  TrackSetup track_setup();
 
  private:
   lm_ctx* CTX = nullptr;
@@ -136,7 +140,6 @@ class LocoMouse {
   int N_PENDING = 0;
   size_t FRAME_BYTES = 0;
   void flush();
-  void append(const lm_batch_result& r);
 };
 
 // LocoMouse_TM (LocoMouse_TM.hpp:30-55): readFrame adds imadjust

@@ -48,8 +48,9 @@ def build(verbose=False):
 def build_host(verbose=False):
     """liblocomouse_host.so: the LocoMouse / Candidate / P22D / MyMat C++
     surface (locomouse_cpp_amd/host) linked against the C-ABI library."""
-    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-I" + os.path.join(ROOT, "include"),
-           "-I" + HOST_DIR, "-o", HOST_LIB_PATH, os.path.join(HOST_DIR, "LocoMouse.cpp"), "-L" + PKG,
+    srcs = [os.path.join(HOST_DIR, f) for f in ("LocoMouse.cpp", "Tracks.cpp", "match2nd.cpp")]
+    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", "-Wextra",
+           "-I" + os.path.join(ROOT, "include"), "-I" + HOST_DIR, "-o", HOST_LIB_PATH, *srcs, "-L" + PKG,
            "-llocomouse_hip", "-Wl,-rpath,$ORIGIN"]
     if verbose:
         print(" ".join(cmd))

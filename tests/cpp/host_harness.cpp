@@ -21,6 +21,9 @@ struct Flat {
   std::vector<double> side_s, unary, pw_pr;
 } g_flat;
 
+locomouse::TrackResults g_tracks;
+std::string g_output_file;
+
 int fail(const std::exception& e, int code, char* err, int errlen) {
   if (err && errlen > 0) {
     std::strncpy(err, e.what(), (size_t)errlen - 1);
@@ -43,6 +46,7 @@ extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_
     in.n_frames = (uint32_t)n_frames;
     in.device = device;
     in.batch = batch;
+    in.output_file = g_output_file;
     const size_t fb = (size_t)setup->video_rows * setup->video_cols;
     int next = 0;
     in.read_frame = [&](uint8_t* dst) {  // V >> F over the frames given
@@ -76,8 +80,14 @@ extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_
       L->computePairwiseCostsBottom();
       L->detectSideCandidates();
       L->matchBottomSideCandidates();
-      if (call_order == 1 && i % 3 == 1) (void)L->candidates_bottom_paw();  // mid-batch reads flush early
+      if ((call_order & 1) && i % 3 == 1) (void)L->candidates_bottom_paw();  // mid-batch reads flush early
       L->storePreviousImage();
+    }
+    if (call_order & 4) {  // main.cpp:86-91
+      L->computeBottomTracks();
+      L->computeSideTracks();
+      L->exportResults();
+      g_tracks = L->tracks();
     }
     Flat& F = g_flat;
     F = Flat();
@@ -157,6 +167,24 @@ extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_
   } catch (const std::exception& e) {
     return fail(e, 3, err, errlen);
   }
+}
+
+// Output file for exportResults (empty: none).
+extern "C" void lmh_set_output(const char* path) { g_output_file = path ? path : ""; }
+
+// The tracks of the last lmh_run with call_order & 4: paw [4][n][3], snout
+// [n][3], tail [3][15n], index_bottom / index_side [5][n].
+extern "C" int lmh_get_tracks(int n, int32_t* paw, int32_t* snout, int32_t* tail, int32_t* idx_b, int32_t* idx_s) {
+  const auto& T = g_tracks;
+  if (T.paw_tracks.size() != 4 || T.tracks_tail.cols != 15 * n) return 1;
+  for (int i = 0; i < 4; ++i) std::copy(T.paw_tracks[i].data.begin(), T.paw_tracks[i].data.end(), paw + (size_t)i * n * 3);
+  std::copy(T.snout_tracks[0].data.begin(), T.snout_tracks[0].data.end(), snout);
+  std::copy(T.tracks_tail.data.begin(), T.tracks_tail.data.end(), tail);
+  std::copy(T.TRACK_INDEX_PAW_BOTTOM.data.begin(), T.TRACK_INDEX_PAW_BOTTOM.data.end(), idx_b);
+  std::copy(T.TRACK_INDEX_SNOUT_BOTTOM.data.begin(), T.TRACK_INDEX_SNOUT_BOTTOM.data.end(), idx_b + 4 * n);
+  std::copy(T.TRACK_INDEX_PAW_SIDE.data.begin(), T.TRACK_INDEX_PAW_SIDE.data.end(), idx_s);
+  std::copy(T.TRACK_INDEX_SNOUT_SIDE.data.begin(), T.TRACK_INDEX_SNOUT_SIDE.data.end(), idx_s + 4 * n);
+  return 0;
 }
 
 // Container semantics that need no GPU (P22D slot-0 rule, MATSPARSE CSC).

@@ -35,6 +35,8 @@ def lib():
         L.lmh_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                               C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_int]
         L.lmh_run.restype = C.c_int
+        L.lmh_set_output.argtypes = [C.c_char_p]
+        L.lmh_get_tracks.argtypes = [C.c_int] + [C.c_void_p] * 5
         L.lmh_selftest.argtypes = [C.c_char_p, C.c_int]
         L.lmh_selftest.restype = C.c_int
         _lib = L
@@ -70,6 +72,27 @@ def run_video(cfg, frames, batch=8, device=0, n_frames=None, call_order=0, bb_pa
     if with_bb:
         return res, corners, (sizes[0].tuple(), sizes[1].tuple())
     return res
+
+
+def run_video_tracks(cfg, frames, batch=8, device=0, output_file=None):
+    """run_video with main.cpp's post-loop calls (computeBottomTracks,
+    computeSideTracks, exportResults): returns (result dict, tracks dict,
+    corners)."""
+    import numpy as np
+    lib().lmh_set_output(os.fsencode(output_file) if output_file else None)
+    try:
+        res, corners, _ = run_video(cfg, frames, batch=batch, device=device, call_order=4, with_bb=True)
+    finally:
+        lib().lmh_set_output(None)
+    n = res["n_frames"]
+    t = {"paw_tracks": np.zeros((4, n, 3), np.int32), "snout_tracks": np.zeros((1, n, 3), np.int32),
+         "tracks_tail": np.zeros((3, 15 * n), np.int32), "track_index_bottom": np.zeros((5, n), np.int32),
+         "track_index_side": np.zeros((5, n), np.int32)}
+    rc = lib().lmh_get_tracks(n, *(t[k].ctypes.data for k in ("paw_tracks", "snout_tracks", "tracks_tail",
+                                                               "track_index_bottom", "track_index_side")))
+    if rc:
+        raise HostError(2, "no tracks recorded")
+    return res, t, corners
 
 
 def selftest():

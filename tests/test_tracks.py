@@ -1,0 +1,278 @@
+"""The tracking stage after the per-frame loop:
+match2nd, computeBottomTracks / computeSideTracks and the track export, host
+C++ (locomouse_cpp_amd/host/match2nd.cpp, Tracks.cpp) through its C-ABI
+(include/locomouse_track.h) against the restatement in oracle/track_oracle.py.
+
+Parity unpinned against the reference itself (no fixtures, no OpenCV here):
+the restatement is pinned by known answers — with one track, match2nd is the
+exact max-sum path (brute force), and tracks never share a candidate — and the
+C++ must equal it bit for bit (labels, costs, exported coordinates)."""
+import ctypes as C
+import itertools
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from locomouse_cpp_amd import abi, runtime
+from locomouse_cpp_amd import synthetic as S
+from locomouse_cpp_amd import tracks as TR
+from oracle import oracle as O
+from oracle import track_oracle as TO
+
+HDR = os.path.join(runtime.ROOT, "include", "locomouse_track.h")
+
+
+def random_problem(rng, frames, points, nong, density=0.6, full=False, max_loc=5, empty_frames=True):
+    """unary (n_loc x points) and CSC transitions, with the occlusion-diagonal
+    always present like the reference's pairwise potentials (:2056-2059)."""
+    lo = 0 if empty_frames else 1
+    nloc = [int(rng.integers(lo, max_loc + 1)) for _ in range(frames)]
+    unary = [rng.uniform(0.0, 1.0, size=(n, points)) for n in nloc]
+    pairwise = []
+    for f in range(frames - 1):
+        rows, cols = nloc[f + 1] + nong, nloc[f] + nong
+        dense = np.where(rng.uniform(size=(rows, cols)) < density, rng.uniform(0.01, 0.3, size=(rows, cols)), 0.0)
+        if full:
+            dense = rng.uniform(0.01, 0.3, size=(rows, cols))
+        for k in range(nong):
+            dense[nloc[f + 1] + k, nloc[f] + k] = 0.05
+        jc, ir, pr = [0], [], []
+        for c in range(cols):
+            for r in range(rows):
+                if dense[r, c] != 0:
+                    ir.append(r)
+                    pr.append(float(dense[r, c]))
+            jc.append(len(ir))
+        pairwise.append((rows, cols, jc, ir, pr))
+    return unary, pairwise
+
+
+def as_oracle_unary(unary):
+    return [(u.shape[0], u.shape[1], u.reshape(-1, order="F").tolist()) for u in unary]
+
+
+def brute_force_single(unary, pairwise, nong, occ_cost=0.0):
+    frames = len(unary)
+    sizes = [u.shape[0] + nong for u in unary]
+    dense = []
+    for (rows, cols, jc, ir, pr) in pairwise:
+        d = np.full((rows, cols), np.nan)
+        for c in range(cols):
+            for k in range(jc[c], jc[c + 1]):
+                d[ir[k], c] = pr[k]
+        dense.append(d)
+    best, arg = -np.inf, None
+    for path in itertools.product(*[range(s) for s in sizes]):
+        v = sum(unary[f][path[f], 0] if path[f] < unary[f].shape[0] else occ_cost for f in range(frames))
+        ok = True
+        for f in range(frames - 1):
+            t = dense[f][path[f + 1], path[f]]
+            if np.isnan(t):
+                ok = False
+                break
+            v += t
+        if ok and v > best:
+            best, arg = v, path
+    return list(arg)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_single_track_is_the_max_sum_path(seed):
+    """One track: margin() then assign() cancel their message updates, so
+    the labelling is the best path of unary + pairwise (occlusion points cost
+    occlusion_point_cost).  Pins the restatement and the C++ to a known answer."""
+    rng = np.random.default_rng(seed)
+    unary, pairwise = random_problem(rng, frames=4, points=1, nong=2, full=True, max_loc=3, empty_frames=False)
+    want = brute_force_single(unary, pairwise, nong=2)
+    ref = TO.match2nd(as_oracle_unary(unary), pairwise, 2, 0.0, 0.0, 4, 1, (0,))
+    assert ref[0] == want
+    got = TR.match2nd(unary, pairwise, nong=2, points=1, perm=[0])
+    assert got[0].tolist() == want
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_tracks_never_share_a_candidate(seed):
+    """Each assigned track bars its candidate locations for the tracks
+    assigned after it (update_unary_second, match2nd.h:391-396)."""
+    rng = np.random.default_rng(100 + seed)
+    unary, pairwise = random_problem(rng, frames=12, points=4, nong=3, density=0.8, max_loc=6, empty_frames=False)
+    lab = TR.match2nd(unary, pairwise, nong=3, points=4, perm=[3, 2, 1, 0])
+    for f in range(12):
+        real = [int(l) for l in lab[:, f] if 0 <= l < unary[f].shape[0]]
+        assert len(real) == len(set(real))
+
+
+CASES = [  # (seed, frames, points, nong, density, occ_cost, bam)
+    (1, 2, 1, 1, 0.5, 0.0, 0.0),
+    (2, 3, 1, 2, 0.7, 0.0, 0.0),
+    (3, 10, 4, 3, 0.5, 0.0, 0.0),
+    (4, 25, 4, 5, 0.4, 0.0, 0.0),
+    (5, 25, 4, 5, 0.9, -0.05, 0.0),
+    (6, 16, 2, 2, 0.6, 0.0, 0.3),
+    (7, 16, 4, 4, 0.6, 0.0, np.inf),
+    (8, 40, 1, 7, 0.3, 0.02, 0.0),
+    (9, 30, 4, 1, 0.2, 0.0, 0.0),
+    (10, 60, 4, 6, 0.5, 0.0, 0.0),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"s{c[0]}" for c in CASES])
+def test_match2nd_bit_exact_vs_restatement(case):
+    seed, frames, points, nong, density, occ, bam = case
+    rng = np.random.default_rng(seed)
+    unary, pairwise = random_problem(rng, frames, points, nong, density=density)
+    perm = list(rng.permutation(points))
+    ref = TO.match2nd(as_oracle_unary(unary), pairwise, nong, occ, bam, frames, points, perm)
+    got = TR.match2nd(unary, pairwise, nong=nong, points=points, perm=perm, occ_cost=occ, bam=bam)
+    assert got.tolist() == ref
+    if points == 4:
+        lab, cost = TR.match2nd(unary, pairwise, nong=nong, points=4, perm=perm, occ_cost=occ, bam=bam,
+                                with_cost=True)
+        assert cost == TO.compute_cost_track(ref, as_oracle_unary(unary), perm)
+
+
+def test_malformed_inputs_give_zero_labels():
+    """match2nd.cpp:24-27, :46-49, :83-100: the reference returns zeros."""
+    rng = np.random.default_rng(0)
+    unary, pairwise = random_problem(rng, 5, 4, 2, empty_frames=False)
+    one = TR.match2nd(unary[:1], [], nong=2, points=4, perm=[0, 1, 2, 3])
+    assert one.shape == (4, 1) and not one.any()
+    assert TO.match2nd(as_oracle_unary(unary[:1]), [], 2, 0.0, 0.0, 1, 4, [0, 1, 2, 3]) == [[0]] * 4
+    bad = list(pairwise)
+    r, c, jc, ir, pr = bad[2]
+    bad[2] = (r + 1, c, jc, ir, pr)  # a pairwise matrix one row too tall
+    got = TR.match2nd(unary, bad, nong=2, points=4, perm=[0, 1, 2, 3])
+    assert not got.any()
+    assert TO.match2nd(as_oracle_unary(unary), bad, 2, 0.0, 0.0, 5, 4, [0, 1, 2, 3]) == [[0] * 5] * 4
+    three = [u[:, :3] for u in unary]  # unary columns != points
+    assert not TR.match2nd(three, pairwise, nong=2, points=4, perm=[0, 1, 2, 2]).any()
+
+
+def test_invalid_arrays_are_rejected():
+    rng = np.random.default_rng(1)
+    unary, pairwise = random_problem(rng, 4, 1, 2, empty_frames=False)
+    r, c, jc, ir, pr = pairwise[1]
+    broken = list(pairwise)
+    broken[1] = (r, c, jc, [r + 5] + ir[1:], pr)  # row index out of range
+    with pytest.raises(TR.TrackError) as e:
+        TR.match2nd(unary, broken, nong=2, points=1, perm=[0])
+    assert e.value.code == abi.LM_ERR_INVALID_ARGUMENT
+    with pytest.raises(TR.TrackError):
+        TR.match2nd(unary, pairwise, nong=2, points=1, perm=[1])
+
+
+def test_cost_track_label_minus_one_reads_the_previous_column():
+    """computeCostTrack's MyMat::get(unsigned) with label -1: element
+    perm*rows - 1 when that is inside the matrix (match2nd.cpp:180-183)."""
+    u = [(3, 4, [float(i) for i in range(12)])] * 2
+    M = [[0, 1], [-1, 2], [5, 0], [1, 1]]
+    c = TO.compute_cost_track(M, u, (3, 2, 1, 0))
+    # t0 col3: 9 + 10; t1 col2: idx 5 + 8; t2 col1: occluded + 3; t3 col0: 1 + 1
+    assert c == 9 + 10 + 5 + 8 + 0 + 3 + 1 + 1
+    with pytest.raises(TO.TrackError):
+        TO.compute_cost_track([[-1, 0]] * 4, u, (0, 1, 2, 3))
+
+
+def _video(n, **kw):
+    cfg = S.SyntheticConfig(**kw)
+    frames = cfg.frames(0, n)
+    res = O.OracleRun(cfg, frames).result
+    g = O.geometry(cfg)
+    p = cfg.params
+    corner = [p.bounding_box_bottom.x + p.bounding_box_bottom.width,
+              p.bounding_box_bottom.y + p.bounding_box_bottom.height,
+              p.bounding_box_side.y + p.bounding_box_side.height]
+    bb = np.tile(np.array(corner, np.uint32), (n, 1))
+    return cfg, res, g, bb
+
+
+def _compare(ref, got):
+    assert got["track_index_bottom"].tolist() == ref["track_index_paw_bottom"] + ref["track_index_snout_bottom"]
+    assert got["track_index_side"].tolist() == ref["track_index_paw_side"] + ref["track_index_snout_side"]
+    for k in ("paw_tracks", "snout_tracks", "tracks_tail"):
+        assert np.array_equal(got[k], np.array(ref[k], np.int32)), k
+
+
+@pytest.mark.parametrize("kw", [{}, {"flip": True}, {"method": 1}], ids=["R", "L", "TM"])
+def test_video_tracks_match_restatement(kw):
+    """Detection results of the oracle on the synthetic video (40 frames) ->
+    lm_compute_tracks vs the restated computeBottomTracks / computeSideTracks /
+    exportResults."""
+    n = 40
+    cfg, res, g, bb = _video(n, **kw)
+    ref = TO.run_tracks(res, g, cfg.params, bb.tolist(), n)
+    got = TR.compute_tracks(res, g, cfg.params, bb)
+    _compare(ref, got)
+    # the synthetic paws are visible in every frame: each paw track holds a
+    # bottom-view position in most frames
+    assert (got["paw_tracks"][:, :, 0] >= 0).mean() > 0.8
+
+
+def test_video_tracks_with_varying_corners():
+    """Per-frame bottom-right corners (a computed box) shift the exported
+    coordinates frame by frame."""
+    n = 12
+    cfg, res, g, bb = _video(n)
+    bb = bb.astype(np.int64)
+    bb[:, 0] += np.arange(n) % 3
+    bb[:, 2] -= np.arange(n) % 2
+    bb = bb.astype(np.uint32)
+    ref = TO.run_tracks(res, g, cfg.params, bb.tolist(), n)
+    got = TR.compute_tracks(res, g, cfg.params, bb)
+    _compare(ref, got)
+
+
+def test_track_yaml(tmp_path):
+    n = 6
+    cfg, res, g, bb = _video(n)
+    t = TR.compute_tracks(res, g, cfg.params, bb)
+    path = tmp_path / "output_synth.yml"
+    TR.write_yaml(str(path), t)
+    text = path.read_text()
+    assert text.startswith("%YAML:1.0\n---\n")
+    names = re.findall(r"^(\w+): !!opencv-matrix", text, flags=re.M)
+    assert names == ["paw_tracks0", "paw_tracks1", "paw_tracks2", "paw_tracks3", "snout_tracks0", "tracks_tail"]
+    blocks = re.findall(r"rows: (\d+)\n\s+cols: (\d+)\n\s+dt: i\n\s+data: \[([^\]]*)\]", text)
+    want = [t["paw_tracks"][i] for i in range(4)] + [t["snout_tracks"][0], t["tracks_tail"]]
+    for (rows, cols, data), w in zip(blocks, want):
+        vals = np.array([int(v) for v in data.replace("\n", " ").split(",")], np.int32)
+        assert (int(rows), int(cols)) == w.shape
+        assert np.array_equal(vals, w.reshape(-1))
+
+
+def test_track_header_exports_and_layout(tmp_path):
+    text = re.sub(r"/\*.*?\*/", "", open(HDR).read(), flags=re.S)
+    names = sorted(set(re.findall(r"^[A-Za-z_][\w\s\*]*?\b(lm_\w+)\s*\(", text, flags=re.M)))
+    assert set(names) == set(TR.EXPORTED)
+    L = TR.lib()
+    for name in names:
+        assert getattr(L, name) is not None
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "locomouse_track.h"\nint main(void){printf("%zu", sizeof(lm_tracks));}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I" + os.path.dirname(HDR), str(src), "-o", str(exe)])
+    assert int(subprocess.check_output([str(exe)])) == C.sizeof(abi.lm_tracks)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [7, 32])
+def test_host_class_tracks_match_oracle(tmp_path, batch):
+    """The host LocoMouse mirror through main.cpp's whole sequence on the GPU
+    (per-frame loop, computeBottomTracks, computeSideTracks, exportResults with
+    the YAML output) against the oracle's detection + the restated tracker."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import host_harness as H
+    n = 48
+    cfg, res_ref, g, bb = _video(n)
+    out = tmp_path / "output_video.yml"
+    res, t, corners = H.run_video_tracks(cfg, cfg.frames(0, n), batch=batch, output_file=str(out))
+    assert np.array_equal(corners, bb)
+    ref = TO.run_tracks(res_ref, g, cfg.params, bb.tolist(), n)
+    _compare(ref, t)
+    again = tmp_path / "again.yml"
+    TR.write_yaml(str(again), t)
+    assert out.read_text() == again.read_text()
