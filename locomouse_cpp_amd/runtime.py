@@ -31,6 +31,7 @@ HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
 
 HOST_DIR = os.path.join(PKG, "host")
 HOST_LIB_PATH = os.path.join(PKG, "liblocomouse_host.so")
+CLI_PATH = os.path.join(PKG, "bin", "LocoMouse")
 
 
 def build(verbose=False):
@@ -48,10 +49,19 @@ def build(verbose=False):
 def build_host(verbose=False):
     """liblocomouse_host.so: the LocoMouse / Candidate / P22D / MyMat C++
     surface (locomouse_cpp_amd/host) linked against the C-ABI library."""
-    srcs = [os.path.join(HOST_DIR, f) for f in ("LocoMouse.cpp", "Tracks.cpp", "match2nd.cpp")]
-    cmd = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", "-Wextra",
-           "-I" + os.path.join(ROOT, "include"), "-I" + HOST_DIR, "-o", HOST_LIB_PATH, *srcs, "-L" + PKG,
-           "-llocomouse_hip", "-Wl,-rpath,$ORIGIN"]
+    srcs = [os.path.join(HOST_DIR, f)
+            for f in ("LocoMouse.cpp", "Tracks.cpp", "match2nd.cpp", "FileStorage.cpp", "Media.cpp")]
+    flags = ["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wextra", "-I" + os.path.join(ROOT, "include"),
+             "-I" + HOST_DIR]
+    cmd = [*flags, "-fPIC", "-shared", "-o", HOST_LIB_PATH, *srcs, "-L" + PKG, "-llocomouse_hip", "-lz",
+           "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    # the reference's command-line program (main.cpp), SURVEY.md §8(f) row 2
+    os.makedirs(os.path.dirname(CLI_PATH), exist_ok=True)
+    cmd = [*flags, "-o", CLI_PATH, os.path.join(HOST_DIR, "Cli.cpp"), "-L" + PKG, "-llocomouse_host",
+           "-llocomouse_hip", "-Wl,-rpath,$ORIGIN/.."]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

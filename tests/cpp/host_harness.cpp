@@ -9,7 +9,9 @@
 #include <string>
 #include <vector>
 
+#include "FileStorage.hpp"
 #include "LocoMouse.hpp"
+#include "Media.hpp"
 
 namespace {
 
@@ -216,5 +218,64 @@ extern "C" int lmh_selftest(char* err, int errlen) {
     return 0;
   } catch (const std::exception& e) {
     return fail(e, 2, err, errlen);
+  }
+}
+
+// Readers behind the CLI (Media.hpp, FileStorage.hpp), CPU only.
+extern "C" int lmh_read_png(const char* path, int* rows, int* cols, uint8_t* out, int64_t cap) {
+  std::vector<uint8_t> px;
+  if (!locomouse::read_png_gray(path, *rows, *cols, px)) return 1;
+  if ((int64_t)px.size() > cap) return 2;
+  std::memcpy(out, px.data(), px.size());
+  return 0;
+}
+
+extern "C" int lmh_read_avi(const char* path, int* rows, int* cols, int* n, uint8_t* out, int64_t cap, int rewind_at) {
+  locomouse::AviReader r;
+  if (!r.open(path)) return 1;
+  *rows = r.rows();
+  *cols = r.cols();
+  *n = (int)r.frame_count();
+  const int64_t fb = (int64_t)r.rows() * r.cols();
+  int64_t k = 0;
+  for (int i = 0;; ++i) {
+    if (i == rewind_at) r.rewind();
+    if ((k + 1) * fb > cap) break;
+    if (!r.read(out + k * fb)) break;
+    ++k;
+  }
+  return -(int)k;  // frames read, as a non-positive number
+}
+
+// A matrix or scalar of a FileStorage file: kind, dims and values (doubles).
+extern "C" int lmh_fs_node(const char* path, const char* key, int* kind, int* rows, int* cols, char* dt, double* out,
+                           int64_t cap, char* text, int textlen) {
+  try {
+    locomouse::FsNode root;
+    if (!locomouse::read_file_storage(path, root)) return 1;
+    const locomouse::FsNode& n = root[key];
+    *kind = (int)n.kind;
+    *rows = *cols = 0;
+    if (n.kind == locomouse::FsNode::MAT) {
+      *rows = n.mat.rows;
+      *cols = n.mat.cols;
+      *dt = n.mat.dt;
+      if ((int64_t)n.mat.v.size() > cap) return 2;
+      std::copy(n.mat.v.begin(), n.mat.v.end(), out);
+    } else if (n.kind == locomouse::FsNode::INT || n.kind == locomouse::FsNode::REAL) {
+      out[0] = n.to_double();
+      out[1] = n.to_int();
+    } else if (n.kind == locomouse::FsNode::STR) {
+      std::strncpy(text, n.s.c_str(), (size_t)textlen - 1);
+      text[textlen - 1] = 0;
+    } else if (n.kind == locomouse::FsNode::SEQ) {
+      *rows = (int)n.seq.size();
+      for (size_t i = 0; i < n.seq.size() && (int64_t)i < cap; ++i) out[i] = n.seq[i].to_double();
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    std::strncpy(text, e.what(), (size_t)textlen - 1);
+    text[textlen - 1] = 0;
+    return 3;
   }
 }

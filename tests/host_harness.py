@@ -36,6 +36,10 @@ def lib():
                               C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_int]
         L.lmh_run.restype = C.c_int
         L.lmh_set_output.argtypes = [C.c_char_p]
+        L.lmh_read_png.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+        L.lmh_read_avi.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int]
+        L.lmh_fs_node.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                  C.c_int64, C.c_char_p, C.c_int]
         L.lmh_get_tracks.argtypes = [C.c_int] + [C.c_void_p] * 5
         L.lmh_selftest.argtypes = [C.c_char_p, C.c_int]
         L.lmh_selftest.restype = C.c_int
