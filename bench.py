@@ -85,6 +85,35 @@ def cpu_baseline(cfg, seconds=10.0, max_frames=2000):
             "cpu": cpu}
 
 
+def cpu_baseline_threads(cfg, seconds=8.0, threads=None):
+    """The fair CPU baseline of SURVEY.md §8(d)(ii): the oracle on T host
+    threads, each on its own contiguous 50-frame chunks (frame-sharded like
+    the multi-GPU path; ctypes releases the GIL inside the oracle call)."""
+    import threading
+    from oracle import oracle as O
+    if threads is None:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    chunk = 50
+    samples = [cfg.frames(chunk * t, chunk) for t in range(threads)]
+    counts = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(t):
+        while time.perf_counter() < stop:
+            O.OracleRun(cfg, samples[t])
+            counts[t] += chunk
+
+    t0 = time.perf_counter()
+    pool = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for th in pool:
+        th.start()
+    for th in pool:
+        th.join()
+    el = time.perf_counter() - t0
+    return {"value": sum(counts) / el, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{sum(counts)} frames, {threads} threads x chunks of {chunk} frames, {el:.1f} s wall"}
+
+
 def run_bb(args):
     """The whole-video bounding-box pass (lm_bb_push_device, method 0) on one
     GPU: frames resident in HBM, `--steps` pushes of `--batch` frames after
@@ -301,6 +330,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        out["cpu_baseline_threads"] = cpu_baseline_threads(cfg, min(8.0, args.cpu_seconds))
     if rank == 0:
         print(json.dumps(out), flush=True)
     for c in ctxs:
