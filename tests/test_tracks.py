@@ -276,3 +276,28 @@ def test_host_class_tracks_match_oracle(tmp_path, batch):
     again = tmp_path / "again.yml"
     TR.write_yaml(str(again), t)
     assert out.read_text() == again.read_text()
+
+
+@pytest.mark.parametrize("case", ["one_frame", "blank"])
+def test_video_tracks_edge_cases(case):
+    """A one-frame video (match2nd returns zeros, match2nd.cpp:24-27, and the
+    zero labels are exported as candidate 0) and a video without any
+    candidate (every track occluded: -1 everywhere)."""
+    n = 1 if case == "one_frame" else 6
+    cfg = S.SyntheticConfig()
+    frames = cfg.frames(0, n) if case == "one_frame" else np.repeat(cfg.background[None], n, axis=0)
+    res = O.OracleRun(cfg, frames).result
+    g = O.geometry(cfg)
+    p = cfg.params
+    corner = [p.bounding_box_bottom.x + p.bounding_box_bottom.width,
+              p.bounding_box_bottom.y + p.bounding_box_bottom.height,
+              p.bounding_box_side.y + p.bounding_box_side.height]
+    bb = np.tile(np.array(corner, np.uint32), (n, 1))
+    ref = TO.run_tracks(res, g, p, bb.tolist(), n)
+    got = TR.compute_tracks(res, g, p, bb)
+    _compare(ref, got)
+    if case == "blank":
+        assert int(res["cand_offset"][-1]) == 0
+        assert (got["paw_tracks"] == -1).all() and (got["tracks_tail"] == -1).all()
+    else:
+        assert (got["track_index_bottom"] == 0).all()
