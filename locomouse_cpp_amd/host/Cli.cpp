@@ -11,6 +11,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <thread>
 #include <cstdlib>
 #include <iostream>
 #include <sstream>
@@ -94,6 +98,82 @@ ParsedInputs parse_inputs(int argc, char** argv) {
   in.BB_BOTTOM_VIEW = lm_rect{(int)V.v[4], (int)V.v[5], (int)V.v[6], (int)V.v[7]};
   return in;
 }
+
+// V >> F with read-ahead: worker threads decode the next frames (independent
+// chunks of the file) into a ring while the per-frame loop and the GPU
+// batches run, so file reads and channel extraction overlap detection.
+class FramePrefetcher {
+ public:
+  FramePrefetcher(std::shared_ptr<AviReader> v, int threads, size_t depth)
+      : V(std::move(v)), T(threads), D(depth), FB((size_t)V->rows() * V->cols()), ring(D * FB), state(D, -1) {
+    start();
+  }
+  ~FramePrefetcher() { stop(); }
+
+  bool read(uint8_t* dst) {
+    std::unique_lock<std::mutex> lk(m);
+    if (cur >= V->frame_count()) return false;
+    const size_t s = cur % D;
+    cv.wait(lk, [&] { return state[s] == (long long)cur || state[s] == -2 - (long long)cur; });
+    if (state[s] != (long long)cur) return false;  // decode failed
+    lk.unlock();
+    std::memcpy(dst, ring.data() + s * FB, FB);
+    lk.lock();
+    ++cur;
+    cv.notify_all();
+    return true;
+  }
+
+  void rewind() {  // V.set(CV_CAP_PROP_POS_FRAMES, 0)
+    stop();
+    start();
+  }
+
+ private:
+  std::shared_ptr<AviReader> V;
+  const int T;
+  const size_t D, FB;
+  std::vector<uint8_t> ring;
+  std::vector<long long> state;  // frame held by a slot, -2-frame on failure, -1 none
+  std::vector<std::thread> pool;
+  std::mutex m;
+  std::condition_variable cv;
+  size_t cur = 0, next = 0;
+  bool stopping = false;
+
+  void start() {
+    cur = next = 0;
+    stopping = false;
+    std::fill(state.begin(), state.end(), -1);
+    for (int t = 0; t < T; ++t) pool.emplace_back([this] { work(); });
+  }
+  void stop() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      stopping = true;
+    }
+    cv.notify_all();
+    for (auto& th : pool) th.join();
+    pool.clear();
+  }
+  void work() {
+    for (;;) {
+      size_t i;
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return stopping || next >= V->frame_count() || next < cur + D; });
+        if (stopping || next >= V->frame_count()) return;
+        i = next++;
+      }
+      const bool ok = V->read_at(i, ring.data() + (i % D) * FB);
+      {
+        std::lock_guard<std::mutex> lk(m);
+        state[i % D] = ok ? (long long)i : -2 - (long long)i;
+      }
+      cv.notify_all();
+    }
+  }
+};
 
 // LocoMouse_Parameters (LocoMouse_class.cpp:4-249): keys in the reference's
 // order, its messages, OpenCV's missing-key-reads-0 semantics.
@@ -257,8 +337,12 @@ int run(int argc, char** argv) {
   li.setup.view_box_side = in.BB_SIDE_VIEW;
   li.setup.view_box_bottom = in.BB_BOTTOM_VIEW;
   li.model = model.m;
-  li.read_frame = [video](uint8_t* dst) { return video->read(dst); };
-  li.rewind = [video] { video->rewind(); };
+  const size_t fbytes = (size_t)video->rows() * video->cols();
+  const int threads = std::max(1, std::min(8, (int)std::thread::hardware_concurrency() - 1));
+  auto reader = std::make_shared<FramePrefetcher>(
+      video, threads, std::max<size_t>(64, std::min<size_t>(1024, ((size_t)256 << 20) / std::max<size_t>(fbytes, 1))));
+  li.read_frame = [reader](uint8_t* dst) { return reader->read(dst); };
+  li.rewind = [reader] { reader->rewind(); };
   li.output_file = in.OUTPUT_PATH + "/output_" + in.FILE_STEM + ".yml";
   if (const char* d = std::getenv("LM_DEVICE")) li.device = std::atoi(d);
   if (const char* b = std::getenv("LM_BATCH")) li.batch = std::max(1, std::atoi(b));

@@ -145,6 +145,7 @@ LocoMouse::LocoMouse(const LocoMouse_Inputs& inputs) : IN(inputs), METHOD(0), N_
 }
 
 LocoMouse::~LocoMouse() {
+  if (INFLIGHT.valid()) INFLIGHT.wait();  // its errors die with the object
   if (CTX) lm_ctx_destroy(CTX);
 }
 
@@ -215,6 +216,7 @@ void LocoMouse::initializeFeatureLoop() {
   IN.setup.method = METHOD;
   throw_on_error(lm_ctx_create(IN.device, &IN.setup, &IN.params, &IN.model, IN.batch, &CTX));
   PENDING.assign(FRAME_BYTES * (size_t)IN.batch, 0);
+  SUBMITTED.assign(FRAME_BYTES * (size_t)IN.batch, 0);
   N_PENDING = 0;
 }
 
@@ -248,6 +250,13 @@ void LocoMouse::storePreviousImage() {
 
 void LocoMouse::sync() {
   if (N_PENDING) flush();
+  wait_inflight();
+}
+
+// Rethrows (once) what the background batch threw: the reference's exception
+// surfaces at the next per-frame call that hands over a batch, or at sync().
+void LocoMouse::wait_inflight() {
+  if (INFLIGHT.valid()) INFLIGHT.get();
 }
 
 lm_geometry LocoMouse::geometry() const {
@@ -257,7 +266,12 @@ lm_geometry LocoMouse::geometry() const {
   return g;
 }
 
+// A full batch goes to the device on a helper thread (std::async) while the
+// caller reads the next frames into the other buffer; the context is used by
+// one batch at a time (the previous one is waited for first) and results are
+// appended in frame order before that wait returns.
 void LocoMouse::flush() {
+  wait_inflight();
   const int n = N_PENDING, first = CURRENT_FRAME + 1 - n;
   std::vector<int32_t> bb((size_t)3 * n);
   for (int i = 0; i < n; ++i) {
@@ -265,10 +279,13 @@ void LocoMouse::flush() {
     bb[3 * i + 1] = (int32_t)BB_Y_BOTTOM_POS[first + i];
     bb[3 * i + 2] = (int32_t)BB_Y_SIDE_POS[first + i];
   }
-  lm_batch_result r{};
-  throw_on_error(lm_detect_batch(CTX, PENDING.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data(), &r));
+  PENDING.swap(SUBMITTED);
   N_PENDING = 0;
-  append(r);
+  INFLIGHT = std::async(std::launch::async, [this, n, first, bb = std::move(bb)] {
+    lm_batch_result r{};
+    throw_on_error(lm_detect_batch(CTX, SUBMITTED.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data(), &r));
+    append(r);
+  });
 }
 
 // After the loop (main.cpp:86-91): the tracker over the containers above.

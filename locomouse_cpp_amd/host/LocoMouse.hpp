@@ -29,6 +29,7 @@
 #include <array>
 #include <cstdint>
 #include <functional>
+#include <future>
 #include <memory>
 #include <string>
 #include <vector>
@@ -137,9 +138,12 @@ class LocoMouse : protected FrameResults {
   void runBoundingBoxPass(int method);  // lm_bb_* over the whole video, then rewind
  private:
   std::vector<uint8_t> PENDING;  // raw frames read but not yet processed
+  std::vector<uint8_t> SUBMITTED;  // the batch being processed by INFLIGHT
+  std::future<void> INFLIGHT;      // lm_detect_batch + append of the previous batch
   int N_PENDING = 0;
   size_t FRAME_BYTES = 0;
   void flush();
+  void wait_inflight();
 };
 
 // LocoMouse_TM (LocoMouse_TM.hpp:30-55): readFrame adds imadjust

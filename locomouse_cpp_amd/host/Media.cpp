@@ -8,6 +8,8 @@
 #include <cstring>
 #include <fstream>
 
+#include <unistd.h>
+
 namespace locomouse {
 
 namespace {
@@ -177,24 +179,44 @@ bool AviReader::open(const std::string& path) {
 
 bool AviReader::read(uint8_t* channel0) {
   if (!f_ || next_ >= frames_.size()) return false;
-  const auto fr = frames_[next_++];
+  return read_at(next_++, channel0);
+}
+
+bool AviReader::read_at(size_t index, uint8_t* channel0) const {
+  if (!f_ || index >= frames_.size()) return false;
+  const auto fr = frames_[index];
   const size_t bpp = (size_t)bits_ / 8, stride = ((size_t)width_ * bpp + 3) & ~(size_t)3;
   const size_t tight = (size_t)width_ * bpp;
   const bool padded = fr.second >= stride * (size_t)height_;
   const size_t row_bytes = padded ? stride : tight;
   if (fr.second < row_bytes * (size_t)height_) return false;
-  buf_.resize(row_bytes * (size_t)height_);
-  std::fseek(f_, fr.first, SEEK_SET);
-  if (std::fread(buf_.data(), 1, buf_.size(), f_) != buf_.size()) return false;
+  const bool direct = bpp == 1 && palette_blue_.empty() && !bottom_up_ && row_bytes == (size_t)width_;
+  thread_local std::vector<uint8_t> buf;
+  uint8_t* data = channel0;
+  if (!direct) {
+    buf.resize(row_bytes * (size_t)height_);
+    data = buf.data();
+  }
+  const size_t want = row_bytes * (size_t)height_;
+  for (size_t got = 0; got < want;) {
+    const ssize_t r = pread(fileno(f_), data + got, want - got, (off_t)(fr.first + (long)got));
+    if (r <= 0) return false;
+    got += (size_t)r;
+  }
+  if (direct) return true;
+  bool identity = !palette_blue_.empty();
+  for (int k = 0; identity && k < 256; ++k) identity = palette_blue_[k] == k;
   for (int y = 0; y < height_; ++y) {
-    const uint8_t* src = &buf_[(size_t)(bottom_up_ ? height_ - 1 - y : y) * row_bytes];
+    const uint8_t* src = data + (size_t)(bottom_up_ ? height_ - 1 - y : y) * row_bytes;
     uint8_t* dst = channel0 + (size_t)y * width_;
-    if (bpp == 3)
+    if (bpp == 3) {
       for (int x = 0; x < width_; ++x) dst[x] = src[3 * x];  // B of BGR
-    else if (!palette_blue_.empty())
-      for (int x = 0; x < width_; ++x) dst[x] = palette_blue_[src[x]];
-    else
-      std::memcpy(dst, src, (size_t)width_);
+    } else if (!palette_blue_.empty() && !identity) {
+      const uint8_t* lut = palette_blue_.data();
+      for (int x = 0; x < width_; ++x) dst[x] = lut[src[x]];
+    } else {
+      std::memcpy(dst, src, (size_t)width_);  // grey, or a palette whose blue is the index
+    }
   }
   return true;
 }

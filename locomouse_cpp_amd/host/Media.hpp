@@ -38,6 +38,9 @@ class AviReader {
   uint32_t frame_count() const { return (uint32_t)frames_.size(); }  // CAP_PROP_FRAME_COUNT
   bool read(uint8_t* channel0);        // V >> F + extractChannel(F, F, 0); false at the end
   void rewind() { next_ = 0; }         // V.set(CV_CAP_PROP_POS_FRAMES, 0)
+  // Frame `index` (0-based) without moving the read position; safe to call
+  // from several threads at once (pread on the file descriptor).
+  bool read_at(size_t index, uint8_t* channel0) const;
 
  private:
   std::FILE* f_ = nullptr;
@@ -46,7 +49,6 @@ class AviReader {
   std::vector<uint8_t> palette_blue_;  // 8-bit palettised: blue of each entry
   std::vector<std::pair<long, uint32_t>> frames_;  // (file offset, size) of each frame chunk
   size_t next_ = 0;
-  std::vector<uint8_t> buf_;
 };
 
 }  // namespace locomouse
