@@ -386,6 +386,7 @@ int run(int argc, char** argv) {
     std::fclose(f);
   }
 
+  const auto t_start = std::chrono::steady_clock::now();
   std::unique_ptr<LocoMouse> L = LocoMouse_Initialize(li);  // main.cpp:45-91
   L->getBoundingBox();
   L->initializeFeatureLoop();
@@ -400,9 +401,16 @@ int run(int argc, char** argv) {
     L->matchBottomSideCandidates();
     L->storePreviousImage();
   }
+  const auto t_loop = std::chrono::steady_clock::now();
   L->computeBottomTracks();
   L->computeSideTracks();
+  const auto t_tracks = std::chrono::steady_clock::now();
   L->exportResults();
+  if (std::getenv("LM_TIMING")) {  // stage times (not in the reference)
+    const auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::cout << "LM_TIMING loop_ms " << ms(t_start, t_loop) << " tracks_ms " << ms(t_loop, t_tracks) << " export_ms "
+              << ms(t_tracks, std::chrono::steady_clock::now()) << std::endl;
+  }
   return EXIT_SUCCESS;
 }
 

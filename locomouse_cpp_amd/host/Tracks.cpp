@@ -2,9 +2,12 @@
 // results it reproduces.
 #include "Tracks.hpp"
 
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <fstream>
+#include <future>
 #include <stdexcept>
 
 namespace locomouse {
@@ -75,12 +78,21 @@ static void check_frames(const FrameResults& R, const TrackSetup& S) {
 // from -1 — wins, and its rows are put back in paw order.
 void computeBottomTracks(const FrameResults& R, const TrackSetup& S, TrackResults& out) {
   check_frames(R, S);
+  // The four orders and the snout are independent match2nd problems: solved
+  // concurrently, then compared in the reference's order (strict >).
+  std::future<IntMat> runs[LM_N_PAWS];
+  for (int ip = 0; ip < LM_N_PAWS; ++ip)
+    runs[ip] = std::async(std::launch::async, [&R, &S, ip] {
+      return match2nd(R.UNARY_BOTTOM_PAW, R.PAIRWISE_BOTTOM_PAW, S.nong_bottom, 0, 0, S.n_frames, LM_N_PAWS,
+                      PAW_ORDERS[ip]);
+    });
+  const int zero = 0;
+  IntMat snout = match2nd(R.UNARY_BOTTOM_SNOUT, R.PAIRWISE_BOTTOM_SNOUT, S.nong_bottom, 0, 0, S.n_frames, 1, &zero);
   double current_cost = -1;
   int current_perm = 0;
   IntMat best;
   for (int ip = 0; ip < LM_N_PAWS; ++ip) {
-    IntMat M = match2nd(R.UNARY_BOTTOM_PAW, R.PAIRWISE_BOTTOM_PAW, S.nong_bottom, 0, 0, S.n_frames, LM_N_PAWS,
-                        PAW_ORDERS[ip]);
+    IntMat M = runs[ip].get();
     const double c = computeCostTrack(M, R.UNARY_BOTTOM_PAW, R.PAIRWISE_BOTTOM_PAW, PAW_ORDERS[ip]);
     if (c > current_cost) {
       current_perm = ip;
@@ -94,9 +106,7 @@ void computeBottomTracks(const FrameResults& R, const TrackSetup& S, TrackResult
   for (int r = 0; r < LM_N_PAWS; ++r)
     std::copy(best.row(r), best.row(r) + best.cols, T.row(PAW_ORDERS[current_perm][r]));
   out.TRACK_INDEX_PAW_BOTTOM = std::move(T);
-  const int zero = 0;
-  out.TRACK_INDEX_SNOUT_BOTTOM =
-      match2nd(R.UNARY_BOTTOM_SNOUT, R.PAIRWISE_BOTTOM_SNOUT, S.nong_bottom, 0, 0, S.n_frames, 1, &zero);
+  out.TRACK_INDEX_SNOUT_BOTTOM = std::move(snout);
 }
 
 // :2073-2150.  D is (|Zip1| + Nong) x (|Zi| + Nong): candidate -> nearest side
@@ -329,8 +339,17 @@ lm_status lm_compute_tracks(const lm_batch_result* video, const lm_geometry* geo
     using namespace locomouse;
     if (!video || !geometry || !params || !bb || !out) throw std::invalid_argument("lm_compute_tracks: NULL argument.");
     if (video->first_frame != 0) throw std::invalid_argument("lm_compute_tracks: results must start at frame 0.");
+    const bool timing = std::getenv("LM_TRACK_TIMING") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+      if (!timing) return;
+      const auto t1 = std::chrono::steady_clock::now();
+      std::fprintf(stderr, "lm_compute_tracks %s: %.3f ms\n", what, std::chrono::duration<double, std::milli>(t1 - t0).count());
+      t0 = t1;
+    };
     FrameResults R;
     R.append(*video);
+    lap("containers");
     const unsigned N = (unsigned)video->n_frames;
     std::vector<uint32_t> bx(N), byb(N), bys(N);
     for (unsigned f = 0; f < N; ++f) {
@@ -344,8 +363,11 @@ lm_status lm_compute_tracks(const lm_batch_result* video, const lm_geometry* geo
     S.bb_y_side_pos = &bys;
     TrackResults T;
     computeBottomTracks(R, S, T);
+    lap("bottom tracks");
     computeSideTracks(R, S, T);
+    lap("side tracks");
     exportTracks(R, S, T);
+    lap("export");
     t_tracks = std::move(T);
     t_paw.clear();
     for (const auto& m : t_tracks.paw_tracks) t_paw.insert(t_paw.end(), m.data.begin(), m.data.end());

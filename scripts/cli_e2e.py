@@ -28,16 +28,18 @@ def main(n=2000, bits=8):
         runs = []
         for _ in range(2):
             t0 = time.perf_counter()
-            p = subprocess.run(args, capture_output=True, text=True, timeout=600)
+            p = subprocess.run(args, capture_output=True, text=True, timeout=600, env=dict(os.environ, LM_TIMING="1"))
             runs.append(time.perf_counter() - t0)
             if p.returncode:
                 print(p.stdout, p.stderr)
                 sys.exit(p.returncode)
         size = os.path.getsize(paths["video"])
+        stages = [line.split()[1:] for line in p.stdout.splitlines() if line.startswith("LM_TIMING")]
+        stages = {k: float(v) for k, v in zip(stages[0][::2], stages[0][1::2])} if stages else {}
     best = min(runs)
     print(json.dumps({"what": "LocoMouse CLI end to end (uncompressed AVI -> output yml)", "frames": n, "bits": bits,
                       "video_bytes": size, "seconds": [round(r, 3) for r in runs],
-                      "frames_per_s": round(n / best, 1), "input_write_s": round(t_write, 1),
+                      "frames_per_s": round(n / best, 1), "last_run_stages_ms": stages, "input_write_s": round(t_write, 1),
                       "note": "includes process start, HIP init, file reads, H2D, detection, tracker, YAML"}))
 
 
