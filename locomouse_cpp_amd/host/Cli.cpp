@@ -11,9 +11,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
-#include <condition_variable>
+#include <atomic>
 #include <cstring>
-#include <mutex>
 #include <thread>
 #include <cstdlib>
 #include <iostream>
@@ -99,80 +98,37 @@ ParsedInputs parse_inputs(int argc, char** argv) {
   return in;
 }
 
-// V >> F with read-ahead: worker threads decode the next frames (independent
-// chunks of the file) into a ring while the per-frame loop and the GPU
-// batches run, so file reads and channel extraction overlap detection.
-class FramePrefetcher {
+// V >> F in video order; a whole batch at a time is decoded straight into
+// the caller's batch buffer by worker threads (pread at each frame's offset
+// in the file), so decoding is parallel and costs no extra copy.
+class VideoFrames {
  public:
-  FramePrefetcher(std::shared_ptr<AviReader> v, int threads, size_t depth)
-      : V(std::move(v)), T(threads), D(depth), FB((size_t)V->rows() * V->cols()), ring(D * FB), state(D, -1) {
-    start();
+  VideoFrames(std::shared_ptr<AviReader> v, int threads)
+      : V(std::move(v)), T(threads), FB((size_t)V->rows() * V->cols()) {}
+  bool read(uint8_t* dst) { return pos < V->frame_count() && V->read_at(pos++, dst); }
+  int read(uint8_t* dst, int n) {
+    n = (int)std::min<size_t>((size_t)std::max(n, 0), V->frame_count() - pos);
+    std::vector<char> ok((size_t)n, 0);
+    std::atomic<int> next{0};
+    auto work = [&] {
+      for (int i; (i = next++) < n;) ok[i] = V->read_at(pos + (size_t)i, dst + (size_t)i * FB) ? 1 : 0;
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < std::min(T, n); ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    int got = 0;
+    while (got < n && ok[got]) ++got;
+    pos += (size_t)got;
+    return got;
   }
-  ~FramePrefetcher() { stop(); }
-
-  bool read(uint8_t* dst) {
-    std::unique_lock<std::mutex> lk(m);
-    if (cur >= V->frame_count()) return false;
-    const size_t s = cur % D;
-    cv.wait(lk, [&] { return state[s] == (long long)cur || state[s] == -2 - (long long)cur; });
-    if (state[s] != (long long)cur) return false;  // decode failed
-    lk.unlock();
-    std::memcpy(dst, ring.data() + s * FB, FB);
-    lk.lock();
-    ++cur;
-    cv.notify_all();
-    return true;
-  }
-
-  void rewind() {  // V.set(CV_CAP_PROP_POS_FRAMES, 0)
-    stop();
-    start();
-  }
+  void rewind() { pos = 0; }  // V.set(CV_CAP_PROP_POS_FRAMES, 0)
 
  private:
   std::shared_ptr<AviReader> V;
   const int T;
-  const size_t D, FB;
-  std::vector<uint8_t> ring;
-  std::vector<long long> state;  // frame held by a slot, -2-frame on failure, -1 none
-  std::vector<std::thread> pool;
-  std::mutex m;
-  std::condition_variable cv;
-  size_t cur = 0, next = 0;
-  bool stopping = false;
-
-  void start() {
-    cur = next = 0;
-    stopping = false;
-    std::fill(state.begin(), state.end(), -1);
-    for (int t = 0; t < T; ++t) pool.emplace_back([this] { work(); });
-  }
-  void stop() {
-    {
-      std::lock_guard<std::mutex> lk(m);
-      stopping = true;
-    }
-    cv.notify_all();
-    for (auto& th : pool) th.join();
-    pool.clear();
-  }
-  void work() {
-    for (;;) {
-      size_t i;
-      {
-        std::unique_lock<std::mutex> lk(m);
-        cv.wait(lk, [&] { return stopping || next >= V->frame_count() || next < cur + D; });
-        if (stopping || next >= V->frame_count()) return;
-        i = next++;
-      }
-      const bool ok = V->read_at(i, ring.data() + (i % D) * FB);
-      {
-        std::lock_guard<std::mutex> lk(m);
-        state[i % D] = ok ? (long long)i : -2 - (long long)i;
-      }
-      cv.notify_all();
-    }
-  }
+  const size_t FB;
+  size_t pos = 0;
 };
 
 // LocoMouse_Parameters (LocoMouse_class.cpp:4-249): keys in the reference's
@@ -337,11 +293,9 @@ int run(int argc, char** argv) {
   li.setup.view_box_side = in.BB_SIDE_VIEW;
   li.setup.view_box_bottom = in.BB_BOTTOM_VIEW;
   li.model = model.m;
-  const size_t fbytes = (size_t)video->rows() * video->cols();
-  const int threads = std::max(1, std::min(8, (int)std::thread::hardware_concurrency() - 1));
-  auto reader = std::make_shared<FramePrefetcher>(
-      video, threads, std::max<size_t>(64, std::min<size_t>(1024, ((size_t)256 << 20) / std::max<size_t>(fbytes, 1))));
+  auto reader = std::make_shared<VideoFrames>(video, std::max(1, std::min(8, (int)std::thread::hardware_concurrency())));
   li.read_frame = [reader](uint8_t* dst) { return reader->read(dst); };
+  li.read_frames = [reader](uint8_t* dst, int n) { return reader->read(dst, n); };
   li.rewind = [reader] { reader->rewind(); };
   li.output_file = in.OUTPUT_PATH + "/output_" + in.FILE_STEM + ".yml";
   if (const char* d = std::getenv("LM_DEVICE")) li.device = std::atoi(d);

@@ -136,7 +136,7 @@ void throw_on_error(lm_status s) {
 }
 
 LocoMouse::LocoMouse(const LocoMouse_Inputs& inputs) : IN(inputs), METHOD(0), N_FRAMES(inputs.n_frames) {
-  if (!IN.read_frame) throw std::invalid_argument("LocoMouse: no frame reader (V) given.");
+  if (!IN.read_frame && !IN.read_frames) throw std::invalid_argument("LocoMouse: no frame reader (V) given.");
   if (IN.batch < 1) throw std::invalid_argument("LocoMouse: batch must be >= 1.");
   if (IN.setup.video_rows <= 0 || IN.setup.video_cols <= 0)
     throw std::invalid_argument("LocoMouse: video size must be positive.");
@@ -186,9 +186,13 @@ void LocoMouse::runBoundingBoxPass(int method) {
   std::vector<uint8_t> buf(FRAME_BYTES * (size_t)IN.batch);
   for (unsigned done = 0; done < N_FRAMES;) {
     const int n = (int)std::min<unsigned>((unsigned)IN.batch, N_FRAMES - done);
-    for (int i = 0; i < n; ++i)
-      if (!IN.read_frame(buf.data() + (size_t)i * FRAME_BYTES))
-        throw std::runtime_error("Error: Failed to read image from video file.\n");  // :1284-1286
+    if (IN.read_frames) {
+      if (IN.read_frames(buf.data(), n) != n) throw std::runtime_error("Error: Failed to read image from video file.\n");
+    } else {
+      for (int i = 0; i < n; ++i)
+        if (!IN.read_frame(buf.data() + (size_t)i * FRAME_BYTES))
+          throw std::runtime_error("Error: Failed to read image from video file.\n");  // :1284-1286
+    }
     throw_on_error(lm_bb_push(bb.get(), buf.data(), (int64_t)FRAME_BYTES, n, nullptr));
     done += (unsigned)n;
   }
@@ -226,8 +230,14 @@ void LocoMouse::initializeFeatureLoop() {
 void LocoMouse::readFrame() {
   if (!CTX) throw std::runtime_error("readFrame: initializeFeatureLoop() has not been called.");
   if (N_PENDING == IN.batch) flush();  // a caller that skips storePreviousImage
-  if ((unsigned)(CURRENT_FRAME + 1) >= N_FRAMES || !IN.read_frame(PENDING.data() + (size_t)N_PENDING * FRAME_BYTES))
-    throw std::runtime_error("Error: Failed to read image from video file.\n");  // :1284-1286
+  const unsigned left = N_FRAMES - (unsigned)(CURRENT_FRAME + 1);
+  if (IN.read_frames && N_PENDING == N_READ_AHEAD && left > 0) {
+    const int want = (int)std::min<unsigned>((unsigned)(IN.batch - N_PENDING), left);
+    N_READ_AHEAD += std::max(0, IN.read_frames(PENDING.data() + (size_t)N_PENDING * FRAME_BYTES, want));
+  }
+  const bool ok = left > 0 && (IN.read_frames ? N_PENDING < N_READ_AHEAD
+                                              : IN.read_frame(PENDING.data() + (size_t)N_PENDING * FRAME_BYTES));
+  if (!ok) throw std::runtime_error("Error: Failed to read image from video file.\n");  // :1284-1286
   ++N_PENDING;
   ++CURRENT_FRAME;
 }
@@ -281,6 +291,7 @@ void LocoMouse::flush() {
   }
   PENDING.swap(SUBMITTED);
   N_PENDING = 0;
+  N_READ_AHEAD = 0;
   INFLIGHT = std::async(std::launch::async, [this, n, first, bb = std::move(bb)] {
     lm_batch_result r{};
     throw_on_error(lm_detect_batch(CTX, SUBMITTED.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data(), &r));

@@ -52,6 +52,11 @@ struct LocoMouse_Inputs {
   // V >> F; extractChannel(F, F, 0): writes the next frame (video_rows x
   // video_cols u8, row-major) and returns false at the end of the video.
   std::function<bool(uint8_t* dst)> read_frame;
+  // Optional: the next (up to) n frames into dst (n x video_rows x video_cols,
+  // contiguous), returning how many were read.  When given, readFrame reads a
+  // whole batch ahead at its first frame (so a decoder can fill it in
+  // parallel, without a per-frame copy); frames are still consumed in order.
+  std::function<int(uint8_t* dst, int n)> read_frames;
   int device = 0;      // HIP device of this instance (one per GPU / host thread)
   int batch = 256;     // frames per lm_detect_batch / lm_bb_push call
   // Whole-video BB pass (use_provided_bounding_box = 0): config.yml's
@@ -141,6 +146,7 @@ class LocoMouse : protected FrameResults {
   std::vector<uint8_t> SUBMITTED;  // the batch being processed by INFLIGHT
   std::future<void> INFLIGHT;      // lm_detect_batch + append of the previous batch
   int N_PENDING = 0;
+  int N_READ_AHEAD = 0;  // frames of PENDING already filled by read_frames
   size_t FRAME_BYTES = 0;
   void flush();
   void wait_inflight();
