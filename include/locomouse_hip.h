@@ -341,6 +341,13 @@ void* lm_bb_stream(lm_bb_ctx* ctx);
 /* Benchmark/test input utility (not a reference interface): writes frames
  * [first_frame, first_frame + n) of the synthetic scene of include/lm_synth.h
  * (rows x cols u8, frame_pitch bytes apart) into device memory of `device`. */
+/* Page-locked host memory (hipHostMalloc) for batches of host frames: frames
+ * in such a buffer reach the device by DMA at full PCIe rate, and a batch of
+ * frames at a common pitch is copied in one 2-D transfer.  No reference
+ * counterpart (the reference reads frames into a cv::Mat). */
+lm_status lm_host_alloc(size_t bytes, void** out);
+void lm_host_free(void* p);
+
 lm_status lm_synth_frames_device(int32_t device, uint8_t* d_out, int32_t rows, int32_t cols, int64_t first_frame,
                                  int32_t n, int64_t frame_pitch);
 

@@ -888,8 +888,8 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   // has landed (see k_prep / k_out for why the stream otherwise holds only
   // kernels).
   if (!device_frames) {
-    for (int s = 1; s <= n; ++s)
-      HIPCHK(hipMemcpyAsync(c->frames.p + (int64_t)s * fstride, frames + (int64_t)(s - 1) * pitch, c->npix,
+    // one 2-D transfer for the batch (DMA from page-locked buffers, e.g. lm_host_alloc)
+    HIPCHK(hipMemcpy2DAsync(c->frames.p + fstride, (size_t)fstride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
                             hipMemcpyHostToDevice, st));
     if (halo) HIPCHK(hipMemcpyAsync(c->halo.p, prev, c->npix, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1309,6 +1309,18 @@ __global__ void k_synth(uint8_t* __restrict__ out, lm_synth_scene sc, int64_t fi
   } else {
     for (int k = 0; k < 4 && q + k < np; ++k) o[k] = (uint8_t)(w >> (8 * k));
   }
+}
+
+LM_API lm_status lm_host_alloc(size_t bytes, void** out) {
+  return guarded([&] {
+    if (!out) throw std::invalid_argument("lm_host_alloc: out is NULL.");
+    *out = nullptr;
+    HIPCHK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  });
+}
+
+LM_API void lm_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 LM_API lm_status lm_synth_frames_device(int32_t device, uint8_t* d_out, int32_t rows, int32_t cols, int64_t first_frame,

@@ -219,8 +219,8 @@ void LocoMouse::initializeFeatureLoop() {
   if (CTX) return;
   IN.setup.method = METHOD;
   throw_on_error(lm_ctx_create(IN.device, &IN.setup, &IN.params, &IN.model, IN.batch, &CTX));
-  PENDING.assign(FRAME_BYTES * (size_t)IN.batch, 0);
-  SUBMITTED.assign(FRAME_BYTES * (size_t)IN.batch, 0);
+  PENDING.allocate(FRAME_BYTES * (size_t)IN.batch);
+  SUBMITTED.allocate(FRAME_BYTES * (size_t)IN.batch);
   N_PENDING = 0;
 }
 
@@ -256,6 +256,14 @@ void LocoMouse::matchBottomSideCandidates() {}
 // frame) is handed over.
 void LocoMouse::storePreviousImage() {
   if (N_PENDING && (N_PENDING == IN.batch || (unsigned)(CURRENT_FRAME + 1) == N_FRAMES)) flush();
+}
+
+void LocoMouse::HostBuffer::allocate(size_t bytes) {
+  lm_host_free(p);
+  p = nullptr;
+  void* q = nullptr;
+  throw_on_error(lm_host_alloc(bytes, &q));
+  p = static_cast<uint8_t*>(q);
 }
 
 void LocoMouse::sync() {

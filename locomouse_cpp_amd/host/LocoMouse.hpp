@@ -32,6 +32,7 @@
 #include <future>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "Candidates.hpp"
@@ -142,8 +143,19 @@ class LocoMouse : protected FrameResults {
  protected:
   void runBoundingBoxPass(int method);  // lm_bb_* over the whole video, then rewind
  private:
-  std::vector<uint8_t> PENDING;  // raw frames read but not yet processed
-  std::vector<uint8_t> SUBMITTED;  // the batch being processed by INFLIGHT
+  // Page-locked (lm_host_alloc) batch buffers: DMA host->device copies.
+  struct HostBuffer {
+    uint8_t* p = nullptr;
+    HostBuffer() = default;
+    HostBuffer(const HostBuffer&) = delete;
+    HostBuffer& operator=(const HostBuffer&) = delete;
+    ~HostBuffer() { lm_host_free(p); }
+    void allocate(size_t bytes);
+    uint8_t* data() { return p; }
+    void swap(HostBuffer& o) { std::swap(p, o.p); }
+  };
+  HostBuffer PENDING;    // raw frames read but not yet processed
+  HostBuffer SUBMITTED;  // the batch being processed by INFLIGHT
   std::future<void> INFLIGHT;      // lm_detect_batch + append of the previous batch
   int N_PENDING = 0;
   int N_READ_AHEAD = 0;  // frames of PENDING already filled by read_frames

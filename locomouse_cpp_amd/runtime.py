@@ -22,7 +22,7 @@ EXPORTED = (
     "lm_detect_batch", "lm_detect_batch_device", "lm_ctx_set_debug", "lm_debug_scores", "lm_debug_tail_mask",
     "lm_debug_kernel_times", "lm_debug_kernel_spans", "lm_synth_frames_device",
     "lm_bb_create", "lm_bb_destroy", "lm_bb_push", "lm_bb_push_device", "lm_bb_finish", "lm_bb_debug_binary",
-    "lm_bb_stream",
+    "lm_bb_stream", "lm_host_alloc", "lm_host_free",
 )
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -109,6 +109,8 @@ def lib():
             fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]
         L.lm_bb_finish.argtypes = [C.c_void_p, C.POINTER(lm_bb_result)]
         L.lm_bb_debug_binary.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
+        L.lm_host_alloc.argtypes = [C.c_size_t, C.POINTER(C.c_void_p)]
+        L.lm_host_free.argtypes = [C.c_void_p]
         L.lm_bb_stream.argtypes = [C.c_void_p]
         L.lm_bb_stream.restype = C.c_void_p
         _lib = L
