@@ -41,6 +41,7 @@ class TrackSolver {
   // point::margin (match2nd.h:398-418)
   void margin() {
     clear();
+    refresh_un();
     for (int f = 0; f < G.L - 1; ++f) forward(f);
     for (int f = G.L - 2; f >= 0; --f) backward(f);
     for (int f = 0; f < G.L - 1; ++f) find_best(f);
@@ -57,6 +58,7 @@ class TrackSolver {
       else if (bestloc[f] < G.nloc[f])
         G.message(f, bestloc[f]) += -second[f] + best[f] + G.bam;
     }
+    refresh_un();
     for (int f = G.L - 2; f >= 0; --f) backward(f);
     for (int f = 0; f < G.L; ++f) set_label(f);
     for (int f = 0; f < G.L; ++f)  // update_unary_second: a taken candidate is barred for later tracks
@@ -69,17 +71,25 @@ class TrackSolver {
   Lattice& G;
   std::vector<const double*> U;  // unary column of this track, per frame
   std::vector<double> fwd, bwd;  // marginforward / marginbackward, by transition
+  std::vector<double> unv;       // point::un of every location, valid for one sweep phase
   std::vector<int> label, bestloc;
   std::vector<double> best, second;
 
   double& F(int f, int k) { return fwd[G.toff[f] + (size_t)k]; }
   double& B(int f, int k) { return bwd[G.toff[f] + (size_t)k]; }
 
-  // point::un: unary (or the occlusion cost) plus the shared message.
-  double un(int f, int b) {
-    const double m = G.message(f, b);
-    return b < G.nloc[f] ? U[f][b] + m : G.occ_cost + m;
+  // point::un: unary (or the occlusion cost) plus the shared message.  The
+  // messages change only between sweep phases, so each phase evaluates it
+  // once per location (same operands, same value) instead of per transition.
+  void refresh_un() {
+    unv.resize(G.moff.back());
+    for (int f = 0; f < G.L; ++f) {
+      double* u = unv.data() + G.moff[f];
+      const double* m = G.msg.data() + G.moff[f];
+      for (int b = 0; b < G.nloc[f] + G.nong; ++b) u[b] = b < G.nloc[f] ? U[f][b] + m[b] : G.occ_cost + m[b];
+    }
   }
+  double un(int f, int b) const { return unv[G.moff[f] + (size_t)b]; }
 
   void clear() {  // clearmargin
     std::fill(label.begin(), label.end(), -2);
