@@ -85,14 +85,24 @@ def cpu_baseline(cfg, seconds=10.0, max_frames=2000):
             "cpu": cpu}
 
 
+def host_cpu_share():
+    """Host threads this GPU's share of the node may use: the CPUs this
+    process may run on, capped by the box's per-GPU share (OMP_NUM_THREADS,
+    16 per MI355X on the pool: a 128-core node split over 8 GPUs)."""
+    n = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(share))) if share and share.isdigit() else n
+
+
 def cpu_baseline_threads(cfg, seconds=8.0, threads=None):
-    """The fair CPU baseline of SURVEY.md §8(d)(ii): the oracle on T host
-    threads, each on its own contiguous 50-frame chunks (frame-sharded like
-    the multi-GPU path; ctypes releases the GIL inside the oracle call)."""
+    """The fair CPU baseline of SURVEY.md §8(d)(ii): the oracle on every host
+    thread of this GPU's CPU share, each on its own contiguous 50-frame chunks
+    (frame-sharded like the multi-GPU path; ctypes releases the GIL inside the
+    oracle call)."""
     import threading
     from oracle import oracle as O
     if threads is None:
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        threads = host_cpu_share()
     chunk = 50
     samples = [cfg.frames(chunk * t, chunk) for t in range(threads)]
     counts = [0] * threads
@@ -112,6 +122,41 @@ def cpu_baseline_threads(cfg, seconds=8.0, threads=None):
     el = time.perf_counter() - t0
     return {"value": sum(counts) / el, "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{sum(counts)} frames, {threads} threads x chunks of {chunk} frames, {el:.1f} s wall"}
+
+
+def gather_results(ctxs, frames, state, vbase, R, B, frame_bytes, world, rank):
+    """The host gather of north_star's multi-GPU design, after the timed
+    region: every stream of every rank runs its next batch, its compact
+    results (the lm_batch_result arrays) go to rank 0 over the host process
+    group, and rank 0 checks that the gathered frame ranges are disjoint and
+    whole.  Returns a summary (rank 0) or None."""
+    import torch.distributed as dist
+
+    from locomouse_cpp_amd.abi import result_to_numpy
+    mine = []
+    for k, c in enumerate(ctxs):
+        f = state[k]["frame"]
+        i = (f - vbase[k]) % R + 1
+        n = min(B, R + 1 - i)
+        # the context processed frame f - 1 last: it carries that frame's state
+        res = result_to_numpy(c.detect_device(frames[k].data_ptr() + i * frame_bytes, frame_bytes, n, f))
+        mine.append({"first": f, "n": res["n_frames"], "cand": res["cand"], "cand_offset": res["cand_offset"],
+                     "tail": res["tail"]})
+    allr = [None] * world if rank == 0 else None
+    if world > 1:
+        dist.gather_object(mine, allr, dst=0)
+    else:
+        allr = [mine]
+    if rank != 0:
+        return None
+    parts = sorted((p for r in allr for p in r), key=lambda p: p["first"])
+    for a, b in zip(parts, parts[1:]):
+        if a["first"] + a["n"] > b["first"]:
+            raise RuntimeError("gathered frame ranges overlap")
+    return {"ranks": world, "streams": len(parts), "frames": int(sum(p["n"] for p in parts)),
+            "candidates": int(sum(len(p["cand"]) for p in parts)),
+            "first_frames": [int(p["first"]) for p in parts][:16], "transport": "gloo gather_object (host)" if world > 1
+            else "local"}
 
 
 def run_bb(args):
@@ -284,6 +329,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    gathered = gather_results(ctxs, frames, state, vbase, R, B, FRAME_BYTES, world, rank)
     total_frames = args.steps * B * NS * world
     fps = total_frames / elapsed
 
@@ -328,6 +374,7 @@ def main():
         "kernel_avg_ms": {k: round(sum(v) / len(v), 5) for k, v in kernel_ms.items()},
         "kernel_busy_ms_per_batch": {k: round(union_ms(v) / len(v), 5) for k, v in spans.items()},
     }
+    out["gathered"] = gathered
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
         out["cpu_baseline_threads"] = cpu_baseline_threads(cfg, min(8.0, args.cpu_seconds))

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LM_ABI_VERSION 1
+#define LM_ABI_VERSION 2
 #define LM_N_PAWS 4          /* LocoMouse_class.hpp:84 */
 #define LM_N_TAIL_POINTS 15  /* LocoMouse_class.hpp:86 */
 #define LM_N_LISTS 4         /* candidate lists per frame */
@@ -90,16 +90,34 @@ typedef struct {
   lm_rect bounding_box_side;                    /* bounding_box_side  (x y w h) */
   lm_rect bounding_box_bottom;                  /* bounding_box_bottom (x y w h) */
   float gray_value_transformation[256];         /* used iff transform_gray_values */
+  int32_t gray_value_transformation_depth;      /* OpenCV depth of that matrix as read from config.yml
+                                                   (dt u -> LM_DEPTH_8U, f -> LM_DEPTH_32F, ...) */
 } lm_params;
 /* Grey-level options, as the reference executes them:
  *  - use_reference_image_brightness: LocoMouse_Parameters computes the
  *    reference CDF with computeNormalizedCDF into an unallocated cv::Mat
  *    (:189, :3392-3405: ptr<float>(0) of an empty Mat), so the reference
  *    cannot start with it set; lm_ctx_create fails with LM_ERR_RUNTIME.
- *  - transform_gray_values: LUT(I_BOTTOM_MOUSE, table, I_BOTTOM_MOUSE) with a
- *    floating-point table re-creates the crop as CV_32F and the later
- *    Mat::setTo(0, mask) asserts (:1448, :849); lm_ctx_create fails with
- *    LM_ERR_RUNTIME. */
+ *  - transform_gray_values: LUT(I_BOTTOM_MOUSE, table, I_BOTTOM_MOUSE)
+ *    (:1445-1448).  A CV_8U table (depth LM_DEPTH_8U, values 0..255) keeps
+ *    the type, so the LUT is applied in place to the bottom crop of I_PAD:
+ *    every later step of that frame (tail, masks, both views where they
+ *    overlap the crop) and the next frame's motion test (I_PREV_PAD) see the
+ *    transformed pixels — supported.  Any other table depth re-creates the
+ *    crop with the table's type and a later threshold / Mat::setTo(0, mask)
+ *    asserts (:782, :849): lm_ctx_create fails with LM_ERR_RUNTIME, as the
+ *    reference would stop.  The in-place LUT also reaches the zero padding
+ *    of I_PAD when a frame's bottom crop leaves the corrected image, and the
+ *    reference keeps those transformed pad pixels across frames; batches
+ *    with such a frame fail with LM_ERR_INVALID_ARGUMENT (never the case
+ *    with a provided bounding box, which must lie inside the image). */
+#define LM_DEPTH_8U 0
+#define LM_DEPTH_8S 1
+#define LM_DEPTH_16U 2
+#define LM_DEPTH_16S 3
+#define LM_DEPTH_32S 4
+#define LM_DEPTH_32F 5
+#define LM_DEPTH_64F 6
 
 /* One linear detector (model.yml modelX_view / biasX_view, :3106-3148).
  * Weights are row-major doubles as read from the model file; they are rounded
@@ -126,7 +144,15 @@ typedef struct {
   int32_t calib_rows, calib_cols; /* N_ROWS x N_COLS of ind_warp_mapping */
   const int32_t* ind_warp_mapping;/* calib_rows x calib_cols, copied at create */
   lm_rect view_box_side, view_box_bottom;
+  int32_t filter_arith;           /* LM_FILTER_FUSED (default) or LM_FILTER_UNFUSED, see below */
 } lm_setup;
+/* filter2D's fp32 tap arithmetic depends on the OpenCV build the reference
+ * links (no version is pinned, CMakeLists.txt:3): AVX2 builds of OpenCV
+ * >= 3.4.9 fuse each tap (fma), SSE2/scalar builds round the product and then
+ * the sum.  Pick the one matching the installation being replaced; both are
+ * bit-exact against the restatement of that build (tests/test_gpu_parity.py). */
+#define LM_FILTER_FUSED 0
+#define LM_FILTER_UNFUSED 1
 
 /* Geometry derived at create time (initializeFeatureLoop :655-769 and the
  * LocoMouse_Model pads :3157-3161 incl. the spost_b = spre_b move-assign at :3173). */

@@ -9,6 +9,8 @@ import numpy as np
 
 LM_OK, LM_ERR_INVALID_ARGUMENT, LM_ERR_RUNTIME, LM_ERR_HIP = 0, 1, 2, 3
 LM_N_TAIL_POINTS = 15
+LM_FILTER_FUSED, LM_FILTER_UNFUSED = 0, 1
+LM_DEPTH_8U, LM_DEPTH_32F, LM_DEPTH_64F = 0, 5, 6
 DETECTORS = ("paw_bottom", "snout_bottom", "tail_bottom", "paw_side", "snout_side", "tail_side")
 
 
@@ -43,6 +45,7 @@ class lm_params(C.Structure):
         ("bounding_box_side", lm_rect),
         ("bounding_box_bottom", lm_rect),
         ("gray_value_transformation", C.c_float * 256),
+        ("gray_value_transformation_depth", C.c_int32),
     ]
 
 
@@ -66,6 +69,7 @@ class lm_setup(C.Structure):
         ("ind_warp_mapping", C.POINTER(C.c_int32)),
         ("view_box_side", lm_rect),
         ("view_box_bottom", lm_rect),
+        ("filter_arith", C.c_int32),
     ]
 
 

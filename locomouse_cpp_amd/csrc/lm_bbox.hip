@@ -16,7 +16,8 @@
 // (k_bb_ring, one workgroup walking the batch's frames in order).
 //
 // Per batch of n frames:
-//   k_minmax_lut  normalize LUT per frame (shared with the detection path)
+//   k_minmax      \ normalize LUT per frame (shared with the detection path)
+//   k_lut         /
 //   k_bb_ingest   I_median centre indicator  M[f] = [corrected frame >= 3]
 //   k_bb_bands    the border bands of M[f] in k_bb_ring's LDS layout
 //   k_bb_ring     ring state recurrence; writes ring_{f-1} into M[f]
@@ -643,9 +644,6 @@ __global__ __launch_bounds__(256) void k_bb_center(const LmBBConst K, const uint
 // (8-connectivity: Grana BBDT 2x2-block raster order of its first block;
 // 4-connectivity: Wu pixel raster order).  Global-memory union-find tables
 // are read with L1-bypassing loads so every wave sees the others' hooks.
-DEV unsigned bb_ld(const unsigned* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-DEV void bb_st(unsigned* a, unsigned v) { __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
 // firstLastOverT's pass test on one row/column sum (LocoMouse_class.hpp:419-421).
 DEV bool bb_pass(const LmBBConst& K, int count) {
   const int v = 255 * count;  // the mask is 0/255 (cv::compare, :945)
@@ -653,171 +651,21 @@ DEV bool bb_pass(const LmBBConst& K, int count) {
   return __int_as_float(v) >= (float)K.min_pixel_visible;  // CV_32S read through ptr<float>
 }
 
-// Row-run labelling.  The view is staged as a bitmap in LDS (16 pixels per
-// lane from 16-byte loads); runs are read off 64-column words, linked to the
-// overlapping runs of the row above (8-connectivity: columns within +-1), and
-// a union-find forest over runs (atomicMin hooking of the larger root under
-// the smaller, so a component's root is its first run in raster order) gives
-// areas and first-label keys.  The run table lives in LDS when a view has at
-// most K.run_cap runs (clean masks: a few per row), else in the global
-// scratch with L1-bypassing loads (noisy masks: thousands per view).
-// Run table: start / end column (u16 in LDS, u32 in global memory),
-// union-find parent, area and first-label key per run; a run's row is found
-// by binary search in the per-row run offsets.
-template <class IX>
-struct BBRuns {
-  IX *rs, *re;
-  unsigned *par, *area, *key;
-};
-
-template <bool G, class T>
-DEV unsigned rld(const T* a) {
-  if constexpr (G) return bb_ld(reinterpret_cast<const unsigned*>(a));
-  else return (unsigned)*a;
-}
-template <bool G, class T>
-DEV void rst(T* a, unsigned v) {
-  if constexpr (G) bb_st(reinterpret_cast<unsigned*>(a), v);
-  else *a = (T)v;
-}
-template <bool G>
-DEV unsigned rfind(const unsigned* par, unsigned a) {
-  unsigned q = rld<G>(&par[a]);
-  while (q != a) {
-    a = q;
-    q = rld<G>(&par[a]);
-  }
-  return a;
-}
-template <bool G>
-DEV void runion(unsigned* par, unsigned a, unsigned b) {
-  while (true) {
-    a = rfind<G>(par, a);
-    b = rfind<G>(par, b);
-    if (a == b) return;
-    if (a < b) {
-      const unsigned t = a;
-      a = b;
-      b = t;
-    }
-    const unsigned old = atomicMin(&par[a], b);
-    if (old == a) return;
-    a = old;
-  }
-}
-
-// Exclusive scan of v[0..n) in place by wave 0; the total goes to *total.
-// Block-wide call.
-DEV void bb_wave0_scan(int* v, int n, int* total) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    int carry = 0;
-    for (int b = 0; b < n; b += 64) {
-      const int i = b + lane;
-      const int x = i < n ? v[i] : 0;
-      int inc = x;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(inc, o);
-        if (lane >= o) inc += y;
-      }
-      if (i < n) v[i] = carry + inc - x;
-      carry += __shfl(inc, 63);
-    }
-    if (lane == 0) *total = carry;
-  }
-  __syncthreads();
-}
-
-// Row of run i: the last y with rowoff[y] <= i (rowoff exclusive offsets).
-DEV int bb_row_of(const int* rowoff, int H, int i) {
-  int lo = 0, hi = H;  // first y with rowoff[y] > i, minus one
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (rowoff[mid] <= i) lo = mid + 1; else hi = mid;
-  }
-  return lo - 1;
-}
-
-// Labels the runs of one view (bitmap rows bm[y][0..nb64], 64 columns per
-// word), picks the largest component (ties: first OpenCV label) and
-// accumulates its per-column (difference array) and per-row pixel counts.
+// The largest component of one view (lm_cc.h: row runs + union-find, run
+// table in LDS when a view has at most K.run_cap runs, else in the global
+// scratch) and its per-column (difference array) and per-row pixel counts.
 // Block-wide call.
 template <bool G, class IX>
-DEV void bb_cc_runs(const BBRuns<IX> S, const unsigned long long* bm, int nb64, int W, int H, int R,
+DEV void bb_cc_runs(const CCRuns<IX> S, const unsigned long long* bm, int nb64, int W, int H, int R,
                     const int* rowoff, bool c8, int* colc, int* rowc, unsigned long long* s_red, unsigned* s_best) {
-  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
-  const unsigned long long lt = (1ull << lane) - 1;
-  const unsigned nbx = (unsigned)(W + 1) / 2;
-  for (int y = wave; y < H; y += nw) {
-    const unsigned long long* row = bm + (int64_t)y * (nb64 + 1);
-    int ns = rowoff[y], ne = rowoff[y];
-    unsigned long long carry = 0;
-    for (int k = 0; k < nb64; ++k) {
-      const unsigned long long bits = row[k], nxt = row[k + 1] & 1ull;  // wave-uniform
-      const unsigned long long st = bits & ~((bits << 1) | carry);
-      const unsigned long long en = bits & ~((bits >> 1) | (nxt << 63));
-      const int x = 64 * k + lane;
-      if ((st >> lane) & 1) rst<G>(&S.rs[ns + __popcll(st & lt)], (unsigned)x);
-      if ((en >> lane) & 1) rst<G>(&S.re[ne + __popcll(en & lt)], (unsigned)x);
-      ns += __popcll(st);
-      ne += __popcll(en);
-      carry = bits >> 63;
-    }
-  }
-  __syncthreads();  // the LDS union-find arrays overlay the bitmap
-  for (int i = tid; i < R; i += nt) {
-    rst<G>(&S.par[i], (unsigned)i);
-    rst<G>(&S.area[i], 0u);
-    rst<G>(&S.key[i], 0xFFFFFFFFu);
-  }
-  __syncthreads();
-  const int d = c8 ? 1 : 0;
-  for (int i = tid; i < R; i += nt) {
-    const int y = bb_row_of(rowoff, H, i);
-    if (y == 0) continue;
-    const int a0 = (int)rld<G>(&S.rs[i]) - d, a1 = (int)rld<G>(&S.re[i]) + d;
-    int lo = rowoff[y - 1], hi = rowoff[y];
-    while (lo < hi) {  // first run of row y-1 ending at or after a0
-      const int mid = (lo + hi) >> 1;
-      if ((int)rld<G>(&S.re[mid]) < a0) lo = mid + 1; else hi = mid;
-    }
-    for (int j = lo; j < rowoff[y] && (int)rld<G>(&S.rs[j]) <= a1; ++j) runion<G>(S.par, i, j);
-  }
-  __syncthreads();
-  for (int i = tid; i < R; i += nt) {
-    const unsigned root = rfind<G>(S.par, i);
-    const unsigned y = (unsigned)bb_row_of(rowoff, H, i), x = rld<G>(&S.rs[i]);
-    atomicAdd(&S.area[root], rld<G>(&S.re[i]) - x + 1);
-    atomicMin(&S.key[root], c8 ? (y >> 1) * nbx + (x >> 1) : y * (unsigned)W + x);
-    rst<G>(&S.par[i], root);
-  }
-  __syncthreads();
-  unsigned long long best = 0;
-  for (int i = tid; i < R; i += nt) {
-    if (rld<G>(&S.par[i]) != (unsigned)i) continue;
-    const unsigned long long val = ((unsigned long long)rld<G>(&S.area[i]) << 32) | (0xFFFFFFFFu - rld<G>(&S.key[i]));
-    best = val > best ? val : best;
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long other = __shfl_xor(best, o);
-    best = other > best ? other : best;
-  }
-  if (lane == 0) s_red[wave] = best;
-  __syncthreads();
-  best = 0;
-  for (int w = 0; w < nw; ++w) best = s_red[w] > best ? s_red[w] : best;
-  if (best) {
-    const unsigned barea = (unsigned)(best >> 32), bkey = 0xFFFFFFFFu - (unsigned)best;
-    for (int i = tid; i < R; i += nt)
-      if (rld<G>(&S.par[i]) == (unsigned)i && rld<G>(&S.area[i]) == barea && rld<G>(&S.key[i]) == bkey) *s_best = i;
-  }
-  __syncthreads();
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
+  cc_label<G>(S, bm, nb64, W, H, R, rowoff, c8, s_red, s_best);
   const unsigned broot = *s_best;
   if (broot != 0xFFFFFFFFu)
     for (int i = tid; i < R; i += nt) {
       if (rld<G>(&S.par[i]) != broot) continue;
       const int x0 = (int)rld<G>(&S.rs[i]), x1 = (int)rld<G>(&S.re[i]);
-      atomicAdd(&rowc[bb_row_of(rowoff, H, i)], x1 - x0 + 1);
+      atomicAdd(&rowc[cc_row_of(rowoff, H, i)], x1 - x0 + 1);
       atomicAdd(&colc[x0], 1);
       atomicSub(&colc[x1 + 1], 1);
     }
@@ -896,48 +744,20 @@ __global__ __launch_bounds__(1024) void k_bb_cc(const LmBBConst K, const uint8_t
     s_lim[tid][2] = 0;
   }
   if (tid == 0) s_best = 0xFFFFFFFFu;
-  // view bitmap (16 pixels per lane, wide loads) and run starts per row
-  const bool vec = (W & 15) == 0;
-  for (int y = wave; y < H; y += nw) {
-    const uint8_t* row = Bv + (int64_t)y * W;
-    uint16_t* brow = reinterpret_cast<uint16_t*>(bm + (int64_t)y * (nb64 + 1));
-    int n = 0;
-    unsigned carry = 0;
-    for (int x0 = 0; x0 < 64 * (nb64 + 1); x0 += 1024) {
-      const int x = x0 + 16 * lane;
-      unsigned m = 0;
-      if (x < W) {
-        if (vec) {
-          const uint4 q = *reinterpret_cast<const uint4*>(row + x);
-          const unsigned w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-          for (int k = 0; k < 16; ++k) m |= (((w4[k >> 2] >> (8 * (k & 3))) & 255u) ? 1u : 0u) << k;
-        } else {
-          for (int k = 0; k < 16 && x + k < W; ++k) m |= (row[x + k] ? 1u : 0u) << k;
-        }
-      }
-      if (x < 64 * (nb64 + 1)) brow[x >> 4] = (uint16_t)m;
-      const unsigned prev = (unsigned)__shfl_up((int)(m >> 15), 1);
-      const unsigned cin = lane ? prev : carry;
-      n += __popc(m & ~((m << 1) | cin) & 0xFFFFu);
-      carry = (unsigned)__shfl((int)(m >> 15), 63);
-    }
-    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-    if (lane == 0) rowoff[y] = n;
-  }
-  __syncthreads();
-  bb_wave0_scan(rowoff, H, &s_total);
+  // view bitmap and run counts per row
+  cc_bitmap_u8(Bv, W, W, H, nb64, (W & 15) == 0, nullptr, bm, rowoff);
+  cc_wave0_scan(rowoff, H, &s_total);
   const int R = s_total;
   const bool c8 = K.conn == 8;
   if (R <= K.run_cap && W <= 65536) {
-    const BBRuns<uint16_t> S{reinterpret_cast<uint16_t*>(smc + L.rs), reinterpret_cast<uint16_t*>(smc + L.re),
+    const CCRuns<uint16_t> S{reinterpret_cast<uint16_t*>(smc + L.rs), reinterpret_cast<uint16_t*>(smc + L.re),
                              reinterpret_cast<unsigned*>(smc + L.par), reinterpret_cast<unsigned*>(smc + L.area),
                              reinterpret_cast<unsigned*>(smc + L.key)};
     bb_cc_runs<false>(S, bm, nb64, W, H, R, rowoff, c8, colc, rowc, s_red, &s_best);
   } else {
     const int64_t cap = (int64_t)H * ((W + 1) / 2);  // at most ceil(W/2) runs per row
     unsigned* b = scratch + (int64_t)f * K.cc_words + (v ? 5 * (int64_t)K.view_h[0] * ((W + 1) / 2) : 0);
-    const BBRuns<unsigned> S{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap};
+    const CCRuns<unsigned> S{b, b + cap, b + 2 * cap, b + 3 * cap, b + 4 * cap};
     bb_cc_runs<true>(S, bm, nb64, W, H, R, rowoff, c8, colc, rowc, s_red, &s_best);
   }
   for (int i = tid; i < W + H; i += nt) {
@@ -1078,6 +898,7 @@ struct lm_bb_ctx {
   LmBBConst K{};
   size_t ring_lds = 0, center_lds = 0, cc_lds = 0;
   DevBuf<uint8_t> bkg, frames, luts, M, ring, bin, bands;
+  DevBuf<unsigned> mm;  // k_minmax partial (min, max) pairs
   DevBuf<uint32_t> rbits;  // bit-packed ring: per-frame band words (published ring_{f-1})
   size_t ring_bits_lds = 0;
   DevBuf<unsigned long long> prof;  // LM_BB_PROF=1: k_bb_ring phase clocks
@@ -1218,13 +1039,14 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
 
   if (method != 0) {
     c->bkg.alloc((size_t)c->frame_stride);
-    HIPCHK(hipMemset(c->bkg.p, 0, c->bkg.n));
-    HIPCHK(hipMemcpy(c->bkg.p, su->background, (size_t)npix, hipMemcpyHostToDevice));
+    SET_SYNC(c->bkg.p, 0, c->bkg.n, c->stream);
+    COPY_SYNC(c->bkg.p, su->background, (size_t)npix, hipMemcpyHostToDevice, c->stream);
     c->cal.alloc((size_t)NR * NC);
-    HIPCHK(hipMemcpy(c->cal.p, su->ind_warp_mapping, sizeof(int32_t) * NR * NC, hipMemcpyHostToDevice));
+    COPY_SYNC(c->cal.p, su->ind_warp_mapping, sizeof(int32_t) * NR * NC, hipMemcpyHostToDevice, c->stream);
     if (method == 2) {
       c->frames.alloc((size_t)c->frame_stride * c->max_batch);
       c->luts.alloc((size_t)256 * c->max_batch);
+      c->mm.alloc((size_t)2 * LM_MM_SPLIT * c->max_batch);
       c->fptr.alloc((size_t)c->max_batch);
       c->bbx.alloc((size_t)c->max_batch);
       HIPCHK(hipFuncSetAttribute((const void*)k_bb_de, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * NC));
@@ -1237,30 +1059,31 @@ void bb_validate_and_build(lm_bb_ctx* c, const lm_setup* su, const lm_bb_params*
 
   const int B = c->max_batch;
   c->bkg.alloc((size_t)c->frame_stride);
-  HIPCHK(hipMemset(c->bkg.p, 0, c->bkg.n));
-  HIPCHK(hipMemcpy(c->bkg.p, su->background, (size_t)npix, hipMemcpyHostToDevice));
+  SET_SYNC(c->bkg.p, 0, c->bkg.n, c->stream);
+  COPY_SYNC(c->bkg.p, su->background, (size_t)npix, hipMemcpyHostToDevice, c->stream);
   c->cal.alloc((size_t)NR * NC);
-  HIPCHK(hipMemcpy(c->cal.p, su->ind_warp_mapping, sizeof(int32_t) * NR * NC, hipMemcpyHostToDevice));
+  COPY_SYNC(c->cal.p, su->ind_warp_mapping, sizeof(int32_t) * NR * NC, hipMemcpyHostToDevice, c->stream);
   c->frames.alloc((size_t)c->frame_stride * B);
   c->luts.alloc((size_t)256 * B);
+  c->mm.alloc((size_t)2 * LM_MM_SPLIT * B);
   c->M.alloc((size_t)K.m_bytes * B);
-  HIPCHK(hipMemset(c->M.p, 0, c->M.n));
+  SET_SYNC(c->M.p, 0, c->M.n, c->stream);
   c->ring.alloc((size_t)std::max(K.ring_n, 1));
-  HIPCHK(hipMemset(c->ring.p, 0, c->ring.n));  // I_median = zeros (:588)
+  SET_SYNC(c->ring.p, 0, c->ring.n, c->stream);  // I_median = zeros (:588)
   c->bin.alloc((size_t)K.bin_bytes * B);
   if (K.bits_nw) {
     const size_t nw = 4 * (size_t)K.p * K.bits_nw + 2 * (size_t)K.hp;
     c->bands.alloc(nw * 4 * B);
     c->rbits.alloc(nw * B);
     c->ring.alloc(nw * 4);
-    HIPCHK(hipMemset(c->ring.p, 0, c->ring.n));  // I_median = zeros (:588)
+    SET_SYNC(c->ring.p, 0, c->ring.n, c->stream);  // I_median = zeros (:588)
   } else {
     c->bands.alloc((size_t)std::max(K.band_n, 16) * B);
     c->rbits.alloc(1);
   }
   if (dbg_env("LM_BB_PROF")) {
     c->prof.alloc(8);
-    HIPCHK(hipMemset(c->prof.p, 0, 8 * sizeof(unsigned long long)));
+    SET_SYNC(c->prof.p, 0, 8 * sizeof(unsigned long long), c->stream);
   }
   c->cc.alloc((size_t)K.cc_words * B);
   c->fptr.alloc((size_t)B);
@@ -1304,7 +1127,7 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
     }
     return;
   }
-  // device frames are read in place when 16-byte aligned (k_minmax_lut loads 16 B per lane)
+  // device frames are read in place when 16-byte aligned (k_minmax loads 16 B per lane)
   const bool direct = device_frames && ((((uintptr_t)frames | (uintptr_t)pitch) & 15) == 0);
   if (device_frames && !direct)
     HIPCHK(hipMemcpy2DAsync(c->frames.p, (size_t)c->frame_stride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
@@ -1321,7 +1144,8 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
     }
   }
   const int64_t np = (int64_t)K.n_rows * K.n_cols;
-  k_minmax_lut<<<n, 1024, 0, s>>>(c->fptr.d, c->bkg.p, (int)c->npix, 0, nullptr, 0, c->luts.p);
+  k_minmax<<<dim3(LM_MM_SPLIT, n), LM_MM_THREADS, 0, s>>>(c->fptr.d, c->bkg.p, (int)c->npix, 0, c->mm.p);
+  k_lut<<<(n + 3) / 4, 256, 0, s>>>(c->mm.p, 0, n, nullptr, 0, c->luts.p);
   if (c->method == 2) {
     k_bb_de<<<n, 1024, 4 * K.n_cols, s>>>(K, c->fptr.d, c->bkg.p, c->cal.p, c->luts.p, c->bbx.d);
     HIPCHK(hipGetLastError());
@@ -1547,7 +1371,7 @@ LM_API lm_status lm_bb_debug_binary(lm_bb_ctx* ctx, int32_t f, uint8_t* out, int
   if (rows != ctx->K.n_rows || cols != ctx->K.n_cols) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
   return guarded([&] {
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipMemcpy(out, ctx->bin.p + (int64_t)f * ctx->K.bin_bytes, (size_t)rows * cols, hipMemcpyDeviceToHost));
+    COPY_SYNC(out, ctx->bin.p + (int64_t)f * ctx->K.bin_bytes, (size_t)rows * cols, hipMemcpyDeviceToHost, ctx->stream);
   });
 }
 

@@ -1,0 +1,411 @@
+// lm_corr.hip — the six filter2D detectors (included by lm_kernels.hip).
+//
+// cv::filter2D(I_VIEW_PAD, scores, CV_32F, W, Point(-1,-1), -rho, BORDER_CONSTANT)
+// at LocoMouse_class.cpp:845, :860, :2575, :2576, restated as
+//     acc = (float)(-rho);  for i in rows, j in cols: acc = acc (+) W[i][j] * I(y+i-kh/2, x+j-kw/2)
+// with (+)* either one fused multiply-add per tap (OpenCV's AVX2 build,
+// v_muladd -> vfmadd; the default) or a rounded multiply then a rounded add
+// (OpenCV's scalar/SSE2 build; LM_FILTER_UNFUSED).  Taps are visited in
+// row-major order, zero-padded taps add +0 (OpenCV skips zero taps; the sum is
+// the same), so every score is bit-identical to the oracle's chain.
+//
+// Kernels:
+//   k_corr_pk<KW, UNF>  width-specialised packed-FP32 kernel (every detector
+//                       width 16..64 that has an instantiation, kh <= 64): the
+//                       production path.
+//   k_corr_gen<UNF>     any width and height: taps in chunks of 4 columns and
+//                       the tap rows in LDS-sized chunks (detectors larger than
+//                       the LDS window, widths without an instantiation).
+//   k_corr_dbg<UNF>     raw scores straight from the ext crops in global memory
+//                       (diagnostics: lm_debug_scores).
+
+#define LM_CORR_THREADS 192
+#define PK_C 5   // columns per thread
+#define PK_R 4   // rows per thread (two packed row pairs)
+
+typedef float lm_f2 __attribute__((ext_vector_type(2)));
+
+// One tap on a packed pair of accumulators (two vertically adjacent outputs of
+// one column; both use the same weight).
+template <bool UNF>
+DEV lm_f2 corr_tap(lm_f2 acc, lm_f2 w2, lm_f2 p) {
+  if constexpr (UNF) {
+    const lm_f2 prod = w2 * p;  // v_pk_mul_f32 (-ffp-contract=off keeps mul and add apart)
+    return acc + prod;          // v_pk_add_f32
+  } else {
+    return __builtin_elementwise_fma(w2, p, acc);  // v_pk_fma_f32
+  }
+}
+
+template <bool UNF>
+DEV float corr_tap1(float acc, float w, float p) {
+  if constexpr (UNF) {
+    const float prod = w * p;
+    return acc + prod;
+  } else {
+    return __builtin_fmaf(w, p, acc);
+  }
+}
+
+// Shared epilogue: point detectors apply the brightness mask of
+// detectBottom/SideCandidates (threshold(25.5 -> 25, BINARY_INV), :782/:817;
+// setTo(0, mask) :849/:864) and append every score > 0 as a sort key
+// (~score_bits << 32 | row-major index) to the frame's list; tail detectors
+// write the binarised map (threshold(>0) + convertTo 8U, :2593-2598).
+// Two passes over a register bitmask keep the accumulators statically indexed.
+template <int R_, int C_>
+DEV void corr_epilogue(const LmConst& K, const LmDet& D, const float (&acc)[R_][C_], const float* lds, int stride, int ly,
+                       int lx, int oy0, int ox0, int slot, unsigned long long* __restrict__ keys,
+                       int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes, int* s_cnt,
+                       int* s_base, const uint8_t* __restrict__ msrc, int mpitch) {
+  static_assert(R_ * C_ <= 32, "bitmask");
+  if (D.kind != 0) {
+    uint8_t* __restrict__ tb = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
+#pragma unroll
+    for (int r = 0; r < R_; ++r)
+#pragma unroll
+      for (int c = 0; c < C_; ++c) {
+        const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
+        if (y < D.oh && x < D.ow) tb[(int64_t)y * D.ow + x] = acc[r][c] > 0.0f ? 1 : 0;
+      }
+    return;
+  }
+  unsigned bits = 0;
+#pragma unroll
+  for (int r = 0; r < R_; ++r)
+#pragma unroll
+    for (int c = 0; c < C_; ++c) {
+      const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
+      // the I_*_MOUSE pixel of this output: from the LDS tile when it holds it,
+      // else (row-chunked generic kernel) from the ext crop
+      const int pix = lds ? (int)lds[(ly * R_ + r + D.m_y - D.in_y) * stride + lx * C_ + c + D.m_x - D.in_x]
+                          : (int)msrc[(int64_t)(ly * R_ + r) * mpitch + lx * C_ + c];
+      if (y < D.oh && x < D.ow && pix > 25 && acc[r][c] > 0.0f) bits |= 1u << (r * C_ + c);
+    }
+  const int nk = __popc(bits);
+  const int off = nk ? atomicAdd(s_cnt, nk) : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) *s_base = *s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], *s_cnt) : 0;
+  __syncthreads();
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + *s_base + off;
+  int k = 0;
+#pragma unroll
+  for (int r = 0; r < R_; ++r)
+#pragma unroll
+    for (int c = 0; c < C_; ++c)
+      if (bits & (1u << (r * C_ + c))) {
+        const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
+        kl[k++] = ((unsigned long long)(~__float_as_uint(acc[r][c])) << 32) | (unsigned)(y * D.ow + x);
+      }
+}
+
+// LDS row stride: == 4 (mod 8) so the two 16-lane row groups of a
+// ds_read2_b32 (4 rows apart) hit disjoint bank halves.
+__host__ __device__ constexpr int pk_stride(int cols) { return cols + ((4 - (cols & 7)) + 8) % 8; }
+
+struct LmDetGroup {
+  int32_t n;
+  int32_t ids[LM_NDET];
+  int32_t tile_end[LM_NDET];  // cumulative tile counts
+};
+
+// Pixel pairs (row t, row t+1) of one column straight into an aligned VGPR
+// pair: ds_read2_b32 with offset1 = offset0 + STRIDE (dwords).  At most 15
+// LDS reads in flight (lgkmcnt is 4 bits); one wait at the end.
+template <int STRIDE, int Q>
+DEV void lds_pair(lm_f2& dst, unsigned base) {
+  static_assert(Q + STRIDE <= 255, "ds_read2_b32 offset range");
+  if constexpr (Q >= 15) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
+  asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(dst) : "v"(base), "i"(Q), "i"(Q + STRIDE) : "memory");
+}
+
+template <int STRIDE, int N, int... Qs>
+DEV void lds_pairs_impl(lm_f2 (&px)[N], unsigned base, std::integer_sequence<int, Qs...>) {
+  (lds_pair<STRIDE, Qs>(px[Qs], base), ...);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int STRIDE, int N>
+DEV void lds_pairs(lm_f2 (&px)[N], unsigned base) {
+  lds_pairs_impl<STRIDE, N>(px, base, std::make_integer_sequence<int, N>{});
+}
+
+// Tile fill: u8 ext-crop window (rows x cols from src, row pitch ew) -> fp32
+// LDS (row stride `stride`).  16-byte aligned vector loads, all of a round
+// issued before any is consumed (a workgroup's fill is one or two load
+// latencies, not one per 4 bytes), then unpacked with v_cvt_f32_ubyte*.
+// ew and the ext-crop base are multiples of 16; src itself need not be.
+// Reads up to 15 bytes past a row's last column (inside the padded row or the
+// next; the ext buffer has slack after its last slot).
+DEV void tile_fill_f32(float* __restrict__ lds, int stride, const uint8_t* __restrict__ src, int ew, int rows,
+                       int cols) {
+  const int mis = (int)((uintptr_t)src & 15);
+  const uint8_t* __restrict__ a = src - mis;
+  const int nch = (mis + cols + 15) >> 4;
+  const int total = rows * nch;
+  for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+      if (e < total) {
+        const int r = e / nch, ch = e - r * nch;
+        v[u] = *reinterpret_cast<const uint4*>(a + (int64_t)r * ew + ch * 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+      if (e < total) {
+        const int r = e / nch, ch = e - r * nch;
+        const int c0 = ch * 16 - mis;
+        float* __restrict__ o = lds + r * stride + c0;
+        const unsigned w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (c0 + k >= 0 && c0 + k < cols) o[k] = (float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+      }
+    }
+  }
+}
+
+// Which detector of the group a block works on, and its tile origin.
+struct CorrTile {
+  int d, oy0, ox0;
+};
+DEV CorrTile corr_tile(const LmConst& K, const LmDetGroup& G) {
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  const int lt = blockIdx.x - tb;
+  const int tx = K.det[d].tiles_x;
+  return CorrTile{d, (lt / tx) * LM_TH, (lt % tx) * LM_TW};
+}
+
+DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext, int64_t ext_slot_bytes, int slot,
+                            int oy0, int ox0) {
+  return ext + (int64_t)slot * ext_slot_bytes + (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+         (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
+}
+
+// ---------------------------------------------------------------- k_corr_pk
+// Packed-FP32 correlation.  gfx950 issues one v_fma_f32 (wave64) per 4 cycles
+// per SIMD; v_pk_fma_f32 does two FMAs per lane in the same slot.  Each
+// accumulator pair holds two vertically adjacent outputs (rows 2p, 2p+1) of
+// one column: for tap (i, j) both use weight w[i][j] (SGPR, broadcast) and
+// pixels (t, t+1) of one column, which one ds_read2_b32 loads into an aligned
+// register pair.  192 threads as 16 (x) x 12 (y), each 5 columns x 4 rows: an
+// 80x48 output tile per workgroup; the input window (48+kh-1 rows x 80+KW-1
+// columns) is converted to fp32 once into LDS.
+template <int KW, bool UNF>
+__global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_pk(const LmConst* __restrict__ Kp, const LmDetGroup G,
+                                                             const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                             const float* __restrict__ weights, int s0,
+                                                             unsigned long long* __restrict__ keys,
+                                                             int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin,
+                                                             int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  extern __shared__ float lds[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  const CorrTile T = corr_tile(K, G);
+  const LmDet D = K.det[T.d];
+  const int oy0 = T.oy0, ox0 = T.ox0;
+  constexpr int cols = LM_TW + KW - 1;
+  constexpr int STR = pk_stride(cols);
+  const int rows = LM_TH + D.kh - 1;
+  tile_fill_f32(lds, STR, corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0), K.ext_w[D.view], rows, cols);
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
+  lm_f2 acc[PK_R / 2][PK_C];
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) acc[p][c] = (lm_f2){D.delta, D.delta};
+  const float* __restrict__ W = weights + D.w_off;
+  const int kh = D.kh, kwp = D.kwp;
+  lm_f2 px[PK_C + KW - 1];
+  for (int t = 0; t < kh + PK_R - 2; ++t) {
+    const float* p0 = lds + (ly * PK_R + t) * STR + lx * PK_C;
+    const unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p0;
+    lds_pairs<STR, PK_C + KW - 1>(px, base);
+#pragma unroll
+    for (int p = 0; p < PK_R / 2; ++p) {
+      const int i = t - 2 * p;
+      if (i >= 0 && i < kh) {
+        const float* wr = W + i * kwp;
+#pragma unroll
+        for (int j = 0; j < KW; ++j) {
+          const float w = wr[j];
+          const lm_f2 w2 = (lm_f2){w, w};
+#pragma unroll
+          for (int c = 0; c < PK_C; ++c) acc[p][c] = corr_tap<UNF>(acc[p][c], w2, px[c + j]);
+        }
+      }
+    }
+  }
+  float accf[PK_R][PK_C];
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) {
+      accf[2 * p][c] = acc[p][c].x;
+      accf[2 * p + 1][c] = acc[p][c].y;
+    }
+  corr_epilogue<PK_R, PK_C>(K, D, accf, lds, STR, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
+                            &s_cnt, &s_base, nullptr, 0);
+}
+
+// ---------------------------------------------------------------- k_corr_gen
+// Any detector size.  Same thread shape and arithmetic as k_corr_pk, but the
+// width is a runtime value (taps in chunks of LM_JC = 4 columns over the
+// zero-padded row of kwp weights) and the detector rows are processed in
+// chunks of D.chunk_rows, each with its own LDS window of 48 + chunk - 1 rows,
+// so a detector of any height fits.  Each output still visits its taps in
+// row-major order (chunks in order, rows in order, columns in order).
+template <bool UNF>
+__global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __restrict__ Kp, const LmDetGroup G,
+                                                              const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                              const float* __restrict__ weights, int s0,
+                                                              unsigned long long* __restrict__ keys,
+                                                              int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin,
+                                                              int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  extern __shared__ float lds[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  const CorrTile T = corr_tile(K, G);
+  const LmDet D = K.det[T.d];
+  const int oy0 = T.oy0, ox0 = T.ox0;
+  const int kh = D.kh, kwp = D.kwp, ch = D.chunk_rows;
+  const int cols = LM_TW + kwp - 1, stride = pk_stride(cols);
+  const int ew = K.ext_w[D.view];
+  const uint8_t* __restrict__ src = corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0);
+  const float* __restrict__ W = weights + D.w_off;
+  if (threadIdx.x == 0) s_cnt = 0;
+  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
+  lm_f2 acc[PK_R / 2][PK_C];
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) acc[p][c] = (lm_f2){D.delta, D.delta};
+  for (int i0 = 0; i0 < kh; i0 += ch) {
+    const int cn = min(ch, kh - i0);
+    __syncthreads();  // the previous chunk's LDS reads are done
+    tile_fill_f32(lds, stride, src + (int64_t)i0 * ew, ew, LM_TH + cn - 1, cols);
+    __syncthreads();
+    for (int t = 0; t < cn + PK_R - 2; ++t) {
+      const float* p0 = lds + (ly * PK_R + t) * stride + lx * PK_C;
+      for (int jc = 0; jc < kwp; jc += LM_JC) {
+        lm_f2 px[PK_C + LM_JC - 1];
+#pragma unroll
+        for (int q = 0; q < PK_C + LM_JC - 1; ++q) px[q] = (lm_f2){p0[jc + q], p0[jc + q + stride]};
+#pragma unroll
+        for (int p = 0; p < PK_R / 2; ++p) {
+          const int i = t - 2 * p;
+          if (i >= 0 && i < cn) {
+            const float* wr = W + (int64_t)(i0 + i) * kwp + jc;
+#pragma unroll
+            for (int j = 0; j < LM_JC; ++j) {
+              const float w = wr[j];
+              const lm_f2 w2 = (lm_f2){w, w};
+#pragma unroll
+              for (int c = 0; c < PK_C; ++c) acc[p][c] = corr_tap<UNF>(acc[p][c], w2, px[c + j]);
+            }
+          }
+        }
+      }
+    }
+  }
+  float accf[PK_R][PK_C];
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) {
+      accf[2 * p][c] = acc[p][c].x;
+      accf[2 * p + 1][c] = acc[p][c].y;
+    }
+  // the mask pixels come from the ext crop (the LDS window holds only the last chunk)
+  const uint8_t* msrc = ext + (int64_t)slot * ext_slot_bytes + (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                        (int64_t)(D.m_y + oy0) * ew + (D.m_x + ox0);
+  corr_epilogue<PK_R, PK_C>(K, D, accf, nullptr, 0, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
+                            &s_cnt, &s_base, msrc, ew);
+}
+
+// ---------------------------------------------------------------- dispatch
+// Widths with a specialised k_corr_pk (detectors up to 64 rows); every other
+// detector runs k_corr_gen.
+#define LM_KW_LIST(X)                                                                                             \
+  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
+      X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+#define LM_PK_MAX_KH 64
+
+static inline bool corr_specialised(int kw, int kh) {
+  if (kh > LM_PK_MAX_KH) return false;
+  switch (kw) {
+#define LM_KW_CASE(n) case n:
+    LM_KW_LIST(LM_KW_CASE)
+#undef LM_KW_CASE
+    return true;
+    default:
+      return false;
+  }
+}
+
+static inline const void* corr_kernel(int kw, int kh, bool unf) {
+  if (corr_specialised(kw, kh)) switch (kw) {
+#define LM_KW_CASE(n) \
+  case n:             \
+    return unf ? (const void*)&k_corr_pk<n, true> : (const void*)&k_corr_pk<n, false>;
+      LM_KW_LIST(LM_KW_CASE)
+#undef LM_KW_CASE
+      default:
+        break;
+    }
+  return unf ? (const void*)&k_corr_gen<true> : (const void*)&k_corr_gen<false>;
+}
+
+// Launch the correlation for one detector group (all detectors of one width
+// that run the same kernel).
+static inline hipError_t launch_corr(const void* fn, dim3 grid, size_t lds, hipStream_t st, const LmConst* K,
+                                     const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes,
+                                     const float* weights, int s0, unsigned long long* keys, int32_t* n_pos,
+                                     uint8_t* tailbin, int64_t tailbin_slot_bytes) {
+  void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
+                  (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
+  return hipLaunchKernel(fn, grid, dim3(LM_CORR_THREADS), args, lds, st);
+}
+
+// Debug copy of raw scores (lm_debug_scores): the same chain per output,
+// computed straight from the ext crops in global memory (no LDS, any size).
+template <bool UNF>
+__global__ __launch_bounds__(256) void k_corr_dbg(const LmConst* __restrict__ Kp, const uint8_t* __restrict__ ext,
+                                                  int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
+                                                  float* __restrict__ dbg, const int64_t* __restrict__ dbg_off,
+                                                  int64_t dbg_slot_floats) {
+  const LmConst& K = *Kp;
+  const int slot = s0 + blockIdx.y;
+  const int d = blockIdx.z;
+  const LmDet D = K.det[d];
+  const int64_t n = (int64_t)D.oh * D.ow;
+  const int ew = K.ext_w[D.view];
+  const uint8_t* __restrict__ base =
+      ext + (int64_t)slot * ext_slot_bytes + (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0);
+  const float* __restrict__ W = weights + D.w_off;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int y = (int)(e / D.ow), x = (int)(e % D.ow);
+    const uint8_t* src = base + (int64_t)(D.in_y + y) * ew + (D.in_x + x);
+    float a = D.delta;
+    for (int i = 0; i < D.kh; ++i)
+      for (int j = 0; j < D.kw; ++j) a = corr_tap1<UNF>(a, W[i * D.kwp + j], (float)src[(int64_t)i * ew + j]);
+    dbg[(int64_t)slot * dbg_slot_floats + dbg_off[d] + e] = a;
+  }
+}

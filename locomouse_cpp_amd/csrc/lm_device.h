@@ -40,6 +40,7 @@ struct LmDet {
   int32_t m_y, m_x;    // ext-crop coords of the I_*_MOUSE pixel of output (0,0)
   int32_t tiles_x, tiles_y, tile_base;
   int32_t box_w, box_h;  // NMS box (detector cols, rows)
+  int32_t chunk_rows;    // k_corr_gen: detector rows per LDS window
 };
 
 struct LmConst {
@@ -57,6 +58,7 @@ struct LmConst {
   int32_t flip;
   // tail
   int32_t tail_w, tail_hb, tail_hs;  // tail box width, bottom/side heights
+  int32_t tail_cap, tail_ntc;        // k_tail: runs held in LDS, 32-column tiles per segment
   int32_t connectivity;
   // per-list capacities (= output area) and list offsets inside a slot's key area
   int32_t list_cap[LM_NLIST];
@@ -75,6 +77,10 @@ struct LmConst {
   int32_t size_b[LM_NFEAT][2];   // detector (cols, rows) bottom
   int32_t size_s[LM_NFEAT][2];   // side
   double prior[5][7];            // location_prior rows
+  // transform_gray_values with a CV_8U table: LUT applied in place to the
+  // bottom crop (LocoMouse_class.cpp:1445-1448)
+  int32_t gray_lut_on;
+  uint8_t gray_lut[256];
 };
 
 // per-slot frame info (uploaded per batch)

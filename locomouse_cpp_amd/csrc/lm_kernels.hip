@@ -1,9 +1,11 @@
 // lm_kernels.hip — gfx950 kernels of the LocoMouse per-frame detection path.
 //
 // Batch pipeline (one launch each, grid over frame slots; see lm_device.h):
-//   k_minmax_lut  per-frame min/max of sat(F - BKG) -> normalize LUT (+ TM imadjust)
+//   k_minmax      per-frame min/max of sat(F - BKG), frames split over workgroups
+//   k_lut         -> normalize LUT (+ TM imadjust)
 //                 LocoMouse_class.cpp:1304-1310, TM.cpp:247, :3204-3242
-//   k_ingest      calibration gather + flip + LUT -> extended padded crops (u8)
+//   k_ingest      calibration gather + flip + LUT (+ the in-place grey-level LUT of
+//                 transform_gray_values) -> extended padded crops (u8)
 //                 :1316-1327 (correctImage :1337-1406), cropBoundingBox :1408-1478
 //   k_corr        all six filter2D detectors, fp32 row-major FMA chains, LDS-tiled;
 //                 epilogue: brightness mask + score>0 compaction / tail binarisation
@@ -43,1538 +45,486 @@ DEV uint8_t ipad_pixel(const uint8_t* __restrict__ F, const uint8_t* __restrict_
   return lut[f > b ? f - b : 0];
 }
 
-DEV float wave_min_u32(unsigned v) {
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
-  return v;
-}
-
-// ------------------------------------------------------------ k_minmax_lut
-// One 1024-thread block per frame slot.  16-byte loads of frame and
-// background; the per-frame LUT folds normalize(NORM_MINMAX) -> convertTo
-// (sat_u8(cvRound((float)p*(float)scale + (float)shift)), OpenCV 3.x) and the
-// LocoMouse_TM imadjust LUT.
-__global__ __launch_bounds__(1024) void k_minmax_lut(const uint8_t* const* __restrict__ frame_ptr,
-                                                     const uint8_t* __restrict__ bkg, int npix, int s0,
-                                                     const uint8_t* __restrict__ adj, int use_adj,
-                                                     uint8_t* __restrict__ luts) {
-  const int slot = s0 + blockIdx.x;
+// --------------------------------------------------------------- k_minmax
+// normalize(F, F, 0, 255, NORM_MINMAX, CV_8UC1) after subtract(F, BKG, F)
+// (LocoMouse_class.cpp:1304-1310) needs min and max of sat(F - BKG) per frame.
+// Each frame is split over LM_MM_SPLIT workgroups (16-byte loads of frame and
+// background, wave and block reductions); each workgroup writes its partial
+// min/max pair, and k_lut folds the LM_MM_SPLIT pairs of a slot into its LUT.
+#define LM_MM_SPLIT 8
+#define LM_MM_THREADS 256
+__global__ __launch_bounds__(LM_MM_THREADS) void k_minmax(const uint8_t* const* __restrict__ frame_ptr,
+                                                          const uint8_t* __restrict__ bkg, int npix, int s0,
+                                                          unsigned* __restrict__ mm) {
+  const int slot = s0 + blockIdx.y;
   const uint8_t* __restrict__ F = frame_ptr[slot];
-  unsigned mn = 255, mx = 0;
   const int nvec = npix >> 4;
+  const int per = (nvec + LM_MM_SPLIT - 1) / LM_MM_SPLIT;
+  const int v0 = blockIdx.x * per, v1 = min(nvec, v0 + per);
   const uint4* F4 = reinterpret_cast<const uint4*>(F);
   const uint4* B4 = reinterpret_cast<const uint4*>(bkg);
-  for (int i = threadIdx.x; i < nvec; i += blockDim.x) {
-    uint4 f = F4[i];
-    uint4 b = B4[i];
-    unsigned fw[4] = {f.x, f.y, f.z, f.w}, bw[4] = {b.x, b.y, b.z, b.w};
+  unsigned mn = 255, mx = 0;
+  auto fold = [&](unsigned fw, unsigned bw) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int k = 0; k < 4; ++k) {
+      const unsigned fv = (fw >> (8 * k)) & 255u, bv = (bw >> (8 * k)) & 255u;
+      const unsigned d = fv > bv ? fv - bv : 0u;
+      mn = min(mn, d);
+      mx = max(mx, d);
+    }
+  };
+  int i = v0 + threadIdx.x;
+  for (; i + 3 * LM_MM_THREADS < v1; i += 4 * LM_MM_THREADS) {  // four 16-byte loads in flight per lane
+    uint4 f[4], b[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        unsigned fv = (fw[q] >> (8 * k)) & 255u, bv = (bw[q] >> (8 * k)) & 255u;
-        unsigned d = fv > bv ? fv - bv : 0u;
-        mn = min(mn, d);
-        mx = max(mx, d);
-      }
+    for (int u = 0; u < 4; ++u) {
+      f[u] = F4[i + u * LM_MM_THREADS];
+      b[u] = B4[i + u * LM_MM_THREADS];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      fold(f[u].x, b[u].x);
+      fold(f[u].y, b[u].y);
+      fold(f[u].z, b[u].z);
+      fold(f[u].w, b[u].w);
     }
   }
-  for (int i = (nvec << 4) + threadIdx.x; i < npix; i += blockDim.x) {
-    unsigned fv = F[i], bv = bkg[i];
-    unsigned d = fv > bv ? fv - bv : 0u;
-    mn = min(mn, d);
-    mx = max(mx, d);
+  for (; i < v1; i += LM_MM_THREADS) {
+    const uint4 f = F4[i], b = B4[i];
+    fold(f.x, b.x);
+    fold(f.y, b.y);
+    fold(f.z, b.z);
+    fold(f.w, b.w);
   }
+  if (blockIdx.x == LM_MM_SPLIT - 1)  // the bytes past the last 16-byte word
+    for (int q = (nvec << 4) + threadIdx.x; q < npix; q += LM_MM_THREADS) {
+      const unsigned fv = F[q], bv = bkg[q];
+      const unsigned d = fv > bv ? fv - bv : 0u;
+      mn = min(mn, d);
+      mx = max(mx, d);
+    }
   for (int o = 32; o > 0; o >>= 1) {
     mn = min(mn, (unsigned)__shfl_xor((int)mn, o));
     mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
   }
-  __shared__ unsigned smn[16], smx[16];
+  __shared__ unsigned smn[LM_MM_THREADS / 64], smx[LM_MM_THREADS / 64];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (lane == 0) {
     smn[wid] = mn;
     smx[wid] = mx;
   }
   __syncthreads();
-  if (threadIdx.x < 256) {
-    unsigned a = 255, b = 0;
-    const int nw = blockDim.x >> 6;
-    for (int w = 0; w < nw; ++w) {
-      a = min(a, smn[w]);
-      b = max(b, smx[w]);
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < LM_MM_THREADS / 64; ++w) {
+      mn = min(mn, smn[w]);
+      mx = max(mx, smx[w]);
     }
-    const double smin = (double)a, smax = (double)b, dmin = 0.0, dmax = 255.0;
-    const double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0.0);
-    const double shift = dmin - smin * scale;
-    const int p = threadIdx.x;
-    int v;
-    if (fabs(scale - 1.0) < 2.220446049250313e-16 && fabs(shift) < 2.220446049250313e-16) {
-      v = p;  // convertTo noScale -> copy
-    } else {
-      const float sf = (float)scale, hf = (float)shift;
-      float t = __fmul_rn((float)p, sf);
-      t = __fadd_rn(t, hf);
-      int iv = (int)rintf(t);
-      v = iv < 0 ? 0 : (iv > 255 ? 255 : iv);
-    }
-    if (use_adj) v = adj[v];
-    luts[slot * 256 + p] = (uint8_t)v;
+    mm[2 * (slot * LM_MM_SPLIT + blockIdx.x)] = mn;
+    mm[2 * (slot * LM_MM_SPLIT + blockIdx.x) + 1] = mx;
   }
 }
 
+// Entry p of a frame's LUT from its min/max: normalize(NORM_MINMAX) ->
+// convertTo(CV_8U, scale, shift) = sat_u8(cvRound((float)p*(float)scale +
+// (float)shift)) (OpenCV 3.x, unfused), the noScale copy when scale == 1 and
+// shift == 0, then the LocoMouse_TM imadjust LUT (methods 1/2, TM.cpp:247).
+DEV int norm_lut_entry(unsigned mnv, unsigned mxv, int p, const uint8_t* adj, int use_adj) {
+  const double smin = (double)mnv, smax = (double)mxv, dmin = 0.0, dmax = 255.0;
+  const double scale = (dmax - dmin) * (smax - smin > 2.220446049250313e-16 ? 1. / (smax - smin) : 0.0);
+  const double shift = dmin - smin * scale;
+  int v;
+  if (fabs(scale - 1.0) < 2.220446049250313e-16 && fabs(shift) < 2.220446049250313e-16) {
+    v = p;  // convertTo noScale -> copy
+  } else {
+    const float sf = (float)scale, hf = (float)shift;
+    float t = __fmul_rn((float)p, sf);
+    t = __fadd_rn(t, hf);
+    const int iv = (int)rintf(t);
+    v = iv < 0 ? 0 : (iv > 255 ? 255 : iv);
+  }
+  return use_adj ? adj[v] : v;
+}
+
+// k_lut: the 256-entry LUT of every slot from k_minmax's partial min/max
+// pairs.  4 slots per block.
+__global__ __launch_bounds__(256) void k_lut(const unsigned* __restrict__ mm, int s0, int s_end,
+                                             const uint8_t* __restrict__ adj, int use_adj, uint8_t* __restrict__ luts) {
+  for (int s = s0 + blockIdx.x * 4; s < min(s_end, s0 + (int)blockIdx.x * 4 + 4); ++s) {
+    unsigned mn = 255, mx = 0;
+#pragma unroll
+    for (int b = 0; b < LM_MM_SPLIT; ++b) {
+      mn = min(mn, mm[2 * (s * LM_MM_SPLIT + b)]);
+      mx = max(mx, mm[2 * (s * LM_MM_SPLIT + b) + 1]);
+    }
+    luts[s * 256 + threadIdx.x] = (uint8_t)norm_lut_entry(mn, mx, threadIdx.x, adj, use_adj);
+  }
+}
+
+// I_PAD(R, C) of frame slot `sl` as the per-frame steps after
+// cropBoundingBox see it: transform_gray_values with a CV_8U table rewrites
+// the frame's bottom crop I_BOTTOM_MOUSE in place (LUT(I_BOTTOM_MOUSE, table,
+// I_BOTTOM_MOUSE), LocoMouse_class.cpp:1445-1448), so that rectangle of I_PAD
+// holds table[v] for the rest of the frame and in I_PREV_PAD for the next.
+DEV bool in_gray_rect(const LmConst& K, const LmSlot& sl, int R, int C) {
+  const int y = R - sl.crop_y[0] - K.unpad_y[0], x = C - sl.crop_x[0] - K.unpad_x[0];
+  return (unsigned)y < (unsigned)K.bb_bottom_h && (unsigned)x < (unsigned)K.bb_bottom_w;
+}
+
+DEV uint8_t ipad_pixel_t(const uint8_t* __restrict__ F, const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+                         const uint8_t* lut, const LmConst& K, const LmSlot& sl, int R, int C) {
+  const uint8_t v = ipad_pixel(F, bkg, cal, lut, K, R, C);
+  return K.gray_lut_on && in_gray_rect(K, sl, R, C) ? K.gray_lut[v] : v;
+}
+
 // ---------------------------------------------------------------- k_ingest
-// Builds the extended padded crops of both views for each slot: every I_PAD
-// pixel any detector tap reads.  Each thread writes 4 consecutive bytes.
+// Builds the extended padded crops of both views for LM_INGEST_FB consecutive
+// slots: every I_PAD pixel any detector tap reads (readFrame's correctImage +
+// flip, :1316-1327 / :1337-1406; cropBoundingBox, :1408-1478).  Each thread
+// owns 16 consecutive crop bytes (one 16-byte store per frame).  The
+// calibration index and background byte of each are loaded once and reused
+// for every slot whose crop sits at the same place (always, with a provided
+// bounding box); per frame only the frame gather, the LUTs and the store
+// remain.  Where the 16 source pixels are consecutive in the frame (a
+// calibration map that is locally a translation, flipped or not) the gather
+// is five aligned dword loads instead of sixteen byte loads.
+#define LM_INGEST_FB 8
+#define LM_INGEST_VEC 16
 __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
                                                 const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
                                                 const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
-                                                int s0, uint8_t* __restrict__ ext, int64_t ext_slot_bytes) {
+                                                int s0, int s_end, uint8_t* __restrict__ ext, int64_t ext_slot_bytes) {
   const LmConst& K = *Kp;
-  const int slot = s0 + blockIdx.y;
-  __shared__ uint8_t lut[256];
-  lut[threadIdx.x] = luts[slot * 256 + threadIdx.x];
-  __syncthreads();
-  const uint8_t* __restrict__ F = frame_ptr[slot];
-  const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
-  const int64_t etot = e0 + (int64_t)K.ext_h[1] * K.ext_w[1];
-  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (q >= etot) return;
-  const int v = q < e0 ? 0 : 1;
-  const int64_t qq = v == 0 ? q : q - e0;
-  const int er = (int)(qq / K.ext_w[v]);
-  const int ec = (int)(qq % K.ext_w[v]);  // multiple of 4 (ext_w % 16 == 0)
-  const LmSlot sl = slots[slot];
-  const int R = sl.crop_y[v] + K.ext_oy[v] + er;
-  const int C0 = sl.crop_x[v] + K.ext_ox[v] + ec;
-  uint32_t word = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) word |= (uint32_t)ipad_pixel(F, bkg, cal, lut, K, R, C0 + k) << (8 * k);
-  *reinterpret_cast<uint32_t*>(ext + (int64_t)slot * ext_slot_bytes + q) = word;
-}
-
-// ---------------------------------------------------------------- k_ingest_fb
-// k_ingest for LM_INGEST_FB consecutive slots per thread: the calibration
-// index and background byte of a crop pixel are loaded once and reused for
-// every slot whose crop sits at the same place (always, with a provided
-// bounding box); only the frame gather and the per-frame LUT are per slot.
-#define LM_INGEST_FB 8
-__global__ __launch_bounds__(256) void k_ingest_fb(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
-                                                   const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
-                                                   const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
-                                                   int s0, int s_end, int fb, uint8_t* __restrict__ ext,
-                                                   int64_t ext_slot_bytes) {
-  const LmConst& K = *Kp;
-  const int sb = s0 + blockIdx.y * fb;
-  const int nf = min(fb, s_end - sb);
+  const int sb = s0 + blockIdx.y * LM_INGEST_FB;
+  const int nf = min(LM_INGEST_FB, s_end - sb);
   __shared__ uint8_t lut[LM_INGEST_FB][256];
+  __shared__ uint8_t glut[256];
   for (int i = threadIdx.x; i < nf * 256; i += blockDim.x) lut[i >> 8][i & 255] = luts[(sb + (i >> 8)) * 256 + (i & 255)];
+  glut[threadIdx.x] = K.gray_lut[threadIdx.x];
   __syncthreads();
   const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
   const int64_t etot = e0 + (int64_t)K.ext_h[1] * K.ext_w[1];
-  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * LM_INGEST_VEC;
   if (q >= etot) return;
   const int v = q < e0 ? 0 : 1;
   const int64_t qq = v == 0 ? q : q - e0;
   const int er = (int)(qq / K.ext_w[v]);
-  const int ec = (int)(qq % K.ext_w[v]);  // multiple of 4 (ext_w % 16 == 0)
-  int idx[4] = {-1, -1, -1, -1}, bv[4] = {0, 0, 0, 0};  // defined before the first crop test
+  const int ec = (int)(qq % K.ext_w[v]);  // multiple of 16 (ext_w % 16 == 0)
+  int idx[LM_INGEST_VEC];
+  uint8_t bv[LM_INGEST_VEC];
+  int run = 0;  // 1: idx[k] = idx[0] + k, -1: idx[k] = idx[0] - k, 0: gather
   int px = INT32_MIN, py = INT32_MIN;
   for (int f = 0; f < nf; ++f) {
     const int slot = sb + f;
     const LmSlot sl = slots[slot];
+    const int R = sl.crop_y[v] + K.ext_oy[v] + er;
+    const int C0 = sl.crop_x[v] + K.ext_ox[v] + ec;
     if (sl.crop_x[v] != px || sl.crop_y[v] != py) {  // crop moved: recompute the gather indices
       px = sl.crop_x[v];
       py = sl.crop_y[v];
-      const int R = py + K.ext_oy[v] + er - K.pad_pre_rows;
+      const int r = R - K.pad_pre_rows;
+      bool up = true, down = true;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int c = px + K.ext_ox[v] + ec + k - K.pad_pre_cols;
-        if (R < 0 || R >= K.n_rows || c < 0 || c >= K.n_cols) {
+      for (int k = 0; k < LM_INGEST_VEC; ++k) {
+        int c = C0 + k - K.pad_pre_cols;
+        if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) {
           idx[k] = -1;
+          bv[k] = 0;
         } else {
           if (K.flip) c = K.n_cols - 1 - c;
-          idx[k] = cal[R * K.n_cols + c];
+          idx[k] = cal[r * K.n_cols + c];
           bv[k] = bkg[idx[k]];
         }
+        up = up && idx[k] >= 0 && idx[k] == idx[0] + k;
+        down = down && idx[k] >= 0 && idx[k] == idx[0] - k;
       }
+      run = up ? 1 : (down ? -1 : 0);
+      const int lo = up ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
+      if (run != 0 && (lo & ~3) + 20 > K.video_rows * K.video_cols) run = 0;  // the fifth dword would pass the frame end
     }
     const uint8_t* __restrict__ F = frame_ptr[slot];
-    uint32_t word = 0;
+    uint8_t pix[LM_INGEST_VEC];
+    if (run != 0) {
+      // the 16 source bytes span [lo, lo + 16): five aligned dwords cover them
+      const int lo = run > 0 ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(F + (lo & ~3));
+      uint32_t d[5];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (idx[k] >= 0) {
-        const int fv = F[idx[k]];
-        word |= (uint32_t)lut[f][fv > bv[k] ? fv - bv[k] : 0] << (8 * k);
+      for (int u = 0; u < 5; ++u) d[u] = w[u];
+      const int sh = lo & 3;
+#pragma unroll
+      for (int k = 0; k < LM_INGEST_VEC; ++k) {
+        const int o = sh + (run > 0 ? k : LM_INGEST_VEC - 1 - k);
+        pix[k] = (uint8_t)(d[o >> 2] >> (8 * (o & 3)));
       }
-    }
-    *reinterpret_cast<uint32_t*>(ext + (int64_t)slot * ext_slot_bytes + q) = word;
-  }
-}
-
-// ------------------------------------------------------------------ k_corr
-// One block = one 80x48 output tile of one detector of one slot; 256 threads
-// as 16x16, each LM_R rows x LM_C columns.  The input tile is staged in LDS as
-// float.  For every output the taps are accumulated as
-//     acc = (float)(-rho);  for i in rows, j in cols: acc = fmaf(w[i][j], I, acc)
-// i.e. exactly cv::filter2D's row-major chain (zero-padded taps add +0).
-// Pixel rows are walked once per thread (t = r + i), so a loaded row feeds all
-// LM_R accumulator rows; weights are wave-uniform scalar loads.
-#define LM_MAXK 64
-
-// Shared epilogue: point detectors apply the brightness mask of
-// detectBottom/SideCandidates (threshold(25.5 -> 25, BINARY_INV), :782/:817;
-// setTo(0, mask) :849/:864) and append every score > 0 as a sort key
-// (~score_bits << 32 | row-major index) to the frame's list; tail detectors
-// write the binarised map (threshold(>0) + convertTo 8U, :2593-2598).
-// Two passes over a register bitmask keep the accumulators statically indexed.
-template <int R_, int C_>
-DEV void corr_epilogue(const LmConst& K, const LmDet& D, const float (&acc)[R_][C_], const float* lds, int stride, int ly,
-                       int lx, int oy0, int ox0, int slot, unsigned long long* __restrict__ keys,
-                       int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes, int* s_cnt,
-                       int* s_base) {
-  static_assert(R_ * C_ <= 32, "bitmask");
-  const int my = D.m_y - D.in_y, mx = D.m_x - D.in_x;  // I_*_MOUSE pixel inside the LDS tile
-  if (D.kind != 0) {
-    uint8_t* __restrict__ tb = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
-#pragma unroll
-    for (int r = 0; r < R_; ++r)
-#pragma unroll
-      for (int c = 0; c < C_; ++c) {
-        const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
-        if (y < D.oh && x < D.ow) tb[(int64_t)y * D.ow + x] = acc[r][c] > 0.0f ? 1 : 0;
-      }
-    return;
-  }
-  unsigned bits = 0;
-#pragma unroll
-  for (int r = 0; r < R_; ++r)
-#pragma unroll
-    for (int c = 0; c < C_; ++c) {
-      const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
-      const float pix = lds[(ly * R_ + r + my) * stride + lx * C_ + c + mx];
-      if (y < D.oh && x < D.ow && pix > 25.0f && acc[r][c] > 0.0f) bits |= 1u << (r * C_ + c);
-    }
-  const int nk = __popc(bits);
-  const int off = nk ? atomicAdd(s_cnt, nk) : 0;
-  __syncthreads();
-  if (threadIdx.x == 0) *s_base = *s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], *s_cnt) : 0;
-  __syncthreads();
-  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + *s_base + off;
-  int k = 0;
-#pragma unroll
-  for (int r = 0; r < R_; ++r)
-#pragma unroll
-    for (int c = 0; c < C_; ++c)
-      if (bits & (1u << (r * C_ + c))) {
-        const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
-        kl[k++] = ((unsigned long long)(~__float_as_uint(acc[r][c])) << 32) | (unsigned)(y * D.ow + x);
-      }
-}
-
-// LDS row stride of the packed kernel: == 4 (mod 8) so the two 16-lane row
-// groups of a ds_read2_b32 (4 rows apart) hit disjoint bank halves.
-__host__ __device__ inline int pk_stride(int cols) { return cols + ((4 - (cols & 7)) + 8) % 8; }
-
-struct LmDetGroup {
-  int32_t n;
-  int32_t ids[LM_NDET];
-  int32_t tile_end[LM_NDET];  // cumulative tile counts
-  int32_t skip_taps;          // diagnostics (LM_CORR_SKIP=1): no FMAs, fill + epilogue only
-};
-
-__global__ __launch_bounds__(256) void k_corr(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
-                                              int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
-                                              unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                              uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  extern __shared__ float lds[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  int gi = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
-      gi = k + 1;
-      tb = G.tile_end[k];
-    }
-  const int d = G.ids[gi];
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - tb;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1, cols = LM_TW + D.kwp - 1;
-  int stride = cols;
-  stride += (16 - (stride & 31) + 32) & 31;  // stride == 16 (mod 32): conflict-free row pairs
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  // stage: 4 bytes per thread-iteration (columns padded to a multiple of 4)
-  const int cols4 = (cols + 3) >> 2;
-  for (int e = threadIdx.x; e < rows * cols4; e += 256) {
-    const int r = e / cols4, c4 = (e - r * cols4) << 2;
-    const uint8_t* p = src + (int64_t)r * ew + c4;
-    float* o = lds + r * stride + c4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c4 + k < stride) o[k] = (float)p[k];
-  }
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-
-  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
-  float acc[LM_R][LM_C];
-#pragma unroll
-  for (int r = 0; r < LM_R; ++r)
-#pragma unroll
-    for (int c = 0; c < LM_C; ++c) acc[r][c] = D.delta;
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  for (int t = 0; t < LM_R + kh - 1; ++t) {
-    const float* prow = lds + (ly * LM_R + t) * stride + lx * LM_C;
-    for (int jc = 0; jc < kwp; jc += LM_JC) {
-      float px[LM_C + LM_JC - 1];
-#pragma unroll
-      for (int q = 0; q < LM_C + LM_JC - 1; ++q) px[q] = prow[jc + q];
-#pragma unroll
-      for (int r = 0; r < LM_R; ++r) {
-        const int i = t - r;
-        if (i >= 0 && i < kh) {
-          const float* wr = W + i * kwp + jc;
-#pragma unroll
-          for (int j = 0; j < LM_JC; ++j) {
-            const float w = wr[j];
-#pragma unroll
-            for (int c = 0; c < LM_C; ++c) acc[r][c] = __builtin_fmaf(w, px[c + j], acc[r][c]);
-          }
-        }
-      }
-    }
-  }
-
-  corr_epilogue<LM_R, LM_C>(K, D, acc, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes, &s_cnt, &s_base);
-}
-
-// k_corr_kw: k_corr specialised on the detector width KW (a weight row is
-// fully unrolled: one scalar-load wait per detector row instead of one per
-// 4 taps).  One launch covers the detectors of one width (ids in G).
-
-template <int KW>
-__global__ __launch_bounds__(256) void k_corr_kw(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
-                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
-                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  extern __shared__ float lds[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  int gi = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
-      gi = k + 1;
-      tb = G.tile_end[k];
-    }
-  const int d = G.ids[gi];
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - tb;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
-  int stride = cols;
-  stride += (16 - (stride & 31) + 32) & 31;
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  const int cols4 = (cols + 3) >> 2;
-  for (int e = threadIdx.x; e < rows * cols4; e += 256) {
-    const int r = e / cols4, c4 = (e - r * cols4) << 2;
-    const uint8_t* p = src + (int64_t)r * ew + c4;
-    float* o = lds + r * stride + c4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c4 + k < stride) o[k] = (float)p[k];
-  }
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-
-  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
-  float acc[LM_R][LM_C];
-#pragma unroll
-  for (int r = 0; r < LM_R; ++r)
-#pragma unroll
-    for (int c = 0; c < LM_C; ++c) acc[r][c] = D.delta;
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  for (int t = 0; t < LM_R + kh - 1; ++t) {
-    const float* prow = lds + (ly * LM_R + t) * stride + lx * LM_C;
-    float px[LM_C + KW - 1];
-#pragma unroll
-    for (int q = 0; q < LM_C + KW - 1; ++q) px[q] = prow[q];
-#pragma unroll
-    for (int r = 0; r < LM_R; ++r) {
-      const int i = t - r;
-      if (i >= 0 && i < kh) {
-        const float* wr = W + i * kwp;
-#pragma unroll
-        for (int j = 0; j < KW; ++j) {
-          const float w = wr[j];
-#pragma unroll
-          for (int c = 0; c < LM_C; ++c) acc[r][c] = __builtin_fmaf(w, px[c + j], acc[r][c]);
-        }
-      }
-    }
-  }
-
-  corr_epilogue<LM_R, LM_C>(K, D, acc, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes, &s_cnt, &s_base);
-}
-
-// k_corr_pk: packed-FP32 correlation.  gfx950 issues one v_fma_f32 (wave64)
-// per 4 cycles per SIMD; v_pk_fma_f32 does two FMAs per lane in the same slot.
-// Each accumulator pair holds two vertically adjacent outputs (rows 2p, 2p+1)
-// of one column: for tap (i, j) both use weight w[i][j] (SGPR, broadcast) and
-// pixels (t, t+1) of one column, which one ds_read2_b32 loads into an aligned
-// register pair.  Every output still accumulates its taps in row-major order
-// with single-rounding FMAs, so results are bit-identical to k_corr.
-// 192 threads as 16 (x) x 12 (y), each 5 columns x 4 rows: the 80x48 tile.
-#define PK_C 5
-#define PK_R 4
-#define PK_TY 12
-
-typedef float lm_f2 __attribute__((ext_vector_type(2)));
-
-// Pixel pairs (row t, row t+1) of one column straight into an aligned VGPR
-// pair: ds_read2_b32 with offset1 = offset0 + STRIDE (dwords).  At most 15
-// LDS reads in flight (lgkmcnt is 4 bits); one wait at the end.
-constexpr int pk_stride_c(int cols) { return cols + ((4 - (cols & 7)) + 8) % 8; }
-
-template <int STRIDE, int Q>
-DEV void lds_pair(lm_f2& dst, unsigned base) {
-  static_assert(Q + STRIDE <= 255, "ds_read2_b32 offset range");
-  if constexpr (Q >= 15) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
-  asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(dst) : "v"(base), "i"(Q), "i"(Q + STRIDE) : "memory");
-}
-
-template <int STRIDE, int N, int... Qs>
-DEV void lds_pairs_impl(lm_f2 (&px)[N], unsigned base, std::integer_sequence<int, Qs...>) {
-  (lds_pair<STRIDE, Qs>(px[Qs], base), ...);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int STRIDE, int N>
-DEV void lds_pairs(lm_f2 (&px)[N], unsigned base) {
-  lds_pairs_impl<STRIDE, N>(px, base, std::make_integer_sequence<int, N>{});
-}
-
-// Tile fill: u8 ext-crop window (rows x cols from src, row pitch ew) -> fp32
-// LDS (row stride `stride`).  16-byte aligned vector loads, all of a round
-// issued before any is consumed (a workgroup's fill is one or two load
-// latencies, not one per 4 bytes), then unpacked with v_cvt_f32_ubyte*.
-// ew and the ext-crop base are multiples of 16; src itself need not be.
-// Reads up to 15 bytes past a row's last column (inside the padded row or the
-// next; the ext buffer has slack after its last slot).
-DEV void tile_fill_f32(float* __restrict__ lds, int stride, const uint8_t* __restrict__ src, int ew, int rows,
-                       int cols) {
-  const int mis = (int)((uintptr_t)src & 15);
-  const uint8_t* __restrict__ a = src - mis;
-  const int nch = (mis + cols + 15) >> 4;
-  const int total = rows * nch;
-  for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
-    uint4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
-      if (e < total) {
-        const int r = e / nch, ch = e - r * nch;
-        v[u] = *reinterpret_cast<const uint4*>(a + (int64_t)r * ew + ch * 16);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
-      if (e < total) {
-        const int r = e / nch, ch = e - r * nch;
-        const int c0 = ch * 16 - mis;
-        float* __restrict__ o = lds + r * stride + c0;
-        const unsigned w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-          if (c0 + k >= 0 && c0 + k < cols) o[k] = (float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-      }
-    }
-  }
-}
-
-template <int KW, bool WLDS, bool ASMLD = false>
-__global__ __launch_bounds__(192) void k_corr_pk(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
-                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
-                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  // WLDS: detector weights staged in LDS (broadcast reads) instead of scalar
-  // loads, so every lgkm wait is an in-order LDS wait the compiler can count.
-  extern __shared__ float lds[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  int gi = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
-      gi = k + 1;
-      tb = G.tile_end[k];
-    }
-  const int d = G.ids[gi];
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - tb;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
-  const int stride = pk_stride(cols);
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  tile_fill_f32(lds, stride, src, ew, rows, cols);
-  float* wl = lds + ((rows * stride + 3) & ~3);
-  if (WLDS)
-    for (int e = threadIdx.x; e < D.kh * D.kwp; e += blockDim.x) wl[e] = weights[D.w_off + e];
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-
-  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
-  lm_f2 acc[PK_R / 2][PK_C];
-#pragma unroll
-  for (int p = 0; p < PK_R / 2; ++p)
-#pragma unroll
-    for (int c = 0; c < PK_C; ++c) acc[p][c] = (lm_f2){D.delta, D.delta};
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  const int tend = (G.skip_taps & 1) ? 0 : kh + PK_R - 2;
-  lm_f2 px[PK_C + KW - 1];
-  for (int t = 0; t < tend; ++t) {
-    const float* p0 = lds + (ly * PK_R + t) * stride + lx * PK_C;
-    if ((G.skip_taps & 4) && t > 0) {
-      // diagnostics: pixel pairs of row 0 reused (no LDS traffic in the loop)
-    } else if constexpr (ASMLD) {
-      constexpr int STR = pk_stride_c(LM_TW + KW - 1);
-      const unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p0;
-      lds_pairs<STR, PK_C + KW - 1>(px, base);
     } else {
 #pragma unroll
-      for (int q = 0; q < PK_C + KW - 1; ++q) px[q] = (lm_f2){p0[q], p0[q + stride]};
+      for (int k = 0; k < LM_INGEST_VEC; ++k) pix[k] = idx[k] >= 0 ? F[idx[k]] : 0;
     }
+    uint32_t word[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int p = 0; p < PK_R / 2; ++p) {
-      const int i = t - 2 * p;
-      if (i >= 0 && i < kh) {
-        const float* wr = (WLDS ? wl : W) + ((G.skip_taps & 2) ? 0 : i * kwp);
-#pragma unroll
-        for (int j = 0; j < KW; ++j) {
-          const float w = wr[j];
-          const lm_f2 w2 = (lm_f2){w, w};
-#pragma unroll
-          for (int c = 0; c < PK_C; ++c) acc[p][c] = __builtin_elementwise_fma(w2, px[c + j], acc[p][c]);
-        }
+    for (int k = 0; k < LM_INGEST_VEC; ++k) {
+      uint32_t o = 0;
+      if (idx[k] >= 0) {
+        o = lut[f][pix[k] > bv[k] ? pix[k] - bv[k] : 0];
+        if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) o = glut[o];
+      } else if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) {
+        o = glut[0];  // only reachable through the pad (rejected on the host)
       }
+      word[k >> 2] |= o << (8 * (k & 3));
     }
-  }
-  float accf[PK_R][PK_C];
-#pragma unroll
-  for (int p = 0; p < PK_R / 2; ++p)
-#pragma unroll
-    for (int c = 0; c < PK_C; ++c) {
-      accf[2 * p][c] = acc[p][c].x;
-      accf[2 * p + 1][c] = acc[p][c].y;
-    }
-  corr_epilogue<PK_R, PK_C>(K, D, accf, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
-                            &s_cnt, &s_base);
-}
-
-// k_corr_p2: one row-pair per thread, 10 columns wide (192 threads as 8 x 24:
-// the same 80x48 tile).  Per input row-pair t only kernel row i = t is
-// needed, so the next row's weights are prefetched into SGPRs one iteration
-// ahead and the FMA block never waits on a scalar load.  LDS traffic: (KW+9)
-// ds_read2 per 10*KW packed FMAs.
-#define P2_C 10
-
-template <int KW>
-__global__ __launch_bounds__(192) void k_corr_p2(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
-                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
-                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  extern __shared__ float lds[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  int gi = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
-      gi = k + 1;
-      tb = G.tile_end[k];
-    }
-  const int d = G.ids[gi];
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - tb;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
-  const int stride = pk_stride(cols);
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  const int cols4 = (cols + 3) >> 2;
-  for (int e = threadIdx.x; e < rows * cols4; e += blockDim.x) {
-    const int r = e / cols4, c4 = (e - r * cols4) << 2;
-    const uint8_t* p = src + (int64_t)r * ew + c4;
-    float* o = lds + r * stride + c4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c4 + k < stride) o[k] = (float)p[k];
-  }
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-
-  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
-  lm_f2 acc[P2_C];
-#pragma unroll
-  for (int c = 0; c < P2_C; ++c) acc[c] = (lm_f2){D.delta, D.delta};
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  float wc[KW];
-#pragma unroll
-  for (int j = 0; j < KW; ++j) wc[j] = W[j];
-  constexpr int STR = pk_stride_c(LM_TW + KW - 1);
-  for (int t = 0; t < kh; ++t) {
-    const float* p0 = lds + (ly * 2 + t) * stride + lx * P2_C;
-    lm_f2 px[P2_C + KW - 1];
-    const unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p0;
-    lds_pairs<STR, P2_C + KW - 1>(px, base);
-    const float* wnr = W + min(t + 1, kh - 1) * kwp;
-    float wn[KW];
-#pragma unroll
-    for (int j = 0; j < KW; ++j) wn[j] = wnr[j];
-    __builtin_amdgcn_sched_barrier(0);  // scalar loads of row t+1 issue before the FMAs of row t
-#pragma unroll
-    for (int j = 0; j < KW; ++j) {
-      const lm_f2 w2 = (lm_f2){wc[j], wc[j]};
-#pragma unroll
-      for (int c = 0; c < P2_C; ++c) acc[c] = __builtin_elementwise_fma(w2, px[c + j], acc[c]);
-    }
-#pragma unroll
-    for (int j = 0; j < KW; ++j) wc[j] = wn[j];
-  }
-  float accf[2][P2_C];
-#pragma unroll
-  for (int c = 0; c < P2_C; ++c) {
-    accf[0][c] = acc[c].x;
-    accf[1][c] = acc[c].y;
-  }
-  corr_epilogue<2, P2_C>(K, D, accf, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
-                         &s_cnt, &s_base);
-}
-
-// k_corr_db: k_corr_p2's shape with the LDS loads double-buffered.  Two
-// pixel-pair buffers: while the FMAs of row-pair t run on one, the ds_read2
-// loads of row-pair t+1 fill the other, so a wave waits on LDS only when its
-// loads have not landed after a whole row of FMAs.  The detector weights of
-// both rows of an iteration are scalar-loaded first and consumed by an empty
-// asm statement, so the compiler's own lgkmcnt(0) for them comes before the
-// pixel loads are issued and never drains the pixel queue.
-template <int STRIDE, int... Qs>
-DEV void db_issue(lm_f2 (&px)[sizeof...(Qs)], unsigned base, std::integer_sequence<int, Qs...>) {
-  (lds_pair<STRIDE, Qs>(px[Qs], base), ...);
-}
-
-DEV void db_use_sgpr(float w) { asm volatile("; weight %0" ::"s"(w)); }
-
-template <int N>
-DEV void db_use_sgprs(const float (&w)[N]) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) db_use_sgpr(w[i]);
-}
-
-template <int KW>
-DEV void db_fma(lm_f2 (&acc)[P2_C], const lm_f2 (&px)[P2_C + KW - 1], const float (&w)[KW]) {
-#pragma unroll
-  for (int j = 0; j < KW; ++j) {
-    const lm_f2 w2 = (lm_f2){w[j], w[j]};
-#pragma unroll
-    for (int c = 0; c < P2_C; ++c) acc[c] = __builtin_elementwise_fma(w2, px[c + j], acc[c]);
+    *reinterpret_cast<uint4*>(ext + (int64_t)slot * ext_slot_bytes + q) = make_uint4(word[0], word[1], word[2], word[3]);
   }
 }
 
-template <int KW>
-__global__ __launch_bounds__(192, 2) void k_corr_db(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
-                                                    int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
-                                                    unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                    uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  constexpr int NQ = P2_C + KW - 1;
-  constexpr int STR = pk_stride_c(LM_TW + KW - 1);
-  extern __shared__ float lds[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  int gi = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
-      gi = k + 1;
-      tb = G.tile_end[k];
-    }
-  const int d = G.ids[gi];
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - tb;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
-  const int stride = pk_stride(cols);
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  const int cols4 = (cols + 3) >> 2;
-  for (int e = threadIdx.x; e < rows * cols4; e += blockDim.x) {
-    const int r = e / cols4, c4 = (e - r * cols4) << 2;
-    const uint8_t* p = src + (int64_t)r * ew + c4;
-    float* o = lds + r * stride + c4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c4 + k < stride) o[k] = (float)p[k];
-  }
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
+#include "lm_corr.hip"
 
-  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
-  lm_f2 acc[P2_C];
-#pragma unroll
-  for (int c = 0; c < P2_C; ++c) acc[c] = (lm_f2){D.delta, D.delta};
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  const unsigned base0 =
-      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(lds + (ly * 2) * stride + lx * P2_C);
-  const unsigned rstep = (unsigned)stride * 4u;
-  lm_f2 pa[NQ], pb[NQ];
-  db_issue<STR>(pa, base0, std::make_integer_sequence<int, NQ>{});
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  for (int t = 0; t < kh; t += 2) {
-    const bool two = t + 1 < kh;
-    float wa[KW], wb[KW];
-#pragma unroll
-    for (int j = 0; j < KW; ++j) wa[j] = W[t * kwp + j];
-#pragma unroll
-    for (int j = 0; j < KW; ++j) wb[j] = W[(two ? t + 1 : t) * kwp + j];
-    db_use_sgprs<KW>(wa);  // the compiler's wait for the scalar loads lands here
-    db_use_sgprs<KW>(wb);
-    __builtin_amdgcn_sched_barrier(0);
-    if (two) db_issue<STR>(pb, base0 + (unsigned)(t + 1) * rstep, std::make_integer_sequence<int, NQ>{});
-    __builtin_amdgcn_sched_barrier(0);
-    db_fma<KW>(acc, pa, wa);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (!two) break;
-    if (t + 2 < kh) db_issue<STR>(pa, base0 + (unsigned)(t + 2) * rstep, std::make_integer_sequence<int, NQ>{});
-    __builtin_amdgcn_sched_barrier(0);
-    db_fma<KW>(acc, pb, wb);
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  float accf[2][P2_C];
-#pragma unroll
-  for (int c = 0; c < P2_C; ++c) {
-    accf[0][c] = acc[c].x;
-    accf[1][c] = acc[c].y;
-  }
-  corr_epilogue<2, P2_C>(K, D, accf, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
-                         &s_cnt, &s_base);
-}
-
-// k_corr_sp: software-pipelined packed correlation.  Thread shape of k_corr_p2
-// (one row pair x 10 columns; 192 threads = 8 x 24 cover the 80x48 tile), one
-// detector row per iteration t.  The loads for row pair t+1 are spread over
-// row t's FMA stream: pixel pair q is dead once FMA block j = q is done
-// (blocks run j = 0..KW-1 and block j reads pairs j..j+9), so its ds_read2 for
-// t+1 is issued right after that block, into the same registers; the 9 pairs
-// q >= KW follow the last block.  Row t+1's weights are scalar-loaded at the
-// top of iteration t.  A wave therefore waits on LDS only for the last 9
-// loads and never on the weights, instead of draining every load and scalar
-// load before its FMAs (k_corr_pk / k_corr_p2).  Same fmaf chain per output
-// (taps in row-major order from delta), so the scores stay bit-exact.
-template <int STRIDE, int Q>
-DEV void sp_load(lm_f2& dst, unsigned base) {
-  static_assert(Q + STRIDE <= 255, "ds_read2_b32 offset range");
-  asm volatile("s_waitcnt lgkmcnt(12)\n\tds_read2_b32 %0, %1 offset0:%2 offset1:%3"
-               : "=v"(dst)
-               : "v"(base), "i"(Q), "i"(Q + STRIDE)
-               : "memory");
-}
-
-template <int KW, int STRIDE, int... Qs>
-DEV void sp_tail(lm_f2 (&px)[P2_C + KW - 1], unsigned nbase, std::integer_sequence<int, Qs...>) {
-  (sp_load<STRIDE, KW + Qs>(px[KW + Qs], nbase), ...);
-}
-
-template <int KW, int STRIDE, int J>
-DEV void sp_block(lm_f2 (&acc)[P2_C], lm_f2 (&px)[P2_C + KW - 1], const float (&w)[KW], unsigned nbase) {
-  const lm_f2 w2 = (lm_f2){w[J], w[J]};
-#pragma unroll
-  for (int c = 0; c < P2_C; ++c) acc[c] = __builtin_elementwise_fma(w2, px[c + J], acc[c]);
-  __builtin_amdgcn_sched_barrier(0);
-  sp_load<STRIDE, J>(px[J], nbase);  // pair J is dead for row t: refill it for row t+1
-  if constexpr (J == KW - 1) sp_tail<KW, STRIDE>(px, nbase, std::make_integer_sequence<int, P2_C - 1>{});
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int KW, int STRIDE, int... Js>
-DEV void sp_row(lm_f2 (&acc)[P2_C], lm_f2 (&px)[P2_C + KW - 1], const float (&w)[KW], unsigned nbase,
-                std::integer_sequence<int, Js...>) {
-  (sp_block<KW, STRIDE, Js>(acc, px, w, nbase), ...);
-}
-
-template <int KW>
-__global__ __launch_bounds__(192) void k_corr_sp(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
-                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
-                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  constexpr int NQ = P2_C + KW - 1;
-  constexpr int STR = pk_stride_c(LM_TW + KW - 1);
-  extern __shared__ float lds[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  int gi = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
-      gi = k + 1;
-      tb = G.tile_end[k];
-    }
-  const int d = G.ids[gi];
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - tb;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1, cols = LM_TW + KW - 1;
-  const int stride = STR;
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  const int cols4 = (cols + 3) >> 2;
-  for (int e = threadIdx.x; e < rows * cols4; e += blockDim.x) {
-    const int r = e / cols4, c4 = (e - r * cols4) << 2;
-    const uint8_t* p = src + (int64_t)r * ew + c4;
-    float* o = lds + r * stride + c4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c4 + k < stride) o[k] = (float)p[k];
-  }
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-
-  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
-  lm_f2 acc[P2_C];
-#pragma unroll
-  for (int c = 0; c < P2_C; ++c) acc[c] = (lm_f2){D.delta, D.delta};
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  unsigned base =
-      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)(lds + (ly * 2) * stride + lx * P2_C);
-  const unsigned rstep = (unsigned)stride * 4u;
-  lm_f2 px[NQ];
-  lds_pairs<STR, NQ>(px, base);  // row pair 0 (waits)
-  float wc[KW];
-#pragma unroll
-  for (int j = 0; j < KW; ++j) wc[j] = W[j];
-  for (int t = 0; t < kh; ++t) {
-    // the last iteration loads a (dead) row pair kh: the LDS tile has 2 spare rows
-    const float* wnr = W + min(t + 1, kh - 1) * kwp;
-    float wn[KW];
-#pragma unroll
-    for (int j = 0; j < KW; ++j) wn[j] = wnr[j];
-    __builtin_amdgcn_sched_barrier(0);  // row t+1's scalar loads issue before row t's FMAs
-    base += rstep;
-    sp_row<KW, STR>(acc, px, wc, base, std::make_integer_sequence<int, KW>{});
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // row t+1's pairs (and weights) have landed
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < KW; ++j) wc[j] = wn[j];
-  }
-  float accf[2][P2_C];
-#pragma unroll
-  for (int c = 0; c < P2_C; ++c) {
-    accf[0][c] = acc[c].x;
-    accf[1][c] = acc[c].y;
-  }
-  corr_epilogue<2, P2_C>(K, D, accf, lds, stride, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
-                         &s_cnt, &s_base);
-}
-
-// k_corr_cb: column-block pairs.  A packed accumulator holds outputs
-// (y, x) and (y, x + 40) of an 80 x 48 tile, so the two operands of every
-// v_pk_fma_f32 are pixels 40 columns apart in the same row.  The tile is kept
-// in LDS as float pairs LP[r][c] = (I[r][c], I[r][c + 40]), so each operand
-// pair is one ds_read_b64 (2 LDS cycles per wave, 256 B/clk) where the
-// row-pair kernels need a ds_read2_b32 (4 cycles, 128 B/clk): half the LDS
-// time for the same FMA count.  Thread (lx, ly), 8 x 24 threads: outputs
-// rows 2ly + {0, 1}, columns 5lx + {0..4} and 40 + 5lx + {0..4}.  Input row
-// T = 2ly + t feeds output row r through detector row i = t - r, so each
-// iteration uses weight rows t and t - 1.  Same fmaf chain per output (taps in
-// row-major order from delta): bit-exact with the reference restatement.
-#define CB_C 5
-#define CB_H 40
-constexpr int cb_stride_c(int kw) {  // pairs per LDS row: >= 40 + kw - 1 and == 4 or 12 (mod 16)
-  int s = CB_H + kw - 1;
-  while ((s & 7) != 4) ++s;
-  return s;
-}
-
-template <int Q>
-DEV void cb_load(lm_f2& dst, unsigned base) {
-  if constexpr (Q >= 15) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
-  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(Q * 8) : "memory");
-}
-
-template <int N, int... Qs>
-DEV void cb_loads_impl(lm_f2 (&px)[N], unsigned base, std::integer_sequence<int, Qs...>) {
-  (cb_load<Qs>(px[Qs], base), ...);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int KW, bool WLDS = false>
-__global__ __launch_bounds__(192) void k_corr_cb(const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext,
-                                                 int64_t ext_slot_bytes, const float* __restrict__ weights, int s0,
-                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  constexpr int NQ = CB_C + KW - 1;
-  constexpr int S2 = cb_stride_c(KW);
-  extern __shared__ lm_f2 lp[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  int gi = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
-      gi = k + 1;
-      tb = G.tile_end[k];
-    }
-  const int d = G.ids[gi];
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - tb;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1;
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  constexpr int PC = CB_H + KW - 1;  // pair columns used
-  for (int e = threadIdx.x; e < rows * PC; e += blockDim.x) {
-    const int r = e / PC, c = e - r * PC;
-    const uint8_t* p = src + (int64_t)r * ew + c;
-    lp[r * S2 + c] = (lm_f2){(float)p[0], (float)p[CB_H]};
-  }
-  // WLDS: detector weights staged in LDS after the tile and read as broadcast
-  // ds_reads (no scalar loads, whose waits also drain the LDS queue)
-  float* wl = reinterpret_cast<float*>(lp + rows * S2);
-  if (WLDS)
-    for (int e = threadIdx.x; e < D.kh * D.kwp; e += blockDim.x) wl[e] = weights[D.w_off + e];
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-
-  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
-  lm_f2 acc[2][CB_C];
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int c = 0; c < CB_C; ++c) acc[r][c] = (lm_f2){D.delta, D.delta};
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  const unsigned base0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) lm_f2*)(lp + (ly * 2) * S2 + lx * CB_C);
-  for (int t = 0; t <= kh; ++t) {
-    lm_f2 px[NQ];
-    cb_loads_impl<NQ>(px, base0 + (unsigned)(t * S2 * 8), std::make_integer_sequence<int, NQ>{});
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int i = t - r;
-      if (i >= 0 && i < kh) {
-        const float* wr = (WLDS ? wl : W) + ((G.skip_taps & 2) ? 0 : i * kwp);
-#pragma unroll
-        for (int j = 0; j < KW; ++j) {
-          const float w = wr[j];
-          const lm_f2 w2 = (lm_f2){w, w};
-#pragma unroll
-          for (int c = 0; c < CB_C; ++c) acc[r][c] = __builtin_elementwise_fma(w2, px[c + j], acc[r][c]);
-        }
-      }
-    }
-  }
-  // epilogue (see corr_epilogue): outputs (2ly + r, 5lx + c) in .x and (2ly + r, 40 + 5lx + c) in .y
-  const int my = D.m_y - D.in_y, mx = D.m_x - D.in_x;
-  if (D.kind != 0) {
-    uint8_t* __restrict__ tbm = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int c = 0; c < CB_C; ++c)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int y = oy0 + ly * 2 + r, x = ox0 + h * CB_H + lx * CB_C + c;
-          const float a = h ? acc[r][c].y : acc[r][c].x;
-          if (y < D.oh && x < D.ow) tbm[(int64_t)y * D.ow + x] = a > 0.0f ? 1 : 0;
-        }
-    return;
-  }
-  unsigned bits = 0;
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int c = 0; c < CB_C; ++c) {
-      const lm_f2 pix = lp[(ly * 2 + r + my) * S2 + lx * CB_C + c + mx];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int y = oy0 + ly * 2 + r, x = ox0 + h * CB_H + lx * CB_C + c;
-        const float a = h ? acc[r][c].y : acc[r][c].x;
-        const float pv = h ? pix.y : pix.x;
-        if (y < D.oh && x < D.ow && pv > 25.0f && a > 0.0f) bits |= 1u << ((r * CB_C + c) * 2 + h);
-      }
-    }
-  const int nk = __popc(bits);
-  const int off = nk ? atomicAdd(&s_cnt, nk) : 0;
-  __syncthreads();
-  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
-  __syncthreads();
-  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + s_base + off;
-  int k = 0;
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int c = 0; c < CB_C; ++c)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if (bits & (1u << ((r * CB_C + c) * 2 + h))) {
-          const int y = oy0 + ly * 2 + r, x = ox0 + h * CB_H + lx * CB_C + c;
-          const float a = h ? acc[r][c].y : acc[r][c].x;
-          kl[k++] = ((unsigned long long)(~__float_as_uint(a)) << 32) | (unsigned)(y * D.ow + x);
-        }
-}
-
-// k_corr_c1: column-block pairs (as k_corr_cb) with one output row per
-// thread: 384 threads = 8 x 48 cover the 80 x 48 tile, each owning columns
-// 5lx+{0..4} and 40+5lx+{0..4} of row ly.  Twice the waves of the row-pair
-// kernels for the same LDS (up to 6 waves/SIMD), one detector row per
-// iteration, so row t+1's weights are scalar-loaded during row t, and row
-// t+1's pixel pairs (ds_read_b64) are loaded into each register as soon as
-// row t's FMA block j = q no longer needs pair q (as k_corr_sp).
-template <int Q>
-DEV void c1_load(lm_f2& dst, unsigned base) {
-  asm volatile("s_waitcnt lgkmcnt(10)\n\tds_read_b64 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(Q * 8) : "memory");
-}
-
-template <int KW, int... Qs>
-DEV void c1_tail(lm_f2 (&px)[CB_C + KW - 1], unsigned nbase, std::integer_sequence<int, Qs...>) {
-  (c1_load<KW + Qs>(px[KW + Qs], nbase), ...);
-}
-
-template <int KW, int J>
-DEV void c1_block(lm_f2 (&acc)[CB_C], lm_f2 (&px)[CB_C + KW - 1], const float (&w)[KW], unsigned nbase) {
-  const lm_f2 w2 = (lm_f2){w[J], w[J]};
-#pragma unroll
-  for (int c = 0; c < CB_C; ++c) acc[c] = __builtin_elementwise_fma(w2, px[c + J], acc[c]);
-  __builtin_amdgcn_sched_barrier(0);
-  c1_load<J>(px[J], nbase);  // pair J is dead for row t: refill it for row t+1
-  if constexpr (J == KW - 1) c1_tail<KW>(px, nbase, std::make_integer_sequence<int, CB_C - 1>{});
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int KW, int... Js>
-DEV void c1_row(lm_f2 (&acc)[CB_C], lm_f2 (&px)[CB_C + KW - 1], const float (&w)[KW], unsigned nbase,
-                std::integer_sequence<int, Js...>) {
-  (c1_block<KW, Js>(acc, px, w, nbase), ...);
-}
-
-template <int KW>
-__global__ __launch_bounds__(384) void k_corr_c1(const LmConst* __restrict__ Kp, const LmDetGroup G,
-                                                 const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
-                                                 const float* __restrict__ weights, int s0,
-                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  constexpr int NQ = CB_C + KW - 1;
-  constexpr int S2 = cb_stride_c(KW);
-  extern __shared__ lm_f2 lp[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  int gi = 0, tb = 0;
-#pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && (int)blockIdx.x >= G.tile_end[k]) {
-      gi = k + 1;
-      tb = G.tile_end[k];
-    }
-  const int d = G.ids[gi];
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - tb;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1;
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  constexpr int PC = CB_H + KW - 1;
-  for (int e = threadIdx.x; e < rows * PC; e += blockDim.x) {
-    const int r = e / PC, c = e - r * PC;
-    const uint8_t* p = src + (int64_t)r * ew + c;
-    lp[r * S2 + c] = (lm_f2){(float)p[0], (float)p[CB_H]};
-  }
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-
-  const int ly = threadIdx.x >> 3, lx = threadIdx.x & 7;
-  lm_f2 acc[CB_C];
-#pragma unroll
-  for (int c = 0; c < CB_C; ++c) acc[c] = (lm_f2){D.delta, D.delta};
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) lm_f2*)(lp + ly * S2 + lx * CB_C);
-  const unsigned rstep = (unsigned)S2 * 8u;
-  lm_f2 px[NQ];
-  cb_loads_impl<NQ>(px, base, std::make_integer_sequence<int, NQ>{});  // row 0 (waits)
-  float wc[KW];
-#pragma unroll
-  for (int j = 0; j < KW; ++j) wc[j] = W[j];
-  for (int t = 0; t < kh; ++t) {
-    // the last iteration loads a (dead) row kh: the LDS tile has a spare row
-    const float* wnr = W + min(t + 1, kh - 1) * kwp;
-    float wn[KW];
-#pragma unroll
-    for (int j = 0; j < KW; ++j) wn[j] = wnr[j];
-    __builtin_amdgcn_sched_barrier(0);  // row t+1's scalar loads issue before row t's FMAs
-    base += rstep;
-    c1_row<KW>(acc, px, wc, base, std::make_integer_sequence<int, KW>{});
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // row t+1's pairs (and weights) have landed
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < KW; ++j) wc[j] = wn[j];
-  }
-  // epilogue: outputs (ly, 5lx + c) in .x and (ly, 40 + 5lx + c) in .y
-  const int my = D.m_y - D.in_y, mx = D.m_x - D.in_x;
-  if (D.kind != 0) {
-    uint8_t* __restrict__ tbm = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
-#pragma unroll
-    for (int c = 0; c < CB_C; ++c)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int y = oy0 + ly, x = ox0 + h * CB_H + lx * CB_C + c;
-        const float a = h ? acc[c].y : acc[c].x;
-        if (y < D.oh && x < D.ow) tbm[(int64_t)y * D.ow + x] = a > 0.0f ? 1 : 0;
-      }
-    return;
-  }
-  unsigned bits = 0;
-#pragma unroll
-  for (int c = 0; c < CB_C; ++c) {
-    const lm_f2 pix = lp[(ly + my) * S2 + lx * CB_C + c + mx];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int y = oy0 + ly, x = ox0 + h * CB_H + lx * CB_C + c;
-      const float a = h ? acc[c].y : acc[c].x;
-      const float pv = h ? pix.y : pix.x;
-      if (y < D.oh && x < D.ow && pv > 25.0f && a > 0.0f) bits |= 1u << (c * 2 + h);
-    }
-  }
-  const int nk = __popc(bits);
-  const int off = nk ? atomicAdd(&s_cnt, nk) : 0;
-  __syncthreads();
-  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
-  __syncthreads();
-  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + s_base + off;
-  int k = 0;
-#pragma unroll
-  for (int c = 0; c < CB_C; ++c)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      if (bits & (1u << (c * 2 + h))) {
-        const int y = oy0 + ly, x = ox0 + h * CB_H + lx * CB_C + c;
-        const float a = h ? acc[c].y : acc[c].x;
-        kl[k++] = ((unsigned long long)(~__float_as_uint(a)) << 32) | (unsigned)(y * D.ow + x);
-      }
-}
-
-// widths with a specialised kernel; others use the generic k_corr
-#define LM_KW_LIST(X) \
-  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
-
-// Correlation variants: 0 generic (runtime width), 1 width-specialised plain
-// FMA (k_corr_kw), 2 packed FMA with compiler-scheduled LDS loads, 3 packed
-// FMA with explicit (row t, row t+1) ds_read2_b32 pair loads (default).
-enum {
-  CORR_GENERIC = 0, CORR_KW = 1, CORR_PK = 2, CORR_PK_ASM = 3, CORR_P2 = 4, CORR_DB = 5, CORR_SP = 6, CORR_CB = 7,
-  CORR_PK_WLDS = 8, CORR_CB_WLDS = 9, CORR_C1 = 10
-};
-
-template <int n>
-static inline const void* corr_fn(int variant) {
-  if (variant == CORR_C1) return (const void*)&k_corr_c1<n>;
-  if (variant == CORR_CB_WLDS) return (const void*)&k_corr_cb<n, true>;
-  if (variant == CORR_PK_WLDS) return (const void*)&k_corr_pk<n, true, true>;
-  if (variant == CORR_CB) return (const void*)&k_corr_cb<n>;
-  if (variant == CORR_SP) return (const void*)&k_corr_sp<n>;
-  if (variant == CORR_DB) return (const void*)&k_corr_db<n>;
-  if (variant == CORR_P2) return (const void*)&k_corr_p2<n>;
-  if (variant == CORR_PK_ASM) return (const void*)&k_corr_pk<n, false, true>;
-  if (variant == CORR_PK) return (const void*)&k_corr_pk<n, false, false>;
-  return (const void*)&k_corr_kw<n>;
-}
-
-// wide detectors (the 1920x512 geometry of config C5: 44, 48, 52, 60) get the
-// production variant only; other variants fall back to the generic kernel
-#define LM_KW_WIDE_LIST(X) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
-
-template <int n>
-static inline const void* corr_fn_wide(int variant) {
-  if (variant == CORR_C1) return (const void*)&k_corr_c1<n>;
-  if (variant == CORR_CB_WLDS) return (const void*)&k_corr_cb<n, true>;
-  if (variant == CORR_PK_WLDS) return (const void*)&k_corr_pk<n, true, true>;
-  if (variant == CORR_CB) return (const void*)&k_corr_cb<n>;
-  if (variant == CORR_SP) return (const void*)&k_corr_sp<n>;
-  return variant == CORR_PK_ASM ? (const void*)&k_corr_pk<n, false, true> : nullptr;
-}
-
-static inline const void* corr_kernel(int variant, int kw, int* threads) {
-  if (variant == CORR_C1) *threads = 384;
-  else *threads = (variant == CORR_PK || variant == CORR_PK_ASM || variant == CORR_P2 || variant == CORR_DB ||
-              variant == CORR_SP || variant == CORR_CB || variant == CORR_PK_WLDS || variant == CORR_CB_WLDS)
-                 ? 192
-                 : 256;
-  const void* fn = nullptr;
-  if (variant != CORR_GENERIC) switch (kw) {
-#define LM_KW_CASE(n) \
-  case n:             \
-    fn = corr_fn<n>(variant);  \
-    break;
-      LM_KW_LIST(LM_KW_CASE)
-#undef LM_KW_CASE
-#define LM_KW_CASE(n)             \
-  case n:                         \
-    fn = corr_fn_wide<n>(variant); \
-    break;
-      LM_KW_WIDE_LIST(LM_KW_CASE)
-#undef LM_KW_CASE
-      default:
-        break;
-    }
-  if (fn) return fn;
-  *threads = 256;
-  return (const void*)&k_corr;
-}
-
-static inline hipError_t corr_set_lds(int variant, int kw, size_t lds) {
-  int th;
-  return hipFuncSetAttribute(corr_kernel(variant, kw, &th), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-}
-
-// Launch the correlation for one detector group (all detectors of one width).
-static inline hipError_t launch_corr(int variant, int kw, dim3 grid, size_t lds, hipStream_t st, const LmConst* K,
-                                     const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes,
-                                     const float* weights, int s0, unsigned long long* keys, int32_t* n_pos,
-                                     uint8_t* tailbin, int64_t tailbin_slot_bytes) {
-  int th;
-  const void* fn = corr_kernel(variant, kw, &th);
-  void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
-                  (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
-  return hipLaunchKernel(fn, grid, dim3(th), args, lds, st);
-}
-
-
-// Debug copy of raw scores: same arithmetic as k_corr, no compaction.
-__global__ __launch_bounds__(256) void k_corr_dbg(const LmConst* __restrict__ Kp, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
-                                                  const float* __restrict__ weights, int s0, float* __restrict__ dbg,
-                                                  const int64_t* __restrict__ dbg_off, int64_t dbg_slot_floats) {
-  const LmConst& K = *Kp;
-  extern __shared__ float lds[];
-  const int slot = s0 + blockIdx.y;
-  int d = 0;
-#pragma unroll
-  for (int k = 1; k < LM_NDET; ++k)
-    if ((int)blockIdx.x >= K.det[k].tile_base) d = k;
-  const LmDet D = K.det[d];
-  const int lt = blockIdx.x - D.tile_base;
-  const int oy0 = (lt / D.tiles_x) * LM_TH, ox0 = (lt % D.tiles_x) * LM_TW;
-  const int rows = LM_TH + D.kh - 1, cols = LM_TW + D.kwp - 1;
-  int stride = cols;
-  stride += (16 - (stride & 31) + 32) & 31;
-  const uint8_t* __restrict__ src = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                                    (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
-  const int ew = K.ext_w[D.view];
-  const int cols4 = (cols + 3) >> 2;
-  for (int e = threadIdx.x; e < rows * cols4; e += 256) {
-    const int r = e / cols4, c4 = (e - r * cols4) << 2;
-    const uint8_t* p = src + (int64_t)r * ew + c4;
-    float* o = lds + r * stride + c4;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (c4 + k < stride) o[k] = (float)p[k];
-  }
-  __syncthreads();
-  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
-  const float* __restrict__ W = weights + D.w_off;
-  for (int r = 0; r < LM_R; ++r)
-    for (int c = 0; c < LM_C; ++c) {
-      const int y = oy0 + ly * LM_R + r, x = ox0 + lx * LM_C + c;
-      if (y >= D.oh || x >= D.ow) continue;
-      float a = D.delta;
-      for (int i = 0; i < D.kh; ++i)
-        for (int j = 0; j < D.kwp; ++j)
-          a = __builtin_fmaf(W[i * D.kwp + j], lds[(ly * LM_R + r + i) * stride + lx * LM_C + c + j], a);
-      dbg[(int64_t)slot * dbg_slot_floats + dbg_off[d] + (int64_t)y * D.ow + x] = a;
-    }
-}
+#include "lm_cc.h"
 
 // ------------------------------------------------------------------ k_tail
-// Connected components by lock-free union-find (atomicMin hooking) over the
-// compacted foreground of a tail binary map, in LDS.  The largest component
-// wins; on equal areas the one OpenCV labels first (8-connectivity: Grana
-// BBDT 2x2-block raster order; 4-connectivity: Wu pixel raster order).
-#define LM_TAIL_FG_MAX 6144
+// detectTail (:2541-2555) -> detectLineCandidates (:2558-2742), one
+// workgroup per frame:
+//   bottom: largest component of (tail_b > 0) (selectLargestRegion :2604,
+//     lm_cc.h) -> TAIL_MASK (:2611, a bitmap here: 64 columns per word),
+//     colmax = reduce(MAX) over rows (:2615), first / last occupied columns
+//     (:2642-2670), tail_width = last - first (:2677), 15 segments, the first
+//     tail_width % 15 one column wider (:2678-2685), per segment the binary
+//     moments m00, m10, m01 (:2702-2725) -> track x, y;
+//   side: largest component of (tail_s > 0) & repeat(colmax) (:2623-2626),
+//     then at every track x > 0 the moments of that one column (:2728-2737)
+//     -> track z.
+// cv::moments(binary) walks 32x32 tiles in raster order, accumulates integer
+// tile sums (count, sum of x and of y inside the tile), scales them by 1/255
+// and adds x0*m00 / y0*m00 of the tile origin; the sums are built here from
+// the component's runs (arithmetic series per run and tile) and turned into
+// doubles in that same tile order, so the tracks are bit-identical.
+// No size limit: run tables beyond the LDS capacity go to global scratch.
+#define LM_TAIL_THREADS 256
+#define LM_TAIL_SEGS 15
 
-struct CCWork {
-  unsigned* fg;      // pixel index of each foreground element
-  unsigned* parent;  // union-find forest over element ids
-  unsigned* area;    // per root
-  unsigned* key;     // per root: first-label key
+struct TailLayout {  // byte offsets into k_tail's dynamic LDS
+  int rowoff, colc, colm, mask, bm, par, area, key, rs, re, mb, ms, bytes;
 };
-
-DEV unsigned cc_find(unsigned* parent, unsigned a) {
-  unsigned p = parent[a];
-  while (p != a) {
-    a = p;
-    p = parent[a];
-  }
-  return a;
+__host__ __device__ inline TailLayout tail_layout(int TW, int HB, int HS, int cap, int ntc) {
+  const int Hm = HB > HS ? HB : HS, nb64 = (TW + 63) / 64;
+  const int ntrb = (HB + 31) / 32, ntrs = (HS + 31) / 32;
+  TailLayout L;
+  int o = 0;
+  L.rowoff = o;
+  o += 4 * (Hm + 1);
+  L.colc = o;
+  o += 4 * (TW + 2);
+  o = (o + 15) & ~15;
+  L.colm = o;
+  o += 8 * nb64;
+  L.mask = o;
+  o += 8 * HB * nb64;
+  L.bm = o;
+  L.par = o;
+  L.area = o + 4 * cap;
+  L.key = o + 8 * cap;
+  const int bmb = 8 * Hm * (nb64 + 1), ufb = 12 * cap;
+  o += bmb > ufb ? bmb : ufb;
+  L.rs = o;
+  o += 2 * cap;
+  L.re = o;
+  o += 2 * cap;
+  o = (o + 15) & ~15;
+  L.mb = o;
+  o += 4 * LM_TAIL_SEGS * ntrb * ntc * 3;
+  L.ms = o;
+  o += 4 * LM_TAIL_SEGS * ntrs * 2;
+  L.bytes = o;
+  return L;
 }
 
-DEV void cc_union(unsigned* parent, unsigned a, unsigned b) {
-  while (true) {
-    a = cc_find(parent, a);
-    b = cc_find(parent, b);
-    if (a == b) return;
-    if (a < b) {
-      unsigned t = a;
-      a = b;
-      b = t;
+// Segment of column offset rx in [0, tail_width) and its start (:2678-2685).
+DEV void tail_segment(int rx, int rem, int reg, int* seg, int* sx) {
+  if (rx < rem * (reg + 1)) {
+    *seg = rx / (reg + 1);
+    *sx = *seg * (reg + 1);
+  } else {
+    *seg = rem + (rx - rem * (reg + 1)) / reg;
+    *sx = rem * (reg + 1) + (*seg - rem) * reg;
+  }
+}
+
+// Bottom pass 1 over the chosen component's runs: TAIL_MASK bits, the column
+// counts (difference array) and the first / last occupied columns.
+template <bool G, class IX>
+DEV void tail_bottom_runs(const CCRuns<IX> S, int R, const int* rowoff, int H, unsigned broot, int nb64,
+                          unsigned long long* mask, int* colc, int* s_first, int* s_last) {
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {
+    if (rld<G>(&S.par[i]) != broot) continue;
+    const int y = cc_row_of(rowoff, H, i);
+    const int x0 = (int)rld<G>(&S.rs[i]), x1 = (int)rld<G>(&S.re[i]);
+    for (int k = x0 >> 6; k <= (x1 >> 6); ++k) {
+      const int a = max(x0, 64 * k) - 64 * k, b = min(x1, 64 * k + 63) - 64 * k;
+      const unsigned long long bits = (b == 63 ? ~0ull : ((1ull << (b + 1)) - 1)) & ~((1ull << a) - 1);
+      atomicOr(&mask[(int64_t)y * nb64 + k], bits);
     }
-    // a > b: hook a under b
-    unsigned old = atomicMin(&parent[a], b);
-    if (old == a) return;
-    a = old;
+    atomicAdd(&colc[x0], 1);
+    atomicSub(&colc[x1 + 1], 1);
+    atomicMin(s_first, x0);
+    atomicMax(s_last, x1);
   }
 }
 
-// Labels the foreground (given as element list fg[0..n) with pixel indices
-// into a rows x cols map where `is_fg(p)` tells membership and `id_of(p)`
-// maps a foreground pixel to its element id).  Returns the chosen root (or
-// 0xFFFFFFFF when n == 0) in *s_best.  Block-wide; all threads call.
-template <class IsFg, class IdOf>
-DEV void cc_largest(CCWork W, int n, int rows, int cols, int conn, IsFg is_fg, IdOf id_of, unsigned* s_best) {
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    W.parent[k] = k;
-    W.area[k] = 0;
-    W.key[k] = 0xFFFFFFFFu;
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    const unsigned p = W.fg[k];
-    const int y = p / cols, x = p % cols;
-    if (x > 0 && is_fg(p - 1)) cc_union(W.parent, k, id_of(p - 1));
-    if (y > 0) {
-      if (is_fg(p - cols)) cc_union(W.parent, k, id_of(p - cols));
-      if (conn == 8) {
-        if (x > 0 && is_fg(p - cols - 1)) cc_union(W.parent, k, id_of(p - cols - 1));
-        if (x + 1 < cols && is_fg(p - cols + 1)) cc_union(W.parent, k, id_of(p - cols + 1));
+// Bottom pass 2: integer tile sums of every segment's moments from the runs
+// inside [first, first + tail_width).
+template <bool G, class IX>
+DEV void tail_bottom_moments(const CCRuns<IX> S, int R, const int* rowoff, int H, unsigned broot, int first, int tw,
+                             int rem, int reg, unsigned* mb, int ntrb, int ntc) {
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {
+    if (rld<G>(&S.par[i]) != broot) continue;
+    const int y = cc_row_of(rowoff, H, i);
+    const int a = max((int)rld<G>(&S.rs[i]), first) - first, b = min((int)rld<G>(&S.re[i]), first + tw - 1) - first;
+    int rx = a;
+    while (rx <= b) {
+      int seg, sx;
+      tail_segment(rx, rem, reg, &seg, &sx);
+      const int wseg = seg < rem ? reg + 1 : reg;
+      const int end = min(b, sx + wseg - 1);  // this segment's part of the run
+      for (int l0 = rx - sx; l0 <= end - sx;) {  // 32-column tiles inside the segment
+        const int tx = l0 >> 5, l1 = min(end - sx, 32 * tx + 31);
+        const unsigned cnt = (unsigned)(l1 - l0 + 1);
+        const unsigned sumx = (unsigned)((l0 + l1 - 64 * tx) * (int)cnt / 2);  // sum of (l - 32 tx), l in [l0, l1]
+        unsigned* t = mb + ((seg * ntrb + (y >> 5)) * ntc + tx) * 3;
+        atomicAdd(&t[0], cnt);
+        atomicAdd(&t[1], sumx);
+        atomicAdd(&t[2], (unsigned)(y & 31) * cnt);
+        l0 = l1 + 1;
       }
+      rx = end + 1;
     }
   }
-  __syncthreads();
-  const int nbx = (cols + 1) / 2;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    const unsigned root = cc_find(W.parent, k);
-    const unsigned p = W.fg[k];
-    const int y = p / cols, x = p % cols;
-    const unsigned key = conn == 8 ? (unsigned)((y >> 1) * nbx + (x >> 1)) : p;
-    atomicAdd(&W.area[root], 1u);
-    atomicMin(&W.key[root], key);
-  }
-  __syncthreads();
-  // max area, then min key
-  unsigned long long best = 0;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) {
-    if (W.parent[k] == (unsigned)k) {  // root (parents are final roots after find? roots satisfy parent==self)
-      unsigned long long v = ((unsigned long long)W.area[k] << 32) | (0xFFFFFFFFu - W.key[k]);
-      if (v > best) best = v;
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    unsigned long long other = __shfl_xor(best, o);
-    if (other > best) best = other;
-  }
-  __shared__ unsigned long long s_red[16];
-  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = best;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long b = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w)
-      if (s_red[w] > b) b = s_red[w];
-    unsigned chosen = 0xFFFFFFFFu;
-    if (b) {
-      // find the root with this (area, key): keys are unique per component
-      const unsigned key = 0xFFFFFFFFu - (unsigned)(b & 0xFFFFFFFFu);
-      for (int k = 0; k < n; ++k)
-        if (W.parent[k] == (unsigned)k && W.key[k] == key) {
-          chosen = k;
-          break;
-        }
-    }
-    *s_best = chosen;
-  }
-  __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void k_tail(const LmConst* __restrict__ Kp, int s0, const uint8_t* __restrict__ tailbin,
-                                               int64_t tailbin_slot_bytes, uint8_t* __restrict__ tailmask,
-                                               unsigned* __restrict__ scratch, int64_t scratch_slot_words,
-                                               LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err) {
+// Side: every track column x > 0 the chosen component covers in a row adds
+// that row to the column's tile sums.
+template <bool G, class IX>
+DEV void tail_side_moments(const CCRuns<IX> S, int R, const int* rowoff, int H, unsigned broot, const int* s_tx,
+                           unsigned* ms, int ntrs) {
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {
+    if (rld<G>(&S.par[i]) != broot) continue;
+    const int y = cc_row_of(rowoff, H, i);
+    const int x0 = (int)rld<G>(&S.rs[i]), x1 = (int)rld<G>(&S.re[i]);
+    for (int k = 0; k < LM_TAIL_SEGS; ++k)
+      if (s_tx[k] > 0 && s_tx[k] >= x0 && s_tx[k] <= x1) {
+        atomicAdd(&ms[(k * ntrs + (y >> 5)) * 2], 1u);
+        atomicAdd(&ms[(k * ntrs + (y >> 5)) * 2 + 1], (unsigned)(y & 31));
+      }
+  }
+}
+
+__global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restrict__ Kp, int s0,
+                                                          const uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
+                                                          unsigned long long* __restrict__ tailmask,
+                                                          unsigned* __restrict__ scratch, LmSlotOut* __restrict__ hdr) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smt[];
   const LmConst& K = *Kp;
   const int slot = s0 + blockIdx.x;
-  const int TW = K.tail_w, HB = K.tail_hb, HS = K.tail_hs;
+  const int TW = K.tail_w, HB = K.tail_hb, HS = K.tail_hs, nb64 = (TW + 63) / 64;
+  const int cap = K.tail_cap, ntc = K.tail_ntc, ntrb = (HB + 31) / 32, ntrs = (HS + 31) / 32;
+  const TailLayout L = tail_layout(TW, HB, HS, cap, ntc);
+  int* rowoff = reinterpret_cast<int*>(smt + L.rowoff);
+  int* colc = reinterpret_cast<int*>(smt + L.colc);
+  unsigned long long* colm = reinterpret_cast<unsigned long long*>(smt + L.colm);
+  unsigned long long* mask = reinterpret_cast<unsigned long long*>(smt + L.mask);
+  unsigned long long* bm = reinterpret_cast<unsigned long long*>(smt + L.bm);
+  unsigned* mb = reinterpret_cast<unsigned*>(smt + L.mb);
+  unsigned* ms = reinterpret_cast<unsigned*>(smt + L.ms);
+  const CCRuns<uint16_t> SL{reinterpret_cast<uint16_t*>(smt + L.rs), reinterpret_cast<uint16_t*>(smt + L.re),
+                            reinterpret_cast<unsigned*>(smt + L.par), reinterpret_cast<unsigned*>(smt + L.area),
+                            reinterpret_cast<unsigned*>(smt + L.key)};
+  const int64_t capg = (int64_t)max(HB, HS) * ((TW + 1) / 2);  // at most ceil(TW/2) runs per row
+  unsigned* gb = scratch + (int64_t)slot * 5 * capg;
+  const CCRuns<unsigned> SG{gb, gb + capg, gb + 2 * capg, gb + 3 * capg, gb + 4 * capg};
+  __shared__ unsigned long long s_red[LM_TAIL_THREADS / 64];
+  __shared__ unsigned s_best;
+  __shared__ int s_total, s_first, s_last;
+  __shared__ int s_tx[LM_TAIL_SEGS];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const bool c8 = K.connectivity == 8;
+  const bool lds_ok = TW <= 65535;
   const uint8_t* __restrict__ binb = tailbin + (int64_t)slot * tailbin_slot_bytes;
   const uint8_t* __restrict__ bins = binb + (int64_t)HB * TW;
-  uint8_t* __restrict__ mask = tailmask + (int64_t)slot * HB * TW;
-  unsigned* __restrict__ idmap = scratch + (int64_t)slot * scratch_slot_words;  // [HB*TW] element ids
+  const bool vec = (TW & 15) == 0 && (tailbin_slot_bytes & 15) == 0;
 
-  __shared__ unsigned s_fg[LM_TAIL_FG_MAX], s_parent[LM_TAIL_FG_MAX], s_area[LM_TAIL_FG_MAX], s_key[LM_TAIL_FG_MAX];
-  __shared__ int s_n;
-  __shared__ unsigned s_best;
-  __shared__ int s_first, s_last;
-  __shared__ uint8_t s_col[1024];
-  // moments accumulators: [segment 15][tile rows <= 16][tile cols <= 2] x (n, sx, sy)
-  __shared__ unsigned s_mb[15][16][2][3];
-  __shared__ unsigned s_ms[15][16][2];  // side: per track column, per tile row: (n, sy)
-
-  CCWork Wk{s_fg, s_parent, s_area, s_key};
-  const int conn = K.connectivity;
-
-  // zero TAIL_MASK, column mask
-  for (int p = threadIdx.x; p < HB * TW; p += blockDim.x) mask[p] = 0;
-  for (int c = threadIdx.x; c < TW; c += blockDim.x) s_col[c] = 0;
-  if (threadIdx.x == 0) {
-    s_n = 0;
+  for (int i = tid; i < TW + 2; i += nt) colc[i] = 0;
+  for (int i = tid; i < HB * nb64; i += nt) mask[i] = 0;
+  for (int i = tid; i < LM_TAIL_SEGS * ntrb * ntc * 3; i += nt) mb[i] = 0;
+  for (int i = tid; i < LM_TAIL_SEGS * ntrs * 2; i += nt) ms[i] = 0;
+  if (tid == 0) {
     s_first = 0x7FFFFFFF;
     s_last = -1;
   }
-  for (int e = threadIdx.x; e < 15 * 16 * 2 * 3; e += blockDim.x) (&s_mb[0][0][0][0])[e] = 0;
-  for (int e = threadIdx.x; e < 15 * 16 * 2; e += blockDim.x) (&s_ms[0][0][0])[e] = 0;
-  __syncthreads();
 
-  // ---- bottom: compact foreground
-  for (int p = threadIdx.x; p < HB * TW; p += blockDim.x)
-    if (binb[p]) {
-      int k = atomicAdd(&s_n, 1);
-      if (k < LM_TAIL_FG_MAX) {
-        s_fg[k] = p;
-        idmap[p] = k;
-      }
-    }
-  __syncthreads();
-  int n = s_n;
-  if (n > LM_TAIL_FG_MAX) {
-    if (threadIdx.x == 0) atomicOr(err, 2);  // tail foreground exceeds the LDS capacity
-    return;
-  }
-  cc_largest(Wk, n, HB, TW, conn, [&](unsigned p) { return binb[p] != 0; }, [&](unsigned p) { return idmap[p]; }, &s_best);
+  // ---- bottom: largest component, TAIL_MASK, column mask, segment moments
+  cc_bitmap_u8(binb, TW, TW, HB, nb64, vec, nullptr, bm, rowoff);
+  cc_wave0_scan(rowoff, HB, &s_total);
+  int R = s_total;
+  const bool gb_b = !(lds_ok && R <= cap);
+  if (!gb_b) cc_label<false>(SL, bm, nb64, TW, HB, R, rowoff, c8, s_red, &s_best);
+  else cc_label<true>(SG, bm, nb64, TW, HB, R, rowoff, c8, s_red, &s_best);
   const unsigned best_b = s_best;
-  if (best_b != 0xFFFFFFFFu) {
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-      if (cc_find(s_parent, k) == best_b) {
-        const unsigned p = s_fg[k];
-        mask[p] = 255;
-        const int x = p % TW;
-        s_col[x] = 255;
-        atomicMin(&s_first, x);
-        atomicMax(&s_last, x);
-      }
-    }
+  const bool have = best_b != 0xFFFFFFFFu;
+  if (have) {
+    if (!gb_b) tail_bottom_runs<false>(SL, R, rowoff, HB, best_b, nb64, mask, colc, &s_first, &s_last);
+    else tail_bottom_runs<true>(SG, R, rowoff, HB, best_b, nb64, mask, colc, &s_first, &s_last);
   }
   __syncthreads();
   const int first = s_first, last = s_last;
-  const bool have = best_b != 0xFFFFFFFFu;
-  // segment geometry (:2677-2685)
-  const int tail_width = have ? last - first : 0;
-  const int rem = tail_width % 15, reg = (tail_width - rem) / 15;
-  // bottom segment moments: per selected pixel, integer per-tile sums
+  const int tail_width = have ? last - first : 0;  // :2677 (no +1)
+  const int rem = tail_width % LM_TAIL_SEGS, reg = (tail_width - rem) / LM_TAIL_SEGS;
   if (have) {
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-      if (cc_find(s_parent, k) != best_b) continue;
-      const unsigned p = s_fg[k];
-      const int y = p / TW, x = p % TW;
-      if (x < first || x >= first + tail_width) continue;  // segments cover [first, last)
-      const int rx = x - first;
-      int seg, sx;
-      if (rx < rem * (reg + 1)) {
-        seg = rx / (reg + 1);
-        sx = seg * (reg + 1);
-      } else {
-        seg = rem + (rx - rem * (reg + 1)) / reg;
-        sx = rem * (reg + 1) + (seg - rem) * reg;
+    if (!gb_b) tail_bottom_moments<false>(SL, R, rowoff, HB, best_b, first, tail_width, rem, reg, mb, ntrb, ntc);
+    else tail_bottom_moments<true>(SG, R, rowoff, HB, best_b, first, tail_width, rem, reg, mb, ntrb, ntc);
+  }
+  // column counts -> colmax bitmap (reduce(MAX, dim 0), :2615)
+  if (tid < 64) {
+    const int lane = tid;
+    int carry = 0;
+    for (int k = 0; k < nb64; ++k) {
+      const int x = 64 * k + lane;
+      int inc = x < TW ? colc[x] : 0;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
       }
-      const int lxs = rx - sx;  // x inside the segment ROI
-      const int ty = y >> 5, tx = lxs >> 5;
-      atomicAdd(&s_mb[seg][ty][tx][0], 1u);
-      atomicAdd(&s_mb[seg][ty][tx][1], (unsigned)(lxs & 31));
-      atomicAdd(&s_mb[seg][ty][tx][2], (unsigned)(y & 31));
+      const unsigned long long b = __ballot(x < TW && carry + inc > 0);
+      if (lane == 0) colm[k] = b;
+      carry += __shfl(inc, 63);
     }
   }
   __syncthreads();
+  unsigned long long* __restrict__ tm = tailmask + (int64_t)slot * HB * nb64;
+  for (int i = tid; i < HB * nb64; i += nt) tm[i] = mask[i];
 
   // ---- side: (tail_s > 0) & repeat(colmax) -> largest component
-  if (threadIdx.x == 0) s_n = 0;
-  __syncthreads();
-  for (int p = threadIdx.x; p < HS * TW; p += blockDim.x)
-    if (bins[p] && s_col[p % TW]) {
-      int k = atomicAdd(&s_n, 1);
-      if (k < LM_TAIL_FG_MAX) {
-        s_fg[k] = p;
-        idmap[p] = k;
-      }
-    }
-  __syncthreads();
-  n = s_n;
-  if (n > LM_TAIL_FG_MAX) {
-    if (threadIdx.x == 0) atomicOr(err, 2);
-    return;
-  }
-  auto side_fg = [&](unsigned p) { return bins[p] != 0 && s_col[p % TW] != 0; };
-  cc_largest(Wk, n, HS, TW, conn, side_fg, [&](unsigned p) { return idmap[p]; }, &s_best);
+  cc_bitmap_u8(bins, TW, TW, HS, nb64, vec, colm, bm, rowoff);
+  cc_wave0_scan(rowoff, HS, &s_total);
+  R = s_total;
+  const bool gb_s = !(lds_ok && R <= cap);
+  if (!gb_s) cc_label<false>(SL, bm, nb64, TW, HS, R, rowoff, c8, s_red, &s_best);
+  else cc_label<true>(SG, bm, nb64, TW, HS, R, rowoff, c8, s_red, &s_best);
   const unsigned best_s = s_best;
 
-  // track x (per segment) — needed to know which side columns to measure
-  __shared__ int s_tx[15];
-  if (threadIdx.x < 15) {
-    const int i = threadIdx.x;
+  // track x, y per segment (moments of the bottom component, :2702-2725)
+  if (tid < LM_TAIL_SEGS) {
+    const int i = tid;
     int tx_ = -1, ty_ = -1;
     if (have) {
       const int sx = first + (i < rem ? i * (reg + 1) : rem * (reg + 1) + (i - rem) * reg);
       const int wseg = i < rem ? reg + 1 : reg;
       double m00 = 0, m10 = 0, m01 = 0;
       const double s = 1. / 255;
-      const int ntr = (HB + 31) >> 5, ntc = (wseg + 31) >> 5;
-      for (int ty = 0; ty < ntr; ++ty)
-        for (int tx = 0; tx < ntc; ++tx) {
-          const unsigned cnt = s_mb[i][ty][tx][0];
-          const double mom0 = (double)(255u * cnt) * s;
-          const double mom1 = (double)(255u * s_mb[i][ty][tx][1] + 0u) * s;
-          const double mom2 = (double)(255u * s_mb[i][ty][tx][2]) * s;
+      const int nc = (wseg + 31) >> 5;
+      for (int ty = 0; ty < ntrb; ++ty)
+        for (int tx = 0; tx < nc; ++tx) {
+          const unsigned* t = mb + ((i * ntrb + ty) * ntc + tx) * 3;
+          const double mom0 = (double)(255u * t[0]) * s;
+          const double mom1 = (double)(255u * t[1]) * s;
+          const double mom2 = (double)(255u * t[2]) * s;
           const double xm = (double)(tx * 32) * mom0, ym = (double)(ty * 32) * mom0;
           m00 += mom0;
           m10 += mom1 + xm;
@@ -1587,40 +537,31 @@ __global__ __launch_bounds__(1024) void k_tail(const LmConst* __restrict__ Kp, i
     }
     s_tx[i] = tx_;
     hdr[slot].tail[i] = tx_;
-    hdr[slot].tail[15 + i] = ty_;
+    hdr[slot].tail[LM_TAIL_SEGS + i] = ty_;
   }
   __syncthreads();
   if (best_s != 0xFFFFFFFFu) {
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-      if (cc_find(s_parent, k) != best_s) continue;
-      const unsigned p = s_fg[k];
-      const int y = p / TW, x = p % TW;
-      for (int i = 0; i < 15; ++i)
-        if (s_tx[i] > 0 && s_tx[i] == x) {
-          atomicAdd(&s_ms[i][y >> 5][0], 1u);
-          atomicAdd(&s_ms[i][y >> 5][1], (unsigned)(y & 31));
-        }
-    }
+    if (!gb_s) tail_side_moments<false>(SL, R, rowoff, HS, best_s, s_tx, ms, ntrs);
+    else tail_side_moments<true>(SG, R, rowoff, HS, best_s, s_tx, ms, ntrs);
   }
   __syncthreads();
-  if (threadIdx.x < 15) {
-    const int i = threadIdx.x;
+  // track z (:2728-2737): the side moments of column x_i when x_i > 0
+  if (tid < LM_TAIL_SEGS) {
+    const int i = tid;
     int tz = -1;
     if (s_tx[i] > 0) {
       double m00 = 0, m01 = 0;
       const double s = 1. / 255;
-      const int ntr = (HS + 31) >> 5;
-      for (int ty = 0; ty < ntr; ++ty) {
-        const double mom0 = (double)(255u * s_ms[i][ty][0]) * s;
-        const double mom2 = (double)(255u * s_ms[i][ty][1]) * s;
-        const double xm = 0.0 * mom0, ym = (double)(ty * 32) * mom0;
-        (void)xm;
+      for (int ty = 0; ty < ntrs; ++ty) {
+        const double mom0 = (double)(255u * ms[(i * ntrs + ty) * 2]) * s;
+        const double mom2 = (double)(255u * ms[(i * ntrs + ty) * 2 + 1]) * s;
+        const double ym = (double)(ty * 32) * mom0;
         m00 += mom0;
         m01 += mom2 + ym;
       }
       if (m00 > 0) tz = (int)(m01 / m00) + 0;
     }
-    hdr[slot].tail[30 + i] = tz;
+    hdr[slot].tail[2 * LM_TAIL_SEGS + i] = tz;
   }
 }
 
@@ -1890,7 +831,7 @@ DEV double readlane_f64(double v, int lane) {
 }
 
 __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
-                                                       const int32_t* __restrict__ n_pos, const uint8_t* __restrict__ tailmask,
+                                                       const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
                                                        unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
                                                        LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
                                                        long long* __restrict__ prof) {
@@ -1942,14 +883,15 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
   }
   __syncthreads();
   // load + TAIL_MASK filter (bottom: mask(BB_BOTTOM_TAIL).setTo(255, TAIL_MASK), :783)
-  const uint8_t* __restrict__ tm = tailmask + (int64_t)slot * K.tail_hb * K.tail_w;
+  const int tnb = (K.tail_w + 63) / 64;  // TAIL_MASK bitmap words per row
+  const unsigned long long* __restrict__ tm = tailmask + (int64_t)slot * K.tail_hb * tnb;
   for (int k = threadIdx.x; k < n_in; k += blockDim.x) {
     const unsigned long long v = src[k];
     bool keep = true;
     if (!side) {
       const unsigned idx = key_lo(v);
       const int y = idx / D.ow, x = idx - y * D.ow;
-      if (x < K.tail_w && y < K.tail_hb && tm[y * K.tail_w + x]) keep = false;
+      if (x < K.tail_w && y < K.tail_hb && ((tm[y * tnb + (x >> 6)] >> (x & 63)) & 1)) keep = false;
     }
     if (keep) a[atomicAdd(&s_n, 1)] = v;
   }
@@ -2148,7 +1090,8 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
 #define LM_POST_MAXOFF 2048  // CSC columns (Ni + Nong) + 1
 
 DEV bool vel_criterion(const LmConst& K, const uint8_t* Fc, const uint8_t* Fp, const uint8_t* bkg, const int32_t* cal,
-                       const uint8_t* lutc, const uint8_t* lutp, int crop_x, int crop_y, int crop_w, int crop_h,
+                       const uint8_t* lutc, const uint8_t* lutp, const LmSlot& slc, const LmSlot& slp, int crop_x,
+                       int crop_y, int crop_w, int crop_h,
                        int bx, int by, int bwid, int bhei, int area, double alpha, int32_t* err, int tag) {
   // checkVelCriterion (:1256-1267): sum(sat_u8(I - I_prev) > 25) >= area*alpha
   if (bx < 0 || by < 0 || bwid < 0 || bhei < 0 || bx + bwid > crop_w || by + bhei > crop_h) {
@@ -2168,8 +1111,8 @@ DEV bool vel_criterion(const LmConst& K, const uint8_t* Fc, const uint8_t* Fp, c
   for (int r = 0; r < bhei; ++r)
     for (int c = 0; c < bwid; ++c) {
       const int R = crop_y + by + r, C = crop_x + bx + c;
-      const int a = ipad_pixel(Fc, bkg, cal, lutc, K, R, C);
-      const int b = ipad_pixel(Fp, bkg, cal, lutp, K, R, C);
+      const int a = ipad_pixel_t(Fc, bkg, cal, lutc, K, slc, R, C);  // I_*_MOUSE_PAD
+      const int b = ipad_pixel_t(Fp, bkg, cal, lutp, K, slp, R, C);  // I_*_MOUSE_PAD_PREV
       const int s = a > b ? a - b : 0;
       sum += s > 25;
     }
@@ -2383,7 +1326,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restr
   }
   __syncthreads();
   // motion status where the reference evaluates it
-  const LmSlot sl = slots[slot];
+  const LmSlot sl = slots[slot], slp = slots[slot - 1];
   const uint8_t* Fc = frame_ptr[slot];
   const uint8_t* Fp = frame_ptr[slot - 1];
   const uint8_t* lutc = luts + slot * 256;
@@ -2395,7 +1338,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restr
       bool need = false;
       for (int j = 0; j < Ns; ++j) need |= boolD(i, j) && s_bps[j] > 1;
       if (need)
-        s_mb[i] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl.crop_x[0], sl.crop_y[0], K.crop_w[0], K.crop_h[0],
+        s_mb[i] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl, slp, sl.crop_x[0], sl.crop_y[0], K.crop_w[0], K.crop_h[0],
                                 mbox[0] + sb[i].x + K.spre_b_w, mbox[1] + sb[i].y + K.spre_b_h, mbox[2], mbox[3],
                                 K.size_b[feat][0] * K.size_b[feat][1], 0.02, err, (slot << 16) | (feat << 12) | i);
     }
@@ -2404,7 +1347,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restr
       if (s_bps[j] > 1)
         for (int i = 0; i < Nb; ++i) need |= boolD(i, j);
       if (need)
-        s_mt[j] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl.crop_x[1], sl.crop_y[1], K.crop_w[1], K.crop_h[1],
+        s_mt[j] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl, slp, sl.crop_x[1], sl.crop_y[1], K.crop_w[1], K.crop_h[1],
                                 tbox[0] + st[j].x + K.spre_t_w, tbox[1] + st[j].y + K.spre_t_h, tbox[2], tbox[3],
                                 K.size_s[feat][0] * K.size_s[feat][1], 0.05, err, (slot << 16) | (feat << 12) | 0x800 | j);
     }

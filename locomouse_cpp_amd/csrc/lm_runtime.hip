@@ -37,6 +37,21 @@ void hip_check(hipError_t e, const char* what) {
 }
 #define HIPCHK(x) hip_check((x), #x)
 
+// Copies and fills on a context's own (non-blocking) stream, waited for.
+// Never the synchronous hipMemcpy / hipMemset: they run on the legacy stream,
+// which HIP refuses while any other thread's stream is capturing a graph
+// (several contexts, one per host thread).
+#define COPY_SYNC(dst, src, bytes, kind, st) \
+  do {                                              \
+    HIPCHK(hipMemcpyAsync((dst), (src), (bytes), (kind), (st))); \
+    HIPCHK(hipStreamSynchronize(st));                \
+  } while (0)
+#define SET_SYNC(dst, v, bytes, st)                   \
+  do {                                              \
+    HIPCHK(hipMemsetAsync((dst), (v), (bytes), (st))); \
+    HIPCHK(hipStreamSynchronize(st));                \
+  } while (0)
+
 bool dbg_env(const char* name) {  // diagnostics switches (LM_* environment variables)
   const char* v = getenv(name);
   return v && atoi(v) != 0;
@@ -46,6 +61,8 @@ bool dbg_env(const char* name) {  // diagnostics switches (LM_* environment vari
 // both sides filled with 0xA5; lm_detect_batch* checks them after each batch
 // and fails with the buffer's address if a kernel wrote outside it.
 constexpr size_t kGuard = 64 * 1024;
+// LDS window of one k_corr_gen workgroup (row chunks are sized to fit it)
+constexpr size_t kCorrLdsBudget = 64 * 1024;
 bool guard_mode() {
   static const bool on = [] {
     const char* v = getenv("LM_GUARD");
@@ -202,20 +219,22 @@ struct lm_ctx {
   int64_t ext_slot_bytes = 0, tailbin_slot_bytes = 0, dbg_slot_floats = 0;
   int64_t dbg_off[LM_NDET] = {0};
   int64_t gscratch_slot = 0;
-  size_t corr_lds = 0;
-  int corr_variant = 2;
-  std::vector<std::pair<int, LmDetGroup>> corr_groups;  // (detector width, detectors)
+  bool unfused = false;                                         // LM_FILTER_UNFUSED
+  std::vector<std::pair<const void*, LmDetGroup>> corr_groups;  // (correlation kernel, its detectors)
   std::vector<size_t> corr_group_lds;                    // dynamic LDS bytes per group launch
   // device buffers
-  DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin, tailmask;
+  DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin;
+  DevBuf<unsigned long long> tailmask;  // TAIL_MASK bitmaps, 64 columns per word
   DevBuf<int32_t> cal, npos, err;
+  DevBuf<unsigned> mm;  // k_minmax partial (min, max) pairs per slot
   DevBuf<float> weights, dbg;
   DevBuf<int64_t> dbg_offd;
   DevBuf<const uint8_t*> frame_ptr;
   DevBuf<LmSlot> slots;
   DevBuf<unsigned long long> keys, gscratch;
   DevBuf<LmConst> dK;  // the per-context constants, passed to every kernel by pointer
-  DevBuf<unsigned> tscratch;
+  DevBuf<unsigned> tscratch;  // k_tail run tables beyond its LDS
+  size_t tail_lds = 0;
   DevBuf<long long> kprof;  // LM_KPROF=1: k_nms phase timestamps
   bool kprof_on = false;
   Arena arena[2];
@@ -231,6 +250,7 @@ struct lm_ctx {
   // state carried between batches
   bool have_state = false;
   int last_frame = -1, last_n = 0, last_parity = 0;
+  int last_bb[3] = {0, 0, 0};  // bottom-right corners of frame last_frame
   // last batch info
   int batch_n = 0, batch_s0 = 1;
   // timing
@@ -288,9 +308,18 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     throw std::runtime_error(
         "use_reference_image_brightness: computeNormalizedCDF writes the reference CDF through an unallocated cv::Mat "
         "(LocoMouse_class.cpp:189, :3392-3405); the reference cannot start with this option.");
-  if (P->transform_gray_values)
-    throw std::runtime_error(
-        "transform_gray_values: LUT re-types the bottom mask to CV_32F and Mat::setTo asserts (LocoMouse_class.cpp:1448, :849).");
+  if (P->transform_gray_values && !P->use_reference_image_brightness) {
+    // LUT(I_BOTTOM_MOUSE, REF_CDF_GLT, I_BOTTOM_MOUSE) (:1445-1448): dst takes the table's depth
+    if (P->gray_value_transformation_depth != LM_DEPTH_8U)
+      throw std::runtime_error(
+          "transform_gray_values: LUT with a non-8U table re-creates the bottom crop with the table's type; the mask "
+          "threshold / Mat::setTo(0, mask) then asserts (LocoMouse_class.cpp:1448, :782, :849).");
+    for (int i = 0; i < 256; ++i) {
+      const float v = P->gray_value_transformation[i];
+      if (!(v >= 0.f && v <= 255.f && v == std::floor(v)))
+        throw std::invalid_argument("gray_value_transformation: a CV_8U table holds integers 0..255.");
+    }
+  }
   if (P->occlusion_grid_spacing_pixels_bottom <= 0) throw std::invalid_argument("occlusion_grid_spacing_pixels_bottom must be > 0.");
   // loaders / validateImageVideoSize
   if (!su->background || !su->ind_warp_mapping) throw std::invalid_argument("background / calibration missing.");
@@ -319,8 +348,10 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   for (int d = 0; d < 6; ++d) {
     if (!dets[d]->weights || dets[d]->rows <= 0 || dets[d]->cols <= 0)
       throw std::invalid_argument(std::string("Error: ") + names[d] + " cannot be empty.");
-    if (dets[d]->rows > LM_MAXK || dets[d]->cols > LM_MAXK)
-      throw std::invalid_argument(std::string(names[d]) + ": detectors larger than 64x64 are not supported.");
+    // any size: k_corr_gen walks the taps in LDS-sized row chunks; one LDS row
+    // of the 80-column tile window must still fit (a detector wider than ~40k)
+    if ((size_t)(LM_TH + 1) * pk_stride(LM_TW + dets[d]->cols + LM_JC) * sizeof(float) > kCorrLdsBudget)
+      throw std::invalid_argument(std::string(names[d]) + ": detector too wide for the correlation window.");
   }
 
   c->setup = *su;
@@ -463,6 +494,15 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   K.tail_hb = ub.height;
   K.tail_hs = us.height;
   K.connectivity = P->conn_comp_connectivity;
+  // k_tail's LDS: bitmaps, column tables and moment tiles from the geometry,
+  // plus as many runs as fit 64 KiB (more go to global scratch)
+  K.tail_ntc = (((tw - 1) / 15 + 1) + 31) / 32;
+  K.tail_cap = 4096;
+  while (K.tail_cap > 64 && tail_layout(tw, ub.height, us.height, K.tail_cap, K.tail_ntc).bytes > 64 * 1024) K.tail_cap -= 64;
+  c->tail_lds = (size_t)tail_layout(tw, ub.height, us.height, K.tail_cap, K.tail_ntc).bytes;
+  if (c->tail_lds > 160 * 1024)
+    throw std::invalid_argument("tail box " + std::to_string(tw) + "x" + std::to_string(std::max(ub.height, us.height)) +
+                                " exceeds k_tail's LDS (bitmaps of the tail box).");
   int64_t off = 0;
   for (int l = 0; l < LM_NLIST; ++l) {
     const int d = l == 0 ? DET_PAW_B : l == 1 ? DET_SNOUT_B : l == 2 ? DET_PAW_S : DET_SNOUT_S;
@@ -510,6 +550,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     for (int j = 0; j < 7; ++j) K.prior[k][j] = row[j];
   }
   if (g.ong_nx * g.ong_ny + 1 + 512 > LM_POST_MAXOFF) throw std::invalid_argument("occlusion grid too large.");
+  K.gray_lut_on = P->transform_gray_values && !P->use_reference_image_brightness ? 1 : 0;
+  for (int i = 0; i < 256; ++i) K.gray_lut[i] = K.gray_lut_on ? (uint8_t)P->gray_value_transformation[i] : (uint8_t)i;
 
   // per-slot sizes
   c->ext_slot_bytes = ((int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1] + 255) / 256 * 256;
@@ -523,67 +565,40 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   int np = 1;
   while (np < std::max(K.list_cap[0], K.list_cap[2])) np <<= 1;
   c->gscratch_slot = 3 * (int64_t)np;  // keys (u64) + assign, cluster list, xy (32-bit) per entry
-  size_t lds = 0;
-  for (int d = 0; d < 6; ++d) {
-    const LmDet& D = K.det[d];
-    int cols = LM_TW + D.kwp - 1;
-    int stride = std::max(cols + ((16 - (cols & 31) + 32) & 31), pk_stride(cols));
-    lds = std::max(lds, (size_t)(LM_TH + D.kh - 1) * stride * sizeof(float) + 16 + (size_t)D.kh * D.kwp * sizeof(float));
-  }
-  c->corr_lds = lds;
-  c->corr_variant = CORR_PK_ASM;
-  if (const char* v = getenv("LM_CORR_VARIANT")) c->corr_variant = atoi(v);
+  c->unfused = su->filter_arith == LM_FILTER_UNFUSED;
   if (const char* v = getenv("LM_KPROF")) c->kprof_on = atoi(v) != 0;
-  // detectors grouped by width: one width-specialised correlation launch each
+  // Detectors grouped by correlation kernel: one width-specialised k_corr_pk
+  // launch per width, every other detector in one k_corr_gen launch.  Each
+  // launch gets exactly the LDS its detectors' windows need, so narrow groups
+  // keep more workgroups per CU.
   c->corr_groups.clear();
+  c->corr_group_lds.clear();
   for (int d = 0; d < 6; ++d) {
-    const int kw = K.det[d].kw;
-    auto it = std::find_if(c->corr_groups.begin(), c->corr_groups.end(), [&](const auto& p) { return p.first == kw; });
-    if (it == c->corr_groups.end()) {
+    LmDet& D = K.det[d];
+    const void* fn = corr_kernel(D.kw, D.kh, c->unfused);
+    size_t need;
+    if (corr_specialised(D.kw, D.kh)) {
+      D.chunk_rows = D.kh;
+      need = (size_t)(LM_TH + D.kh - 1) * pk_stride(LM_TW + D.kw - 1) * sizeof(float);
+    } else {
+      const size_t row = (size_t)pk_stride(LM_TW + D.kwp - 1) * sizeof(float);
+      D.chunk_rows = std::max(1, std::min(D.kh, (int)(kCorrLdsBudget / row) - (LM_TH - 1)));
+      need = (size_t)(LM_TH + D.chunk_rows - 1) * row;
+    }
+    size_t gi = 0;
+    while (gi < c->corr_groups.size() && c->corr_groups[gi].first != fn) ++gi;
+    if (gi == c->corr_groups.size()) {
       LmDetGroup G;
       std::memset(&G, 0, sizeof(G));
-      if (const char* v = getenv("LM_CORR_SKIP")) G.skip_taps = atoi(v);  // diagnostics
-      c->corr_groups.push_back({kw, G});
-      it = c->corr_groups.end() - 1;
+      c->corr_groups.push_back({fn, G});
+      c->corr_group_lds.push_back(0);
     }
-    LmDetGroup& G = it->second;
+    LmDetGroup& G = c->corr_groups[gi].second;
     const int prev = G.n ? G.tile_end[G.n - 1] : 0;
     G.ids[G.n] = d;
-    G.tile_end[G.n] = prev + K.det[d].tiles_x * K.det[d].tiles_y;
+    G.tile_end[G.n] = prev + D.tiles_x * D.tiles_y;
     ++G.n;
-  }
-  // LDS per group: the packed kernel needs only its own tile window
-  // (LM_TH+kh-1 rows at pk_stride), so narrow groups are not sized for the
-  // widest detector and keep more workgroups per CU; other variants use the
-  // common size.
-  c->corr_group_lds.clear();
-  for (const auto& grp : c->corr_groups) {
-    size_t need = c->corr_lds;
-    int th = 0;
-    (void)corr_kernel(c->corr_variant, grp.first, &th);  // th == 256: generic fallback kernel
-    const int v = c->corr_variant;
-    if ((v == CORR_CB || v == CORR_CB_WLDS || v == CORR_C1) && th != 256) {
-      need = 0;
-      int sc = CB_H + grp.first - 1;
-      while ((sc & 7) != 4) ++sc;
-      for (int k = 0; k < grp.second.n; ++k) {
-        const LmDet& D = K.det[grp.second.ids[k]];
-        const int spare = v == CORR_C1 ? 1 : 0;  // k_corr_c1 reads a spare row in its last iteration
-        need = std::max(need, (size_t)(LM_TH + D.kh - 1 + spare) * sc * 2 * sizeof(float) +
-                                  (v == CORR_CB_WLDS ? (size_t)D.kh * D.kwp * sizeof(float) : 0));
-      }
-    } else if ((v == CORR_PK_ASM || v == CORR_SP || v == CORR_PK_WLDS) && th == 192) {
-      need = 0;
-      for (int k = 0; k < grp.second.n; ++k) {
-        const LmDet& D = K.det[grp.second.ids[k]];
-        // k_corr_sp reads two spare rows past the tile in its last iteration
-        const int spare = v == CORR_SP ? 2 : 0;
-        const size_t tile = (size_t)(LM_TH + D.kh - 1 + spare) * pk_stride(LM_TW + grp.first - 1);
-        need = std::max(need, (((tile + 3) & ~(size_t)3) + (v == CORR_PK_WLDS ? (size_t)D.kh * D.kwp : 0)) *
-                                  sizeof(float));
-      }
-    }
-    c->corr_group_lds.push_back(need);
+    c->corr_group_lds[gi] = std::max(c->corr_group_lds[gi], need);
   }
 
   // weights (float, rows zero-padded to kwp) and TM imadjust LUT
@@ -610,26 +625,27 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   // ---------------- device allocations
   const int ns = c->nslots;
   c->bkg.alloc(nv);
-  HIPCHK(hipMemcpy(c->bkg.p, su->background, nv, hipMemcpyHostToDevice));
+  COPY_SYNC(c->bkg.p, su->background, nv, hipMemcpyHostToDevice, c->stream);
   c->cal.alloc(nc);
-  HIPCHK(hipMemcpy(c->cal.p, su->ind_warp_mapping, nc * sizeof(int32_t), hipMemcpyHostToDevice));
+  COPY_SYNC(c->cal.p, su->ind_warp_mapping, nc * sizeof(int32_t), hipMemcpyHostToDevice, c->stream);
   c->weights.alloc(wts.size());
-  HIPCHK(hipMemcpy(c->weights.p, wts.data(), wts.size() * sizeof(float), hipMemcpyHostToDevice));
+  COPY_SYNC(c->weights.p, wts.data(), wts.size() * sizeof(float), hipMemcpyHostToDevice, c->stream);
   c->adj.alloc(256);
-  HIPCHK(hipMemcpy(c->adj.p, adj, 256, hipMemcpyHostToDevice));
+  COPY_SYNC(c->adj.p, adj, 256, hipMemcpyHostToDevice, c->stream);
   c->dK.alloc(1);
-  HIPCHK(hipMemcpy(c->dK.p, &c->K, sizeof(LmConst), hipMemcpyHostToDevice));
+  COPY_SYNC(c->dK.p, &c->K, sizeof(LmConst), hipMemcpyHostToDevice, c->stream);
   const int64_t fstride = (nv + 255) / 256 * 256;
   c->frames.alloc((size_t)fstride * ns);
   c->halo.alloc(fstride);
-  HIPCHK(hipMemset(c->halo.p, 0, fstride));
+  SET_SYNC(c->halo.p, 0, fstride, c->stream);
   c->luts.alloc((size_t)256 * ns);
+  c->mm.alloc((size_t)2 * LM_MM_SPLIT * ns);
   // slack: the last tiles' windows (and the fill's 16-byte rounding) read past
   // the last slot's side view; those pixels only feed outputs that are discarded
   c->ext.alloc((size_t)c->ext_slot_bytes * ns + (size_t)(LM_TH + 16) * std::max(K.ext_w[0], K.ext_w[1]) + 64);
   c->tailbin.alloc((size_t)c->tailbin_slot_bytes * ns);
-  c->tailmask.alloc((size_t)K.tail_hb * K.tail_w * ns);
-  c->tscratch.alloc((size_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w * ns);
+  c->tailmask.alloc((size_t)K.tail_hb * ((K.tail_w + 63) / 64) * ns);
+  c->tscratch.alloc((size_t)5 * std::max(K.tail_hb, K.tail_hs) * ((K.tail_w + 1) / 2) * ns);
   c->keys.alloc((size_t)K.keys_per_slot * ns);
   c->npos.alloc((size_t)LM_NLIST * ns);
   c->err.alloc(16);
@@ -640,7 +656,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->h_ctl.alloc(1);
   c->h_ph.alloc(1);
   c->zero_ph.alloc(1);  // an all-zero pack header: k_out with it copies only the halo
-  HIPCHK(hipMemset(c->zero_ph.p, 0, sizeof(LmPackHdr)));
+  SET_SYNC(c->zero_ph.p, 0, sizeof(LmPackHdr), c->stream);
   c->h_err.alloc(16);
   int cap[AR_COUNT];
   cap[AR_CAND] = ns * LM_NLIST * 64;
@@ -651,9 +667,10 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   cap[AR_PWNZ] = ns * LM_NFEAT * 1024;
   for (int a = 0; a < 2; ++a) c->arena[a].alloc(cap, ns);
   c->h_pack.alloc((size_t)c->arena[0].pack_cap);
+  HIPCHK(hipFuncSetAttribute((const void*)k_tail, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->tail_lds));
   for (size_t g = 0; g < c->corr_groups.size(); ++g)
-    HIPCHK(corr_set_lds(c->corr_variant, c->corr_groups[g].first, c->corr_group_lds[g]));
-  HIPCHK(hipFuncSetAttribute((const void*)k_corr_dbg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->corr_lds));
+    HIPCHK(hipFuncSetAttribute(c->corr_groups[g].first, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)c->corr_group_lds[g]));
 }
 
 
@@ -743,7 +760,7 @@ struct Timer {
 // LM_KPROF=1: mean cycles per k_nms phase over the batch's blocks (stderr)
 void kprof_report(lm_ctx* c, int n) {
   std::vector<long long> h((size_t)2 * 16 * 2 * c->nslots);
-  HIPCHK(hipMemcpy(h.data(), c->kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost));
+  COPY_SYNC(h.data(), c->kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
   for (int side = 0; side < 2; ++side) {
     double acc[16] = {0}, life = 0, wlife = 0;
     int cnt[16] = {0}, nb = 0;
@@ -808,9 +825,9 @@ void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first
 void dump_slot(lm_ctx* c, const char* dir, int frame, int slot, int feat) {
   const LmConst& K = c->K;
   std::vector<int32_t> np(LM_NLIST);
-  HIPCHK(hipMemcpy(np.data(), c->npos.p + (int64_t)slot * LM_NLIST, LM_NLIST * sizeof(int32_t), hipMemcpyDeviceToHost));
+  COPY_SYNC(np.data(), c->npos.p + (int64_t)slot * LM_NLIST, LM_NLIST * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
   LmSlotOut h;
-  HIPCHK(hipMemcpy(&h, c->arena[c->parity].hdr.p + slot, sizeof(h), hipMemcpyDeviceToHost));
+  COPY_SYNC(&h, c->arena[c->parity].hdr.p + slot, sizeof(h), hipMemcpyDeviceToHost, c->stream);
   std::string path = std::string(dir) + "/dump_" + std::to_string(frame) + ".bin";
   FILE* f = fopen(path.c_str(), "wb");
   if (!f) return;
@@ -854,6 +871,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   const bool direct = device_frames && ((((uintptr_t)frames | (uintptr_t)pitch) & 15) == 0);
   // ---- slots: frame pointers and crop rectangles (cropBoundingBox :1420-1470)
   const int s_lut0 = first > 0 ? 0 : 1, s_proc0 = halo ? 0 : 1;
+  int new_last_bb[3] = {c->bb_x, c->bb_yb, c->bb_ys};
   for (int s = 0; s <= n; ++s) {
     LmSlot& S = c->h_slots.p[s];
     std::memset(&S, 0, sizeof(S));
@@ -869,6 +887,15 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       bx = bb[3 * bi];
       byb = bb[3 * bi + 1];
       bys = bb[3 * bi + 2];
+    } else if (s == 0 && carry) {  // the previous batch's last frame
+      bx = c->last_bb[0];
+      byb = c->last_bb[1];
+      bys = c->last_bb[2];
+    }
+    if (s == n) {
+      new_last_bb[0] = bx;
+      new_last_bb[1] = byb;
+      new_last_bb[2] = bys;
     }
     S.crop_x[0] = (int)((unsigned)(bx + g.pad_pre_cols) - (unsigned)(g.bb_bottom_mouse_pad.width - g.spost_b_w) + 1u);
     S.crop_y[0] = (int)((unsigned)(byb + g.pad_pre_rows) - (unsigned)(g.bb_bottom_mouse_pad.height - g.spost_b_h) + 1u);
@@ -880,6 +907,14 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       for (int v = 0; v < 2; ++v)
         if (S.crop_x[v] < 0 || S.crop_y[v] < 0 || S.crop_x[v] + w[v] > g.ipad_cols || S.crop_y[v] + h[v] > g.ipad_rows)
           throw std::runtime_error(std::string("ROI out of image bounds: ") + (v ? "BB_SIDE_MOUSE_PAD" : "BB_BOTTOM_MOUSE_PAD"));
+    if (K.gray_lut_on) {  // the in-place LUT must stay inside I_UNPAD (see locomouse_hip.h)
+      const int ux = S.crop_x[0] + g.spre_b_w, uy = S.crop_y[0] + g.spre_b_h;
+      if (ux < g.pad_pre_cols || uy < g.pad_pre_rows || ux + g.bb_bottom_mouse.width > g.pad_pre_cols + g.n_cols ||
+          uy + g.bb_bottom_mouse.height > g.pad_pre_rows + g.n_rows)
+        throw std::invalid_argument("transform_gray_values: frame " + std::to_string(S.frame) +
+                                    ": the bottom crop leaves the corrected image, so the in-place LUT would reach "
+                                    "I_PAD's zero padding (not supported).");
+    }
   }
   (void)K;
 
@@ -905,10 +940,6 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
 
   const int cur = c->parity, prv = c->last_parity;
   if (!c->gscratch.p) c->gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
-  static const int ingest_fb = [] {  // slots per k_ingest_fb thread; LM_INGEST_FB=0: k_ingest
-    const char* v = getenv("LM_INGEST_FB");
-    return v ? std::max(0, std::min(LM_INGEST_FB, atoi(v))) : LM_INGEST_FB;
-  }();
   static const bool graphs_env = [] {
     const char* v = getenv("LM_GRAPH");
     return !v || atoi(v) != 0;
@@ -927,49 +958,24 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
         k_carry<<<1, 256, 0, st>>>(dK, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
         T.end();
       }
-      T.begin("k_minmax_lut");
-      k_minmax_lut<<<n + 1 - s_lut0, 1024, 0, st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0, c->adj.p,
-                                                   c->setup.method != 0, c->luts.p);
+      T.begin("k_minmax");
+      k_minmax<<<dim3(LM_MM_SPLIT, n + 1 - s_lut0), LM_MM_THREADS, 0, st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0,
+                                                                          c->mm.p);
+      k_lut<<<(n + 1 - s_lut0 + 3) / 4, 256, 0, st>>>(c->mm.p, s_lut0, n + 1, c->adj.p, c->setup.method != 0, c->luts.p);
       T.end();
       const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
       T.begin("k_ingest");
-      if (ingest_fb)
-        k_ingest_fb<<<dim3((unsigned)((etot / 4 + 255) / 256), (unsigned)((nproc + ingest_fb - 1) / ingest_fb)), 256, 0,
-                      st>>>(dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, n + 1, ingest_fb,
-                            c->ext.p, c->ext_slot_bytes);
-      else
-        k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
-            dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, c->ext.p, c->ext_slot_bytes);
+      k_ingest<<<dim3((unsigned)((etot / LM_INGEST_VEC + 255) / 256), (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)),
+                 256, 0, st>>>(dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, n + 1, c->ext.p,
+                               c->ext_slot_bytes);
       T.end();
-      if (ingest_fb && dbg_env("LM_INGEST_CHECK")) {  // diagnostics: compare with k_ingest
-        DevBuf<uint8_t> e2;
-        e2.alloc((size_t)c->ext_slot_bytes * c->nslots);
-        k_ingest<<<dim3((unsigned)((etot / 4 + 255) / 256), nproc), 256, 0, st>>>(
-            dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, e2.p, c->ext_slot_bytes);
-        HIPCHK(hipStreamSynchronize(st));
-        std::vector<uint8_t> a((size_t)c->ext_slot_bytes), b((size_t)c->ext_slot_bytes);
-        for (int sl = s_proc0; sl <= n; ++sl) {
-          HIPCHK(hipMemcpy(a.data(), c->ext.p + (int64_t)sl * c->ext_slot_bytes, a.size(), hipMemcpyDeviceToHost));
-          HIPCHK(hipMemcpy(b.data(), e2.p + (int64_t)sl * c->ext_slot_bytes, b.size(), hipMemcpyDeviceToHost));
-          int64_t bad = -1, nbad = 0;
-          for (int64_t q = 0; q < etot; ++q)
-            if (a[q] != b[q]) {
-              if (bad < 0) bad = q;
-              ++nbad;
-            }
-          if (bad >= 0)
-            fprintf(stderr, "[ingest check] slot %d: %ld bytes differ, first at %ld (fb %d vs ref %d), e0 %ld ext_w %d,%d\n",
-                    sl, (long)nbad, (long)bad, a[bad], b[bad], (long)((int64_t)K.ext_h[0] * K.ext_w[0]), K.ext_w[0],
-                    K.ext_w[1]);
-        }
-      }
     }
     if (part == 1 || part < 0) {
       T.begin("k_corr");
       for (size_t gi = 0; gi < c->corr_groups.size(); ++gi) {
         const auto& grp = c->corr_groups[gi];
         const LmDetGroup& G = grp.second;
-        HIPCHK(launch_corr(c->corr_variant, grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_lds[gi], st, dK, G,
+        HIPCHK(launch_corr(grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_lds[gi], st, dK, G,
                            c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->keys.p, c->npos.p, c->tailbin.p,
                            c->tailbin_slot_bytes));
       }
@@ -980,14 +986,19 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
         if (!c->dbg.p) {
           c->dbg.alloc((size_t)c->dbg_slot_floats * c->nslots);
           c->dbg_offd.alloc(LM_NDET);
-          HIPCHK(hipMemcpy(c->dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice));
+          COPY_SYNC(c->dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice, c->stream);
         }
-        k_corr_dbg<<<dim3(K.n_tiles, nproc), 256, c->corr_lds, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0,
-                                                                     c->dbg.p, c->dbg_offd.p, c->dbg_slot_floats);
+        const dim3 dgrid(64, nproc, LM_NDET);
+        if (c->unfused)
+          k_corr_dbg<true><<<dgrid, 256, 0, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->dbg.p,
+                                                  c->dbg_offd.p, c->dbg_slot_floats);
+        else
+          k_corr_dbg<false><<<dgrid, 256, 0, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->dbg.p,
+                                                   c->dbg_offd.p, c->dbg_slot_floats);
       }
       T.begin("k_tail");
-      k_tail<<<nproc, 1024, 0, st>>>(dK, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p, c->tscratch.p,
-                                     (int64_t)std::max(K.tail_hb, K.tail_hs) * K.tail_w, A.hdr.p, c->err.p);
+      k_tail<<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p,
+                                                          c->tscratch.p, A.hdr.p);
       T.end();
       long long *kp0 = nullptr, *kp1 = nullptr;
       if (c->kprof_on) {
@@ -1077,13 +1088,13 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
     const LmPackHdr& ph = *c->h_ph.p;
     const int e = (c->debug & 4) ? (ph.err & ~4) : ph.err;  // debug bit 2: report but keep going
     if ((c->debug & 4) && (ph.err & 4)) {
-      HIPCHK(hipMemcpy(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost));
+      COPY_SYNC(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
       const int32_t* d = c->h_err.p;
       fprintf(stderr, "[lm debug] vel box error frame %d tag %x box (%d,%d,%d,%d)\n", first - 1 + (d[2] >> 16), d[2],
               d[3], d[4], d[5], d[6]);
     }
     if (e & 4) {
-      HIPCHK(hipMemcpy(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost));
+      COPY_SYNC(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
       const int32_t* d = c->h_err.p;
       const int tag = d[2], slot = tag >> 16;
       if (const char* dir = getenv("LM_DUMP_DIR")) dump_slot(c, dir, first - 1 + slot, slot, (tag >> 12) & 1);
@@ -1095,7 +1106,6 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
                                            "assertion).") + buf);
     }
     if (e & 16) throw std::runtime_error("P22D::add_side_candidate_safe: CV_Assert(S >= 0) failed.");
-    if (e & 2) throw std::runtime_error("tail foreground exceeds the kernel's LDS capacity.");
     if (e & 8) throw std::runtime_error("candidate list exceeds the k_post LDS capacity.");
     if (e & 32) throw std::runtime_error("candidate staging overflow.");
     if (e) throw std::runtime_error("device error flags " + std::to_string(e));
@@ -1144,6 +1154,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   const LmPackLayout L = lm_pack_layout(n, ph.tot);
   const uint8_t* hp = c->h_pack.p;
   c->have_state = true;
+  for (int k = 0; k < 3; ++k) c->last_bb[k] = new_last_bb[k];
   c->last_frame = first + n - 1;
   c->last_n = n;
   c->last_parity = cur;
@@ -1265,8 +1276,8 @@ LM_API lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out
   if (rows != D.oh || cols != D.ow) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
   return guarded([&] {
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipMemcpy(out, ctx->dbg.p + (int64_t)(f + 1) * ctx->dbg_slot_floats + ctx->dbg_off[det],
-                     sizeof(float) * rows * cols, hipMemcpyDeviceToHost));
+    COPY_SYNC(out, ctx->dbg.p + (int64_t)(f + 1) * ctx->dbg_slot_floats + ctx->dbg_off[det], sizeof(float) * rows * cols,
+              hipMemcpyDeviceToHost, ctx->stream);
   });
 }
 
@@ -1276,7 +1287,11 @@ LM_API lm_status lm_debug_tail_mask(lm_ctx* ctx, int32_t f, uint8_t* out, int32_
   if (rows != ctx->K.tail_hb || cols != ctx->K.tail_w) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
   return guarded([&] {
     HIPCHK(hipSetDevice(ctx->device));
-    HIPCHK(hipMemcpy(out, ctx->tailmask.p + (int64_t)(f + 1) * rows * cols, (size_t)rows * cols, hipMemcpyDeviceToHost));
+    const int nb = (cols + 63) / 64;
+    std::vector<unsigned long long> bits((size_t)rows * nb);
+    COPY_SYNC(bits.data(), ctx->tailmask.p + (int64_t)(f + 1) * rows * nb, bits.size() * 8, hipMemcpyDeviceToHost, ctx->stream);
+    for (int r = 0; r < rows; ++r)
+      for (int x = 0; x < cols; ++x) out[(size_t)r * cols + x] = ((bits[(size_t)r * nb + (x >> 6)] >> (x & 63)) & 1) ? 255 : 0;
   });
 }
 

@@ -215,6 +215,10 @@ void load_config(const std::string& file, const std::string& ref_path, lm_params
       bad("The gray level transformation must be a 1x256 matrix, was " + std::to_string(G.rows) + "x" +
           std::to_string(G.cols) + ".");
     for (int k = 0; k < 256; ++k) P.gray_value_transformation[k] = (float)G.v[k];
+    // the table keeps its FileStorage depth: LUT() gives its output that type (:1448)
+    static const char kDt[] = "ucwsifd";
+    const char* d = std::strchr(kDt, G.dt);
+    P.gray_value_transformation_depth = d ? (int32_t)(d - kDt) : LM_DEPTH_64F;
   }
   P.use_provided_bounding_box = c["use_provided_bounding_box"].to_int();
   if (P.use_provided_bounding_box) {

@@ -298,8 +298,15 @@ void LocoMouse::flush() {
     bb[3 * i + 2] = (int32_t)BB_Y_SIDE_POS[first + i];
   }
   PENDING.swap(SUBMITTED);
+  // Frames already read ahead past this batch (read_frames fills up to a whole
+  // batch; a caller that reads results mid-batch flushes early) move to the
+  // front of the new pending buffer, so the reader's position and the frame
+  // numbering stay in step.
+  const int ahead = std::max(0, N_READ_AHEAD - n);
+  if (ahead)
+    std::memcpy(PENDING.data(), SUBMITTED.data() + (size_t)n * FRAME_BYTES, (size_t)ahead * FRAME_BYTES);
   N_PENDING = 0;
-  N_READ_AHEAD = 0;
+  N_READ_AHEAD = ahead;
   INFLIGHT = std::async(std::launch::async, [this, n, first, bb = std::move(bb)] {
     lm_batch_result r{};
     throw_on_error(lm_detect_batch(CTX, SUBMITTED.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data(), &r));

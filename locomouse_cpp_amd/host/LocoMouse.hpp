@@ -57,6 +57,10 @@ struct LocoMouse_Inputs {
   // contiguous), returning how many were read.  When given, readFrame reads a
   // whole batch ahead at its first frame (so a decoder can fill it in
   // parallel, without a per-frame copy); frames are still consumed in order.
+  // It may return fewer than n frames only at the end of the video or on a
+  // read error: the shortfall is reported ("Failed to read image") when the
+  // missing frame is consumed.  Frames read ahead survive a batch handed over
+  // early (a result accessor called mid-batch).
   std::function<int(uint8_t* dst, int n)> read_frames;
   int device = 0;      // HIP device of this instance (one per GPU / host thread)
   int batch = 256;     // frames per lm_detect_batch / lm_bb_push call

@@ -476,8 +476,20 @@ class LocoMouseOracle {
       throw std::invalid_argument("use_provided_bounding_box = 0 needs the whole-video BB pass (not on this path).");
     if (P.use_reference_image_brightness)
       throw std::runtime_error("use_reference_image_brightness: computeNormalizedCDF into an unallocated cv::Mat (LocoMouse_class.cpp:189, :3392-3405).");
-    if (P.transform_gray_values)
-      throw std::runtime_error("transform_gray_values: LUT re-types the bottom mask to CV_32F and Mat::setTo asserts (LocoMouse_class.cpp:1448, :849).");
+    if (P.transform_gray_values && !P.use_reference_image_brightness) {
+      // LUT(I_BOTTOM_MOUSE, REF_CDF_GLT, I_BOTTOM_MOUSE) (:1445-1448): cv::LUT creates dst with the
+      // table's depth; only a CV_8U table leaves the ROI of I_PAD in place, any other depth makes
+      // I_BOTTOM_MOUSE a new Mat whose threshold / setTo(0, mask) asserts (:782, :849).
+      if (P.gray_value_transformation_depth != LM_DEPTH_8U)
+        throw std::runtime_error("transform_gray_values: LUT with a non-8U table re-creates the bottom crop with the table's type (LocoMouse_class.cpp:1448, :782, :849).");
+      for (int i = 0; i < 256; ++i) {
+        const float v = P.gray_value_transformation[i];
+        if (!(v >= 0.f && v <= 255.f && v == std::floor(v)))
+          throw std::invalid_argument("gray_value_transformation: a CV_8U table holds integers 0..255.");
+        GLT[i] = (uint8_t)v;
+      }
+      use_glt = true;
+    }
     for (int k = 0; k < 4; ++k) prior_paw.emplace_back(P.location_prior[k]);
     prior_snout.emplace_back(P.location_prior[4]);
     // --- loaders / validateImageVideoSize (:402-540)
@@ -499,6 +511,7 @@ class LocoMouseOracle {
       throw std::runtime_error("Provided bounding box for the side view exceeds the image dimensions.");
     METHOD = su.method;
     IMAGE_FLIP = su.flip != 0;
+    FILTER_ARITH = su.filter_arith;
     // --- LocoMouse_Model (:3095-3179)
     auto chk = [](const lm_detector& d, const char* n) {
       if (!d.weights || d.rows <= 0 || d.cols <= 0)
@@ -674,6 +687,11 @@ class LocoMouseOracle {
     BB_BOTTOM_MOUSE_PAD.x = (int)((bx + PAD_PRE_COLS) - (BB_BOTTOM_MOUSE_PAD.width - spost_b.x) + 1);
     BB_BOTTOM_MOUSE_PAD.y = (int)((byb + PAD_PRE_ROWS) - (BB_BOTTOM_MOUSE_PAD.height - spost_b.y) + 1);
     check_roi(BB_BOTTOM_MOUSE_PAD, I_PAD.rows, I_PAD.cols, "BB_BOTTOM_MOUSE_PAD");
+    if (use_glt)  // LUT(I_BOTTOM_MOUSE, REF_CDF_GLT, I_BOTTOM_MOUSE), in place on I_PAD (:1445-1448)
+      for (int r = 0; r < BB_BOTTOM_MOUSE.height; ++r) {
+        uint8_t* row = I_PAD.row(BB_BOTTOM_MOUSE_PAD.y + BB_UNPAD_MOUSE_BOTTOM.y + r) + BB_BOTTOM_MOUSE_PAD.x + BB_UNPAD_MOUSE_BOTTOM.x;
+        for (int c = 0; c < BB_BOTTOM_MOUSE.width; ++c) row[c] = GLT[row[c]];
+      }
     BB_SIDE_MOUSE_PAD.x = (int)((PAD_PRE_COLS + bx) - (BB_SIDE_MOUSE_PAD.width - spost_t.x) + 1);
     BB_SIDE_MOUSE_PAD.y = (int)((PAD_PRE_ROWS + bys) - (BB_SIDE_MOUSE_PAD.height - spost_t.y) + 1);
     check_roi(BB_SIDE_MOUSE_PAD, I_PAD.rows, I_PAD.cols, "BB_SIDE_MOUSE_PAD");
@@ -686,7 +704,7 @@ class LocoMouseOracle {
     return I_PAD.at(BB_SIDE_MOUSE_PAD.y + BB_UNPAD_MOUSE_SIDE.y + r, BB_SIDE_MOUSE_PAD.x + BB_UNPAD_MOUSE_SIDE.x + c);
   }
 
-  bool fused() const { return !(flags_ & LMO_UNFUSED_FILTER); }
+  bool fused() const { return !(flags_ & LMO_UNFUSED_FILTER) && FILTER_ARITH != LM_FILTER_UNFUSED; }
 
   // detectTail :2541-2555 -> detectLineCandidates :2558-2742
   void detectTail() {
@@ -1023,8 +1041,10 @@ class LocoMouseOracle {
   int flags_;
   lm_params P;
   std::vector<LocationPrior> prior_paw, prior_snout;
-  int VR = 0, VC = 0, N_ROWS = 0, N_COLS = 0, METHOD = 0;
+  int VR = 0, VC = 0, N_ROWS = 0, N_COLS = 0, METHOD = 0, FILTER_ARITH = 0;
   bool IMAGE_FLIP = false;
+  bool use_glt = false;  // transform_gray_values with a CV_8U table
+  uint8_t GLT[256] = {0};
   std::vector<uint8_t> BKG;
   std::vector<int32_t> CAL;
   Feature paw, snout, tail;

@@ -56,6 +56,13 @@ extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_
       std::memcpy(dst, frames + (size_t)next++ * fb, fb);
       return true;
     };
+    if (call_order & 8) {  // the batch reader (read_frames), as the CLI uses it
+      in.read_frames = [&](uint8_t* dst, int n) {
+        int k = 0;
+        for (; k < n && next < n_read; ++k, ++next) std::memcpy(dst + (size_t)k * fb, frames + (size_t)next * fb, fb);
+        return k;
+      };
+    }
     if (bb_params) {
       in.bb_params = *bb_params;
       in.rewind = [&] { next = 0; };  // V.set(CV_CAP_PROP_POS_FRAMES, 0)

@@ -1,0 +1,191 @@
+"""GPU parity on the reference's edge paths (tests/edge_scenes.py): the HIP
+path through the C-ABI against the oracle, bit for bit, on blank and
+half-blank frames across batch seams, zero-positive lists, dense and
+checkerboard tail maps (k_tail's global run tables), detectors of sizes the
+width-specialised kernels do not cover, the unfused filter2D arithmetic, the
+CV_8U grey-level LUT, and three contexts on a tie-heavy configuration."""
+import threading
+
+import numpy as np
+import pytest
+
+import edge_scenes as E
+from locomouse_cpp_amd import abi
+from locomouse_cpp_amd import synthetic as S
+from locomouse_cpp_amd.results import concat_results
+from test_gpu_parity import _ctx, _oracle, _quantized_config, assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def _batched(cfg, frames, B, bb=None):
+    ctx = _ctx(cfg, max_batch=B)
+    parts = []
+    for i in range(0, len(frames), B):
+        parts.append(ctx.detect(frames[i:i + B], i, bb=None if bb is None else bb[i:i + B]))
+    ctx.close()
+    return concat_results(parts)
+
+
+@pytest.mark.parametrize("B", [5, 14])
+def test_blank_and_half_blank_frames(B):
+    """Blank frames mid-batch and on both sides of a batch seam (B = 5),
+    bottom-blank frames (side lists skipped, :820-833) and a side-blank frame
+    (zero side positives, P22D without side candidates)."""
+    cfg = S.SyntheticConfig()
+    frames = E.edge_video(cfg)
+    assert_same(_batched(cfg, frames, B), _oracle(cfg, frames).result, f"edges B{B}: ")
+
+
+def test_half_blank_shard_start():
+    """A shard that starts right after a blank frame (halo = the blank frame)
+    and one whose halo frame has an empty bottom list."""
+    cfg = S.SyntheticConfig()
+    frames = E.edge_video(cfg)
+    ref = _oracle(cfg, frames).result
+    from locomouse_cpp_amd.results import slice_results
+    for start in (6, 8):
+        got = _ctx(cfg, max_batch=8).detect(frames[start:], start, prev_frame=frames[start - 1])
+        assert_same(got, slice_results(ref, start), f"halo {start}: ")
+
+
+@pytest.mark.parametrize("names", [("snout_bottom",), ("paw_side", "snout_side"), ("paw_bottom", "snout_bottom"),
+                                   ("paw_bottom", "snout_bottom", "paw_side", "snout_side", "tail_bottom",
+                                    "tail_side")])
+def test_detectors_without_positives(names):
+    cfg = E.silent_config(names)
+    frames = cfg.frames(3, 9)
+    assert_same(_batched(cfg, frames, 4), _oracle(cfg, frames).result, f"silent {names}: ")
+
+
+def test_dense_tail_map():
+    """Every tail score positive: one component filling the tail box (far
+    beyond round 1's 6,144-pixel LDS limit), TAIL_MASK over the whole box."""
+    cfg = E.dense_tail_config()
+    frames = cfg.frames(0, 6)
+    ctx = _ctx(cfg, max_batch=6)
+    ctx.set_debug(1)
+    got = ctx.detect(frames, 0)
+    from oracle import oracle as O
+    ref = _oracle(cfg, frames, flags=O.KEEP_DEBUG)
+    assert_same(got, ref.result, "dense tail: ")
+    g = ctx.geometry()
+    for f in range(6):
+        m = ctx.debug_tail_mask(f)
+        assert np.array_equal(m, ref.tail_mask(f, (g.bb_bottom_mouse.height, g.tail_box_width)))
+        assert m.all()
+
+
+@pytest.mark.parametrize("conn", [8, 4])
+def test_checkerboard_tail_maps(conn):
+    """1x1 tail detectors over checkerboard frames: ~120 runs per tail row
+    (more than k_tail keeps in LDS, so the run tables go to global memory);
+    8-connectivity joins the diagonal cells into one component, with
+    4-connectivity every cell is its own component and the first OpenCV label
+    wins the area tie."""
+    cfg = E.pixel_tail_config(conn)
+    frames = E.checker_frames(cfg, 4)
+    assert_same(_batched(cfg, frames, 4), _oracle(cfg, frames).result, f"checker c{conn}: ")
+
+
+def test_detector_sizes_beyond_specialised_kernels():
+    """70x70, 13x13 and 9x33 detectors (generic correlation kernel, row
+    chunks); raw score maps bit-exact too."""
+    cfg = E.odd_size_config()
+    frames = cfg.frames(0, 4)
+    ctx = _ctx(cfg, max_batch=4)
+    ctx.set_debug(1)
+    got = ctx.detect(frames, 0)
+    from oracle import oracle as O
+    ref = _oracle(cfg, frames, flags=O.KEEP_DEBUG)
+    assert_same(got, ref.result, "odd sizes: ")
+    for f in range(4):
+        for det in range(6):
+            s = ctx.debug_scores(f, det)
+            assert np.array_equal(s.view(np.uint32), ref.scores(f, det, s.shape).view(np.uint32)), (f, det)
+
+
+def test_unfused_filter_arithmetic():
+    """LM_FILTER_UNFUSED (OpenCV's SSE2/scalar filter2D: rounded product,
+    rounded sum) against the oracle's unfused restatement, bit for bit; its
+    raw scores differ from the fused ones somewhere."""
+    cfg = S.SyntheticConfig()
+    cfg.setup.filter_arith = abi.LM_FILTER_UNFUSED
+    frames = cfg.frames(0, 6)
+    ctx = _ctx(cfg, max_batch=3)
+    ctx.set_debug(1)
+    parts = [ctx.detect(frames[:3], 0)]
+    s_unf = ctx.debug_scores(1, 1).copy()
+    parts.append(ctx.detect(frames[3:], 3))
+    from oracle import oracle as O
+    ref = _oracle(cfg, frames, flags=O.KEEP_DEBUG)
+    assert_same(concat_results(parts), ref.result, "unfused: ")
+    assert np.array_equal(s_unf.view(np.uint32), ref.scores(1, 1, s_unf.shape).view(np.uint32))
+    fused = _oracle(S.SyntheticConfig(), frames[:2], flags=O.KEEP_DEBUG)
+    assert not np.array_equal(s_unf.view(np.uint32), fused.scores(1, 1, s_unf.shape).view(np.uint32))
+
+
+@pytest.mark.parametrize("moving", [False, True])
+def test_gray_value_transformation_u8(moving):
+    """transform_gray_values with a CV_8U table: LUT applied in place to the
+    bottom crop (:1445-1448); later masks, the tail, and the next frame's
+    motion test see the transformed pixels.  With moving crops the previous
+    frame's transformed rectangle differs from the current one."""
+    cfg = E.gray_lut_config()
+    frames = cfg.frames(30, 10)
+    bb = E.moving_corners(cfg, 10) if moving else None
+    ref = _oracle(cfg, frames, bb=bb).result
+    assert_same(_batched(cfg, frames, 4, bb=bb), ref, f"gray u8 moving={moving}: ")
+    plain = _oracle(S.SyntheticConfig(), frames, bb=bb).result
+    assert not np.array_equal(ref["cand"]["score"], plain["cand"]["score"]) if len(ref["cand"]) == len(plain["cand"]) \
+        else True
+
+
+def test_gray_value_transformation_side_overlap():
+    """A side box low enough that its padded crop covers rows of the bottom
+    crop: the side detectors read transformed pixels there."""
+    cfg = E.gray_lut_config(bounding_boxes={"side": (300, 20, 400, 90), "bottom": (300, 106, 400, 140)})
+    frames = cfg.frames(50, 6)
+    assert_same(_batched(cfg, frames, 3), _oracle(cfg, frames).result, "gray overlap: ")
+
+
+def test_gray_value_transformation_errors():
+    from locomouse_cpp_amd.runtime import LMError
+    cfg = E.gray_lut_config(depth=abi.LM_DEPTH_32F)
+    with pytest.raises(LMError) as e:
+        _ctx(cfg)
+    assert e.value.code == 2  # the reference stops (cv::Exception / runtime_error)
+    cfg = E.gray_lut_config()
+    ctx = _ctx(cfg, max_batch=2)
+    bb = E.moving_corners(cfg, 2)
+    bb[:, 0] = 200  # bottom crop x in [-199, 200]: leaves the corrected image
+    with pytest.raises(LMError) as e:
+        ctx.detect(cfg.frames(0, 2), 0, bb=bb)
+    assert e.value.code == 1
+
+
+def test_three_contexts_tie_heavy_against_oracle():
+    """Three contexts in three host threads on the exact-tie configuration
+    (k_nms's std::sort replica path, whose missing barrier caused round 1's
+    intermittent garbage candidates), each compared with the oracle."""
+    c, dups = _quantized_config(1500)
+    assert dups > 20
+    frames = [c.frames(100 * k, 8) for k in range(3)]
+    refs = [_oracle(c, fr).result for fr in frames]
+    outs = [None] * 3
+
+    def run(k):
+        ctx = _ctx(c, max_batch=4)
+        try:
+            outs[k] = concat_results([ctx.detect(frames[k][i:i + 4], i) for i in (0, 4)])
+        except Exception as e:  # reported below
+            outs[k] = e
+        ctx.close()
+    th = [threading.Thread(target=run, args=(k,)) for k in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for k in range(3):
+        assert not isinstance(outs[k], Exception), outs[k]
+        assert_same(outs[k], refs[k], f"ctx {k}: ")

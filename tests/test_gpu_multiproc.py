@@ -1,0 +1,60 @@
+"""The frame-sharded multi-GPU path (locomouse_cpp_amd/shard.py) with REAL HIP
+contexts: two processes over gloo (world size 2), both ranks on GPU 0 here
+(the driver's 8-GPU run gives each rank its own GPU), each running its shard
+through lm_detect_batch with a one-frame halo; rank 0 gathers the compact
+results in frame order.  Must equal the oracle's unsharded run bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from locomouse_cpp_amd import synthetic as S
+from locomouse_cpp_amd.results import KEYS
+
+pytestmark = pytest.mark.gpu
+
+N_FRAMES = 21
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_path, batch):
+    import torch.distributed as dist
+
+    from locomouse_cpp_amd.runtime import Context
+    from locomouse_cpp_amd.shard import run_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = S.SyntheticConfig()
+    frames = cfg.frames(0, N_FRAMES)
+    ctx = Context(cfg, max_batch=batch, device=0)
+    res = run_sharded(lambda fr, first, prev: ctx.detect(fr, first, prev_frame=prev), frames, N_FRAMES, batch=batch)
+    ctx.close()
+    if rank == 0:
+        np.savez(out_path, **{k: res[k] for k in KEYS}, n_frames=res["n_frames"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("batch", [4, 16])
+def test_world2_hip_shards_match_oracle(tmp_path, batch):
+    import torch.multiprocessing as mp
+
+    from oracle import oracle as O
+    from test_gpu_parity import assert_same
+    out = str(tmp_path / "r0.npz")
+    mp.spawn(_worker, args=(2, _free_port(), out, batch), nprocs=2, join=True)
+    cfg = S.SyntheticConfig()
+    ref = O.OracleRun(cfg, cfg.frames(0, N_FRAMES)).result
+    z = np.load(out)
+    assert int(z["n_frames"]) == N_FRAMES
+    got = {k: z[k] for k in KEYS}
+    got["n_frames"] = N_FRAMES
+    assert_same(got, ref, f"world2 b{batch}: ")

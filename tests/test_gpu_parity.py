@@ -19,9 +19,9 @@ def _ctx(cfg, max_batch=16):
     return Context(cfg, max_batch=max_batch)
 
 
-def _oracle(cfg, frames, flags=0):
+def _oracle(cfg, frames, flags=0, bb=None):
     from oracle import oracle as O
-    return O.OracleRun(cfg, frames, flags=flags)
+    return O.OracleRun(cfg, frames, bb=bb, flags=flags)
 
 
 def assert_same(got, ref, label=""):
@@ -153,6 +153,7 @@ def test_error_mapping(cfg):
     for option in ("use_reference_image_brightness", "transform_gray_values"):  # §8(f) row 4, as executed
         bad = S.SyntheticConfig()
         setattr(bad.params, option, 1)
+        bad.params.gray_value_transformation_depth = 5  # a CV_32F table (the CV_8U one works: test_gpu_edges.py)
         with pytest.raises(LMError) as e:
             _ctx(bad)
         assert e.value.code == 2

@@ -56,8 +56,12 @@ def test_computed_bounding_box_then_main_loop_matches_oracle(batch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch,order", [(8, 0), (5, 1), (64, 0)])
+@pytest.mark.parametrize("batch,order", [(8, 0), (5, 1), (64, 0), (8, 8), (5, 1 | 8), (7, 1 | 8)])
 def test_main_loop_matches_oracle(batch, order):
+    """order bit 0: a result accessor called mid-batch (the batch is handed
+    over early); bit 3: frames come from the batch reader read_frames, which
+    reads a whole batch ahead — the read-ahead frames must survive an early
+    hand-over."""
     from oracle import oracle as O
     from test_gpu_parity import assert_same
     cfg = S.SyntheticConfig()
