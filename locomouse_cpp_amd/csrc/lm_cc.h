@@ -105,39 +105,54 @@ DEV int cc_row_of(const int* rowoff, int H, int i) {
 // Bitmap of a u8 map (nonzero = foreground; H rows of W bytes at `pitch`)
 // into bm[y][0..nb64] (the last word of a row stays zero), optionally ANDed
 // with a column mask (colm[nb64] words, bit x = column x), and the number of
-// runs of each row into rowoff[y].  One wave per row, 16 columns per lane from
-// one 16-byte load when `vec` (W % 16 == 0 and 16-byte aligned rows).
-// Block-wide call (ends with a barrier).
+// runs of each row into rowoff[y].  Every thread takes 16-column pieces of
+// any row, four pieces' loads in flight before any is used (16-byte loads when
+// `vec`: W % 16 == 0 and 16-byte aligned rows), so the map streams in at a
+// few load latencies instead of one per row; then one thread per row counts
+// the run starts.  Block-wide call (ends with a barrier).
 DEV void cc_bitmap_u8(const uint8_t* __restrict__ src, int64_t pitch, int W, int H, int nb64, bool vec,
                       const unsigned long long* colm, unsigned long long* bm, int* rowoff) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int y = wave; y < H; y += nw) {
-    const uint8_t* row = src + (int64_t)y * pitch;
-    uint16_t* brow = reinterpret_cast<uint16_t*>(bm + (int64_t)y * (nb64 + 1));
-    int n = 0;
-    unsigned carry = 0;
-    for (int x0 = 0; x0 < 64 * (nb64 + 1); x0 += 1024) {
-      const int x = x0 + 16 * lane;
+  const int npc = 4 * (nb64 + 1);  // 16-bit pieces per bitmap row (incl. the spare word)
+  const int total = H * npc;
+  for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
+    uint4 q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+      const int y = e / npc, x = 16 * (e - y * npc);
+      if (vec && e < total && x < W) q[u] = *reinterpret_cast<const uint4*>(src + (int64_t)y * pitch + x);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+      if (e >= total) continue;
+      const int y = e / npc, pc = e - y * npc, x = 16 * pc;
       unsigned m = 0;
       if (x < W) {
         if (vec) {
-          const uint4 q = *reinterpret_cast<const uint4*>(row + x);
-          const unsigned w4[4] = {q.x, q.y, q.z, q.w};
+          const unsigned w4[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
 #pragma unroll
           for (int k = 0; k < 16; ++k) m |= (((w4[k >> 2] >> (8 * (k & 3))) & 255u) ? 1u : 0u) << k;
         } else {
+          const uint8_t* row = src + (int64_t)y * pitch;
           for (int k = 0; k < 16 && x + k < W; ++k) m |= (row[x + k] ? 1u : 0u) << k;
         }
         if (colm) m &= (unsigned)(colm[x >> 6] >> (x & 63)) & 0xFFFFu;
       }
-      if (x < 64 * (nb64 + 1)) brow[x >> 4] = (uint16_t)m;
-      const unsigned prev = (unsigned)__shfl_up((int)(m >> 15), 1);
-      const unsigned cin = lane ? prev : carry;
-      n += __popc(m & ~((m << 1) | cin) & 0xFFFFu);
-      carry = (unsigned)__shfl((int)(m >> 15), 63);
+      reinterpret_cast<uint16_t*>(bm + (int64_t)y * (nb64 + 1))[pc] = (uint16_t)m;
     }
-    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-    if (lane == 0) rowoff[y] = n;
+  }
+  __syncthreads();
+  for (int y = threadIdx.x; y < H; y += blockDim.x) {
+    const unsigned long long* row = bm + (int64_t)y * (nb64 + 1);
+    unsigned long long carry = 0;
+    int n = 0;
+    for (int k = 0; k < nb64; ++k) {
+      const unsigned long long bits = row[k];
+      n += __popcll(bits & ~((bits << 1) | carry));
+      carry = bits >> 63;
+    }
+    rowoff[y] = n;
   }
   __syncthreads();
 }

@@ -162,9 +162,14 @@ DEV void tile_fill_f32(float* __restrict__ lds, int stride, const uint8_t* __res
         const int c0 = ch * 16 - mis;
         float* __restrict__ o = lds + r * stride + c0;
         const unsigned w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        if (c0 >= 0 && c0 + 16 <= cols) {  // whole chunk inside the window: straight-line stores
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-          if (c0 + k >= 0 && c0 + k < cols) o[k] = (float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+          for (int k = 0; k < 16; ++k) o[k] = (float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if (c0 + k >= 0 && c0 + k < cols) o[k] = (float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+        }
       }
     }
   }
@@ -185,7 +190,7 @@ DEV CorrTile corr_tile(const LmConst& K, const LmDetGroup& G) {
   const int d = G.ids[gi];
   const int lt = blockIdx.x - tb;
   const int tx = K.det[d].tiles_x;
-  return CorrTile{d, (lt / tx) * LM_TH, (lt % tx) * LM_TW};
+  return CorrTile{d, (lt / tx) * K.det[d].tile_h, (lt % tx) * LM_TW};
 }
 
 DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext, int64_t ext_slot_bytes, int slot,

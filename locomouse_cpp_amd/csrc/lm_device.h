@@ -39,6 +39,7 @@ struct LmDet {
   int32_t in_y, in_x;  // ext-crop coords of tap (0,0) of output (0,0)
   int32_t m_y, m_x;    // ext-crop coords of the I_*_MOUSE pixel of output (0,0)
   int32_t tiles_x, tiles_y, tile_base;
+  int32_t tile_h;        // output rows per correlation tile (LM_TH)
   int32_t box_w, box_h;  // NMS box (detector cols, rows)
   int32_t chunk_rows;    // k_corr_gen: detector rows per LDS window
 };

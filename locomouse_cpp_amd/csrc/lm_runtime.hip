@@ -441,8 +441,9 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     D.delta = (float)(-src.bias);  // saturate_cast<float>(delta)
     D.oh = out_rel[d].h;
     D.ow = out_rel[d].w;
+    D.tile_h = LM_TH;
     D.tiles_x = (D.ow + LM_TW - 1) / LM_TW;
-    D.tiles_y = (D.oh + LM_TH - 1) / LM_TH;
+    D.tiles_y = (D.oh + D.tile_h - 1) / D.tile_h;
     D.tile_base = tile;
     tile += D.tiles_x * D.tiles_y;
     D.box_w = src.cols;
@@ -452,7 +453,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     const int v = D.view;
     ey0[v] = std::min(ey0[v], y0);
     ex0[v] = std::min(ex0[v], x0);
-    ey1[v] = std::max(ey1[v], y0 + D.tiles_y * LM_TH + D.kh - 1);
+    ey1[v] = std::max(ey1[v], y0 + D.tiles_y * D.tile_h + D.kh - 1);
     ex1[v] = std::max(ex1[v], x0 + D.tiles_x * LM_TW + D.kwp - 1 + 4);
     D.in_y = y0;  // rebased below
     D.in_x = x0;
