@@ -133,13 +133,21 @@ class VideoFrames {
 
 // LocoMouse_Parameters (LocoMouse_class.cpp:4-249): keys in the reference's
 // order, its messages, OpenCV's missing-key-reads-0 semantics.
-void load_config(const std::string& file, const std::string& ref_path, lm_params& P, lm_bb_params& B) {
+struct DebugConfig {
+  bool verbose = false;  // LM_DEBUG (verbose_debug, :17-19)
+  int n_frames = 0;      // LM_N_FRAMES_TO_DEBUG (N_debug_frames, :21-26)
+};
+
+void load_config(const std::string& file, const std::string& ref_path, lm_params& P, lm_bb_params& B,
+                 DebugConfig& D) {
   FsNode c;
   if (!read_file_storage(file, c)) throw std::invalid_argument("Failed to read config file: " + file + ".");
   const std::string E = "Invalid configuration parameter: ";
   auto bad = [&](const std::string& m) { throw std::invalid_argument(E + m); };
   auto num = [](double v) { return std::to_string(v); };
-  if (c["N_debug_frames"].to_int() < 0) bad("N_debug_frames must not be negative.");
+  D.verbose = c["verbose_debug"].to_int() != 0;
+  D.n_frames = c["N_debug_frames"].to_int();
+  if (D.n_frames < 0) bad("N_debug_frames must not be negative.");
   P.conn_comp_connectivity = c["conn_comp_connectivity"].to_int();
   if (P.conn_comp_connectivity != 4 && P.conn_comp_connectivity != 8)
     bad("conn_comp_connectivity must be either 4 or 8. Was " + std::to_string(P.conn_comp_connectivity) + ".");
@@ -267,10 +275,16 @@ int run(int argc, char** argv) {
   ParsedInputs in = parse_inputs(argc, argv);
   LocoMouse_Inputs li;
   const int method = std::stoi(in.METHOD);  // LocoMouse::initializePaths
-  load_config(in.CONFIG_FILE, in.REF_PATH, li.params, li.bb_params);
+  DebugConfig dbg;
+  load_config(in.CONFIG_FILE, in.REF_PATH, li.params, li.bb_params, dbg);
   auto video = std::make_shared<AviReader>();
   if (!video->open(in.VIDEO_FILE)) throw std::invalid_argument("Could not open the video file: " + in.VIDEO_FILE + ".");
   li.n_frames = video->frame_count();
+  if (dbg.verbose && dbg.n_frames > 0)  // loadVideo (:380-389): debugging runs the first N_debug_frames only
+    li.n_frames = std::min<uint32_t>(li.n_frames, (uint32_t)dbg.n_frames);
+  li.verbose_debug = dbg.verbose;
+  li.debug_file = in.OUTPUT_PATH + "/debug_" + in.FILE_STEM + ".yml";  // initializePaths (:361-362)
+  li.debug_text = in.OUTPUT_PATH + "/debug_" + in.FILE_STEM + ".txt";
   if (li.n_frames < 1) throw std::invalid_argument("Error: Video has no images to read from.");
   int br = 0, bc = 0;
   std::vector<uint8_t> bkg;
@@ -297,7 +311,11 @@ int run(int argc, char** argv) {
   li.setup.view_box_side = in.BB_SIDE_VIEW;
   li.setup.view_box_bottom = in.BB_BOTTOM_VIEW;
   li.model = model.m;
-  auto reader = std::make_shared<VideoFrames>(video, std::max(1, std::min(8, (int)std::thread::hardware_concurrency())));
+  // Decode threads: MJPEG frames decode at a few hundred per second per core,
+  // so a batch is spread over up to 16 (LM_READ_THREADS overrides).
+  int read_threads = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+  if (const char* t = std::getenv("LM_READ_THREADS")) read_threads = std::max(1, std::atoi(t));
+  auto reader = std::make_shared<VideoFrames>(video, read_threads);
   li.read_frame = [reader](uint8_t* dst) { return reader->read(dst); };
   li.read_frames = [reader](uint8_t* dst, int n) { return reader->read(dst, n); };
   li.rewind = [reader] { reader->rewind(); };

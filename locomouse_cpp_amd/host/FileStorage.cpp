@@ -4,6 +4,8 @@
 #include <cerrno>
 #include <climits>
 #include <cmath>
+#include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <fstream>
 #include <sstream>
@@ -218,7 +220,11 @@ class BlockParser {
     }
     FsNode n;
     if (rest.empty()) {
-      if (k < L.size() && L[k].indent > indent) n = block(L[k].indent);
+      if (k < L.size() && L[k].indent > indent && (L[k].text[0] == '[' || L[k].text[0] == '{')) {
+        const std::string t = gather(L[k++].text);  // "-" then an indented flow value ("[]" of an empty entry)
+        Flow fl{t};
+        n = fl.value();
+      } else if (k < L.size() && L[k].indent > indent) n = block(L[k].indent);
       else if (k < L.size() && L[k].indent == indent && L[k].text.rfind("- ", 0) == 0) n = block(indent);
     } else if (rest[0] == '[' || rest[0] == '{') {
       std::string t = gather(rest);
@@ -312,6 +318,172 @@ bool read_file_storage(const std::string& path, FsNode& root) {
   ss << f.rdbuf();
   root = parse_file_storage(ss.str());
   return true;
+}
+
+// ------------------------------------------------------------------ writer
+// OpenCV's YAML emitter (persistence_yml.cpp: writeScalar, startWriteStruct,
+// endWriteStruct; FileStorage::Impl::flush and operator<< (const String&)).
+
+struct FsWriter::Impl {
+  std::ofstream out;
+};
+
+static constexpr int kYmlIndent = 3, kWrapMargin = 71;
+
+std::string fs_real(double v) {
+  char buf[64];
+  if (std::isnan(v)) return ".Nan";
+  if (std::isinf(v)) return v < 0 ? "-.Inf" : ".Inf";
+  const double r = std::nearbyint(v);  // cvRound
+  if (r == v && std::fabs(r) <= (double)INT_MAX) {
+    std::snprintf(buf, sizeof buf, "%d.", (int)r);
+  } else {
+    std::snprintf(buf, sizeof buf, "%.16e", v);
+  }
+  return buf;
+}
+
+FsWriter::FsWriter(const std::string& path) : f_(new Impl) {
+  f_->out.open(path, std::ios::binary);
+  if (f_->out) f_->out << "%YAML:1.0\n---\n";
+  stack_.push_back({0, true, false, true});
+}
+
+FsWriter::~FsWriter() {
+  release();
+  delete f_;
+}
+
+bool FsWriter::isOpened() const { return (bool)f_->out && f_->out.is_open(); }
+
+void FsWriter::release() {
+  if (!f_->out.is_open()) return;
+  while (stack_.size() > 1) end();
+  flush();
+  f_->out.close();
+}
+
+void FsWriter::flush() {
+  if ((int)line_.size() > space_) f_->out << line_ << '\n';
+  const int ind = stack_.back().indent;
+  line_.assign((size_t)ind, ' ');
+  space_ = ind;
+}
+
+void FsWriter::scalar(const char* key, const std::string* data) {
+  Level& cur = stack_.back();
+  if (key && !*key) key = nullptr;
+  if (cur.map != (key != nullptr))
+    throw std::runtime_error("FsWriter: an element without a name in a map, or with a name in a sequence.");
+  const int keylen = key ? (int)std::strlen(key) : 0, datalen = data ? (int)data->size() : 0;
+  if (cur.flow) {
+    if (!cur.empty) line_ += ',';
+    const int new_offset = (int)line_.size() + keylen + datalen;
+    if (new_offset > kWrapMargin && new_offset - cur.indent > 10) flush();
+    else line_ += ' ';
+  } else {
+    flush();
+    if (!cur.map) {
+      line_ += '-';
+      if (data) line_ += ' ';
+    }
+  }
+  if (key) {
+    line_ += key;
+    line_ += ':';
+    if (!cur.flow && data) line_ += ' ';
+  }
+  if (data) line_ += *data;
+  cur.empty = false;
+}
+
+void FsWriter::start(const char* key, bool map, bool flow, const char* type) {
+  std::string data;
+  bool has = false;
+  if (type && !*type) type = nullptr;
+  if (flow) {
+    data = type ? std::string("!!") + type + " " + (map ? '{' : '[') : std::string(1, map ? '{' : '[');
+    has = true;
+  } else if (type) {
+    data = std::string("!!") + type;
+    has = true;
+  }
+  const Level parent = stack_.back();
+  scalar(key, has ? &data : nullptr);
+  stack_.push_back({parent.indent + (parent.flow ? 0 : kYmlIndent + (flow ? 1 : 0)), map, flow, true});
+  if (!flow) flush();
+}
+
+void FsWriter::end() {
+  if (stack_.size() < 2) throw std::runtime_error("FsWriter: extra closing bracket.");
+  const Level cur = stack_.back();
+  if (cur.flow) {
+    if ((int)line_.size() > cur.indent && !cur.empty) line_ += ' ';
+    line_ += cur.map ? '}' : ']';
+  } else if (cur.empty) {
+    flush();
+    line_ += cur.map ? "{}" : "[]";
+  }
+  stack_.pop_back();
+  stack_.back().empty = false;
+}
+
+void FsWriter::value(const std::string& text) {
+  const bool in_map = stack_.back().map;
+  if (in_map && name_expected_) throw std::runtime_error("FsWriter: no element name has been given.");
+  scalar(in_map ? elname_.c_str() : nullptr, &text);
+  elname_.clear();
+  name_expected_ = stack_.back().map;
+}
+
+FsWriter& FsWriter::operator<<(const char* s) {
+  if (!isOpened() || !s) return *this;
+  const char c = *s;
+  const bool in_map = stack_.back().map;
+  if (c == '}' || c == ']') {
+    if ((c == '}') != in_map) throw std::runtime_error("FsWriter: closing bracket does not match.");
+    end();
+    name_expected_ = stack_.back().map;
+    elname_.clear();
+  } else if (in_map && name_expected_) {
+    elname_ = s;
+    name_expected_ = false;
+  } else if (c == '{' || c == '[') {
+    bool flow = false;
+    const char* t = s + 1;
+    if (*t == ':') {
+      ++t;
+      if (!*t) flow = true;
+    }
+    start(in_map ? elname_.c_str() : nullptr, c == '{', flow, t);
+    elname_.clear();
+    name_expected_ = c == '{';
+  } else {
+    value(s);
+  }
+  return *this;
+}
+
+FsWriter& FsWriter::operator<<(int v) {
+  if (isOpened()) value(std::to_string(v));
+  return *this;
+}
+
+FsWriter& FsWriter::operator<<(double v) {
+  if (isOpened()) value(fs_real(v));
+  return *this;
+}
+
+void FsWriter::write_mat_i(const int* data, int rows, int cols) {
+  if (!isOpened()) return;
+  start(stack_.back().map ? elname_.c_str() : nullptr, true, false, "opencv-matrix");
+  elname_.clear();
+  name_expected_ = true;
+  *this << "rows" << rows << "cols" << cols << "dt" << "i" << "data" << "[:";
+  for (long long k = 0; k < (long long)rows * cols; ++k) *this << data[k];
+  *this << "]";
+  end();
+  name_expected_ = stack_.back().map;
 }
 
 }  // namespace locomouse

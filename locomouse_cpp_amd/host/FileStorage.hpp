@@ -50,6 +50,50 @@ class FsNode {
 bool read_file_storage(const std::string& path, FsNode& root);
 FsNode parse_file_storage(const std::string& text);
 
+// cv::FileStorage(path, WRITE) for YAML, with the reference's stream protocol:
+//   fs << "name" << value;   fs << "name" << "{" ... "}";   fs << "name" << "[" ... "]";
+//   "[:" / "{:" open flow collections; inside a sequence values take no name.
+// The text follows OpenCV's YAML emitter: "%YAML:1.0" / "---" header, block
+// collections indented by 3, flow collections opened on the key's line and
+// wrapped past column 71, ints as %d, reals as "%d." when integral else
+// "%.16e", !!opencv-matrix maps for matrices (rows, cols, dt, data).
+class FsWriter {
+ public:
+  explicit FsWriter(const std::string& path);
+  ~FsWriter();
+  FsWriter(const FsWriter&) = delete;
+  FsWriter& operator=(const FsWriter&) = delete;
+  bool isOpened() const;
+  void release();  // closes open collections and the file
+
+  FsWriter& operator<<(const char* s);  // a name, a bracket, or a string value
+  FsWriter& operator<<(const std::string& s) { return *this << s.c_str(); }
+  FsWriter& operator<<(int v);
+  FsWriter& operator<<(double v);
+  // An int32 matrix (rows x cols, row-major) as !!opencv-matrix with dt: i.
+  void write_mat_i(const int* data, int rows, int cols);
+
+ private:
+  struct Level {
+    int indent;
+    bool map, flow, empty;
+  };
+  void scalar(const char* key, const std::string* data);
+  void start(const char* key, bool map, bool flow, const char* type);
+  void end();
+  void flush();
+  void value(const std::string& text);
+  struct Impl;
+  Impl* f_;
+  std::vector<Level> stack_;
+  std::string line_;
+  int space_ = 0;
+  bool name_expected_ = true;
+  std::string elname_;
+};
+
+std::string fs_real(double v);  // OpenCV's YAML text of a double
+
 }  // namespace locomouse
 
 #endif

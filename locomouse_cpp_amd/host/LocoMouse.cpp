@@ -142,6 +142,7 @@ LocoMouse::LocoMouse(const LocoMouse_Inputs& inputs) : IN(inputs), METHOD(0), N_
     throw std::invalid_argument("LocoMouse: video size must be positive.");
   FRAME_BYTES = (size_t)IN.setup.video_rows * IN.setup.video_cols;
   IN.setup.method = 0;
+  if (IN.verbose_debug && !IN.debug_text.empty()) DEBUG_TEXT.open(IN.debug_text);  // :341-343
 }
 
 LocoMouse::~LocoMouse() {
@@ -162,7 +163,14 @@ void LocoMouse::getBoundingBox() {
     BB_SIDE_MOUSE = lm_rect{0, 0, s.width, s.height};
     HAVE_BB = true;
   } else {
+    if (DEBUG_TEXT.is_open()) DEBUG_TEXT << "===== Computing the bounding box coordinates: " << std::endl;  // :582
     computeBoundingBox();
+    if (DEBUG_TEXT.is_open())  // :638-650
+      DEBUG_TEXT << "----- Final BB sizes: " << std::endl
+                 << "BB_SIDE_MOUSE: " << debug_rect(BB_SIDE_MOUSE) << std::endl
+                 << "BB_BOTTOM_MOUSE: " << debug_rect(BB_BOTTOM_MOUSE) << std::endl
+                 << "===== END " << std::endl
+                 << std::endl;
   }
 }
 
@@ -218,10 +226,28 @@ void LocoMouse::initializeFeatureLoop() {
   if (!HAVE_BB) throw std::runtime_error("initializeFeatureLoop: getBoundingBox() has not been called.");
   if (CTX) return;
   IN.setup.method = METHOD;
+  if (DEBUG_TEXT.is_open())  // :662-667
+    DEBUG_TEXT << "===== Preparing Feature Tracking Loop: " << std::endl
+               << "BB_SIDE_MOUSE: " << debug_rect(BB_SIDE_MOUSE) << std::endl
+               << "BB_BOTTOM_MOUSE: " << debug_rect(BB_BOTTOM_MOUSE) << std::endl;
   throw_on_error(lm_ctx_create(IN.device, &IN.setup, &IN.params, &IN.model, IN.batch, &CTX));
   PENDING.allocate(FRAME_BYTES * (size_t)IN.batch);
   SUBMITTED.allocate(FRAME_BYTES * (size_t)IN.batch);
   N_PENDING = 0;
+  if (DEBUG_TEXT.is_open()) {  // :700-704, :766
+    const lm_geometry g = geometry();
+    DEBUG_TEXT << "M_size_pre_side().height, M_size_pre_bottom().height: " << g.spre_t_h << " " << g.spre_b_h
+               << std::endl
+               << "M_size_pre_side().width, M_size_pre_bottom().width: " << g.spre_t_w << " " << g.spre_b_w
+               << std::endl
+               << "I_PAD: [" << g.ipad_cols << " x " << g.ipad_rows << "]" << std::endl
+               << "I_UNPAD: " << debug_rect(lm_rect{g.pad_pre_cols, g.pad_pre_rows, g.n_cols, g.n_rows}) << std::endl
+               << "BB_BOTTOM_MOUSE_PAD, UNPAD: " << debug_rect(g.bb_bottom_mouse_pad) << " "
+               << debug_rect(g.bb_unpad_mouse_bottom) << std::endl
+               << "BB_SIDE_MOUSE_PAD, UNPAD: " << debug_rect(g.bb_side_mouse_pad) << " "
+               << debug_rect(g.bb_unpad_mouse_side) << std::endl
+               << "===== Done " << std::endl;
+  }
 }
 
 // :1273-1333 reads the next frame (V >> F, channel 0).  The frame is queued;
@@ -311,6 +337,7 @@ void LocoMouse::flush() {
     lm_batch_result r{};
     throw_on_error(lm_detect_batch(CTX, SUBMITTED.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data(), &r));
     append(r);
+    if (DEBUG_TEXT.is_open()) debug_frames(first, n);
   });
 }
 
@@ -326,11 +353,33 @@ TrackSetup LocoMouse::track_setup() {
   return S;
 }
 
-void LocoMouse::computeBottomTracks() { locomouse::computeBottomTracks(*this, track_setup(), TRACKS); }
-void LocoMouse::computeSideTracks() { locomouse::computeSideTracks(*this, track_setup(), TRACKS); }
-void LocoMouse::exportResults() {
-  exportTracks(*this, track_setup(), TRACKS);
+void LocoMouse::computeBottomTracks() {
+  const TrackSetup S = track_setup();
+  if (DEBUG_TEXT.is_open()) DEBUG_TEXT << "=== Compute Bottom Tracks: " << std::endl;  // :2161-2197
+  locomouse::computeBottomTracks(*this, S, TRACKS);
+  if (DEBUG_TEXT.is_open()) DEBUG_TEXT << "=== Done " << std::endl;
+}
+
+void LocoMouse::computeSideTracks() {
+  const TrackSetup S = track_setup();
+  if (DEBUG_TEXT.is_open()) DEBUG_TEXT << "=== computeSideTracks(): " << std::endl;  // :2205-2214
+  locomouse::computeSideTracks(*this, S, TRACKS);
+  if (DEBUG_TEXT.is_open()) DEBUG_TEXT << "=== Done " << std::endl;
+}
+
+void LocoMouse::exportResults() {  // :2348-2383
+  const TrackSetup S = track_setup();
+  if (DEBUG_TEXT.is_open()) DEBUG_TEXT << "=== exportResults: " << std::endl;
+  exportTracks(*this, S, TRACKS);
   if (!IN.output_file.empty()) writeOutputYaml(IN.output_file, TRACKS);
+  if (DEBUG_TEXT.is_open())
+    DEBUG_TEXT << "Paw tracks exported" << std::endl
+               << "Snout tracks exported" << std::endl
+               << "Tail Tracks exported" << std::endl;
+  if (IN.verbose_debug) {
+    exportDebugVariables();
+    if (DEBUG_TEXT.is_open()) DEBUG_TEXT << "=== Done " << std::endl;
+  }
 }
 
 #define LM_ACCESSOR(fn, member) \

@@ -28,6 +28,7 @@
 
 #include <array>
 #include <cstdint>
+#include <fstream>
 #include <functional>
 #include <future>
 #include <memory>
@@ -73,6 +74,12 @@ struct LocoMouse_Inputs {
   // exportResults writes <output_file> (the reference's
   // <outdir>/output_<stem>.yml, :360) when non-empty.
   std::string output_file;
+  // config.yml's verbose_debug (LM_DEBUG, :17-19): a text log of the stages
+  // (DEBUG_TEXT, opened at :341-343) into debug_text, and exportResults'
+  // exportDebugVariables (:2769-2920) into debug_file — the reference's
+  // <outdir>/debug_<stem>.txt / .yml (:361-362).  Empty paths: not written.
+  bool verbose_debug = false;
+  std::string debug_file, debug_text;
 };
 
 class LocoMouse : protected FrameResults {
@@ -98,6 +105,7 @@ class LocoMouse : protected FrameResults {
   void computeBottomTracks();         // :2153-2200 (match2nd, 4 paw orders + snout)
   void computeSideTracks();           // :2202-2214 (bestSideViewMatch)
   void exportResults();               // :2348-2482 (track export; YAML when output_file is set)
+  void exportDebugVariables();        // :2769-2920 (debug_<stem>.yml; called by exportResults when verbose_debug)
   unsigned int N_frames() const { return N_FRAMES; }
 
   // The reference's protected result vectors (LocoMouse_class.hpp:219-236),
@@ -158,6 +166,8 @@ class LocoMouse : protected FrameResults {
     uint8_t* data() { return p; }
     void swap(HostBuffer& o) { std::swap(p, o.p); }
   };
+  std::ofstream DEBUG_TEXT;  // verbose_debug log (LocoMouse_class.hpp:180)
+  void debug_frames(int first, int n);  // the per-frame stage lines of frames [first, first + n)
   HostBuffer PENDING;    // raw frames read but not yet processed
   HostBuffer SUBMITTED;  // the batch being processed by INFLIGHT
   std::future<void> INFLIGHT;      // lm_detect_batch + append of the previous batch
@@ -191,6 +201,9 @@ std::unique_ptr<LocoMouse> LocoMouse_Initialize(const LocoMouse_Inputs& inputs);
 
 // lm_status -> the reference's exception types (main.cpp:94-101).
 void throw_on_error(lm_status s);
+
+// cv::Rect's operator<<: "[w x h from (x, y)]" (debug log lines).
+std::string debug_rect(const lm_rect& r);
 
 }  // namespace locomouse
 

@@ -1,6 +1,8 @@
 // Media.cpp — see Media.hpp.
 #include "Media.hpp"
 
+#include "Jpeg.hpp"
+
 #include <zlib.h>
 
 #include <algorithm>
@@ -166,14 +168,17 @@ bool AviReader::open(const std::string& path) {
     }
   }
   const bool grey = compression == 0x30303859u /* 'Y800' */ || compression == 0x59455247u /* 'GREY' */;
+  mjpeg_ = compression == 0x47504A4Du /* 'MJPG' */ || compression == 0x67706A6Du /* 'mjpg' */ ||
+           compression == 0x4745504Au /* 'JPEG' */ || compression == 0x6765706Au /* 'jpeg' */ ||
+           compression == 0x31495641u /* 'AVI1' */;
   const bool ok = have_format && width_ > 0 && height_ > 0 &&
-                  ((compression == 0 && (bits_ == 24 || bits_ == 8)) || (grey && bits_ == 8));
+                  ((compression == 0 && (bits_ == 24 || bits_ == 8)) || (grey && bits_ == 8) || mjpeg_);
   if (!ok) {
     std::fclose(f_);
     f_ = nullptr;
     return false;
   }
-  if (grey) palette_blue_.clear(), bottom_up_ = false;
+  if (grey || mjpeg_) palette_blue_.clear(), bottom_up_ = false;
   return true;
 }
 
@@ -185,6 +190,16 @@ bool AviReader::read(uint8_t* channel0) {
 bool AviReader::read_at(size_t index, uint8_t* channel0) const {
   if (!f_ || index >= frames_.size()) return false;
   const auto fr = frames_[index];
+  if (mjpeg_) {  // one JPEG image per chunk, decoded to channel 0 of its BGR rendering (Jpeg.hpp)
+    thread_local std::vector<uint8_t> jpg;
+    jpg.resize(fr.second);
+    for (size_t got = 0; got < fr.second;) {
+      const ssize_t r = pread(fileno(f_), jpg.data() + got, fr.second - got, (off_t)(fr.first + (long)got));
+      if (r <= 0) return false;
+      got += (size_t)r;
+    }
+    return decode_jpeg_channel0_into(jpg.data(), jpg.size(), height_, width_, channel0);
+  }
   const size_t bpp = (size_t)bits_ / 8, stride = ((size_t)width_ * bpp + 3) & ~(size_t)3;
   const size_t tight = (size_t)width_ * bpp;
   const bool padded = fr.second >= stride * (size_t)height_;

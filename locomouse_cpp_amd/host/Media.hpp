@@ -4,10 +4,11 @@
 //   read_png_gray  cv::imread(BKG_FILE, CV_LOAD_IMAGE_GRAYSCALE)  (LocoMouse_class.cpp:405-419)
 //   AviReader      cv::VideoCapture(VIDEO_FILE); V >> F; extractChannel(F, F, 0)
 //                  (:376-403, :1273-1293) for uncompressed AVI (BI_RGB 24-bit
-//                  BGR or 8-bit palettised, and 8-bit 'Y800'/'GREY'); channel 0
-//                  of the decoded BGR frame is blue.  Compressed codecs
-//                  (MJPEG, H.264 …) are not decoded: opening such a file fails
-//                  like a VideoCapture that cannot open it.
+//                  BGR or 8-bit palettised, and 8-bit 'Y800'/'GREY') and MJPEG
+//                  AVI ('MJPG'/'JPEG'/'AVI1': sequential Huffman JPEG per
+//                  frame, Jpeg.hpp); channel 0 of the decoded BGR frame is
+//                  blue.  Other codecs (H.264 …) are not decoded: opening
+//                  such a file fails like a VideoCapture that cannot open it.
 #ifndef LOCOMOUSE_HOST_MEDIA_HPP
 #define LOCOMOUSE_HOST_MEDIA_HPP
 
@@ -46,6 +47,7 @@ class AviReader {
   std::FILE* f_ = nullptr;
   int width_ = 0, height_ = 0, bits_ = 0;
   bool bottom_up_ = true;
+  bool mjpeg_ = false;
   std::vector<uint8_t> palette_blue_;  // 8-bit palettised: blue of each entry
   std::vector<std::pair<long, uint32_t>> frames_;  // (file offset, size) of each frame chunk
   size_t next_ = 0;

@@ -2,6 +2,8 @@
 // results it reproduces.
 #include "Tracks.hpp"
 
+#include "FileStorage.hpp"
+
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -237,24 +239,17 @@ void exportTracks(const FrameResults& R, const TrackSetup& S, TrackResults& out)
   out.tracks_tail = exportLineTracks(R.TRACKS_TAIL, S, LM_N_TAIL_POINTS);
 }
 
-static void write_matrix(std::ofstream& o, const std::string& name, const IntMat& M) {
-  o << name << ": !!opencv-matrix\n   rows: " << M.rows << "\n   cols: " << M.cols << "\n   dt: i\n   data: [";
-  for (size_t i = 0; i < M.data.size(); ++i) {
-    if (i) o << ",";
-    o << ((i % 16 == 0 && i) ? "\n       " : " ") << M.data[i];
-  }
-  o << " ]\n";
-}
-
-void writeOutputYaml(const std::string& path, const TrackResults& T) {
-  std::ofstream o(path);
-  if (!o) throw std::runtime_error("exportResults: cannot open " + path + " for writing.");
-  o << "%YAML:1.0\n---\n";
-  for (size_t i = 0; i < T.paw_tracks.size(); ++i) write_matrix(o, "paw_tracks" + std::to_string(i), T.paw_tracks[i]);
-  for (size_t i = 0; i < T.snout_tracks.size(); ++i)
-    write_matrix(o, "snout_tracks" + std::to_string(i), T.snout_tracks[i]);
-  write_matrix(o, "tracks_tail", T.tracks_tail);
-  if (!o) throw std::runtime_error("exportResults: writing " + path + " failed.");
+void writeOutputYaml(const std::string& path, const TrackResults& T) {  // OUTPUT << name << M (:2384-2482)
+  FsWriter fs(path);
+  if (!fs.isOpened()) throw std::runtime_error("exportResults: cannot open " + path + " for writing.");
+  auto put = [&](const std::string& name, const IntMat& M) {
+    fs << name;
+    fs.write_mat_i(M.data.data(), M.rows, M.cols);
+  };
+  for (size_t i = 0; i < T.paw_tracks.size(); ++i) put("paw_tracks" + std::to_string(i), T.paw_tracks[i]);
+  for (size_t i = 0; i < T.snout_tracks.size(); ++i) put("snout_tracks" + std::to_string(i), T.snout_tracks[i]);
+  put("tracks_tail", T.tracks_tail);
+  fs.release();
 }
 
 }  // namespace locomouse

@@ -50,7 +50,7 @@ def build_host(verbose=False):
     """liblocomouse_host.so: the LocoMouse / Candidate / P22D / MyMat C++
     surface (locomouse_cpp_amd/host) linked against the C-ABI library."""
     srcs = [os.path.join(HOST_DIR, f)
-            for f in ("LocoMouse.cpp", "Tracks.cpp", "match2nd.cpp", "FileStorage.cpp", "Media.cpp")]
+            for f in ("LocoMouse.cpp", "Tracks.cpp", "match2nd.cpp", "FileStorage.cpp", "Media.cpp", "Jpeg.cpp", "Debug.cpp")]
     flags = ["g++", "-O3", "-std=c++17", "-ffp-contract=off", "-pthread", "-Wall", "-Wextra", "-I" + os.path.join(ROOT, "include"),
              "-I" + HOST_DIR]
     cmd = [*flags, "-fPIC", "-shared", "-o", HOST_LIB_PATH, *srcs, "-L" + PKG, "-llocomouse_hip", "-lz",

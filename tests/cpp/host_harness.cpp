@@ -286,3 +286,30 @@ extern "C" int lmh_fs_node(const char* path, const char* key, int* kind, int* ro
     return 3;
   }
 }
+
+// FsWriter (cv::FileStorage WRITE, YAML) on a document with every construct
+// exportResults / exportDebugVariables use.
+extern "C" int lmh_fs_write_demo(const char* path) {
+  locomouse::FsWriter fs(path);
+  if (!fs.isOpened()) return 1;
+  fs << "N_opencv_matrices" << 7;
+  const int m[6] = {1, -2, 3, 4, 5, 6};
+  fs << "M";
+  fs.write_mat_i(m, 2, 3);
+  fs << "real" << 0.5 << "whole" << 15.0 << "neg" << -0.375;
+  fs << "BB" << "{" << "x" << 1 << "y" << 2 << "}";
+  fs << "seq" << "[:";
+  for (int k = 0; k < 40; ++k) fs << 1000 * k;
+  fs << "]";
+  fs << "nested" << "[";
+  fs << "[";
+  fs << "{" << "Candidate_bottom" << "{" << "Point_x" << 3 << "Score" << 0.25 << "}";
+  fs << "side" << "[:" << 4 << "]" << "}";
+  fs << "]";
+  fs << "[" << "]";
+  fs << "]";
+  fs << "empty_flow" << "[:" << "]";
+  fs << "last" << "text";
+  fs.release();
+  return 0;
+}

@@ -41,6 +41,7 @@ def lib():
         L.lmh_fs_node.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                   C.c_int64, C.c_char_p, C.c_int]
         L.lmh_get_tracks.argtypes = [C.c_int] + [C.c_void_p] * 5
+        L.lmh_fs_write_demo.argtypes = [C.c_char_p]
         L.lmh_selftest.argtypes = [C.c_char_p, C.c_int]
         L.lmh_selftest.restype = C.c_int
         _lib = L

@@ -1,6 +1,6 @@
 """Writers of the reference CLI's input files, for tests: OpenCV FileStorage
-YAML (config.yml, the model and calibration files), 8-bit PNG and
-uncompressed AVI.  Test infrastructure: these produce the files the
+YAML (config.yml, the model and calibration files), 8-bit PNG,
+uncompressed AVI and MJPEG AVI (frames encoded by Pillow).  Test infrastructure: these produce the files the
 reference's users hand to `LocoMouse`."""
 import struct
 import zlib
@@ -164,7 +164,84 @@ def write_avi(path, frames, bits=24, other=None, fps=30):
         fh.write(b"RIFF" + struct.pack("<I", len(body)) + body)
 
 
-def write_inputs(dirpath, cfg, n_frames, stem="synth_R", bits=24, config_overrides=None, bb_params=None):
+def jpeg_frames(frames, mode="L", other=None, strip_dht=False, **save_kw):
+    """Each frame (H x W u8) as a JPEG encoded by Pillow (libjpeg-turbo): grey
+    ('L'), or colour ('RGB') whose blue channel is the frame (red / green from
+    `other` or a pattern) — channel 0 of the BGR rendering is then the frame
+    up to the codec's loss.  save_kw go to Image.save (quality, subsampling,
+    optimize, restart_marker_blocks, progressive ...).  strip_dht drops the
+    Huffman table segments, as MJPEG "AVI1" frames do (valid only with the
+    standard tables, i.e. without optimize)."""
+    import io
+
+    from PIL import Image
+    out = []
+    for f, img in enumerate(np.asarray(frames, np.uint8)):
+        if mode == "L":
+            im = Image.fromarray(img, "L")
+        else:
+            g = other[f] if other is not None else (img.astype(np.int32) * 3 + 17) & 0xFF
+            rgb = np.stack([(255 - img), g.astype(np.uint8), img], axis=2)
+            im = Image.fromarray(rgb, "RGB")
+        b = io.BytesIO()
+        im.save(b, "JPEG", **save_kw)
+        d = b.getvalue()
+        if strip_dht:
+            d = _strip_segments(d, 0xC4)
+        out.append(d)
+    return out
+
+
+def _strip_segments(d, marker):
+    out, i = bytearray(d[:2]), 2
+    while i < len(d):
+        m = d[i + 1]
+        if m == 0xDA:
+            out += d[i:]
+            break
+        n = 2 + (d[i + 2] << 8 | d[i + 3])
+        if m != marker:
+            out += d[i:i + n]
+        i += n
+    return bytes(out)
+
+
+def decode_jpeg_channel0(data):
+    """Pillow's (libjpeg-turbo's) decoding of one JPEG, as channel 0 of BGR:
+    the blue plane of its RGB rendering, or the grey plane itself."""
+    import io
+
+    from PIL import Image
+    im = Image.open(io.BytesIO(data))
+    im.load()
+    a = np.asarray(im)
+    return a if a.ndim == 2 else a[:, :, 2]
+
+
+def write_mjpeg_avi(path, jpegs, w, h, fps=30, fourcc=b"MJPG"):
+    """MJPEG AVI: one JPEG per '00dc' chunk, BITMAPINFOHEADER compression
+    `fourcc` (24 bits), frame size w x h."""
+    n = len(jpegs)
+    size = max(len(j) for j in jpegs)
+    strh = b"vids" + fourcc + struct.pack("<IHHIIIIIIIIhhhh", 0, 0, 0, 0, 1, fps, 0, n, size, 0xFFFFFFFF, 0, 0, 0, w, h)
+    bih = struct.pack("<IiiHH", 40, w, h, 1, 24) + fourcc + struct.pack("<IiiII", w * h * 3, 0, 0, 0, 0)
+
+    def ck(tag, data):
+        return tag + struct.pack("<I", len(data)) + data + (b"\0" if len(data) & 1 else b"")
+
+    def lst(tag, data):
+        return b"LIST" + struct.pack("<I", len(data) + 4) + tag + data
+
+    avih = struct.pack("<IIIIIIIIIIIIII", 1000000 // fps, 0, 0, 0x10, n, 0, 1, size, w, h, 0, 0, 0, 0)
+    hdrl = lst(b"hdrl", ck(b"avih", avih) + lst(b"strl", ck(b"strh", strh) + ck(b"strf", bih)))
+    movi = b"".join(ck(b"00dc", j) for j in jpegs)
+    body = b"AVI " + hdrl + lst(b"movi", movi)
+    with open(path, "wb") as fh:
+        fh.write(b"RIFF" + struct.pack("<I", len(body)) + body)
+
+
+def write_inputs(dirpath, cfg, n_frames, stem="synth_R", bits=24, config_overrides=None, bb_params=None,
+                 jpeg=None):
     """The five input files of one CLI run; returns their paths."""
     import os
     paths = {k: os.path.join(dirpath, v) for k, v in (
@@ -174,5 +251,10 @@ def write_inputs(dirpath, cfg, n_frames, stem="synth_R", bits=24, config_overrid
     write_model(paths["model"], cfg)
     write_calibration(paths["calibration"], cfg)
     write_png(paths["background"], cfg.background)
-    write_avi(paths["video"], cfg.frames(0, n_frames), bits=bits)
+    if jpeg is None:
+        write_avi(paths["video"], cfg.frames(0, n_frames), bits=bits)
+    else:  # MJPEG: jpeg = jpeg_frames keyword arguments; the decoded frames are returned too
+        js = jpeg_frames(cfg.frames(0, n_frames), **jpeg)
+        write_mjpeg_avi(paths["video"], js, cfg.cols, cfg.rows)
+        paths["decoded"] = np.stack([decode_jpeg_channel0(j) for j in js])
     return paths

@@ -1,6 +1,6 @@
 """The `LocoMouse` command-line program and its file readers (SURVEY.md §8(f)
 row 2): OpenCV FileStorage YAML (config, model, calibration, output), 8-bit
-PNG background, uncompressed AVI video; the reference's arguments, messages
+PNG background, uncompressed and MJPEG AVI video (tests/test_mjpeg.py); the reference's arguments, messages
 and exit codes (main.cpp:38-105, LocoMouse_ParseInputs.cpp, LocoMouse_class.cpp:
 12-540, :3095-3162).  The GPU test runs the whole program on synthetic files
 and compares its output YAML with the oracle's detection + restated tracker.
@@ -164,6 +164,35 @@ def test_file_storage_yaml_forms(tmp_path):
         fs_node(bad, "m")
 
 
+def test_file_storage_writer_layout(tmp_path):
+    """FsWriter follows OpenCV's YAML emitter (persistence_yml.cpp): header,
+    3-space block indent, flow sequences wrapped past column 71 with the
+    struct's indent, "%d." / "%.16e" reals, "-" lines for nested block
+    entries, "[]" for empty collections; and our reader reads it back."""
+    p = tmp_path / "w.yml"
+    assert H.lib().lmh_fs_write_demo(os.fsencode(p)) == 0
+    text = p.read_text()
+    head = ("%YAML:1.0\n---\nN_opencv_matrices: 7\nM: !!opencv-matrix\n   rows: 2\n   cols: 3\n   dt: i\n"
+            "   data: [ 1, -2, 3, 4, 5, 6 ]\nreal: 5.0000000000000000e-01\nwhole: 15.\n"
+            "neg: -3.7500000000000000e-01\nBB:\n   x: 1\n   y: 2\nseq: [ 0, 1000,")
+    assert text.startswith(head), text[:400]
+    tail = ("nested:\n   -\n      -\n         Candidate_bottom:\n            Point_x: 3\n"
+            "            Score: 2.5000000000000000e-01\n         side: [ 4 ]\n   -\n      []\n"
+            "empty_flow: []\nlast: text\n")
+    assert text.endswith(tail), text[-300:]
+    seq = text[text.index("seq: ["):text.index("nested:")].splitlines()
+    assert len(seq) > 2 and all(len(line) <= 73 for line in seq)  # margin 71, plus " " and ","
+    assert all(line.startswith("    ") and line[4] != " " for line in seq[1:])
+    assert all(line.endswith(",") for line in seq[:-1]) and seq[-1].endswith(" ]")
+    k, vals = fs_node(p, "seq")
+    assert k == "seq" and vals.tolist() == [1000 * k for k in range(40)]
+    k, dt, m = fs_node(p, "M")
+    assert dt == "i" and m.tolist() == [[1, -2, 3], [4, 5, 6]]
+    assert fs_node(p, "neg")[1] == -0.375 and fs_node(p, "whole")[1] == 15.0
+    assert fs_node(p, "last") == ("str", "text")
+    assert fs_node(p, "nested")[0] == "seq"
+
+
 # ------------------------------------------------------- CLI, no GPU needed
 
 def test_cli_reads_every_input(tmp_path):
@@ -244,21 +273,23 @@ def test_cli_errors_match_the_reference(tmp_path, case):
 # ------------------------------------------------------------- GPU: full run
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["R24", "L8"])
+@pytest.mark.parametrize("variant", ["R24", "L8", "RJ"])
 def test_cli_end_to_end_matches_oracle(tmp_path, variant):
     """The whole program on synthetic files: its output YAML holds the
     oracle's tracks (oracle detection on the same frames + the restated
-    tracker)."""
+    tracker).  "RJ": an MJPEG video (4:2:0 colour JPEG frames), the oracle
+    fed Pillow's decoding of the same frames."""
     from oracle import oracle as O
     from oracle import track_oracle as TO
     flip = variant.startswith("L")
     n = 40
     cfg = S.SyntheticConfig(flip=flip)
     stem = "mouse_" + variant[0]
-    paths = MW.write_inputs(str(tmp_path), cfg, n, stem=stem, bits=int(variant[1:]))
+    jpeg = dict(mode="RGB", quality=92, subsampling=2) if variant.endswith("J") else None
+    paths = MW.write_inputs(str(tmp_path), cfg, n, stem=stem, bits=24 if jpeg else int(variant[1:]), jpeg=jpeg)
     rc, out = run_cli(cli_args(paths, side=variant[0], outdir=str(tmp_path)), env={"LM_BATCH": "16"})
     assert rc == 0, out
-    res = O.OracleRun(cfg, cfg.frames(0, n)).result
+    res = O.OracleRun(cfg, paths["decoded"] if jpeg else cfg.frames(0, n)).result
     p = cfg.params
     corner = [p.bounding_box_bottom.x + p.bounding_box_bottom.width,
               p.bounding_box_bottom.y + p.bounding_box_bottom.height,
@@ -273,3 +304,100 @@ def test_cli_end_to_end_matches_oracle(tmp_path, variant):
     assert np.array_equal(m.astype(np.int32), np.array(ref["snout_tracks"][0], np.int32))
     k, dt, m = fs_node(yml, "tracks_tail")
     assert np.array_equal(m.astype(np.int32), np.array(ref["tracks_tail"], np.int32))
+
+
+def _load_cv_yaml(path):
+    """An independent reader for the FileStorage YAML (PyYAML, safe loader with
+    a constructor for !!opencv-matrix)."""
+    import yaml
+
+    class Loader(yaml.SafeLoader):
+        pass
+
+    def mat(loader, node):
+        m = loader.construct_mapping(node, deep=True)
+        return np.array(m["data"]).reshape(m["rows"], m["cols"])
+
+    Loader.add_constructor("tag:yaml.org,2002:opencv-matrix", mat)
+    text = open(path).read().replace("%YAML:1.0", "", 1)
+    return yaml.load(text, Loader=Loader)
+
+
+@pytest.mark.gpu
+def test_cli_verbose_debug_outputs(tmp_path):
+    """verbose_debug: 1 with N_debug_frames: 30 of a 40-frame video — the run
+    stops after 30 frames (loadVideo :380-389), and debug_<stem>.yml holds
+    exportDebugVariables' content (:2769-2920) equal to the oracle's
+    containers and tracks; debug_<stem>.txt logs each frame's stages."""
+    import re
+
+    from oracle import oracle as O
+    from oracle import track_oracle as TO
+    n, nd = 40, 30
+    cfg = S.SyntheticConfig()
+    stem = "dbg_R"
+    paths = MW.write_inputs(str(tmp_path), cfg, n, stem=stem,
+                            config_overrides={"verbose_debug": 1, "N_debug_frames": nd})
+    rc, out = run_cli(cli_args(paths, outdir=str(tmp_path)), env={"LM_BATCH": "16"})
+    assert rc == 0, out
+    res = O.OracleRun(cfg, cfg.frames(0, nd)).result
+    p = cfg.params
+    corner = [p.bounding_box_bottom.x + p.bounding_box_bottom.width,
+              p.bounding_box_bottom.y + p.bounding_box_bottom.height,
+              p.bounding_box_side.y + p.bounding_box_side.height]
+    geom = O.geometry(cfg)
+    ref = TO.run_tracks(res, geom, p, [corner] * nd, nd)
+    k, dt, m = fs_node(str(tmp_path / f"output_{stem}.yml"), "paw_tracks0")
+    assert np.array_equal(m.astype(np.int32), np.array(ref["paw_tracks"][0], np.int32))
+
+    d = _load_cv_yaml(tmp_path / f"debug_{stem}.yml")
+    assert d["N_opencv_matrices"] == 7 and d["N_frames"] == nd
+    assert np.array_equal(d["M_paw_bottom"], np.array(ref["track_index_paw_bottom"]))
+    assert np.array_equal(d["M_snout_bottom"], np.array(ref["track_index_snout_bottom"]))
+    for i in range(4):
+        assert d[f"M_paw_side_{i}"].ravel().tolist() == list(ref["track_index_paw_side"][i])
+    assert d["M_snout_side_0"].ravel().tolist() == list(ref["track_index_snout_side"][0])
+    assert d["occluded_distance"] == p.max_displacement_bottom
+    assert d["BB_bottom"] == {"x": 0, "y": 0, "width": p.bounding_box_bottom.width,
+                              "height": p.bounding_box_bottom.height}
+    assert d["bb_x_avg"] == [corner[0]] * nd and d["bb_yb_avg"] == [corner[1]] * nd
+    assert d["bb_yt_avg"] == [corner[2]] * nd
+    ong = d["ONG"]
+    assert ong["points"] == geom.ong_nx * geom.ong_ny == len(ong["x_y_coordinates"]) // 2
+    assert ong["x_y_coordinates"][:2] == [geom.ong_br_x, geom.ong_br_y]
+    assert d["ONG_side"]["z_coordinates"][0] == geom.ong_side_lowest
+    for feat, key in ((0, "candidates_paw_bottom_side_matched"), (1, "candidates_snout_bottom_side_matched")):
+        ml = TO.matched_list(res, feat)
+        assert len(d[key]) == nd
+        for f in range(nd):
+            got = d[key][f] or []
+            assert len(got) == len(ml[f])
+            for e, (x, y, ys, ss) in zip(got, ml[f]):
+                assert (e["Candidate_bottom"]["Point_x"], e["Candidate_bottom"]["Point_y"]) == (x, y)
+                assert e["n_candidates_side"] == len(e["Candidates_side"])
+                if e["Scores_side"][0] >= 0:
+                    assert e["Candidates_side"] == ys and e["Scores_side"] == ss
+                else:
+                    assert ys == []
+    for feat, key in ((0, "Unary_paws"), (1, "Unary_snout")):
+        assert len(d[key]) == nd
+        for f in range(nd):
+            lo, hi = int(res["unary_offset"][2 * f + feat]), int(res["unary_offset"][2 * f + feat + 1])
+            u = d[key][f]
+            assert u["n_rows"] * u["n_cols"] == hi - lo and u["n_cols"] == (4 if feat == 0 else 1)
+            assert (u["data"] or []) == [float(v) for v in res["unary"][lo:hi]]  # %.16e round-trips
+    for feat, key in ((0, "Pairwise_paws"), (1, "Pairwise_snout")):
+        assert len(d[key]) == nd - 1
+        for f in range(1, nd):
+            q = 2 * f + feat
+            lo, hi = int(res["pw_nz_offset"][q]), int(res["pw_nz_offset"][q + 1])
+            e = d[key][f - 1]
+            assert (e["data"] or []) == [float(v) for v in res["pw_pr"][lo:hi]]
+            assert (e["row_index"] or []) == [int(v) for v in res["pw_ir"][lo:hi]]
+
+    txt = (tmp_path / f"debug_{stem}.txt").read_text()
+    counts = [int(c) for c in re.findall(r"Detected (\d+) paw candidates\.", txt)]
+    want = [int(res["cand_offset"][4 * f + 1] - res["cand_offset"][4 * f]) for f in range(nd)]
+    assert counts == want
+    assert txt.count("=== readFrame: ") == nd and "=== exportResults: " in txt
+    assert "--- exportDebugVariables() " in txt and txt.rstrip().endswith("=== Done")
