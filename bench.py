@@ -28,6 +28,7 @@ CONFIGS = {  # BASELINE.json configs with a GPU bench line: (rows, cols, descrip
                       "full per-frame path incl. D2H of results"),
 }
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
+F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16 MFMA peak (MI355X_MICROARCH.md: ~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -210,6 +211,8 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
+    ap.add_argument("--precision", choices=["fp32", "f16"], default="fp32",
+                    help="f16: the non-parity LM_CORR_F16 correlation (BASELINE config 5)")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--resident", type=int, default=6400, help="frames resident in HBM per stream (cycled)")
     ap.add_argument("--streams", type=int, default=3,
@@ -254,6 +257,11 @@ def main():
     rows, cols, workload = CONFIGS[args.config]
     FRAME_BYTES = rows * cols
     cfg = S.SyntheticConfig(rows=rows, cols=cols)
+    f16 = args.precision == "f16"
+    if f16:  # non-parity mode (LM_CORR_F16): f16 weights, fp32 accumulation on the matrix cores
+        cfg.setup.corr_precision = 1
+        workload = workload.replace("(fp32, bit-exact mode)", "(LM_CORR_F16: f16 weights, fp32 accumulation, non-parity)")
+        workload += "" if "LM_CORR_F16" in workload else " [LM_CORR_F16 non-parity correlation]"
     # NS contexts per GPU, each with its own HIP stream and host thread, each
     # on its own contiguous range of the video (rank-major): like a shard, its
     # first batch gets the previous frame as a 1-frame halo.
@@ -342,6 +350,7 @@ def main():
     corr_spans = spans.get("k_corr", [])
     corr_avg_ms = union_ms(corr_spans) / max(1, len(corr_spans))
     achieved_tf = flops * B / (corr_avg_ms * 1e-3) / 1e12
+    peak_tf = F16_PEAK_TFLOPS if f16 else FP32_PEAK_TFLOPS
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_corr.json")
     if os.path.exists(pmc):
@@ -358,16 +367,19 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f16xf16->f32 (non-parity LM_CORR_F16)" if f16 else "f32",
         "data": "synthetic (lm_synth.h scene, resident in HBM)",
         "config": {"workload": workload,
                    "batch_frames": B, "streams_per_gpu": NS, "frames_per_rank": args.steps * B * NS,
                    "resident_frames_per_stream": R,
                    "parallelism": f"frame shards x{world} (no collective)"},
         "hbm_gbs": round(fps * FRAME_BYTES / 1e9, 3),
-        "roofline": {"bound": "mfma", "compute_roof": "fp32 (v_fma_f32 VALU; equals the f32 MFMA peak)",
-                     "kernel": "k_corr", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+        "roofline": {"bound": "mfma",
+                     "compute_roof": "dense f16 MFMA (v_mfma_f32_32x32x16_f16)" if f16 else
+                     "fp32 (v_fma_f32 VALU; equals the f32 MFMA peak)",
+                     "kernel": "k_corr", "achieved": round(achieved_tf, 3), "peak": peak_tf,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
+                     "traffic": traffic if not f16 and args.config == "c3" else None,
                      "algorithmic_flop_per_launch": flops * B, "avg_launch_ms": round(corr_avg_ms, 5),
                      "launches": len(corr_spans),
                      "duration": "union of k_corr HIP-event spans over all streams / launches"},

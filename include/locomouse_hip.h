@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LM_ABI_VERSION 2
+#define LM_ABI_VERSION 3
 #define LM_N_PAWS 4          /* LocoMouse_class.hpp:84 */
 #define LM_N_TAIL_POINTS 15  /* LocoMouse_class.hpp:86 */
 #define LM_N_LISTS 4         /* candidate lists per frame */
@@ -145,6 +145,7 @@ typedef struct {
   const int32_t* ind_warp_mapping;/* calib_rows x calib_cols, copied at create */
   lm_rect view_box_side, view_box_bottom;
   int32_t filter_arith;           /* LM_FILTER_FUSED (default) or LM_FILTER_UNFUSED, see below */
+  int32_t corr_precision;         /* LM_CORR_FP32 (default, bit-exact) or LM_CORR_F16, see below */
 } lm_setup;
 /* filter2D's fp32 tap arithmetic depends on the OpenCV build the reference
  * links (no version is pinned, CMakeLists.txt:3): AVX2 builds of OpenCV
@@ -153,6 +154,17 @@ typedef struct {
  * bit-exact against the restatement of that build (tests/test_gpu_parity.py). */
 #define LM_FILTER_FUSED 0
 #define LM_FILTER_UNFUSED 1
+/* LM_CORR_F16 is a NON-PARITY mode (BASELINE config 5, "fp16 correlation
+ * accumulators"): the six correlations run on f16 matrix cores with each
+ * detector's weights rounded to f16 (after an exact power-of-two scaling) and
+ * fp32 accumulation.  Pixels are exact; scores differ from the fp32 chain by
+ * the weight rounding (about 2^-12 relative per tap) and the summation order,
+ * so candidates near a threshold or a score tie can differ.  filter_arith is
+ * ignored in this mode.  Detectors must fit the kernel's LDS window
+ * (LM_ERR_INVALID_ARGUMENT otherwise); lm_debug_scores still returns the
+ * fp32 chain. */
+#define LM_CORR_FP32 0
+#define LM_CORR_F16 1
 
 /* Geometry derived at create time (initializeFeatureLoop :655-769 and the
  * LocoMouse_Model pads :3157-3161 incl. the spost_b = spre_b move-assign at :3173). */

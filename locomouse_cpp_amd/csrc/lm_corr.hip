@@ -16,6 +16,8 @@
 //   k_corr_gen<UNF>     any width and height: taps in chunks of 4 columns and
 //                       the tap rows in LDS-sized chunks (detectors larger than
 //                       the LDS window, widths without an instantiation).
+//   k_corr_f16<NCH>     NON-PARITY half-precision mode (LM_CORR_F16): f16
+//                       weights, fp32 accumulation on the matrix cores.
 //   k_corr_dbg<UNF>     raw scores straight from the ext crops in global memory
 //                       (diagnostics: lm_debug_scores).
 
@@ -190,7 +192,7 @@ DEV CorrTile corr_tile(const LmConst& K, const LmDetGroup& G) {
   const int d = G.ids[gi];
   const int lt = blockIdx.x - tb;
   const int tx = K.det[d].tiles_x;
-  return CorrTile{d, (lt / tx) * K.det[d].tile_h, (lt % tx) * LM_TW};
+  return CorrTile{d, (lt / tx) * K.det[d].tile_h, (lt % tx) * K.det[d].tile_w};
 }
 
 DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext, int64_t ext_slot_bytes, int slot,
@@ -345,6 +347,216 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
                             &s_cnt, &s_base, msrc, ew);
 }
 
+// ---------------------------------------------------------------- k_corr_f16
+// Non-parity half-precision mode (lm_setup.corr_precision = LM_CORR_F16,
+// BASELINE config 5): u8 pixels (exact in f16) times f16 weights (each
+// detector's scaled by a power of two, so the rounding is 2^-12 relative and
+// nothing is subnormal), accumulated in fp32 by v_mfma_f32_32x32x16_f16.
+// Kernel row i of a detector is a banded (Toeplitz) product
+//     C[y][x] += sum_k A_i[y][k] * B_i[k][x],  A_i[y][k] = I(y + i, x0 + k),
+//                                              B_i[k][x] = w[i][k - x] (0 off the band)
+// over k < 16 * NCH (32 + kw - 1 rounded up to 16).  A fragments are aligned
+// 16-byte reads of the f16 window in LDS (row stride = 8 mod 16 halfs: the
+// 32 rows a read touches fall in distinct bank groups).  B fragments do not
+// depend on the output tile: the host lays them out once per detector in the
+// MFMA's lane order ([i][chunk][lane] x 8 halfs), and each workgroup stages
+// row i + 1's NCH KiB into LDS (double buffer, one barrier per row) while
+// it multiplies with row i's; every wave reads them with one aligned
+// ds_read_b128 per chunk and uses each for its two 32 x 32 output tiles.
+// Four waves side by side: a 128 x 64 output tile per workgroup.
+// Accumulator layout (32x32 MFMA): column = lane & 31, row = (reg & 3) +
+// 8 (reg >> 2) + 4 (lane >> 5).
+#define LM_F16_TW 128
+#define LM_F16_TH 64
+#define LM_F16_T 2      // 32-row accumulator tiles per wave
+#define LM_F16_THREADS 256
+#define LM_F16_MAX_NCH 10
+#ifndef LM_F16_EXP
+#define LM_F16_EXP 0  // experiments: 1 = no B staging, no barrier; 2 = no B staging, barrier kept
+#endif
+
+typedef _Float16 lm_h8 __attribute__((ext_vector_type(8)));
+typedef float lm_f32x16 __attribute__((ext_vector_type(16)));
+
+__host__ __device__ constexpr int f16_nch(int kw) { return (kw + 31 + 15) / 16; }
+__host__ __device__ constexpr int f16_cols(int nch) { return LM_F16_TW - 32 + 16 * nch; }
+__host__ __device__ constexpr int f16_stride(int cols) { return (cols + 7) / 16 * 16 + 8; }
+__host__ __device__ constexpr size_t f16_lds_bytes(int nch, int kh) {
+  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2 + (size_t)2 * nch * 64 * 16;
+}
+// Host: the B fragment of (row i, chunk c) for lane l, element j (0 off the band).
+static inline float f16_bfrag_weight(const double* w, int kw, int i, int c, int l, int j) {
+  const int r = l & 31, h = l >> 5, jj = 16 * c + 8 * h + j - r;
+  return (jj >= 0 && jj < kw) ? (float)w[(size_t)i * kw + jj] : 0.0f;
+}
+
+// u8 window -> f16 LDS (same loads as tile_fill_f32, one half per pixel).
+DEV void tile_fill_f16(_Float16* __restrict__ lds, int stride, const uint8_t* __restrict__ src, int ew, int rows,
+                       int cols) {
+  const int mis = (int)((uintptr_t)src & 15);
+  const uint8_t* __restrict__ a = src - mis;
+  const int nch = (mis + cols + 15) >> 4;
+  const int total = rows * nch;
+  for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
+    uint4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+      if (e < total) {
+        const int r = e / nch, ch = e - r * nch;
+        v[u] = *reinterpret_cast<const uint4*>(a + (int64_t)r * ew + ch * 16);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
+      if (e < total) {
+        const int r = e / nch, ch = e - r * nch;
+        const int c0 = ch * 16 - mis;
+        _Float16* __restrict__ o = lds + r * stride + c0;
+        const unsigned w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        if (c0 >= 0 && c0 + 16 <= cols) {  // whole chunk inside the window: straight-line stores
+#pragma unroll
+          for (int k = 0; k < 16; ++k) o[k] = (_Float16)(float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if (c0 + k >= 0 && c0 + k < cols) o[k] = (_Float16)(float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+        }
+      }
+    }
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __restrict__ Kp, const LmDetGroup G,
+                                                            const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                            const uint4* __restrict__ bfrag, int s0,
+                                                            unsigned long long* __restrict__ keys,
+                                                            int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin,
+                                                            int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  // uint4: the dynamic area starts 16-byte aligned after the static variables
+  // (with a float array it would start 8 bytes in, and every ds_read_b128 of
+  // the window would be misaligned — an order of magnitude slower)
+  extern __shared__ uint4 lds_f16[];
+  __shared__ int s_cnt, s_base;
+  const int slot = s0 + blockIdx.y;
+  const CorrTile T = corr_tile(K, G);
+  const LmDet D = K.det[T.d];
+  const int oy0 = T.oy0, ox0 = T.ox0, kh = D.kh;
+  constexpr int cols = f16_cols(NCH), STR = f16_stride(cols);
+  constexpr int NB = NCH * 64;  // 16-byte B fragments per detector row
+  const int rows = LM_F16_TH + kh - 1;
+  _Float16* __restrict__ img = reinterpret_cast<_Float16*>(lds_f16);
+  uint4* __restrict__ bbuf = reinterpret_cast<uint4*>(img + rows * STR);  // [2][NB]
+  const uint4* __restrict__ bsrc = bfrag + D.w16_off;
+  // B staging: each thread moves fragments tid, tid + 256, tid + 512 of a row
+  // (loads clamped into the row, so they need no branch; stores guarded)
+  static_assert(NB <= 3 * LM_F16_THREADS, "B staging");
+  const int e0 = threadIdx.x;
+  uint4 st0, st1, st2;
+  auto stage_load = [&](int row) {
+    const uint4* __restrict__ p = bsrc + (int64_t)row * NB;
+    st0 = p[min(e0, NB - 1)];
+    if constexpr (NB > LM_F16_THREADS) st1 = p[min(e0 + LM_F16_THREADS, NB - 1)];
+    if constexpr (NB > 2 * LM_F16_THREADS) st2 = p[min(e0 + 2 * LM_F16_THREADS, NB - 1)];
+  };
+  auto stage_store = [&](uint4* __restrict__ dst) {
+    if (e0 < NB) dst[e0] = st0;
+    if constexpr (NB > LM_F16_THREADS)
+      if (e0 + LM_F16_THREADS < NB) dst[e0 + LM_F16_THREADS] = st1;
+    if constexpr (NB > 2 * LM_F16_THREADS)
+      if (e0 + 2 * LM_F16_THREADS < NB) dst[e0 + 2 * LM_F16_THREADS] = st2;
+  };
+  stage_load(0);
+  tile_fill_f16(img, STR, corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0), K.ext_w[D.view], rows, cols);
+  stage_store(bbuf);
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const float init = D.delta * D.wscale;
+  lm_f32x16 acc[LM_F16_T];
+#pragma unroll
+  for (int t = 0; t < LM_F16_T; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[t][q] = init;
+  const _Float16* __restrict__ arow = img + r * STR + 32 * wave + 8 * h;
+  for (int i = 0; i < (LM_F16_EXP == 3 ? 0 : kh); ++i) {
+    const bool more = LM_F16_EXP == 0 && i + 1 < kh;
+    if (more) stage_load(i + 1);  // row i + 1's fragments: global -> registers now, -> LDS after this row's MFMAs
+    const lm_h8* __restrict__ bi = reinterpret_cast<const lm_h8*>(bbuf + (LM_F16_EXP ? 0 : (i & 1) * NB)) + lane;
+    const _Float16* __restrict__ ai = arow + i * STR;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const lm_h8 b = bi[64 * c];
+#pragma unroll
+      for (int t = 0; t < LM_F16_T; ++t) {
+        const lm_h8 a = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR + 16 * c);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[t], 0, 0, 0);
+      }
+    }
+    if (more) stage_store(bbuf + ((i + 1) & 1) * NB);
+    if (LM_F16_EXP != 1) __syncthreads();
+  }
+
+  const int x = ox0 + 32 * wave + r;
+  if (D.kind != 0) {
+    uint8_t* __restrict__ tb = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
+#pragma unroll
+    for (int t = 0; t < LM_F16_T; ++t)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int y = oy0 + 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (y < D.oh && x < D.ow) tb[(int64_t)y * D.ow + x] = acc[t][q] > 0.0f ? 1 : 0;
+      }
+    return;
+  }
+  unsigned bits = 0;
+  const _Float16* __restrict__ mrow = img + (D.m_y - D.in_y) * STR + 32 * wave + r + (D.m_x - D.in_x);
+#pragma unroll
+  for (int t = 0; t < LM_F16_T; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ly = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+      const int y = oy0 + ly;
+      const float pix = (float)mrow[ly * STR];
+      if (y < D.oh && x < D.ow && pix > 25.0f && acc[t][q] > 0.0f) bits |= 1u << (16 * t + q);
+    }
+  const int nk = __popc(bits);
+  const int off = nk ? atomicAdd(&s_cnt, nk) : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
+  __syncthreads();
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + s_base + off;
+  int k = 0;
+#pragma unroll
+  for (int t = 0; t < LM_F16_T; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (bits & (1u << (16 * t + q))) {
+        const int y = oy0 + 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const float score = acc[t][q] * D.inv_wscale;
+        kl[k++] = ((unsigned long long)(~__float_as_uint(score)) << 32) | (unsigned)(y * D.ow + x);
+      }
+}
+
+static inline const void* corr_kernel_f16(int kw) {
+  switch (f16_nch(kw)) {
+    case 2: return (const void*)&k_corr_f16<2>;
+    case 3: return (const void*)&k_corr_f16<3>;
+    case 4: return (const void*)&k_corr_f16<4>;
+    case 5: return (const void*)&k_corr_f16<5>;
+    case 6: return (const void*)&k_corr_f16<6>;
+    case 7: return (const void*)&k_corr_f16<7>;
+    case 8: return (const void*)&k_corr_f16<8>;
+    case 9: return (const void*)&k_corr_f16<9>;
+    case 10: return (const void*)&k_corr_f16<10>;
+    default: return nullptr;
+  }
+}
+
 // ---------------------------------------------------------------- dispatch
 // Widths with a specialised k_corr_pk (detectors up to 64 rows); every other
 // detector runs k_corr_gen.
@@ -380,13 +592,14 @@ static inline const void* corr_kernel(int kw, int kh, bool unf) {
 
 // Launch the correlation for one detector group (all detectors of one width
 // that run the same kernel).
-static inline hipError_t launch_corr(const void* fn, dim3 grid, size_t lds, hipStream_t st, const LmConst* K,
-                                     const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes,
-                                     const float* weights, int s0, unsigned long long* keys, int32_t* n_pos,
+// `weights`: the fp32 rows (k_corr_pk / k_corr_gen) or the f16 rows (k_corr_f16).
+static inline hipError_t launch_corr(const void* fn, dim3 grid, int threads, size_t lds, hipStream_t st,
+                                     const LmConst* K, const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes,
+                                     const void* weights, int s0, unsigned long long* keys, int32_t* n_pos,
                                      uint8_t* tailbin, int64_t tailbin_slot_bytes) {
   void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
                   (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
-  return hipLaunchKernel(fn, grid, dim3(LM_CORR_THREADS), args, lds, st);
+  return hipLaunchKernel(fn, grid, dim3(threads), args, lds, st);
 }
 
 // Debug copy of raw scores (lm_debug_scores): the same chain per output,

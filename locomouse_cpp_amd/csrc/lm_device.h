@@ -39,9 +39,13 @@ struct LmDet {
   int32_t in_y, in_x;  // ext-crop coords of tap (0,0) of output (0,0)
   int32_t m_y, m_x;    // ext-crop coords of the I_*_MOUSE pixel of output (0,0)
   int32_t tiles_x, tiles_y, tile_base;
-  int32_t tile_h;        // output rows per correlation tile (LM_TH)
+  int32_t tile_w, tile_h;  // output columns / rows per correlation tile (LM_TW x LM_TH; f16 mode 128 x 64)
   int32_t box_w, box_h;  // NMS box (detector cols, rows)
   int32_t chunk_rows;    // k_corr_gen: detector rows per LDS window
+  // LM_CORR_F16: f16 weight rows (kh x f16_wrow, zero-padded) at w16_off
+  // halfs, scaled by wscale = 2^s (inv_wscale = 2^-s, both exact)
+  int32_t w16_off;
+  float wscale, inv_wscale;
 };
 
 struct LmConst {

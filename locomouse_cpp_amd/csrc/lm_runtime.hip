@@ -63,6 +63,7 @@ bool dbg_env(const char* name) {  // diagnostics switches (LM_* environment vari
 constexpr size_t kGuard = 64 * 1024;
 // LDS window of one k_corr_gen workgroup (row chunks are sized to fit it)
 constexpr size_t kCorrLdsBudget = 64 * 1024;
+constexpr size_t kF16LdsMax = 160 * 1024;  // one k_corr_f16 workgroup per CU at most
 bool guard_mode() {
   static const bool on = [] {
     const char* v = getenv("LM_GUARD");
@@ -222,12 +223,14 @@ struct lm_ctx {
   bool unfused = false;                                         // LM_FILTER_UNFUSED
   std::vector<std::pair<const void*, LmDetGroup>> corr_groups;  // (correlation kernel, its detectors)
   std::vector<size_t> corr_group_lds;                    // dynamic LDS bytes per group launch
+  std::vector<int> corr_group_threads;                   // block size per group launch
   // device buffers
   DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin;
   DevBuf<unsigned long long> tailmask;  // TAIL_MASK bitmaps, 64 columns per word
   DevBuf<int32_t> cal, npos, err;
   DevBuf<unsigned> mm;  // k_minmax partial (min, max) pairs per slot
   DevBuf<float> weights, dbg;
+  DevBuf<_Float16> weights16;  // LM_CORR_F16 rows (LmDet::w16_off)
   DevBuf<int64_t> dbg_offd;
   DevBuf<const uint8_t*> frame_ptr;
   DevBuf<LmSlot> slots;
@@ -352,7 +355,12 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     // of the 80-column tile window must still fit (a detector wider than ~40k)
     if ((size_t)(LM_TH + 1) * pk_stride(LM_TW + dets[d]->cols + LM_JC) * sizeof(float) > kCorrLdsBudget)
       throw std::invalid_argument(std::string(names[d]) + ": detector too wide for the correlation window.");
+    if (su->corr_precision == LM_CORR_F16 &&
+        (f16_nch(dets[d]->cols) > LM_F16_MAX_NCH || f16_lds_bytes(f16_nch(dets[d]->cols), dets[d]->rows) > kF16LdsMax))
+      throw std::invalid_argument(std::string(names[d]) + ": detector too large for the f16 correlation (LM_CORR_F16).");
   }
+  if (su->corr_precision != LM_CORR_FP32 && su->corr_precision != LM_CORR_F16)
+    throw std::invalid_argument("corr_precision must be LM_CORR_FP32 or LM_CORR_F16.");
 
   c->setup = *su;
   c->params = *P;
@@ -441,8 +449,10 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     D.delta = (float)(-src.bias);  // saturate_cast<float>(delta)
     D.oh = out_rel[d].h;
     D.ow = out_rel[d].w;
-    D.tile_h = LM_TH;
-    D.tiles_x = (D.ow + LM_TW - 1) / LM_TW;
+    const bool f16 = su->corr_precision == LM_CORR_F16;
+    D.tile_w = f16 ? LM_F16_TW : LM_TW;
+    D.tile_h = f16 ? LM_F16_TH : LM_TH;
+    D.tiles_x = (D.ow + D.tile_w - 1) / D.tile_w;
     D.tiles_y = (D.oh + D.tile_h - 1) / D.tile_h;
     D.tile_base = tile;
     tile += D.tiles_x * D.tiles_y;
@@ -454,7 +464,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     ey0[v] = std::min(ey0[v], y0);
     ex0[v] = std::min(ex0[v], x0);
     ey1[v] = std::max(ey1[v], y0 + D.tiles_y * D.tile_h + D.kh - 1);
-    ex1[v] = std::max(ex1[v], x0 + D.tiles_x * LM_TW + D.kwp - 1 + 4);
+    const int win_w = f16 ? f16_cols(f16_nch(D.kw)) : LM_TW + D.kwp - 1 + 4;  // columns a tile's window reads
+    ex1[v] = std::max(ex1[v], x0 + (D.tiles_x - 1) * D.tile_w + win_w);
     D.in_y = y0;  // rebased below
     D.in_x = x0;
     D.m_y = out_rel[d].y;
@@ -574,11 +585,16 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   // keep more workgroups per CU.
   c->corr_groups.clear();
   c->corr_group_lds.clear();
+  c->corr_group_threads.clear();
   for (int d = 0; d < 6; ++d) {
     LmDet& D = K.det[d];
-    const void* fn = corr_kernel(D.kw, D.kh, c->unfused);
+    const bool f16 = su->corr_precision == LM_CORR_F16;
+    const void* fn = f16 ? corr_kernel_f16(D.kw) : corr_kernel(D.kw, D.kh, c->unfused);
     size_t need;
-    if (corr_specialised(D.kw, D.kh)) {
+    if (f16) {
+      D.chunk_rows = D.kh;
+      need = f16_lds_bytes(f16_nch(D.kw), D.kh);
+    } else if (corr_specialised(D.kw, D.kh)) {
       D.chunk_rows = D.kh;
       need = (size_t)(LM_TH + D.kh - 1) * pk_stride(LM_TW + D.kw - 1) * sizeof(float);
     } else {
@@ -593,6 +609,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       std::memset(&G, 0, sizeof(G));
       c->corr_groups.push_back({fn, G});
       c->corr_group_lds.push_back(0);
+      c->corr_group_threads.push_back(f16 ? LM_F16_THREADS : LM_CORR_THREADS);
     }
     LmDetGroup& G = c->corr_groups[gi].second;
     const int prev = G.n ? G.tile_end[G.n - 1] : 0;
@@ -608,6 +625,30 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     const LmDet& D = K.det[d];
     for (int i = 0; i < D.kh; ++i)
       for (int j = 0; j < D.kw; ++j) wts[(size_t)D.w_off + i * D.kwp + j] = (float)dets[d]->weights[(size_t)i * D.kw + j];
+  }
+  // LM_CORR_F16: each detector's B fragments (lm_corr.hip k_corr_f16) as f16,
+  // scaled by 2^s so that the largest |w| lands in [2^14, 2^15) (the rounding
+  // is then relative and no weight of interest is subnormal; 2^s and 2^-s
+  // are exact in fp32)
+  std::vector<_Float16> w16;
+  if (su->corr_precision == LM_CORR_F16) {
+    for (int d = 0; d < 6; ++d) {
+      LmDet& D = K.det[d];
+      const int nch = f16_nch(D.kw);
+      double mx = 0;
+      for (int k = 0; k < D.kh * D.kw; ++k) mx = std::max(mx, std::fabs(dets[d]->weights[k]));
+      int e = 0;
+      if (mx > 0) std::frexp(mx, &e);  // mx in [2^(e-1), 2^e)
+      const int sc = mx > 0 ? 15 - e : 0;
+      D.wscale = std::ldexp(1.0f, sc);
+      D.inv_wscale = std::ldexp(1.0f, -sc);
+      D.w16_off = (int32_t)(w16.size() / 8);  // in 16-byte fragments
+      for (int i = 0; i < D.kh; ++i)
+        for (int c = 0; c < nch; ++c)
+          for (int l = 0; l < 64; ++l)
+            for (int j = 0; j < 8; ++j)
+              w16.push_back((_Float16)std::ldexp(f16_bfrag_weight(dets[d]->weights, D.kw, i, c, l, j), sc));
+    }
   }
   uint8_t adj[256];
   {
@@ -631,6 +672,10 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   COPY_SYNC(c->cal.p, su->ind_warp_mapping, nc * sizeof(int32_t), hipMemcpyHostToDevice, c->stream);
   c->weights.alloc(wts.size());
   COPY_SYNC(c->weights.p, wts.data(), wts.size() * sizeof(float), hipMemcpyHostToDevice, c->stream);
+  if (!w16.empty()) {
+    c->weights16.alloc(w16.size());
+    COPY_SYNC(c->weights16.p, w16.data(), w16.size() * sizeof(_Float16), hipMemcpyHostToDevice, c->stream);
+  }
   c->adj.alloc(256);
   COPY_SYNC(c->adj.p, adj, 256, hipMemcpyHostToDevice, c->stream);
   c->dK.alloc(1);
@@ -643,7 +688,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->mm.alloc((size_t)2 * LM_MM_SPLIT * ns);
   // slack: the last tiles' windows (and the fill's 16-byte rounding) read past
   // the last slot's side view; those pixels only feed outputs that are discarded
-  c->ext.alloc((size_t)c->ext_slot_bytes * ns + (size_t)(LM_TH + 16) * std::max(K.ext_w[0], K.ext_w[1]) + 64);
+  c->ext.alloc((size_t)c->ext_slot_bytes * ns + (size_t)(LM_F16_TH + 16) * std::max(K.ext_w[0], K.ext_w[1]) + 64);
   c->tailbin.alloc((size_t)c->tailbin_slot_bytes * ns);
   c->tailmask.alloc((size_t)K.tail_hb * ((K.tail_w + 63) / 64) * ns);
   c->tscratch.alloc((size_t)5 * std::max(K.tail_hb, K.tail_hs) * ((K.tail_w + 1) / 2) * ns);
@@ -976,9 +1021,10 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       for (size_t gi = 0; gi < c->corr_groups.size(); ++gi) {
         const auto& grp = c->corr_groups[gi];
         const LmDetGroup& G = grp.second;
-        HIPCHK(launch_corr(grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_lds[gi], st, dK, G,
-                           c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->keys.p, c->npos.p, c->tailbin.p,
-                           c->tailbin_slot_bytes));
+        const void* w = c->setup.corr_precision == LM_CORR_F16 ? (const void*)c->weights16.p : (const void*)c->weights.p;
+        HIPCHK(launch_corr(grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_threads[gi],
+                           c->corr_group_lds[gi], st, dK, G, c->ext.p, c->ext_slot_bytes, w, s_proc0, c->keys.p,
+                           c->npos.p, c->tailbin.p, c->tailbin_slot_bytes));
       }
       T.end();
     }

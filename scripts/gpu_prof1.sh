@@ -17,7 +17,7 @@ i=0
 while read -r line; do
   [ -z "$line" ] && continue
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $line -f csv -d $OUT/p$i -o run -- python3 bench.py --streams 1 --steps 3 --warmup 1 --no-cpu > $OUT/p$i.log 2>&1 || { echo "pass $i failed: $line"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $line -f csv -d $OUT/p$i -o run -- python3 bench.py ${PMC_BENCH_ARGS:---streams 1 --steps 3 --warmup 1 --no-cpu} > $OUT/p$i.log 2>&1 || { echo "pass $i failed: $line"; tail -5 $OUT/p$i.log; exit 1; }
   echo "pass $i ok: $line"
 done < "${PMC_FILE:-scripts/pmc_k_corr.txt}"
 python3 scripts/pmc_summary.py $OUT > $OUT/pmc_summary.txt && cat $OUT/pmc_summary.txt
