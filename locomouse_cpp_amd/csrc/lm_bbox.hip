@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void k_bb_ingest(const LmBBConst K, const uint
   __shared__ uint8_t lut[256];
   lut[threadIdx.x] = luts[f * 256 + threadIdx.x];
   __syncthreads();
-  const uint8_t* __restrict__ F = frame_ptr[f];
+  const lm_gu8* __restrict__ F = as_global(frame_ptr[f]);
   uint8_t* __restrict__ Mf = M + (int64_t)f * K.m_bytes;
   const int64_t np = (int64_t)K.n_rows * K.n_cols;
   const int64_t q0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
@@ -795,7 +795,7 @@ __global__ __launch_bounds__(1024) void k_bb_de(const LmBBConst K, const uint8_t
   __shared__ int s_noscale, s_last, s_cnt;
   const int f = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, wave = tid >> 6;
   const int NC = K.n_cols, vy = K.view_y[0], vh = K.view_h[0];
-  const uint8_t* __restrict__ F = frame_ptr[f];
+  const lm_gu8* __restrict__ F = as_global(frame_ptr[f]);
   if (tid < 256) lut[tid] = luts[f * 256 + tid];
   for (int i = tid; i < 16 * 256; i += nt) (&hist[0][0])[i] = 0;
   for (int i = tid; i < NC; i += nt) colc[i] = 0;

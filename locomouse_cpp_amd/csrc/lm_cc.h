@@ -102,11 +102,19 @@ DEV int cc_row_of(const int* rowoff, int H, int i) {
   return lo - 1;
 }
 
+// Bit i (0..3) = byte i of w is nonzero: bit 7 of each byte set by
+// (w | ((w & 0x7F..) + 0x7F..)), then the four bits gathered by one multiply
+// (the partial products land on distinct bits, so nothing carries into 28-31).
+DEV unsigned cc_nonzero_bytes(unsigned w) {
+  const unsigned t = ((w | ((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu)) & 0x80808080u) >> 7;
+  return (t * 0x10204080u) >> 28;
+}
+
 // Bitmap of a u8 map (nonzero = foreground; H rows of W bytes at `pitch`)
 // into bm[y][0..nb64] (the last word of a row stays zero), optionally ANDed
 // with a column mask (colm[nb64] words, bit x = column x), and the number of
 // runs of each row into rowoff[y].  Every thread takes 16-column pieces of
-// any row, four pieces' loads in flight before any is used (16-byte loads when
+// any row, twelve pieces' loads in flight before any is used (16-byte loads when
 // `vec`: W % 16 == 0 and 16-byte aligned rows), so the map streams in at a
 // few load latencies instead of one per row; then one thread per row counts
 // the run starts.  Block-wide call (ends with a barrier).
@@ -114,16 +122,17 @@ DEV void cc_bitmap_u8(const uint8_t* __restrict__ src, int64_t pitch, int W, int
                       const unsigned long long* colm, unsigned long long* bm, int* rowoff) {
   const int npc = 4 * (nb64 + 1);  // 16-bit pieces per bitmap row (incl. the spare word)
   const int total = H * npc;
-  for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
-    uint4 q[4];
+  constexpr int U = 12;  // pieces per thread per round: a tail map is one or two load latencies
+  for (int e0 = 0; e0 < total; e0 += U * (int)blockDim.x) {
+    uint4 q[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
       const int y = e / npc, x = 16 * (e - y * npc);
       if (vec && e < total && x < W) q[u] = *reinterpret_cast<const uint4*>(src + (int64_t)y * pitch + x);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
       if (e >= total) continue;
       const int y = e / npc, pc = e - y * npc, x = 16 * pc;
@@ -132,7 +141,7 @@ DEV void cc_bitmap_u8(const uint8_t* __restrict__ src, int64_t pitch, int W, int
         if (vec) {
           const unsigned w4[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
 #pragma unroll
-          for (int k = 0; k < 16; ++k) m |= (((w4[k >> 2] >> (8 * (k & 3))) & 255u) ? 1u : 0u) << k;
+          for (int k = 0; k < 4; ++k) m |= cc_nonzero_bytes(w4[k]) << (4 * k);
         } else {
           const uint8_t* row = src + (int64_t)y * pitch;
           for (int k = 0; k < 16 && x + k < W; ++k) m |= (row[x + k] ? 1u : 0u) << k;
@@ -141,6 +150,36 @@ DEV void cc_bitmap_u8(const uint8_t* __restrict__ src, int64_t pitch, int W, int
       }
       reinterpret_cast<uint16_t*>(bm + (int64_t)y * (nb64 + 1))[pc] = (uint16_t)m;
     }
+  }
+  __syncthreads();
+  for (int y = threadIdx.x; y < H; y += blockDim.x) {
+    const unsigned long long* row = bm + (int64_t)y * (nb64 + 1);
+    unsigned long long carry = 0;
+    int n = 0;
+    for (int k = 0; k < nb64; ++k) {
+      const unsigned long long bits = row[k];
+      n += __popcll(bits & ~((bits << 1) | carry));
+      carry = bits >> 63;
+    }
+    rowoff[y] = n;
+  }
+  __syncthreads();
+}
+
+// The same staging from a bitmap already in memory (H rows of nb64 u64 words,
+// bit x = column x; k_corr writes the tail maps this way), optionally ANDed
+// with the column mask.  Block-wide call (ends with a barrier).
+DEV void cc_bitmap_bits(const unsigned long long* __restrict__ src, int H, int nb64, const unsigned long long* colm,
+                        unsigned long long* bm, int* rowoff) {
+  const int total = H * (nb64 + 1);
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int y = e / (nb64 + 1), k = e - y * (nb64 + 1);
+    unsigned long long w = 0;
+    if (k < nb64) {
+      w = src[(int64_t)y * nb64 + k];
+      if (colm) w &= colm[k];
+    }
+    bm[e] = w;
   }
   __syncthreads();
   for (int y = threadIdx.x; y < H; y += blockDim.x) {
@@ -166,23 +205,29 @@ template <bool G, class IX>
 DEV void cc_label(const CCRuns<IX> S, const unsigned long long* bm, int nb64, int W, int H, int R, const int* rowoff,
                   bool c8, unsigned long long* s_red, unsigned* s_best) {
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
-  const unsigned long long lt = (1ull << lane) - 1;
   const unsigned nbx = (unsigned)(W + 1) / 2;
   if (tid == 0) *s_best = 0xFFFFFFFFu;
-  for (int y = wave; y < H; y += nw) {
-    const unsigned long long* row = bm + (int64_t)y * (nb64 + 1);
-    int ns = rowoff[y], ne = rowoff[y];
-    unsigned long long carry = 0;
-    for (int k = 0; k < nb64; ++k) {
-      const unsigned long long bits = row[k], nxt = row[k + 1] & 1ull;  // wave-uniform
-      const unsigned long long st = bits & ~((bits << 1) | carry);
-      const unsigned long long en = bits & ~((bits >> 1) | (nxt << 63));
-      const int x = 64 * k + lane;
-      if ((st >> lane) & 1) rst<G>(&S.rs[ns + __popcll(st & lt)], (unsigned)x);
-      if ((en >> lane) & 1) rst<G>(&S.re[ne + __popcll(en & lt)], (unsigned)x);
-      ns += __popcll(st);
-      ne += __popcll(en);
-      carry = bits >> 63;
+  // Runs: one (row, word) per thread.  Runs are numbered in raster order, so
+  // the starts (ends) in word k of a row are numbered after the starts (ends)
+  // in the row's earlier words: popcounts of those words give the offsets.
+  {
+    const int items = H * nb64;
+    for (int e = tid; e < items; e += nt) {
+      const int y = e / nb64, k = e - y * nb64;
+      const unsigned long long* row = bm + (int64_t)y * (nb64 + 1);
+      const unsigned long long bits = row[k];
+      const unsigned long long prev = k ? row[k - 1] >> 63 : 0ull, nxt = row[k + 1] & 1ull;
+      unsigned long long st = bits & ~((bits << 1) | prev);
+      unsigned long long en = bits & ~((bits >> 1) | (nxt << 63));
+      if (!(st | en)) continue;
+      int ns = rowoff[y], ne = ns;
+      for (int q = 0; q < k; ++q) {
+        const unsigned long long b = row[q], pb = q ? row[q - 1] >> 63 : 0ull, nb = row[q + 1] & 1ull;
+        ns += __popcll(b & ~((b << 1) | pb));
+        ne += __popcll(b & ~((b >> 1) | (nb << 63)));
+      }
+      for (; st; st &= st - 1) rst<G>(&S.rs[ns++], (unsigned)(64 * k + __ffsll((long long)st) - 1));
+      for (; en; en &= en - 1) rst<G>(&S.re[ne++], (unsigned)(64 * k + __ffsll((long long)en) - 1));
     }
   }
   __syncthreads();  // the LDS union-find arrays overlay the bitmap

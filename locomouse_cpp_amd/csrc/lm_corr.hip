@@ -62,14 +62,28 @@ DEV void corr_epilogue(const LmConst& K, const LmDet& D, const float (&acc)[R_][
                        int* s_base, const uint8_t* __restrict__ msrc, int mpitch) {
   static_assert(R_ * C_ <= 32, "bitmask");
   if (D.kind != 0) {
-    uint8_t* __restrict__ tb = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
+    // the tile's bits gathered in LDS (rows of the <= 4 u32 words its LM_TW
+    // columns touch), then ORed into the slot's zeroed bitmap; neighbouring
+    // tiles share the boundary words
+    __shared__ unsigned s_tb[LM_TH * 4];
+    const int w0 = ox0 >> 5;
+    for (int i = threadIdx.x; i < LM_TH * 4; i += blockDim.x) s_tb[i] = 0u;
+    __syncthreads();
 #pragma unroll
     for (int r = 0; r < R_; ++r)
 #pragma unroll
       for (int c = 0; c < C_; ++c) {
         const int y = oy0 + ly * R_ + r, x = ox0 + lx * C_ + c;
-        if (y < D.oh && x < D.ow) tb[(int64_t)y * D.ow + x] = acc[r][c] > 0.0f ? 1 : 0;
+        if (y < D.oh && x < D.ow && acc[r][c] > 0.0f) atomicOr(&s_tb[(ly * R_ + r) * 4 + (x >> 5) - w0], 1u << (x & 31));
       }
+    __syncthreads();
+    unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(tailbin + (int64_t)slot * tailbin_slot_bytes) +
+                                (D.list ? (int64_t)K.tail_hb * K.tail_nw : 0);
+    for (int i = threadIdx.x; i < LM_TH * 4; i += blockDim.x) {
+      const unsigned v = s_tb[i];
+      const int y = oy0 + (i >> 2), gw = w0 + (i & 3);
+      if (v && y < D.oh && gw < K.tail_nw) atomicOr(&tb[(int64_t)y * K.tail_nw + gw], v);
+    }
     return;
   }
   unsigned bits = 0;
@@ -503,13 +517,18 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
 
   const int x = ox0 + 32 * wave + r;
   if (D.kind != 0) {
-    uint8_t* __restrict__ tb = tailbin + (int64_t)slot * tailbin_slot_bytes + (D.list ? (int64_t)K.tail_hb * K.tail_w : 0);
+    // bits straight from a ballot: this wave owns u32 word (ox0 / 32 + wave) of
+    // each of its rows (lanes 0-31: row y, lanes 32-63: row y + 4)
+    unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(tailbin + (int64_t)slot * tailbin_slot_bytes) +
+                                (D.list ? (int64_t)K.tail_hb * K.tail_nw : 0);
+    const int gw = (ox0 >> 5) + wave;
 #pragma unroll
     for (int t = 0; t < LM_F16_T; ++t)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int y = oy0 + 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (y < D.oh && x < D.ow) tb[(int64_t)y * D.ow + x] = acc[t][q] > 0.0f ? 1 : 0;
+        const unsigned long long m = __ballot(y < D.oh && x < D.ow && acc[t][q] > 0.0f);
+        if ((lane & 31) == 0 && y < D.oh && gw < K.tail_nw) tb[(int64_t)y * K.tail_nw + gw] = (unsigned)(m >> (32 * h));
       }
     return;
   }

@@ -64,6 +64,10 @@ struct LmConst {
   // tail
   int32_t tail_w, tail_hb, tail_hs;  // tail box width, bottom/side heights
   int32_t tail_cap, tail_ntc;        // k_tail: runs held in LDS, 32-column tiles per segment
+  // tail detector maps (filter2D > 0) as bitmaps, bottom then side per slot:
+  // rows of tail_nw u32 words (tail_nw = 2 * ceil(tail_w / 64), so a row is
+  // also ceil(tail_w / 64) u64 words); set by k_corr, zeroed by k_ingest
+  int32_t tail_nw, tail_bm_words;
   int32_t connectivity;
   // per-list capacities (= output area) and list offsets inside a slot's key area
   int32_t list_cap[LM_NLIST];

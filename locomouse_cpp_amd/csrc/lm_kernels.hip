@@ -30,9 +30,20 @@
 
 #define DEV __device__ __forceinline__
 
+// Frame pointers come from a device array (frame_ptr), so the compiler cannot
+// tell that they point to global memory and would access the frames with FLAT
+// instructions (longer latency, and they hold the LDS counter too); the casts
+// below make those accesses global_load_*.
+typedef __attribute__((address_space(1))) const uint8_t lm_gu8;
+typedef __attribute__((address_space(1))) const uint32_t lm_gu32;
+typedef unsigned lm_u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const lm_u32x4 lm_gu4;
+DEV const lm_gu8* as_global(const uint8_t* p) { return (const lm_gu8*)p; }
+
 // ------------------------------------------------------------------ helpers
 
-DEV uint8_t ipad_pixel(const uint8_t* __restrict__ F, const uint8_t* __restrict__ bkg,
+template <class FP>
+DEV uint8_t ipad_pixel(FP __restrict__ F, const uint8_t* __restrict__ bkg,
                        const int32_t* __restrict__ cal, const uint8_t* lut, const LmConst& K, int R, int C) {
   // I_PAD(R, C): zero outside I_UNPAD (:684-689); inside, the corrected,
   // normalised, optionally flipped frame.
@@ -57,11 +68,11 @@ __global__ __launch_bounds__(LM_MM_THREADS) void k_minmax(const uint8_t* const* 
                                                           const uint8_t* __restrict__ bkg, int npix, int s0,
                                                           unsigned* __restrict__ mm) {
   const int slot = s0 + blockIdx.y;
-  const uint8_t* __restrict__ F = frame_ptr[slot];
+  const lm_gu8* __restrict__ F = as_global(frame_ptr[slot]);
   const int nvec = npix >> 4;
   const int per = (nvec + LM_MM_SPLIT - 1) / LM_MM_SPLIT;
   const int v0 = blockIdx.x * per, v1 = min(nvec, v0 + per);
-  const uint4* F4 = reinterpret_cast<const uint4*>(F);
+  const lm_gu4* F4 = reinterpret_cast<const lm_gu4*>(F);
   const uint4* B4 = reinterpret_cast<const uint4*>(bkg);
   unsigned mn = 255, mx = 0;
   auto fold = [&](unsigned fw, unsigned bw) {
@@ -75,7 +86,8 @@ __global__ __launch_bounds__(LM_MM_THREADS) void k_minmax(const uint8_t* const* 
   };
   int i = v0 + threadIdx.x;
   for (; i + 3 * LM_MM_THREADS < v1; i += 4 * LM_MM_THREADS) {  // four 16-byte loads in flight per lane
-    uint4 f[4], b[4];
+    lm_u32x4 f[4];
+    uint4 b[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       f[u] = F4[i + u * LM_MM_THREADS];
@@ -90,7 +102,8 @@ __global__ __launch_bounds__(LM_MM_THREADS) void k_minmax(const uint8_t* const* 
     }
   }
   for (; i < v1; i += LM_MM_THREADS) {
-    const uint4 f = F4[i], b = B4[i];
+    const lm_u32x4 f = F4[i];
+    const uint4 b = B4[i];
     fold(f.x, b.x);
     fold(f.y, b.y);
     fold(f.z, b.z);
@@ -170,7 +183,8 @@ DEV bool in_gray_rect(const LmConst& K, const LmSlot& sl, int R, int C) {
   return (unsigned)y < (unsigned)K.bb_bottom_h && (unsigned)x < (unsigned)K.bb_bottom_w;
 }
 
-DEV uint8_t ipad_pixel_t(const uint8_t* __restrict__ F, const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+template <class FP>
+DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
                          const uint8_t* lut, const LmConst& K, const LmSlot& sl, int R, int C) {
   const uint8_t v = ipad_pixel(F, bkg, cal, lut, K, R, C);
   return K.gray_lut_on && in_gray_rect(K, sl, R, C) ? K.gray_lut[v] : v;
@@ -192,10 +206,21 @@ DEV uint8_t ipad_pixel_t(const uint8_t* __restrict__ F, const uint8_t* __restric
 __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
                                                 const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
                                                 const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
-                                                int s0, int s_end, uint8_t* __restrict__ ext, int64_t ext_slot_bytes) {
+                                                int s0, int s_end, uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                unsigned ext_blocks, unsigned* __restrict__ tailbm) {
   const LmConst& K = *Kp;
   const int sb = s0 + blockIdx.y * LM_INGEST_FB;
   const int nf = min(LM_INGEST_FB, s_end - sb);
+  if (blockIdx.x >= ext_blocks) {  // zero the group's tail bitmaps (k_corr ORs the tail detectors' bits in)
+    const int w = 4 * ((blockIdx.x - ext_blocks) * blockDim.x + threadIdx.x);
+    for (int f = 0; f < nf; ++f) {
+      unsigned* __restrict__ t = tailbm + (int64_t)(sb + f) * K.tail_bm_words;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (w + u < K.tail_bm_words) t[w + u] = 0u;
+    }
+    return;
+  }
   __shared__ uint8_t lut[LM_INGEST_FB][256];
   __shared__ uint8_t glut[256];
   for (int i = threadIdx.x; i < nf * 256; i += blockDim.x) lut[i >> 8][i & 255] = luts[(sb + (i >> 8)) * 256 + (i & 255)];
@@ -212,54 +237,50 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
   int idx[LM_INGEST_VEC];
   uint8_t bv[LM_INGEST_VEC];
   int run = 0;  // 1: idx[k] = idx[0] + k, -1: idx[k] = idx[0] - k, 0: gather
-  int px = INT32_MIN, py = INT32_MIN;
-  for (int f = 0; f < nf; ++f) {
-    const int slot = sb + f;
-    const LmSlot sl = slots[slot];
-    const int R = sl.crop_y[v] + K.ext_oy[v] + er;
-    const int C0 = sl.crop_x[v] + K.ext_ox[v] + ec;
-    if (sl.crop_x[v] != px || sl.crop_y[v] != py) {  // crop moved: recompute the gather indices
-      px = sl.crop_x[v];
-      py = sl.crop_y[v];
-      const int r = R - K.pad_pre_rows;
-      bool up = true, down = true;
+  // gather indices and background of this thread's 16 pixels for a crop at (cx, cy)
+  auto locate = [&](int R, int C0) {
+    const int r = R - K.pad_pre_rows;
+    bool up = true, down = true;
 #pragma unroll
-      for (int k = 0; k < LM_INGEST_VEC; ++k) {
-        int c = C0 + k - K.pad_pre_cols;
-        if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) {
-          idx[k] = -1;
-          bv[k] = 0;
-        } else {
-          if (K.flip) c = K.n_cols - 1 - c;
-          idx[k] = cal[r * K.n_cols + c];
-          bv[k] = bkg[idx[k]];
-        }
-        up = up && idx[k] >= 0 && idx[k] == idx[0] + k;
-        down = down && idx[k] >= 0 && idx[k] == idx[0] - k;
+    for (int k = 0; k < LM_INGEST_VEC; ++k) {
+      int c = C0 + k - K.pad_pre_cols;
+      if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) {
+        idx[k] = -1;
+        bv[k] = 0;
+      } else {
+        if (K.flip) c = K.n_cols - 1 - c;
+        idx[k] = cal[r * K.n_cols + c];
+        bv[k] = bkg[idx[k]];
       }
-      run = up ? 1 : (down ? -1 : 0);
-      const int lo = up ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
-      if (run != 0 && (lo & ~3) + 20 > K.video_rows * K.video_cols) run = 0;  // the fifth dword would pass the frame end
+      up = up && idx[k] >= 0 && idx[k] == idx[0] + k;
+      down = down && idx[k] >= 0 && idx[k] == idx[0] - k;
     }
-    const uint8_t* __restrict__ F = frame_ptr[slot];
-    uint8_t pix[LM_INGEST_VEC];
-    if (run != 0) {
-      // the 16 source bytes span [lo, lo + 16): five aligned dwords cover them
-      const int lo = run > 0 ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(F + (lo & ~3));
-      uint32_t d[5];
+    run = up ? 1 : (down ? -1 : 0);
+    const int lo = up ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
+    if (run != 0 && (lo & ~3) + 20 > K.video_rows * K.video_cols) run = 0;  // the fifth dword would pass the frame end
+  };
+  // the 16 source bytes of a run span [lo, lo + 16): five aligned dwords cover them
+  // (funnel shifts by the byte offset, then a byte reversal for a flipped run:
+  // no register array is indexed with a run-time value, so nothing spills)
+  auto run_bytes = [&](const uint32_t (&d)[5], uint8_t (&pix)[LM_INGEST_VEC]) {
+    const int lo = run > 0 ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
+    const unsigned sh = (unsigned)(lo & 3);
+    uint32_t w[4];
 #pragma unroll
-      for (int u = 0; u < 5; ++u) d[u] = w[u];
-      const int sh = lo & 3;
-#pragma unroll
-      for (int k = 0; k < LM_INGEST_VEC; ++k) {
-        const int o = sh + (run > 0 ? k : LM_INGEST_VEC - 1 - k);
-        pix[k] = (uint8_t)(d[o >> 2] >> (8 * (o & 3)));
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < LM_INGEST_VEC; ++k) pix[k] = idx[k] >= 0 ? F[idx[k]] : 0;
+    for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+    if (run < 0) {
+      const uint32_t r0 = __builtin_bswap32(w[3]), r1 = __builtin_bswap32(w[2]), r2 = __builtin_bswap32(w[1]),
+                     r3 = __builtin_bswap32(w[0]);
+      w[0] = r0;
+      w[1] = r1;
+      w[2] = r2;
+      w[3] = r3;
     }
+#pragma unroll
+    for (int k = 0; k < LM_INGEST_VEC; ++k) pix[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  };
+  // background subtraction, the slot's LUT, the grey LUT and the 16-byte store
+  auto emit = [&](int f, const uint8_t (&pix)[LM_INGEST_VEC], const LmSlot& sl, int R, int C0) {
     uint32_t word[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < LM_INGEST_VEC; ++k) {
@@ -272,7 +293,65 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
       }
       word[k >> 2] |= o << (8 * (k & 3));
     }
-    *reinterpret_cast<uint4*>(ext + (int64_t)slot * ext_slot_bytes + q) = make_uint4(word[0], word[1], word[2], word[3]);
+    *reinterpret_cast<uint4*>(ext + (int64_t)(sb + f) * ext_slot_bytes + q) = make_uint4(word[0], word[1], word[2], word[3]);
+  };
+
+  // Common case: every slot of the group has its crop at the same place (a
+  // provided bounding box) and the pixels are a run: all the group's frame
+  // loads are issued before any is used, so the group costs one load latency.
+  const LmSlot sl0 = slots[sb];
+  bool same = true;
+  for (int f = 1; f < nf; ++f)
+    same = same && slots[sb + f].crop_x[v] == sl0.crop_x[v] && slots[sb + f].crop_y[v] == sl0.crop_y[v];
+  {
+    const int R = sl0.crop_y[v] + K.ext_oy[v] + er, C0 = sl0.crop_x[v] + K.ext_ox[v] + ec;
+    locate(R, C0);
+    if (same && run != 0) {
+      const int lo = run > 0 ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
+      uint32_t d[LM_INGEST_FB][5];
+#pragma unroll
+      for (int f = 0; f < LM_INGEST_FB; ++f)
+        if (f < nf) {
+          const lm_gu32* w = reinterpret_cast<const lm_gu32*>(as_global(frame_ptr[sb + f]) + (lo & ~3));
+#pragma unroll
+          for (int u = 0; u < 5; ++u) d[f][u] = w[u];
+        }
+#pragma unroll
+      for (int f = 0; f < LM_INGEST_FB; ++f)
+        if (f < nf) {
+          uint8_t pix[LM_INGEST_VEC];
+          run_bytes(d[f], pix);
+          emit(f, pix, slots[sb + f], R, C0);
+        }
+      return;
+    }
+  }
+  // General case: frame by frame, the indices recomputed whenever the crop moves.
+  int px = sl0.crop_x[v], py = sl0.crop_y[v];
+  for (int f = 0; f < nf; ++f) {
+    const int slot = sb + f;
+    const LmSlot sl = slots[slot];
+    const int R = sl.crop_y[v] + K.ext_oy[v] + er;
+    const int C0 = sl.crop_x[v] + K.ext_ox[v] + ec;
+    if (sl.crop_x[v] != px || sl.crop_y[v] != py) {  // crop moved: recompute the gather indices
+      px = sl.crop_x[v];
+      py = sl.crop_y[v];
+      locate(R, C0);
+    }
+    const lm_gu8* __restrict__ F = as_global(frame_ptr[slot]);
+    uint8_t pix[LM_INGEST_VEC];
+    if (run != 0) {
+      const int lo = run > 0 ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
+      const lm_gu32* w = reinterpret_cast<const lm_gu32*>(F + (lo & ~3));
+      uint32_t d[5];
+#pragma unroll
+      for (int u = 0; u < 5; ++u) d[u] = w[u];
+      run_bytes(d, pix);
+    } else {
+#pragma unroll
+      for (int k = 0; k < LM_INGEST_VEC; ++k) pix[k] = idx[k] >= 0 ? F[idx[k]] : 0;
+    }
+    emit(f, pix, sl, R, C0);
   }
 }
 
@@ -419,8 +498,13 @@ DEV void tail_side_moments(const CCRuns<IX> S, int R, const int* rowoff, int H, 
 __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restrict__ Kp, int s0,
                                                           const uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
                                                           unsigned long long* __restrict__ tailmask,
-                                                          unsigned* __restrict__ scratch, LmSlotOut* __restrict__ hdr) {
+                                                          unsigned* __restrict__ scratch, LmSlotOut* __restrict__ hdr,
+                                                          long long* __restrict__ prof) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smt[];
+#define TAIL_PROF(k) \
+  if (prof && threadIdx.x == 0) prof[blockIdx.x * 16 + (k)] = clock64();
+  TAIL_PROF(0)
+  if (prof && threadIdx.x == 0) prof[blockIdx.x * 16 + 14] = wall_clock64();
   const LmConst& K = *Kp;
   const int slot = s0 + blockIdx.x;
   const int TW = K.tail_w, HB = K.tail_hb, HS = K.tail_hs, nb64 = (TW + 63) / 64;
@@ -446,9 +530,9 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
   const int tid = threadIdx.x, nt = blockDim.x;
   const bool c8 = K.connectivity == 8;
   const bool lds_ok = TW <= 65535;
-  const uint8_t* __restrict__ binb = tailbin + (int64_t)slot * tailbin_slot_bytes;
-  const uint8_t* __restrict__ bins = binb + (int64_t)HB * TW;
-  const bool vec = (TW & 15) == 0 && (tailbin_slot_bytes & 15) == 0;
+  const unsigned long long* __restrict__ binb =
+      reinterpret_cast<const unsigned long long*>(tailbin + (int64_t)slot * tailbin_slot_bytes);
+  const unsigned long long* __restrict__ bins = binb + (int64_t)HB * nb64;
 
   for (int i = tid; i < TW + 2; i += nt) colc[i] = 0;
   for (int i = tid; i < HB * nb64; i += nt) mask[i] = 0;
@@ -460,13 +544,16 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
   }
 
   // ---- bottom: largest component, TAIL_MASK, column mask, segment moments
-  cc_bitmap_u8(binb, TW, TW, HB, nb64, vec, nullptr, bm, rowoff);
+  cc_bitmap_bits(binb, HB, nb64, nullptr, bm, rowoff);
+  TAIL_PROF(1)
   cc_wave0_scan(rowoff, HB, &s_total);
   int R = s_total;
+  TAIL_PROF(2)
   const bool gb_b = !(lds_ok && R <= cap);
   if (!gb_b) cc_label<false>(SL, bm, nb64, TW, HB, R, rowoff, c8, s_red, &s_best);
   else cc_label<true>(SG, bm, nb64, TW, HB, R, rowoff, c8, s_red, &s_best);
   const unsigned best_b = s_best;
+  TAIL_PROF(3)
   const bool have = best_b != 0xFFFFFFFFu;
   if (have) {
     if (!gb_b) tail_bottom_runs<false>(SL, R, rowoff, HB, best_b, nb64, mask, colc, &s_first, &s_last);
@@ -497,17 +584,20 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
     }
   }
   __syncthreads();
+  TAIL_PROF(4)
   unsigned long long* __restrict__ tm = tailmask + (int64_t)slot * HB * nb64;
   for (int i = tid; i < HB * nb64; i += nt) tm[i] = mask[i];
 
   // ---- side: (tail_s > 0) & repeat(colmax) -> largest component
-  cc_bitmap_u8(bins, TW, TW, HS, nb64, vec, colm, bm, rowoff);
+  cc_bitmap_bits(bins, HS, nb64, colm, bm, rowoff);
+  TAIL_PROF(5)
   cc_wave0_scan(rowoff, HS, &s_total);
   R = s_total;
   const bool gb_s = !(lds_ok && R <= cap);
   if (!gb_s) cc_label<false>(SL, bm, nb64, TW, HS, R, rowoff, c8, s_red, &s_best);
   else cc_label<true>(SG, bm, nb64, TW, HS, R, rowoff, c8, s_red, &s_best);
   const unsigned best_s = s_best;
+  TAIL_PROF(6)
 
   // track x, y per segment (moments of the bottom component, :2702-2725)
   if (tid < LM_TAIL_SEGS) {
@@ -540,11 +630,13 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
     hdr[slot].tail[LM_TAIL_SEGS + i] = ty_;
   }
   __syncthreads();
+  TAIL_PROF(7)
   if (best_s != 0xFFFFFFFFu) {
     if (!gb_s) tail_side_moments<false>(SL, R, rowoff, HS, best_s, s_tx, ms, ntrs);
     else tail_side_moments<true>(SG, R, rowoff, HS, best_s, s_tx, ms, ntrs);
   }
   __syncthreads();
+  TAIL_PROF(8)
   // track z (:2728-2737): the side moments of column x_i when x_i > 0
   if (tid < LM_TAIL_SEGS) {
     const int i = tid;
@@ -563,6 +655,12 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
     }
     hdr[slot].tail[2 * LM_TAIL_SEGS + i] = tz;
   }
+  if (prof && threadIdx.x == 0) {
+    prof[blockIdx.x * 16 + 9] = clock64();
+    prof[blockIdx.x * 16 + 13] = R;
+    prof[blockIdx.x * 16 + 15] = wall_clock64();
+  }
+#undef TAIL_PROF
 }
 
 // ------------------------------------------------------------------- k_nms
@@ -830,53 +928,25 @@ DEV double readlane_f64(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
-__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
-                                                       const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
-                                                       unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
-                                                       LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
-                                                       long long* __restrict__ prof) {
-  const LmConst& K = *Kp;
-  const int slot = s0 + blockIdx.x;
-  const int feat = blockIdx.y;  // 0 paw, 1 snout
-  // optional phase timestamps (LM_KPROF=1): clock64() of thread 0 per phase
+// The body of k_nms on its working arrays: LDS (GLOB = false, every access a
+// ds_* instruction) or per-block global scratch for lists above LM_NMS_CAP.
+// Kept as two instantiations so the common case never goes through generic
+// (FLAT) pointers, which cost several times the latency of LDS accesses.
+// optional phase timestamps (LM_KPROF=1): clock64() of thread 0 per phase
 #define NMS_PROF(k) \
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = clock64();
-  NMS_PROF(0)
-  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 14] = wall_clock64();
-  const int list = side ? 2 + feat : feat;
-  const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
-  const LmDet D = K.det[det];
-  LmSlotOut* H = hdr + slot;
-  __shared__ unsigned long long s_keys[LM_NMS_CAP];
-  __shared__ int s_assign[LM_NMS_CAP], s_mlist[LM_NMS_CAP];
-  __shared__ unsigned s_xy[LM_NMS_CAP + 16];
-  __shared__ int s_tmp[LM_NMS_CAP];
-  __shared__ int s_stk[lm_sort::kStackInts];
-  __shared__ int s_wsum[LM_NMS_THREADS / 64 + 1];
-  __shared__ int s_n, s_flag, s_qcnt[2];
-
-  if (side && H->cand_cnt[feat] == 0) {  // detectSideCandidates skips (:820-833)
-    if (threadIdx.x == 0) {
-      H->n_pos[list] = 0;
-      H->cand_cnt[list] = 0;
-      H->ties[list] = 0;
-    }
-    return;
-  }
-  const int n_in = n_pos[slot * LM_NLIST + list];
-  const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
-  unsigned long long* a = s_keys;
-  int* assign = s_assign;
-  int* mlist = s_mlist;
-  unsigned* xy = s_xy;
-  const bool glob = n_in > LM_NMS_CAP;
-  if (glob) {  // rare: most of the crop positive; same algorithm in global scratch
-    const int64_t npg = gscratch_slot / 3;
-    a = gscratch + (int64_t)(blockIdx.y + 2 * blockIdx.x) * gscratch_slot;
-    assign = reinterpret_cast<int*>(a + npg);
-    mlist = assign + npg;
-    xy = reinterpret_cast<unsigned*>(mlist + npg);
-  }
+template <bool GLOB>
+DEV void nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int list, int side, int feat, int n_in,
+                 const unsigned long long* __restrict__ src, const unsigned long long* __restrict__ tailmask,
+                 unsigned long long* a, int* assign, int* mlist, unsigned* xy, int* s_tmp, int* s_stk, int* s_wsum,
+                 int* s_n_, int* s_flag_, int* s_qcnt, unsigned long long* __restrict__ keys, int32_t* __restrict__ err,
+                 long long* __restrict__ prof) {
+  int& s_n = *s_n_;
+  int& s_flag = *s_flag_;
+  constexpr bool glob = GLOB;
+  int* s_assign = assign;
+  int* s_mlist = mlist;
+  unsigned* s_xy = xy;
   if (threadIdx.x == 0) {
     s_n = 0;
     s_flag = 0;
@@ -913,7 +983,7 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
     if ((a[k] >> 32) == (a[k + 1] >> 32)) s_flag = 1;
   __syncthreads();
   const int tie = s_flag;
-  if (tie) {
+  if (tie) {  // (GLOB: the row-major re-sort below is the single-thread replica)
     // exact score tie: std::sort from the row-major order nmsMax builds (:1638-1648)
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
       const unsigned long long v = a[k];
@@ -1081,6 +1151,53 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
     H->cand_cnt[list] = fits ? ncand : 0;
     H->ties[list] = tie;
   }
+}
+
+__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
+                                                       const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
+                                                       unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
+                                                       LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
+                                                       long long* __restrict__ prof) {
+  const LmConst& K = *Kp;
+  const int slot = s0 + blockIdx.x;
+  const int feat = blockIdx.y;  // 0 paw, 1 snout
+  NMS_PROF(0)
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 14] = wall_clock64();
+  const int list = side ? 2 + feat : feat;
+  const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
+  const LmDet D = K.det[det];
+  LmSlotOut* H = hdr + slot;
+  // 16-byte aligned: rank_sort and the nmsMax sweep read them with ds_read_b128
+  __shared__ __attribute__((aligned(16))) unsigned long long s_keys[LM_NMS_CAP];
+  __shared__ __attribute__((aligned(16))) int s_assign[LM_NMS_CAP];
+  __shared__ int s_mlist[LM_NMS_CAP];
+  __shared__ __attribute__((aligned(16))) unsigned s_xy[LM_NMS_CAP + 16];
+  __shared__ int s_tmp[LM_NMS_CAP];
+  __shared__ int s_stk[lm_sort::kStackInts];
+  __shared__ int s_wsum[LM_NMS_THREADS / 64 + 1];
+  __shared__ int s_n, s_flag, s_qcnt[2];
+
+  if (side && H->cand_cnt[feat] == 0) {  // detectSideCandidates skips (:820-833)
+    if (threadIdx.x == 0) {
+      H->n_pos[list] = 0;
+      H->cand_cnt[list] = 0;
+      H->ties[list] = 0;
+    }
+    return;
+  }
+  const int n_in = n_pos[slot * LM_NLIST + list];
+  const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
+  if (n_in <= LM_NMS_CAP)
+    nms_run<false>(K, D, H, slot, list, side, feat, n_in, src, tailmask, s_keys, s_assign, s_mlist, s_xy, s_tmp, s_stk,
+                   s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
+  else {  // rare: most of the crop positive; same algorithm in global scratch
+    const int64_t npg = gscratch_slot / 3;
+    unsigned long long* a = gscratch + (int64_t)(blockIdx.y + 2 * blockIdx.x) * gscratch_slot;
+    int* assign = reinterpret_cast<int*>(a + npg);
+    int* mlist = assign + npg;
+    nms_run<true>(K, D, H, slot, list, side, feat, n_in, src, tailmask, a, assign, mlist,
+                  reinterpret_cast<unsigned*>(mlist + npg), s_tmp, s_stk, s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
+  }
 #undef NMS_PROF
 }
 
@@ -1089,7 +1206,8 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
 #define LM_POST_MAXC 512     // candidates per list handled in LDS
 #define LM_POST_MAXOFF 2048  // CSC columns (Ni + Nong) + 1
 
-DEV bool vel_criterion(const LmConst& K, const uint8_t* Fc, const uint8_t* Fp, const uint8_t* bkg, const int32_t* cal,
+template <class FP>
+DEV bool vel_criterion(const LmConst& K, FP Fc, FP Fp, const uint8_t* bkg, const int32_t* cal,
                        const uint8_t* lutc, const uint8_t* lutp, const LmSlot& slc, const LmSlot& slp, int crop_x,
                        int crop_y, int crop_w, int crop_h,
                        int bx, int by, int bwid, int bhei, int area, double alpha, int32_t* err, int tag) {
@@ -1119,40 +1237,20 @@ DEV bool vel_criterion(const LmConst& K, const uint8_t* Fc, const uint8_t* Fp, c
   return (double)sum >= ((double)area) * alpha;
 }
 
-__global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restrict__ Kp, const LmSlot* __restrict__ slots,
-                                                         const uint8_t* const* __restrict__ frame_ptr,
-                                                         const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
-                                                         const uint8_t* __restrict__ luts, LmSlotOut* __restrict__ hdr,
-                                                         const unsigned long long* __restrict__ keys, LmP22D* __restrict__ arena_p22d,
-                                                         int32_t* __restrict__ arena_side_y, double* __restrict__ arena_side_s,
-                                                         double* __restrict__ arena_unary, int32_t* __restrict__ arena_jc,
-                                                         int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
-                                                         LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err) {
-  const LmConst& K = *Kp;
-  const int slot = 1 + blockIdx.x;
-  const int feat = blockIdx.y;
-  LmSlotOut* H = hdr + slot;
-  const LmSlotOut* HP = hdr + slot - 1;
-  const int frame = slots[slot].frame;
-  __shared__ LmCand sb[LM_POST_MAXC], st[LM_POST_MAXC], sp[LM_POST_MAXC];
-  __shared__ int s_off[LM_POST_MAXOFF];
-  __shared__ int s_mb[LM_POST_MAXC], s_mt[LM_POST_MAXC];  // motion status (-1 unknown)
-  __shared__ float s_bps[LM_POST_MAXC], s_tpb[LM_POST_MAXC];
-  __shared__ int s_all_equal, s_any1, s_any0, s_base[4];
-  const int Nb = H->cand_cnt[feat], Ns = H->cand_cnt[2 + feat];
-  const int Ni = frame > 0 ? HP->cand_cnt[feat] : 0;
-  if (Nb > LM_POST_MAXC || Ns > LM_POST_MAXC || Ni > LM_POST_MAXC || Ni + K.ong_nx * K.ong_ny + 1 > LM_POST_MAXOFF) {
-    if (threadIdx.x == 0) atomicOr(err, 8);
-    return;
-  }
-  const LmCand* cb = LM_CAND_STAGE(K, keys, slot, feat);
-  const LmCand* ct = LM_CAND_STAGE(K, keys, slot, 2 + feat);
-  const LmCand* cp = LM_CAND_STAGE(K, keys, slot - 1, feat);
-  for (int k = threadIdx.x; k < Nb; k += blockDim.x) sb[k] = cb[k];
-  for (int k = threadIdx.x; k < Ns; k += blockDim.x) st[k] = ct[k];
-  for (int k = threadIdx.x; k < Ni; k += blockDim.x) sp[k] = cp[k];
-  __syncthreads();
-
+// The body of k_post on its working arrays: candidate copies and per-list
+// state in LDS (G = false), or, for lists beyond the LDS capacity, the staged
+// candidate lists themselves and per-block global scratch (G = true; the
+// reference has no size limit).  Two instantiations, so the common case stays
+// on ds_* instructions.
+template <bool G>
+DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint8_t* const* __restrict__ frame_ptr,
+                  const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal, const uint8_t* __restrict__ luts,
+                  LmSlotOut* H, int slot, int feat, int frame, int Nb, int Ns, int Ni, const LmCand* sb,
+                  const LmCand* st, const LmCand* sp, int* s_off, int* s_mb, int* s_mt, float* s_bps, float* s_tpb,
+                  int cap, int* s_base, int& s_any1, int& s_any0, LmP22D* __restrict__ arena_p22d,
+                  int32_t* __restrict__ arena_side_y, double* __restrict__ arena_side_s, double* __restrict__ arena_unary,
+                  int32_t* __restrict__ arena_jc, int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
+                  LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err) {
   // ---------------- unary (unaryCostBox :1909-1952), column-major Nb x nprior
   const int nprior = feat == 0 ? 4 : 1;
   const int p0 = feat == 0 ? 0 : 4;
@@ -1299,7 +1397,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restr
     s_any1 = 0;
     s_any0 = 0;
   }
-  for (int k = threadIdx.x; k < LM_POST_MAXC; k += blockDim.x) {
+  for (int k = threadIdx.x; k < cap; k += blockDim.x) {
     s_mb[k] = -1;
     s_mt[k] = -1;
     s_bps[k] = 0.f;
@@ -1327,8 +1425,8 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restr
   __syncthreads();
   // motion status where the reference evaluates it
   const LmSlot sl = slots[slot], slp = slots[slot - 1];
-  const uint8_t* Fc = frame_ptr[slot];
-  const uint8_t* Fp = frame_ptr[slot - 1];
+  const lm_gu8* Fc = as_global(frame_ptr[slot]);
+  const lm_gu8* Fp = as_global(frame_ptr[slot - 1]);
   const uint8_t* lutc = luts + slot * 256;
   const uint8_t* lutp = luts + (slot - 1) * 256;
   const int* mbox = K.match_b[feat];
@@ -1431,6 +1529,61 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restr
     H->p22d_cnt[feat] = Nb;
     H->side_off[feat] = bs;
     H->side_cnt[feat] = s_off[Nb];
+  }
+}
+
+
+__global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restrict__ Kp, const LmSlot* __restrict__ slots,
+                                                         const uint8_t* const* __restrict__ frame_ptr,
+                                                         const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+                                                         const uint8_t* __restrict__ luts, LmSlotOut* __restrict__ hdr,
+                                                         const unsigned long long* __restrict__ keys, LmP22D* __restrict__ arena_p22d,
+                                                         int32_t* __restrict__ arena_side_y, double* __restrict__ arena_side_s,
+                                                         double* __restrict__ arena_unary, int32_t* __restrict__ arena_jc,
+                                                         int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
+                                                         LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err,
+                                                         unsigned long long* __restrict__ gscratch, int64_t gscratch_slot) {
+  const LmConst& K = *Kp;
+  const int slot = 1 + blockIdx.x;
+  const int feat = blockIdx.y;
+  LmSlotOut* H = hdr + slot;
+  const LmSlotOut* HP = hdr + slot - 1;
+  const int frame = slots[slot].frame;
+  __shared__ LmCand sb[LM_POST_MAXC], st[LM_POST_MAXC], sp[LM_POST_MAXC];
+  __shared__ int s_off[LM_POST_MAXOFF];
+  __shared__ int s_mb[LM_POST_MAXC], s_mt[LM_POST_MAXC];  // motion status (-1 unknown)
+  __shared__ float s_bps[LM_POST_MAXC], s_tpb[LM_POST_MAXC];
+  __shared__ int s_all_equal, s_any1, s_any0, s_base[4];
+  (void)s_all_equal;
+  const int Nb = H->cand_cnt[feat], Ns = H->cand_cnt[2 + feat];
+  const int Ni = frame > 0 ? HP->cand_cnt[feat] : 0;
+  const int Nong = K.ong_nx * K.ong_ny;
+  const LmCand* cb = LM_CAND_STAGE(K, keys, slot, feat);
+  const LmCand* ct = LM_CAND_STAGE(K, keys, slot, 2 + feat);
+  const LmCand* cp = LM_CAND_STAGE(K, keys, slot - 1, feat);
+  if (Nb <= LM_POST_MAXC && Ns <= LM_POST_MAXC && Ni <= LM_POST_MAXC && Ni + Nong + 1 <= LM_POST_MAXOFF) {
+    for (int k = threadIdx.x; k < Nb; k += blockDim.x) sb[k] = cb[k];
+    for (int k = threadIdx.x; k < Ns; k += blockDim.x) st[k] = ct[k];
+    for (int k = threadIdx.x; k < Ni; k += blockDim.x) sp[k] = cp[k];
+    __syncthreads();
+    post_run<false>(K, slots, frame_ptr, bkg, cal, luts, H, slot, feat, frame, Nb, Ns, Ni, sb, st, sp, s_off, s_mb, s_mt,
+                    s_bps, s_tpb, LM_POST_MAXC, s_base, s_any1, s_any0, arena_p22d, arena_side_y, arena_side_s,
+                    arena_unary, arena_jc, arena_ir, arena_pr, ctl, err);
+  } else {  // long lists: k_nms's scratch of this (slot, feature) is free again
+    const int big = max(max(Nb, Ns), Ni);
+    int* g = reinterpret_cast<int*>(gscratch + (int64_t)(feat + 2 * blockIdx.x) * gscratch_slot);
+    int* g_off = g;                      // max(Ni + Nong, Nb) + 1
+    int* g_mb = g_off + max(Ni + Nong, Nb) + 1;
+    int* g_mt = g_mb + big;
+    float* g_bps = reinterpret_cast<float*>(g_mt + big);
+    float* g_tpb = g_bps + big;
+    if ((int64_t)(reinterpret_cast<int*>(g_tpb + big) - g) > 2 * gscratch_slot) {  // the host sizes the scratch for it
+      if (threadIdx.x == 0) atomicOr(err, 8);
+      return;
+    }
+    post_run<true>(K, slots, frame_ptr, bkg, cal, luts, H, slot, feat, frame, Nb, Ns, Ni, cb, ct, cp, g_off, g_mb, g_mt,
+                   g_bps, g_tpb, big, s_base, s_any1, s_any0, arena_p22d, arena_side_y, arena_side_s, arena_unary,
+                   arena_jc, arena_ir, arena_pr, ctl, err);
   }
 }
 

@@ -567,7 +567,9 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
 
   // per-slot sizes
   c->ext_slot_bytes = ((int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1] + 255) / 256 * 256;
-  c->tailbin_slot_bytes = (int64_t)(K.tail_hb + K.tail_hs) * K.tail_w;
+  K.tail_nw = 2 * ((K.tail_w + 63) / 64);
+  K.tail_bm_words = (K.tail_hb + K.tail_hs) * K.tail_nw;
+  c->tailbin_slot_bytes = (int64_t)K.tail_bm_words * 4;
   int64_t doff = 0;
   for (int d = 0; d < 6; ++d) {
     c->dbg_off[d] = doff;
@@ -576,7 +578,10 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->dbg_slot_floats = doff;
   int np = 1;
   while (np < std::max(K.list_cap[0], K.list_cap[2])) np <<= 1;
-  c->gscratch_slot = 3 * (int64_t)np;  // keys (u64) + assign, cluster list, xy (32-bit) per entry
+  // per (slot, feature): k_nms's keys (u64) + assign, cluster list, xy (32-bit)
+  // per entry; then reused by k_post for lists beyond its LDS capacity
+  // (offsets np + Nong + 1, motion flags 2 np, counts 2 np: 32-bit each)
+  c->gscratch_slot = std::max(3 * (int64_t)np, (5 * (int64_t)np + K.ong_nx * K.ong_ny + 2) / 2 + 1);
   c->unfused = su->filter_arith == LM_FILTER_UNFUSED;
   if (const char* v = getenv("LM_KPROF")) c->kprof_on = atoi(v) != 0;
   // Detectors grouped by correlation kernel: one width-specialised k_corr_pk
@@ -690,6 +695,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   // the last slot's side view; those pixels only feed outputs that are discarded
   c->ext.alloc((size_t)c->ext_slot_bytes * ns + (size_t)(LM_F16_TH + 16) * std::max(K.ext_w[0], K.ext_w[1]) + 64);
   c->tailbin.alloc((size_t)c->tailbin_slot_bytes * ns);
+  SET_SYNC(c->tailbin.p, 0, (size_t)c->tailbin_slot_bytes * ns, c->stream);
   c->tailmask.alloc((size_t)K.tail_hb * ((K.tail_w + 63) / 64) * ns);
   c->tscratch.alloc((size_t)5 * std::max(K.tail_hb, K.tail_hs) * ((K.tail_w + 1) / 2) * ns);
   c->keys.alloc((size_t)K.keys_per_slot * ns);
@@ -803,10 +809,33 @@ struct Timer {
   }
 };
 
-// LM_KPROF=1: mean cycles per k_nms phase over the batch's blocks (stderr)
+// LM_KPROF=1: mean cycles per k_nms / k_tail phase over the batch's blocks (stderr)
 void kprof_report(lm_ctx* c, int n) {
-  std::vector<long long> h((size_t)2 * 16 * 2 * c->nslots);
+  std::vector<long long> h((size_t)3 * 16 * 2 * c->nslots);
   COPY_SYNC(h.data(), c->kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
+  {  // k_tail: region 2, one block per processed slot
+    const long long* base = h.data() + (size_t)2 * 16 * 2 * c->nslots;
+    double acc[16] = {0}, life = 0, wlife = 0, runs = 0;
+    int nb = 0;
+    long long t_min = 0, t_max = 0;
+    for (int b = 0; b < 2 * c->nslots; ++b) {
+      const long long* t = base + (size_t)b * 16;
+      if (!t[0] || !t[9]) continue;
+      for (int k = 1; k <= 9; ++k) acc[k] += (double)(t[k] - t[k - 1]);
+      life += (double)(t[9] - t[0]);
+      wlife += (double)(t[15] - t[14]) * 0.01;
+      runs += (double)t[13];
+      t_min = t_min ? std::min(t_min, t[14]) : t[14];
+      t_max = std::max(t_max, t[15]);
+      ++nb;
+    }
+    if (nb) {
+      fprintf(stderr, "kprof k_tail: blocks=%d life=%.0f cyc = %.1f us, span=%.1f us, side runs %.0f:", nb, life / nb,
+              wlife / nb, (t_max - t_min) * 0.01, runs / nb);
+      for (int k = 1; k <= 9; ++k) fprintf(stderr, " p%d=%.0f", k, acc[k] / nb);
+      fprintf(stderr, "\n");
+    }
+  }
   for (int side = 0; side < 2; ++side) {
     double acc[16] = {0}, life = 0, wlife = 0;
     int cnt[16] = {0}, nb = 0;
@@ -1011,9 +1040,11 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       T.end();
       const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
       T.begin("k_ingest");
-      k_ingest<<<dim3((unsigned)((etot / LM_INGEST_VEC + 255) / 256), (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)),
-                 256, 0, st>>>(dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, n + 1, c->ext.p,
-                               c->ext_slot_bytes);
+      const unsigned ext_blocks = (unsigned)((etot / LM_INGEST_VEC + 255) / 256);
+      const unsigned zero_blocks = (unsigned)((K.tail_bm_words + 4 * 256 - 1) / (4 * 256));  // the tail bitmaps
+      k_ingest<<<dim3(ext_blocks + zero_blocks, (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)), 256, 0, st>>>(
+          dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, n + 1, c->ext.p, c->ext_slot_bytes,
+          ext_blocks, reinterpret_cast<unsigned*>(c->tailbin.p));
       T.end();
     }
     if (part == 1 || part < 0) {
@@ -1043,17 +1074,18 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
           k_corr_dbg<false><<<dgrid, 256, 0, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->dbg.p,
                                                    c->dbg_offd.p, c->dbg_slot_floats);
       }
-      T.begin("k_tail");
-      k_tail<<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p,
-                                                          c->tscratch.p, A.hdr.p);
-      T.end();
-      long long *kp0 = nullptr, *kp1 = nullptr;
+      long long *kp0 = nullptr, *kp1 = nullptr, *kp2 = nullptr;
       if (c->kprof_on) {
-        if (!c->kprof.p) c->kprof.alloc((size_t)2 * 16 * 2 * c->nslots);
-        HIPCHK(hipMemsetAsync(c->kprof.p, 0, sizeof(long long) * 2 * 16 * 2 * c->nslots, st));
+        if (!c->kprof.p) c->kprof.alloc((size_t)3 * 16 * 2 * c->nslots);
+        HIPCHK(hipMemsetAsync(c->kprof.p, 0, sizeof(long long) * 3 * 16 * 2 * c->nslots, st));
         kp0 = c->kprof.p;
         kp1 = c->kprof.p + 16 * 2 * c->nslots;
+        kp2 = c->kprof.p + 2 * 16 * 2 * c->nslots;
       }
+      T.begin("k_tail");
+      k_tail<<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p,
+                                                          c->tscratch.p, A.hdr.p, kp2);
+      T.end();
       T.begin("k_nms_bottom");
       k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
                                                       c->gscratch_slot, A.hdr.p, c->err.p, kp0);
@@ -1065,7 +1097,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       T.begin("k_post");
       k_post<<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
                                                      c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
-                                                     A.pr.p, A.ctl.p, c->err.p);
+                                                     A.pr.p, A.ctl.p, c->err.p, c->gscratch.p, c->gscratch_slot);
       T.end();
       T.begin("k_pack");
       k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
@@ -1153,7 +1185,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
                                            "assertion).") + buf);
     }
     if (e & 16) throw std::runtime_error("P22D::add_side_candidate_safe: CV_Assert(S >= 0) failed.");
-    if (e & 8) throw std::runtime_error("candidate list exceeds the k_post LDS capacity.");
+    if (e & 8) throw std::runtime_error("candidate list exceeds the k_post scratch capacity.");
     if (e & 32) throw std::runtime_error("candidate staging overflow.");
     if (e) throw std::runtime_error("device error flags " + std::to_string(e));
     if (!ph.overflow) break;

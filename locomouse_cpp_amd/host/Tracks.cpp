@@ -82,12 +82,20 @@ void computeBottomTracks(const FrameResults& R, const TrackSetup& S, TrackResult
   check_frames(R, S);
   // The four orders and the snout are independent match2nd problems: solved
   // concurrently, then compared in the reference's order (strict >).
+  // Inputs match2nd would reject print a message per call: run those calls
+  // one after another so the messages come out in the reference's order.
+  bool quiet = S.n_frames >= 2;
+  for (unsigned f = 0; quiet && f < S.n_frames && f < R.UNARY_BOTTOM_PAW.size(); ++f)
+    quiet = R.UNARY_BOTTOM_PAW[f].Ncols() == LM_N_PAWS;
+  const auto policy = quiet ? std::launch::async : std::launch::deferred;
   std::future<IntMat> runs[LM_N_PAWS];
   for (int ip = 0; ip < LM_N_PAWS; ++ip)
-    runs[ip] = std::async(std::launch::async, [&R, &S, ip] {
+    runs[ip] = std::async(policy, [&R, &S, ip] {
       return match2nd(R.UNARY_BOTTOM_PAW, R.PAIRWISE_BOTTOM_PAW, S.nong_bottom, 0, 0, S.n_frames, LM_N_PAWS,
                       PAW_ORDERS[ip]);
     });
+  if (!quiet)
+    for (auto& r : runs) r.wait();  // deferred: runs now, in order, before the snout call below
   const int zero = 0;
   IntMat snout = match2nd(R.UNARY_BOTTOM_SNOUT, R.PAIRWISE_BOTTOM_SNOUT, S.nong_bottom, 0, 0, S.n_frames, 1, &zero);
   double current_cost = -1;

@@ -4,10 +4,11 @@ per pass, kernel trace only).  Writes profiles/pmc_k_corr.json, which
 bench.py reports as roofline.traffic.
 
 Units: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB.  MI355X_MICROARCH.md
-(HBM section): FETCH_SIZE reads exactly 1/2 of the bytes only for 16-B/lane
-coalesced streaming reads; other widths are uncalibrated.  k_corr's tile
-loads are 1-byte-per-element reads of the u8 ext crops, so FETCH_SIZE is
-taken as is (no x2) and the figure is labelled uncalibrated.
+(HBM section, :298): on gfx950 FETCH_SIZE reports exactly 1/2 of the bytes of
+a wide coalesced streaming read (16 B/lane; 128-B requests tallied at 64 B).
+k_corr's tile fill issues 16-B/lane uint4 loads of the u8 ext crops
+(tile_fill_f32 / tile_fill_f16), so its FETCH_SIZE is doubled; so are
+k_minmax's (uint4) and, for the per-kernel table, every kernel's (labelled).
 
 Usage: python scripts/pmc_traffic.py gpurun_out/pmc_<tag> <batch> [out.json]
 """
@@ -31,7 +32,7 @@ def main(root, batch, out=None):
     fetch = per_kernel(os.path.join(root, "FETCH_SIZE", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(root, "WRITE_SIZE", "run_counter_collection.csv"))
     corr = sorted(k for k in fetch if "k_corr" in k)
-    f_kib = sum(fetch[k] for k in corr)
+    f_kib = 2 * sum(fetch[k] for k in corr)  # x2: 16-B/lane reads (MI355X_MICROARCH.md:298)
     w_kib = sum(write.get(k, 0.0) for k in corr)
     res = {
         "kernel": "k_corr (sum of the width-group dispatches of one batch)",
@@ -41,8 +42,9 @@ def main(root, batch, out=None):
         "write_bytes_per_launch": int(w_kib * 1024),
         "hbm_bytes_per_launch": int((f_kib + w_kib) * 1024),
         "hbm_bytes_per_frame": round((f_kib + w_kib) * 1024 / batch, 1),
-        "correction": "none (1-byte loads; the x2 FETCH_SIZE correction is calibrated for 16-B/lane reads only)",
-        "all_kernels_kib_per_dispatch": {k: {"fetch": round(fetch[k], 1), "write": round(write.get(k, 0.0), 1)}
+        "correction": "FETCH_SIZE x2 (16-B/lane uint4 tile loads; gfx950 tallies 128-B requests at 64 B, "
+                      "MI355X_MICROARCH.md:298); WRITE_SIZE as reported",
+        "all_kernels_kib_per_dispatch": {k: {"fetch_x2": round(2 * fetch[k], 1), "write": round(write.get(k, 0.0), 1)}
                                          for k in sorted(fetch)},
     }
     text = json.dumps(res, indent=1)

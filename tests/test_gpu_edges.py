@@ -189,3 +189,18 @@ def test_three_contexts_tie_heavy_against_oracle():
     for k in range(3):
         assert not isinstance(outs[k], Exception), outs[k]
         assert_same(outs[k], refs[k], f"ctx {k}: ")
+
+
+def test_long_candidate_lists_take_the_global_paths():
+    """4x4 mean-filter paw detectors with a low threshold: ~2,000 bottom and
+    ~5,800 side paw candidates per frame after clustering.  k_nms sorts and
+    clusters from global scratch (> LM_NMS_CAP positives), and k_post builds
+    the pairwise costs (~4M transitions) and the side matching from global
+    scratch (> LM_POST_MAXC candidates; the reference has no limit)."""
+    w = np.ones((4, 4)) / 16
+    cfg = S.SyntheticConfig(weights={"paw_bottom": w, "paw_side": w}, biases={"paw_bottom": 60.5, "paw_side": 60.5})
+    frames = cfg.frames(0, 4)
+    ref = _oracle(cfg, frames).result
+    co = ref["cand_offset"]
+    assert min(int(co[4 * f + 1] - co[4 * f]) for f in range(4)) > 1500
+    assert_same(_batched(cfg, frames, 3), ref, "long lists: ")

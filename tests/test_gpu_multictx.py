@@ -1,7 +1,9 @@
 """Several contexts on one GPU driven from several host threads (one HIP
 stream each, bench.py --streams): every batch must equal the same range run
-alone (no shared state between contexts; the host-side enqueue is
-serialised per device, lm_runtime.hip g_enqueue_mu)."""
+alone.  The contexts share no state: each has its own non-blocking stream,
+device buffers and result arenas, and nothing on a context's path uses the
+legacy stream (create/debug copies are stream-ordered), so graph capture on
+one stream never meets another context's work."""
 import threading
 
 import numpy as np
