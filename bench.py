@@ -215,7 +215,7 @@ def main():
                     help="f16: the non-parity LM_CORR_F16 correlation (BASELINE config 5)")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--resident", type=int, default=6400, help="frames resident in HBM per stream (cycled)")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--streams", type=int, default=4,
                     help="contexts (HIP streams + host threads) per GPU")
     ap.add_argument("--round-robin", action="store_true", help="one host thread drives all streams in turn")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)

@@ -59,14 +59,16 @@ template <int R_, int C_>
 DEV void corr_epilogue(const LmConst& K, const LmDet& D, const float (&acc)[R_][C_], const float* lds, int stride, int ly,
                        int lx, int oy0, int ox0, int slot, unsigned long long* __restrict__ keys,
                        int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes, int* s_cnt,
-                       int* s_base, const uint8_t* __restrict__ msrc, int mpitch) {
+                       int* s_base, const uint8_t* __restrict__ msrc, int mpitch, float* __restrict__ tile) {
   static_assert(R_ * C_ <= 32, "bitmask");
   if (D.kind != 0) {
     // the tile's bits gathered in LDS (rows of the <= 4 u32 words its LM_TW
-    // columns touch), then ORed into the slot's zeroed bitmap; neighbouring
-    // tiles share the boundary words
-    __shared__ unsigned s_tb[LM_TH * 4];
+    // columns touch; in the dead window once every wave is past its taps),
+    // then ORed into the slot's zeroed bitmap; neighbouring tiles share the
+    // boundary words
+    unsigned* s_tb = reinterpret_cast<unsigned*>(tile);
     const int w0 = ox0 >> 5;
+    __syncthreads();
     for (int i = threadIdx.x; i < LM_TH * 4; i += blockDim.x) s_tb[i] = 0u;
     __syncthreads();
 #pragma unroll
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_pk(const LmConst* __re
       accf[2 * p + 1][c] = acc[p][c].y;
     }
   corr_epilogue<PK_R, PK_C>(K, D, accf, lds, STR, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
-                            &s_cnt, &s_base, nullptr, 0);
+                            &s_cnt, &s_base, nullptr, 0, lds);
 }
 
 // ---------------------------------------------------------------- k_corr_gen
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
   const uint8_t* msrc = ext + (int64_t)slot * ext_slot_bytes + (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
                         (int64_t)(D.m_y + oy0) * ew + (D.m_x + ox0);
   corr_epilogue<PK_R, PK_C>(K, D, accf, nullptr, 0, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
-                            &s_cnt, &s_base, msrc, ew);
+                            &s_cnt, &s_base, msrc, ew, lds);
 }
 
 // ---------------------------------------------------------------- k_corr_f16
@@ -385,9 +387,6 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
 #define LM_F16_T 2      // 32-row accumulator tiles per wave
 #define LM_F16_THREADS 256
 #define LM_F16_MAX_NCH 10
-#ifndef LM_F16_EXP
-#define LM_F16_EXP 0  // experiments: 1 = no B staging, no barrier; 2 = no B staging, barrier kept
-#endif
 
 typedef _Float16 lm_h8 __attribute__((ext_vector_type(8)));
 typedef float lm_f32x16 __attribute__((ext_vector_type(16)));
@@ -497,10 +496,10 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[t][q] = init;
   const _Float16* __restrict__ arow = img + r * STR + 32 * wave + 8 * h;
-  for (int i = 0; i < (LM_F16_EXP == 3 ? 0 : kh); ++i) {
-    const bool more = LM_F16_EXP == 0 && i + 1 < kh;
+  for (int i = 0; i < kh; ++i) {
+    const bool more = i + 1 < kh;
     if (more) stage_load(i + 1);  // row i + 1's fragments: global -> registers now, -> LDS after this row's MFMAs
-    const lm_h8* __restrict__ bi = reinterpret_cast<const lm_h8*>(bbuf + (LM_F16_EXP ? 0 : (i & 1) * NB)) + lane;
+    const lm_h8* __restrict__ bi = reinterpret_cast<const lm_h8*>(bbuf + (i & 1) * NB) + lane;
     const _Float16* __restrict__ ai = arow + i * STR;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -512,7 +511,7 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
       }
     }
     if (more) stage_store(bbuf + ((i + 1) & 1) * NB);
-    if (LM_F16_EXP != 1) __syncthreads();
+    __syncthreads();
   }
 
   const int x = ox0 + 32 * wave + r;

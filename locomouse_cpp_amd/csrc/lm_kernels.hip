@@ -1153,14 +1153,15 @@ DEV void nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   }
 }
 
-__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
-                                                       const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
-                                                       unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
-                                                       LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
-                                                       long long* __restrict__ prof) {
+// Two instantiations on the same grid, launched back to back: <false> for
+// lists of at most LM_NMS_CAP positives (LDS), <true> for longer ones.
+template <bool GLOB>
+DEV void nms_block(int bx, int feat, const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
+                   const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
+                   unsigned long long* __restrict__ gscratch, int64_t gscratch_slot, LmSlotOut* __restrict__ hdr,
+                   int32_t* __restrict__ err, long long* __restrict__ prof) {
   const LmConst& K = *Kp;
-  const int slot = s0 + blockIdx.x;
-  const int feat = blockIdx.y;  // 0 paw, 1 snout
+  const int slot = s0 + bx;  // feat: 0 paw, 1 snout
   NMS_PROF(0)
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 14] = wall_clock64();
   const int list = side ? 2 + feat : feat;
@@ -1178,7 +1179,7 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
   __shared__ int s_n, s_flag, s_qcnt[2];
 
   if (side && H->cand_cnt[feat] == 0) {  // detectSideCandidates skips (:820-833)
-    if (threadIdx.x == 0) {
+    if (!GLOB && threadIdx.x == 0) {
       H->n_pos[list] = 0;
       H->cand_cnt[list] = 0;
       H->ties[list] = 0;
@@ -1187,17 +1188,65 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
   }
   const int n_in = n_pos[slot * LM_NLIST + list];
   const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
-  if (n_in <= LM_NMS_CAP)
+  if ((n_in > LM_NMS_CAP) != GLOB) return;  // the other instantiation's block
+  if constexpr (!GLOB)
     nms_run<false>(K, D, H, slot, list, side, feat, n_in, src, tailmask, s_keys, s_assign, s_mlist, s_xy, s_tmp, s_stk,
                    s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
   else {  // rare: most of the crop positive; same algorithm in global scratch
     const int64_t npg = gscratch_slot / 3;
-    unsigned long long* a = gscratch + (int64_t)(blockIdx.y + 2 * blockIdx.x) * gscratch_slot;
+    unsigned long long* a = gscratch + (int64_t)(feat + 2 * bx) * gscratch_slot;
     int* assign = reinterpret_cast<int*>(a + npg);
     int* mlist = assign + npg;
     nms_run<true>(K, D, H, slot, list, side, feat, n_in, src, tailmask, a, assign, mlist,
                   reinterpret_cast<unsigned*>(mlist + npg), s_tmp, s_stk, s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
   }
+}
+
+// For the <true> (global-scratch) instantiations of k_nms / k_post: a small
+// grid finds the (slot, feature) pairs that need it — every thread tests one
+// pair, so the usual "none" costs one round of header reads — and the blocks
+// share them out.  fn(pair) runs block-wide.
+template <class Pred, class Fn>
+DEV void for_overflow_pairs(int npairs, Pred overflow, Fn fn) {
+  __shared__ int s_list[1024], s_cnt;
+  for (int c0 = 0; c0 < npairs; c0 += 1024) {
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    for (int p = c0 + threadIdx.x; p < min(npairs, c0 + 1024); p += blockDim.x)
+      if (overflow(p)) s_list[atomicAdd(&s_cnt, 1)] = p;
+    __syncthreads();
+    const int cnt = s_cnt;
+    for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
+      fn(s_list[i]);
+      __syncthreads();  // the next pair reuses the block's shared variables
+    }
+    __syncthreads();
+  }
+}
+
+// <false>: one block per (slot, feature), lists of at most LM_NMS_CAP
+// positives in LDS.  <true>: the longer lists, from global scratch, by a
+// small grid that walks all npairs (slot, feature) pairs — usually none
+// qualifies, so it costs a launch and a few header reads.  One kernel
+// holding both paths ran the common one slower (register allocation).
+template <bool GLOB>
+__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
+                                                       const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
+                                                       unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
+                                                       LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
+                                                       long long* __restrict__ prof, int npairs) {
+  if constexpr (!GLOB)
+    nms_block<false>(blockIdx.x, blockIdx.y, Kp, s0, side, keys, n_pos, tailmask, gscratch, gscratch_slot, hdr, err, prof);
+  else
+    for_overflow_pairs(
+        npairs,
+        [&](int p) {
+          const int slot = s0 + (p >> 1), feat = p & 1, list = side ? 2 + feat : feat;
+          return !(side && hdr[slot].cand_cnt[feat] == 0) && n_pos[slot * LM_NLIST + list] > LM_NMS_CAP;
+        },
+        [&](int p) {
+          nms_block<true>(p >> 1, p & 1, Kp, s0, side, keys, n_pos, tailmask, gscratch, gscratch_slot, hdr, err, nullptr);
+        });
 #undef NMS_PROF
 }
 
@@ -1533,35 +1582,42 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
 }
 
 
-__global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restrict__ Kp, const LmSlot* __restrict__ slots,
-                                                         const uint8_t* const* __restrict__ frame_ptr,
-                                                         const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
-                                                         const uint8_t* __restrict__ luts, LmSlotOut* __restrict__ hdr,
-                                                         const unsigned long long* __restrict__ keys, LmP22D* __restrict__ arena_p22d,
-                                                         int32_t* __restrict__ arena_side_y, double* __restrict__ arena_side_s,
-                                                         double* __restrict__ arena_unary, int32_t* __restrict__ arena_jc,
-                                                         int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
-                                                         LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err,
-                                                         unsigned long long* __restrict__ gscratch, int64_t gscratch_slot) {
+// Two instantiations, launched back to back on the same grid: <false> takes
+// the (slot, feature) blocks whose lists fit the LDS arrays, <true> the rest
+// (global scratch).  One kernel holding both paths ran the common one 60 %
+// slower (register allocation and code layout of the larger body).
+#define LM_POST_ARGS                                                                                               \
+  const LmConst *__restrict__ Kp, const LmSlot *__restrict__ slots, const uint8_t *const *__restrict__ frame_ptr,  \
+      const uint8_t *__restrict__ bkg, const int32_t *__restrict__ cal, const uint8_t *__restrict__ luts,           \
+      LmSlotOut *__restrict__ hdr, const unsigned long long *__restrict__ keys, LmP22D *__restrict__ arena_p22d,    \
+      int32_t *__restrict__ arena_side_y, double *__restrict__ arena_side_s, double *__restrict__ arena_unary,      \
+      int32_t *__restrict__ arena_jc, int32_t *__restrict__ arena_ir, double *__restrict__ arena_pr,                \
+      LmArenaCtl *__restrict__ ctl, int32_t *__restrict__ err, unsigned long long *__restrict__ gscratch,          \
+      int64_t gscratch_slot
+#define LM_POST_PASS                                                                                                \
+  Kp, slots, frame_ptr, bkg, cal, luts, hdr, keys, arena_p22d, arena_side_y, arena_side_s, arena_unary, arena_jc,    \
+      arena_ir, arena_pr, ctl, err, gscratch, gscratch_slot
+template <bool GLOB>
+DEV void post_block(int bx, int feat, LM_POST_ARGS) {
   const LmConst& K = *Kp;
-  const int slot = 1 + blockIdx.x;
-  const int feat = blockIdx.y;
+  const int slot = 1 + bx;
   LmSlotOut* H = hdr + slot;
   const LmSlotOut* HP = hdr + slot - 1;
   const int frame = slots[slot].frame;
-  __shared__ LmCand sb[LM_POST_MAXC], st[LM_POST_MAXC], sp[LM_POST_MAXC];
-  __shared__ int s_off[LM_POST_MAXOFF];
-  __shared__ int s_mb[LM_POST_MAXC], s_mt[LM_POST_MAXC];  // motion status (-1 unknown)
-  __shared__ float s_bps[LM_POST_MAXC], s_tpb[LM_POST_MAXC];
-  __shared__ int s_all_equal, s_any1, s_any0, s_base[4];
-  (void)s_all_equal;
+  __shared__ int s_any1, s_any0, s_base[4];
   const int Nb = H->cand_cnt[feat], Ns = H->cand_cnt[2 + feat];
   const int Ni = frame > 0 ? HP->cand_cnt[feat] : 0;
   const int Nong = K.ong_nx * K.ong_ny;
   const LmCand* cb = LM_CAND_STAGE(K, keys, slot, feat);
   const LmCand* ct = LM_CAND_STAGE(K, keys, slot, 2 + feat);
   const LmCand* cp = LM_CAND_STAGE(K, keys, slot - 1, feat);
-  if (Nb <= LM_POST_MAXC && Ns <= LM_POST_MAXC && Ni <= LM_POST_MAXC && Ni + Nong + 1 <= LM_POST_MAXOFF) {
+  const bool fits = Nb <= LM_POST_MAXC && Ns <= LM_POST_MAXC && Ni <= LM_POST_MAXC && Ni + Nong + 1 <= LM_POST_MAXOFF;
+  if (fits == GLOB) return;  // the other instantiation's block
+  if constexpr (!GLOB) {
+    __shared__ LmCand sb[LM_POST_MAXC], st[LM_POST_MAXC], sp[LM_POST_MAXC];
+    __shared__ int s_off[LM_POST_MAXOFF];
+    __shared__ int s_mb[LM_POST_MAXC], s_mt[LM_POST_MAXC];  // motion status (-1 unknown)
+    __shared__ float s_bps[LM_POST_MAXC], s_tpb[LM_POST_MAXC];
     for (int k = threadIdx.x; k < Nb; k += blockDim.x) sb[k] = cb[k];
     for (int k = threadIdx.x; k < Ns; k += blockDim.x) st[k] = ct[k];
     for (int k = threadIdx.x; k < Ni; k += blockDim.x) sp[k] = cp[k];
@@ -1571,7 +1627,7 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restr
                     arena_unary, arena_jc, arena_ir, arena_pr, ctl, err);
   } else {  // long lists: k_nms's scratch of this (slot, feature) is free again
     const int big = max(max(Nb, Ns), Ni);
-    int* g = reinterpret_cast<int*>(gscratch + (int64_t)(feat + 2 * blockIdx.x) * gscratch_slot);
+    int* g = reinterpret_cast<int*>(gscratch + (int64_t)(feat + 2 * bx) * gscratch_slot);
     int* g_off = g;                      // max(Ni + Nong, Nb) + 1
     int* g_mb = g_off + max(Ni + Nong, Nb) + 1;
     int* g_mt = g_mb + big;
@@ -1585,6 +1641,28 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(const LmConst* __restr
                    g_bps, g_tpb, big, s_base, s_any1, s_any0, arena_p22d, arena_side_y, arena_side_s, arena_unary,
                    arena_jc, arena_ir, arena_pr, ctl, err);
   }
+}
+
+// <false>: one block per (slot, feature) whose lists fit the LDS arrays;
+// <true>: the others, from global scratch, by a small grid walking all npairs
+// (slot, feature) pairs (usually none).  Kept apart: one kernel holding both
+// paths ran the common one 60 % slower.
+template <bool GLOB>
+__global__ __launch_bounds__(LM_POST_THREADS) void k_post(LM_POST_ARGS, int npairs) {
+  if constexpr (!GLOB)
+    post_block<false>(blockIdx.x, blockIdx.y, LM_POST_PASS);
+  else
+    for_overflow_pairs(
+        npairs,
+        [&](int p) {
+          const int slot = 1 + (p >> 1), feat = p & 1;
+          const LmSlotOut* H = hdr + slot;
+          const int Nb = H->cand_cnt[feat], Ns = H->cand_cnt[2 + feat];
+          const int Ni = slots[slot].frame > 0 ? hdr[slot - 1].cand_cnt[feat] : 0;
+          return !(Nb <= LM_POST_MAXC && Ns <= LM_POST_MAXC && Ni <= LM_POST_MAXC &&
+                   Ni + Kp->ong_nx * Kp->ong_ny + 1 <= LM_POST_MAXOFF);
+        },
+        [&](int p) { post_block<true>(p >> 1, p & 1, LM_POST_PASS); });
 }
 
 // ----------------------------------------------------------------- k_carry

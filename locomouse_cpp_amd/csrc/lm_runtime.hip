@@ -1087,17 +1087,25 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
                                                           c->tscratch.p, A.hdr.p, kp2);
       T.end();
       T.begin("k_nms_bottom");
-      k_nms<<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                      c->gscratch_slot, A.hdr.p, c->err.p, kp0);
+      // each list goes to one of the two instantiations (LDS / global scratch)
+      k_nms<false><<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p,
+                                                             c->gscratch.p, c->gscratch_slot, A.hdr.p, c->err.p, kp0, 0);
+      k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+                                                c->gscratch_slot, A.hdr.p, c->err.p, nullptr, 2 * nproc);
       T.end();
       T.begin("k_nms_side");
-      k_nms<<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                  c->gscratch_slot, A.hdr.p, c->err.p, kp1);
+      k_nms<false><<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+                                                         c->gscratch_slot, A.hdr.p, c->err.p, kp1, 0);
+      k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
+                                                c->gscratch_slot, A.hdr.p, c->err.p, nullptr, 2 * n);
       T.end();
       T.begin("k_post");
-      k_post<<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
+      k_post<false><<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
                                                      c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
-                                                     A.pr.p, A.ctl.p, c->err.p, c->gscratch.p, c->gscratch_slot);
+                                                     A.pr.p, A.ctl.p, c->err.p, c->gscratch.p, c->gscratch_slot, 0);
+      k_post<true><<<16, LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
+                                                     c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
+                                                     A.pr.p, A.ctl.p, c->err.p, c->gscratch.p, c->gscratch_slot, 2 * n);
       T.end();
       T.begin("k_pack");
       k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
