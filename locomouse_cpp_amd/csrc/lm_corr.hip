@@ -287,6 +287,209 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_pk(const LmConst* __re
                             &s_cnt, &s_base, nullptr, 0, lds);
 }
 
+// ---------------------------------------------------------------- k_corr_rw
+// Rolling-window form of k_corr_pk: same thread shape and arithmetic (5 columns
+// x 4 rows per thread as two packed row pairs, weights broadcast from SGPRs,
+// pixel pairs by ds_read2_b32), but every wave is an independent 80 x 16
+// output tile that streams its window through a private LDS ring of
+// LM_RW_SLOTS rows instead of holding all 16 + kh - 1 rows.  At step t the
+// wave's 4 row groups read window rows t + 4 ly, t + 4 ly + 1 (rows t..t+13),
+// so 16 slots hold them plus the row being written (row t + 14, into the slot
+// of row t - 2); slot 16 mirrors slot 0 so a pair never wraps.  A wave's LDS
+// operations execute in order, so the ring needs no barrier at all.  LDS per
+// wave is 17 rows (7.9 KB at KW = 30 vs 11.9 KB per wave for k_corr_pk's 48-row
+// window), any kh fits, and no wave waits for another.
+#define LM_RW_WAVES 4
+#define LM_RW_THREADS (64 * LM_RW_WAVES)
+#define LM_RW_TH 16     // output rows per wave tile
+#define LM_RW_SLOTS 16  // ring rows (+ 1 mirror)
+
+// window row: 80 + KW - 1 columns plus up to 3 before them (the loads start on
+// a 4-byte boundary); stride == 4 (mod 8) as in k_corr_pk
+__host__ __device__ constexpr int rw_stride(int kw) { return pk_stride(LM_TW + kw - 1 + 3); }
+__host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
+  return (size_t)LM_RW_WAVES * (LM_RW_SLOTS + 1) * rw_stride(kw) * sizeof(float);
+}
+
+// Wave tile g of a launch (tiles of all slots of the batch flattened, so no
+// wave idles at a slot's end): slot and detector tile.
+DEV CorrTile corr_tile_rw(const LmConst& K, const LmDetGroup& G, int lt) {
+  int gi = 0, tb = 0;
+#pragma unroll
+  for (int k = 0; k < LM_NDET - 1; ++k)
+    if (k + 1 < G.n && lt >= G.tile_end[k]) {
+      gi = k + 1;
+      tb = G.tile_end[k];
+    }
+  const int d = G.ids[gi];
+  lt -= tb;
+  const int tx = K.det[d].tiles_x;
+  return CorrTile{d, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
+}
+
+template <int KW, bool UNF>
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? 5 : 1, 8))) void k_corr_rw(const LmConst* __restrict__ Kp, const LmDetGroup G,
+                                                           const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                           const float* __restrict__ weights, int s0, int nslots,
+                                                           unsigned long long* __restrict__ keys,
+                                                           int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin,
+                                                           int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  extern __shared__ uint4 lds_rw[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int per_slot = G.tile_end[G.n - 1];
+  const int g = blockIdx.x * LM_RW_WAVES + wave;
+  if (g >= per_slot * nslots) return;
+  const int slot = s0 + g / per_slot;
+  const CorrTile T = corr_tile_rw(K, G, g % per_slot);
+  const LmDet D = K.det[T.d];
+  const int oy0 = T.oy0, ox0 = T.ox0;
+  constexpr int STR = rw_stride(KW);
+  constexpr int NL = (3 + LM_TW + KW - 1 + 3) / 4;  // lanes that load a window row (4 bytes each)
+  static_assert(NL <= 64, "window row wider than a wave's loads");
+  float* ring = reinterpret_cast<float*>(lds_rw) + wave * (LM_RW_SLOTS + 1) * STR;
+  const int kh = D.kh, kwp = D.kwp;
+  const int nrows = LM_RW_TH + kh - 1;
+  const int ew = K.ext_w[D.view];
+  const uint8_t* src = corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0);
+  const int mis = (int)((uintptr_t)src & 3);
+  const unsigned* __restrict__ a = reinterpret_cast<const unsigned*>(src - mis) + lane;
+  const int ew4 = ew >> 2;  // ext rows are padded to 16 bytes
+  const bool ld = lane < NL;
+  const int ly = lane >> 4, lx = lane & 15;
+
+  // brightness mask of the point detectors' outputs (crop pixel > 25), read
+  // from the ext crop now so the loads are long done by the epilogue
+  unsigned mbits = 0;
+  if (D.kind == 0) {
+    const uint8_t* __restrict__ m = ext + (int64_t)slot * ext_slot_bytes +
+                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) + (int64_t)(D.m_y + oy0 + ly * PK_R) * ew +
+                                    (D.m_x + ox0 + lx * PK_C);
+#pragma unroll
+    for (int r = 0; r < PK_R; ++r)
+#pragma unroll
+      for (int c = 0; c < PK_C; ++c) mbits |= (m[(int64_t)r * ew + c] > 25 ? 1u : 0u) << (r * PK_C + c);
+  }
+
+  auto load_row = [&](int r) -> unsigned { return (ld && r < nrows) ? a[(int64_t)r * ew4] : 0u; };
+  auto store_row = [&](int r, unsigned v) {
+    if (ld && r < nrows) {
+      const int s = r & (LM_RW_SLOTS - 1);
+      const float4 f = make_float4((float)(v & 0xFFu), (float)((v >> 8) & 0xFFu), (float)((v >> 16) & 0xFFu),
+                                   (float)(v >> 24));
+      *reinterpret_cast<float4*>(ring + s * STR + 4 * lane) = f;
+      if (s == 0) *reinterpret_cast<float4*>(ring + LM_RW_SLOTS * STR + 4 * lane) = f;
+    }
+  };
+  {
+    unsigned v0[LM_RW_SLOTS - 2];
+#pragma unroll
+    for (int r = 0; r < LM_RW_SLOTS - 2; ++r) v0[r] = load_row(r);
+#pragma unroll
+    for (int r = 0; r < LM_RW_SLOTS - 2; ++r) store_row(r, v0[r]);
+  }
+  unsigned pa = load_row(LM_RW_SLOTS - 2), pb = load_row(LM_RW_SLOTS - 1);
+
+  lm_f2 acc[PK_R / 2][PK_C];
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) acc[p][c] = (lm_f2){D.delta, D.delta};
+  const float* __restrict__ W = weights + D.w_off;
+  const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring;
+  lm_f2 px[PK_C + KW - 1];
+  for (int t = 0; t < kh + PK_R - 2; ++t) {
+    // row t + 14 is read from step t + 1 on; its slot held row t - 2, which
+    // no read of this step touches
+    store_row(t + LM_RW_SLOTS - 2, pa);
+    pa = pb;
+    pb = load_row(t + LM_RW_SLOTS);
+    const unsigned base =
+        ring_base + (unsigned)((((t + ly * PK_R) & (LM_RW_SLOTS - 1)) * STR + lx * PK_C + mis) * (int)sizeof(float));
+    lds_pairs<STR, PK_C + KW - 1>(px, base);
+#pragma unroll
+    for (int p = 0; p < PK_R / 2; ++p) {
+      const int i = t - 2 * p;
+      if (i >= 0 && i < kh) {
+        const float* wr = W + i * kwp;
+#pragma unroll
+        for (int j = 0; j < KW; ++j) {
+          const float w = wr[j];
+          const lm_f2 w2 = (lm_f2){w, w};
+#pragma unroll
+          for (int c = 0; c < PK_C; ++c) acc[p][c] = corr_tap<UNF>(acc[p][c], w2, px[c + j]);
+        }
+      }
+    }
+  }
+
+  // epilogue, per wave (the ring is dead: this wave's reads were issued first)
+  unsigned bits = 0;
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) {
+      const int x = ox0 + lx * PK_C + c;
+      const int y0 = oy0 + ly * PK_R + 2 * p;
+      if (x < D.ow && y0 < D.oh && acc[p][c].x > 0.0f) bits |= 1u << ((2 * p) * PK_C + c);
+      if (x < D.ow && y0 + 1 < D.oh && acc[p][c].y > 0.0f) bits |= 1u << ((2 * p + 1) * PK_C + c);
+    }
+  if (D.kind != 0) {
+    // tail map: the tile's 16 rows x <= 4 u32 words (ox0 is a multiple of 80,
+    // so 80 columns touch at most 4 words) = one word per lane, gathered in
+    // the ring, then ORed into the slot's bitmap
+    unsigned* s_tb = reinterpret_cast<unsigned*>(ring);
+    const int w0 = ox0 >> 5;
+    s_tb[lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < PK_R; ++r)
+#pragma unroll
+      for (int c = 0; c < PK_C; ++c)
+        if (bits & (1u << (r * PK_C + c))) {
+          const int x = ox0 + lx * PK_C + c;
+          atomicOr(&s_tb[(ly * PK_R + r) * 4 + (x >> 5) - w0], 1u << (x & 31));
+        }
+    __builtin_amdgcn_wave_barrier();
+    const unsigned v = s_tb[lane];
+    unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(tailbin + (int64_t)slot * tailbin_slot_bytes) +
+                                (D.list ? (int64_t)K.tail_hb * K.tail_nw : 0);
+    const int y = oy0 + (lane >> 2), gw = w0 + (lane & 3);
+    if (v && y < D.oh && gw < K.tail_nw) atomicOr(&tb[(int64_t)y * K.tail_nw + gw], v);
+    return;
+  }
+  bits &= mbits;
+  // keys: one slot per set bit, bit position by bit position (ballot + mbcnt),
+  // one global atomic per wave
+  int off[PK_R * PK_C];
+  int tot = 0;
+#pragma unroll
+  for (int k = 0; k < PK_R * PK_C; ++k) {
+    const unsigned long long m = __ballot((bits >> k) & 1u);
+    off[k] = tot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    tot += __popcll(m);
+  }
+  if (tot == 0) return;
+  int base_k = 0;
+  if (lane == 0) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
+  base_k = __shfl(base_k, 0);
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k;
+#pragma unroll
+  for (int p = 0; p < PK_R / 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int r = 2 * p + h, k = r * PK_C + c;
+        if (bits & (1u << k)) {
+          const int y = oy0 + ly * PK_R + r, x = ox0 + lx * PK_C + c;
+          const float s = h ? acc[p][c].y : acc[p][c].x;
+          kl[off[k]] = ((unsigned long long)(~__float_as_uint(s)) << 32) | (unsigned)(y * D.ow + x);
+        }
+      }
+}
+
 // ---------------------------------------------------------------- k_corr_gen
 // Any detector size.  Same thread shape and arithmetic as k_corr_pk, but the
 // width is a runtime value (taps in chunks of LM_JC = 4 columns over the
@@ -595,8 +798,21 @@ static inline bool corr_specialised(int kw, int kh) {
   }
 }
 
-static inline const void* corr_kernel(int kw, int kh, bool unf) {
-  if (corr_specialised(kw, kh)) switch (kw) {
+// k_corr_rw's ring does not depend on the detector height: every width of
+// LM_KW_LIST, any kh
+static inline bool corr_ring(int kw) { return corr_specialised(kw, 1); }
+
+static inline const void* corr_kernel(int kw, int kh, bool unf, bool ring) {
+  if (ring && corr_ring(kw)) switch (kw) {
+#define LM_KW_CASE(n) \
+  case n:             \
+    return unf ? (const void*)&k_corr_rw<n, true> : (const void*)&k_corr_rw<n, false>;
+      LM_KW_LIST(LM_KW_CASE)
+#undef LM_KW_CASE
+      default:
+        break;
+    }
+  if (!ring && corr_specialised(kw, kh)) switch (kw) {
 #define LM_KW_CASE(n) \
   case n:             \
     return unf ? (const void*)&k_corr_pk<n, true> : (const void*)&k_corr_pk<n, false>;
@@ -610,11 +826,21 @@ static inline const void* corr_kernel(int kw, int kh, bool unf) {
 
 // Launch the correlation for one detector group (all detectors of one width
 // that run the same kernel).
-// `weights`: the fp32 rows (k_corr_pk / k_corr_gen) or the f16 rows (k_corr_f16).
-static inline hipError_t launch_corr(const void* fn, dim3 grid, int threads, size_t lds, hipStream_t st,
+// `weights`: the fp32 rows (k_corr_rw / k_corr_pk / k_corr_gen) or the f16 rows (k_corr_f16).
+// k_corr_rw takes one wave per tile with the batch's tiles flattened (`grid`
+// is then ignored but for its y = slot count); the others one workgroup per
+// (tile, slot).
+static inline hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t lds, hipStream_t st,
                                      const LmConst* K, const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes,
                                      const void* weights, int s0, unsigned long long* keys, int32_t* n_pos,
                                      uint8_t* tailbin, int64_t tailbin_slot_bytes) {
+  if (ring) {
+    int nslots = (int)grid.y;
+    const unsigned waves = (unsigned)(G.tile_end[G.n - 1] * nslots);
+    void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
+                    (void*)&nslots, (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
+    return hipLaunchKernel(fn, dim3((waves + LM_RW_WAVES - 1) / LM_RW_WAVES), dim3(LM_RW_THREADS), args, lds, st);
+  }
   void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
                   (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
   return hipLaunchKernel(fn, grid, dim3(threads), args, lds, st);

@@ -224,6 +224,8 @@ struct lm_ctx {
   std::vector<std::pair<const void*, LmDetGroup>> corr_groups;  // (correlation kernel, its detectors)
   std::vector<size_t> corr_group_lds;                    // dynamic LDS bytes per group launch
   std::vector<int> corr_group_threads;                   // block size per group launch
+  std::vector<char> corr_group_ring;                     // group runs k_corr_rw (one wave per tile)
+  bool corr_ring_on = true;                              // k_corr_rw for the widths it covers (LM_CORR_PK=1: k_corr_pk)
   // device buffers
   DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin;
   DevBuf<unsigned long long> tailmask;  // TAIL_MASK bitmaps, 64 columns per word
@@ -363,6 +365,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     throw std::invalid_argument("corr_precision must be LM_CORR_FP32 or LM_CORR_F16.");
 
   c->setup = *su;
+  if (const char* v = getenv("LM_CORR_PK")) c->corr_ring_on = atoi(v) == 0;
   c->params = *P;
   lm_geometry& g = c->geo;
   std::memset(&g, 0, sizeof(g));
@@ -450,8 +453,9 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     D.oh = out_rel[d].h;
     D.ow = out_rel[d].w;
     const bool f16 = su->corr_precision == LM_CORR_F16;
+    const bool ring = !f16 && c->corr_ring_on && corr_ring(D.kw);
     D.tile_w = f16 ? LM_F16_TW : LM_TW;
-    D.tile_h = f16 ? LM_F16_TH : LM_TH;
+    D.tile_h = f16 ? LM_F16_TH : ring ? LM_RW_TH : LM_TH;
     D.tiles_x = (D.ow + D.tile_w - 1) / D.tile_w;
     D.tiles_y = (D.oh + D.tile_h - 1) / D.tile_h;
     D.tile_base = tile;
@@ -591,14 +595,19 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->corr_groups.clear();
   c->corr_group_lds.clear();
   c->corr_group_threads.clear();
+  c->corr_group_ring.clear();
   for (int d = 0; d < 6; ++d) {
     LmDet& D = K.det[d];
     const bool f16 = su->corr_precision == LM_CORR_F16;
-    const void* fn = f16 ? corr_kernel_f16(D.kw) : corr_kernel(D.kw, D.kh, c->unfused);
+    const bool ring = !f16 && c->corr_ring_on && corr_ring(D.kw);
+    const void* fn = f16 ? corr_kernel_f16(D.kw) : corr_kernel(D.kw, D.kh, c->unfused, ring);
     size_t need;
     if (f16) {
       D.chunk_rows = D.kh;
       need = f16_lds_bytes(f16_nch(D.kw), D.kh);
+    } else if (ring) {
+      D.chunk_rows = D.kh;
+      need = rw_lds_bytes(D.kw);
     } else if (corr_specialised(D.kw, D.kh)) {
       D.chunk_rows = D.kh;
       need = (size_t)(LM_TH + D.kh - 1) * pk_stride(LM_TW + D.kw - 1) * sizeof(float);
@@ -614,7 +623,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       std::memset(&G, 0, sizeof(G));
       c->corr_groups.push_back({fn, G});
       c->corr_group_lds.push_back(0);
-      c->corr_group_threads.push_back(f16 ? LM_F16_THREADS : LM_CORR_THREADS);
+      c->corr_group_threads.push_back(f16 ? LM_F16_THREADS : ring ? LM_RW_THREADS : LM_CORR_THREADS);
+      c->corr_group_ring.push_back(ring);
     }
     LmDetGroup& G = c->corr_groups[gi].second;
     const int prev = G.n ? G.tile_end[G.n - 1] : 0;
@@ -1053,7 +1063,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
         const auto& grp = c->corr_groups[gi];
         const LmDetGroup& G = grp.second;
         const void* w = c->setup.corr_precision == LM_CORR_F16 ? (const void*)c->weights16.p : (const void*)c->weights.p;
-        HIPCHK(launch_corr(grp.first, dim3(G.tile_end[G.n - 1], nproc), c->corr_group_threads[gi],
+        HIPCHK(launch_corr(grp.first, c->corr_group_ring[gi], dim3(G.tile_end[G.n - 1], nproc), c->corr_group_threads[gi],
                            c->corr_group_lds[gi], st, dK, G, c->ext.p, c->ext_slot_bytes, w, s_proc0, c->keys.p,
                            c->npos.p, c->tailbin.p, c->tailbin_slot_bytes));
       }
