@@ -10,9 +10,10 @@
 // the same), so every score is bit-identical to the oracle's chain.
 //
 // Kernels:
-//   k_corr_pk<KW, UNF>  width-specialised packed-FP32 kernel (every detector
-//                       width 16..64 that has an instantiation, kh <= 64): the
-//                       production path.
+//   k_corr_rw<KW, UNF>  width-specialised packed-FP32 kernel (every detector
+//                       width of LM_KW_LIST, any height): one wave per 80 x 16
+//                       output tile streaming its window through a private
+//                       LDS ring; the production path.
 //   k_corr_gen<UNF>     any width and height: taps in chunks of 4 columns and
 //                       the tap rows in LDS-sized chunks (detectors larger than
 //                       the LDS window, widths without an instantiation).
@@ -127,28 +128,6 @@ struct LmDetGroup {
   int32_t tile_end[LM_NDET];  // cumulative tile counts
 };
 
-// Pixel pairs (row t, row t+1) of one column straight into an aligned VGPR
-// pair: ds_read2_b32 with offset1 = offset0 + STRIDE (dwords).  At most 15
-// LDS reads in flight (lgkmcnt is 4 bits); one wait at the end.
-template <int STRIDE, int Q>
-DEV void lds_pair(lm_f2& dst, unsigned base) {
-  static_assert(Q + STRIDE <= 255, "ds_read2_b32 offset range");
-  if constexpr (Q >= 15) asm volatile("s_waitcnt lgkmcnt(14)" ::: "memory");
-  asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(dst) : "v"(base), "i"(Q), "i"(Q + STRIDE) : "memory");
-}
-
-template <int STRIDE, int N, int... Qs>
-DEV void lds_pairs_impl(lm_f2 (&px)[N], unsigned base, std::integer_sequence<int, Qs...>) {
-  (lds_pair<STRIDE, Qs>(px[Qs], base), ...);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int STRIDE, int N>
-DEV void lds_pairs(lm_f2 (&px)[N], unsigned base) {
-  lds_pairs_impl<STRIDE, N>(px, base, std::make_integer_sequence<int, N>{});
-}
-
 // Tile fill: u8 ext-crop window (rows x cols from src, row pitch ew) -> fp32
 // LDS (row stride `stride`).  16-byte aligned vector loads, all of a round
 // issued before any is consumed (a workgroup's fill is one or two load
@@ -217,82 +196,17 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
          (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
 }
 
-// ---------------------------------------------------------------- k_corr_pk
+// ---------------------------------------------------------------- k_corr_rw
 // Packed-FP32 correlation.  gfx950 issues one v_fma_f32 (wave64) per 4 cycles
 // per SIMD; v_pk_fma_f32 does two FMAs per lane in the same slot.  Each
 // accumulator pair holds two vertically adjacent outputs (rows 2p, 2p+1) of
 // one column: for tap (i, j) both use weight w[i][j] (SGPR, broadcast) and
 // pixels (t, t+1) of one column, which one ds_read2_b32 loads into an aligned
-// register pair.  192 threads as 16 (x) x 12 (y), each 5 columns x 4 rows: an
-// 80x48 output tile per workgroup; the input window (48+kh-1 rows x 80+KW-1
-// columns) is converted to fp32 once into LDS.
-template <int KW, bool UNF>
-__global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_pk(const LmConst* __restrict__ Kp, const LmDetGroup G,
-                                                             const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
-                                                             const float* __restrict__ weights, int s0,
-                                                             unsigned long long* __restrict__ keys,
-                                                             int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin,
-                                                             int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  extern __shared__ float lds[];
-  __shared__ int s_cnt, s_base;
-  const int slot = s0 + blockIdx.y;
-  const CorrTile T = corr_tile(K, G);
-  const LmDet D = K.det[T.d];
-  const int oy0 = T.oy0, ox0 = T.ox0;
-  constexpr int cols = LM_TW + KW - 1;
-  constexpr int STR = pk_stride(cols);
-  const int rows = LM_TH + D.kh - 1;
-  tile_fill_f32(lds, STR, corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0), K.ext_w[D.view], rows, cols);
-  if (threadIdx.x == 0) s_cnt = 0;
-  __syncthreads();
-
-  const int ly = threadIdx.x >> 4, lx = threadIdx.x & 15;
-  lm_f2 acc[PK_R / 2][PK_C];
-#pragma unroll
-  for (int p = 0; p < PK_R / 2; ++p)
-#pragma unroll
-    for (int c = 0; c < PK_C; ++c) acc[p][c] = (lm_f2){D.delta, D.delta};
-  const float* __restrict__ W = weights + D.w_off;
-  const int kh = D.kh, kwp = D.kwp;
-  lm_f2 px[PK_C + KW - 1];
-  for (int t = 0; t < kh + PK_R - 2; ++t) {
-    const float* p0 = lds + (ly * PK_R + t) * STR + lx * PK_C;
-    const unsigned base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)p0;
-    lds_pairs<STR, PK_C + KW - 1>(px, base);
-#pragma unroll
-    for (int p = 0; p < PK_R / 2; ++p) {
-      const int i = t - 2 * p;
-      if (i >= 0 && i < kh) {
-        const float* wr = W + i * kwp;
-#pragma unroll
-        for (int j = 0; j < KW; ++j) {
-          const float w = wr[j];
-          const lm_f2 w2 = (lm_f2){w, w};
-#pragma unroll
-          for (int c = 0; c < PK_C; ++c) acc[p][c] = corr_tap<UNF>(acc[p][c], w2, px[c + j]);
-        }
-      }
-    }
-  }
-  float accf[PK_R][PK_C];
-#pragma unroll
-  for (int p = 0; p < PK_R / 2; ++p)
-#pragma unroll
-    for (int c = 0; c < PK_C; ++c) {
-      accf[2 * p][c] = acc[p][c].x;
-      accf[2 * p + 1][c] = acc[p][c].y;
-    }
-  corr_epilogue<PK_R, PK_C>(K, D, accf, lds, STR, ly, lx, oy0, ox0, slot, keys, n_pos, tailbin, tailbin_slot_bytes,
-                            &s_cnt, &s_base, nullptr, 0, lds);
-}
-
-// ---------------------------------------------------------------- k_corr_rw
-// Rolling-window form of k_corr_pk: same thread shape and arithmetic (5 columns
-// x 4 rows per thread as two packed row pairs, weights broadcast from SGPRs,
-// pixel pairs by ds_read2_b32), but every wave is an independent 80 x 16
-// output tile that streams its window through a private LDS ring of
-// LM_RW_SLOTS rows instead of holding all 16 + kh - 1 rows.  At step t the
+// register pair.  A thread owns 5 columns x 4 rows (two row pairs sharing the
+// pixel rows of a step with weight rows t and t - 2); a wave is 16 x 4
+// threads = an independent 80 x 16 output tile that streams its window
+// through a private LDS ring of LM_RW_SLOTS rows (round 1's k_corr_pk held a
+// 48 + kh - 1 row window per 3-wave workgroup instead).  At step t the
 // wave's 4 row groups read window rows t + 4 ly, t + 4 ly + 1 (rows t..t+13),
 // so 16 slots hold them plus the row being written (row t + 14, into the slot
 // of row t - 2); slot 16 mirrors slot 0 so a pair never wraps.  A wave's LDS
@@ -326,6 +240,104 @@ DEV CorrTile corr_tile_rw(const LmConst& K, const LmDetGroup& G, int lt) {
   const int tx = K.det[d].tiles_x;
   return CorrTile{d, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
 }
+
+// Software pipeline of k_corr_rw's step (PIPE): a detector row's taps in
+// chunks (the first of 8 taps, the others of <= 12); while a chunk's FMAs run,
+// the pixel pairs and weights of the next chunk (the next step's first chunk
+// after the last) are already in flight, so a wave waits on LDS / scalar
+// loads only when they are late, and at most 12 + 4 pairs are live.
+template <int KW>
+struct RwPlan {
+  static_assert(KW >= 10, "k_corr_rw pipeline: at least 10 taps per row");
+  static constexpr int T0 = 8;
+  static constexpr int NR0 = (KW - T0 + 11) / 12;
+  static constexpr int NR = NR0 < 2 ? 2 : NR0;  // >= 3 chunks: the first chunk's pairs are dead by the last
+  static constexpr int N = 1 + NR;
+  static constexpr int WMAX = 12;
+  static constexpr int beg(int c) { return c == 0 ? 0 : T0 + ((c - 1) * (KW - T0)) / NR; }
+  static constexpr int end(int c) { return c == N - 1 ? KW : beg(c + 1); }
+  // pixel pairs a chunk needs that the previous chunk of its step did not load
+  static constexpr int pbeg(int c) { return c == 0 ? 0 : beg(c) + PK_C - 1; }
+  static constexpr int pend(int c) { return end(c) + PK_C - 1; }
+};
+
+template <int STRIDE, int Q>
+DEV void lds_pair_nw(lm_f2& dst, unsigned base) {
+  static_assert(Q + STRIDE <= 255, "ds_read2_b32 offset range");
+  asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(dst) : "v"(base), "i"(Q), "i"(Q + STRIDE) : "memory");
+}
+
+template <int KW, bool UNF>
+struct RwPipe {
+  using P = RwPlan<KW>;
+  static constexpr int STR = rw_stride(KW);
+  lm_f2 px[PK_C + KW - 1];
+  lm_f2 acc[2][PK_C];
+  float wa[P::WMAX], wb[P::WMAX];  // weights of the chunk being computed (rows t, t - 2)
+
+  template <int Q0, int Q1>
+  DEV void issue(unsigned base) {
+    if constexpr (Q0 < Q1) {
+      lds_pair_nw<STR, Q0>(px[Q0], base);
+      issue<Q0 + 1, Q1>(base);
+    }
+  }
+  // chunk C's weights of rows ra (pair 0) and rb (pair 1) into na / nb
+  template <int C>
+  DEV void load_w(float (&na)[P::WMAX], float (&nb)[P::WMAX], const float* __restrict__ ra,
+                  const float* __restrict__ rb) {
+#pragma unroll
+    for (int j = 0; j < P::end(C) - P::beg(C); ++j) {
+      na[j] = ra[P::beg(C) + j];
+      nb[j] = rb[P::beg(C) + j];
+    }
+  }
+  template <int C, bool A, bool B>
+  DEV void compute() {
+#pragma unroll
+    for (int j = P::beg(C); j < P::end(C); ++j) {
+      if constexpr (A) {
+        const lm_f2 w2 = (lm_f2){wa[j - P::beg(C)], wa[j - P::beg(C)]};
+#pragma unroll
+        for (int c = 0; c < PK_C; ++c) acc[0][c] = corr_tap<UNF>(acc[0][c], w2, px[c + j]);
+      }
+      if constexpr (B) {
+        const lm_f2 w2 = (lm_f2){wb[j - P::beg(C)], wb[j - P::beg(C)]};
+#pragma unroll
+        for (int c = 0; c < PK_C; ++c) acc[1][c] = corr_tap<UNF>(acc[1][c], w2, px[c + j]);
+      }
+    }
+  }
+  // step t, chunk C onwards.  On entry chunk C's pairs and weights are in
+  // flight; on exit the next step's first chunk is.  `base_n` addresses the
+  // next step's pixel rows, rows_n its weight rows.
+  template <int C, bool A, bool B, typename F>
+  DEV void chunks(unsigned base, unsigned base_n, const float* __restrict__ ra, const float* __restrict__ rb,
+                  const float* __restrict__ ra_n, const float* __restrict__ rb_n, F&& at_start) {
+    // lgkmcnt(0) through the builtin (vmcnt / expcnt left at their maxima), so
+    // the compiler's own wait insertion knows the scalar loads are done too
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (C == 0) at_start();
+    float na[P::WMAX], nb[P::WMAX];
+    if constexpr (C + 1 < P::N) {
+      load_w<C + 1>(na, nb, ra, rb);
+      issue<P::pbeg(C + 1), P::pend(C + 1)>(base);
+    } else {
+      load_w<0>(na, nb, ra_n, rb_n);
+      issue<P::pbeg(0), P::pend(0)>(base_n);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    compute<C, A, B>();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < P::WMAX; ++j) {
+      wa[j] = na[j];
+      wb[j] = nb[j];
+    }
+    if constexpr (C + 1 < P::N) chunks<C + 1, A, B>(base, base_n, ra, rb, ra_n, rb_n, at_start);
+  }
+};
 
 template <int KW, bool UNF>
 __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? 5 : 1, 8))) void k_corr_rw(const LmConst* __restrict__ Kp, const LmDetGroup G,
@@ -392,37 +404,45 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
   unsigned pa = load_row(LM_RW_SLOTS - 2), pb = load_row(LM_RW_SLOTS - 1);
 
   lm_f2 acc[PK_R / 2][PK_C];
-#pragma unroll
-  for (int p = 0; p < PK_R / 2; ++p)
-#pragma unroll
-    for (int c = 0; c < PK_C; ++c) acc[p][c] = (lm_f2){D.delta, D.delta};
   const float* __restrict__ W = weights + D.w_off;
   const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring;
-  lm_f2 px[PK_C + KW - 1];
-  for (int t = 0; t < kh + PK_R - 2; ++t) {
-    // row t + 14 is read from step t + 1 on; its slot held row t - 2, which
-    // no read of this step touches
-    store_row(t + LM_RW_SLOTS - 2, pa);
-    pa = pb;
-    pb = load_row(t + LM_RW_SLOTS);
-    const unsigned base =
-        ring_base + (unsigned)((((t + ly * PK_R) & (LM_RW_SLOTS - 1)) * STR + lx * PK_C + mis) * (int)sizeof(float));
-    lds_pairs<STR, PK_C + KW - 1>(px, base);
+  const unsigned lane_off = (unsigned)((lx * PK_C + mis) * (int)sizeof(float));
+  auto row_base = [&](int t) -> unsigned {
+    return ring_base + (unsigned)(((t + ly * PK_R) & (LM_RW_SLOTS - 1)) * STR * (int)sizeof(float)) + lane_off;
+  };
+  RwPipe<KW, UNF> S;
 #pragma unroll
-    for (int p = 0; p < PK_R / 2; ++p) {
-      const int i = t - 2 * p;
-      if (i >= 0 && i < kh) {
-        const float* wr = W + i * kwp;
+  for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int j = 0; j < KW; ++j) {
-          const float w = wr[j];
-          const lm_f2 w2 = (lm_f2){w, w};
+    for (int c = 0; c < PK_C; ++c) S.acc[p][c] = (lm_f2){D.delta, D.delta};
+  auto wrow = [&](int i) { return W + min(max(i, 0), kh - 1) * kwp; };
+  S.template load_w<0>(S.wa, S.wb, wrow(0), wrow(-2));
+  S.template issue<RwPlan<KW>::pbeg(0), RwPlan<KW>::pend(0)>(row_base(0));
+  auto step = [&](int t, auto A, auto B) {
+    auto at_start = [&]() {
+      // row t + 14 is read from the next step on (its pairs are issued in
+      // this step's last chunk); its slot held row t - 2
+      store_row(t + LM_RW_SLOTS - 2, pa);
+      pa = pb;
+      pb = load_row(t + LM_RW_SLOTS);
+    };
+    S.template chunks<0, decltype(A)::value, decltype(B)::value>(row_base(t), row_base(t + 1), wrow(t), wrow(t - 2),
+                                                                  wrow(t + 1), wrow(t - 1), at_start);
+  };
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+  // pair 0 (tap row t) runs while t < kh, pair 1 (tap row t - 2) from t = 2
+  const int e1 = min(2, kh);
+  int t = 0;
+  for (; t < e1; ++t) step(t, T1{}, F0{});
+  for (; t < 2; ++t) step(t, F0{}, F0{});
+  for (; t < kh; ++t) step(t, T1{}, T1{});
+  for (; t < kh + 2; ++t) step(t, F0{}, T1{});
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // the last (unused) prefetch
 #pragma unroll
-          for (int c = 0; c < PK_C; ++c) acc[p][c] = corr_tap<UNF>(acc[p][c], w2, px[c + j]);
-        }
-      }
-    }
-  }
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int c = 0; c < PK_C; ++c) acc[p][c] = S.acc[p][c];
 
   // epilogue, per wave (the ring is dead: this wave's reads were issued first)
   unsigned bits = 0;
@@ -784,10 +804,10 @@ static inline const void* corr_kernel_f16(int kw) {
 #define LM_KW_LIST(X)                                                                                             \
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
       X(40) X(44) X(48) X(52) X(56) X(60) X(64)
-#define LM_PK_MAX_KH 64
 
-static inline bool corr_specialised(int kw, int kh) {
-  if (kh > LM_PK_MAX_KH) return false;
+// k_corr_rw's ring does not depend on the detector height: every width of
+// LM_KW_LIST, any kh; other widths run k_corr_gen
+static inline bool corr_ring(int kw) {
   switch (kw) {
 #define LM_KW_CASE(n) case n:
     LM_KW_LIST(LM_KW_CASE)
@@ -798,30 +818,16 @@ static inline bool corr_specialised(int kw, int kh) {
   }
 }
 
-// k_corr_rw's ring does not depend on the detector height: every width of
-// LM_KW_LIST, any kh
-static inline bool corr_ring(int kw) { return corr_specialised(kw, 1); }
-
-static inline const void* corr_kernel(int kw, int kh, bool unf, bool ring) {
-  if (ring && corr_ring(kw)) switch (kw) {
+static inline const void* corr_kernel(int kw, bool unf) {
+  switch (kw) {
 #define LM_KW_CASE(n) \
   case n:             \
     return unf ? (const void*)&k_corr_rw<n, true> : (const void*)&k_corr_rw<n, false>;
-      LM_KW_LIST(LM_KW_CASE)
+    LM_KW_LIST(LM_KW_CASE)
 #undef LM_KW_CASE
-      default:
-        break;
-    }
-  if (!ring && corr_specialised(kw, kh)) switch (kw) {
-#define LM_KW_CASE(n) \
-  case n:             \
-    return unf ? (const void*)&k_corr_pk<n, true> : (const void*)&k_corr_pk<n, false>;
-      LM_KW_LIST(LM_KW_CASE)
-#undef LM_KW_CASE
-      default:
-        break;
-    }
-  return unf ? (const void*)&k_corr_gen<true> : (const void*)&k_corr_gen<false>;
+    default:
+      return unf ? (const void*)&k_corr_gen<true> : (const void*)&k_corr_gen<false>;
+  }
 }
 
 // Launch the correlation for one detector group (all detectors of one width

@@ -12,7 +12,8 @@
 
 #include <stdint.h>
 
-// Correlation tile: 256 threads as 16 x 16, each LM_C x LM_R outputs.
+// Correlation tile width (k_corr_rw: 80 x 16 per wave; k_corr_gen: 80 x 48
+// per 192-thread workgroup, 16 x 12 threads of LM_C x 4 outputs).
 #define LM_C 5
 #define LM_R 3
 #define LM_TW (16 * LM_C)  // 80

@@ -225,7 +225,6 @@ struct lm_ctx {
   std::vector<size_t> corr_group_lds;                    // dynamic LDS bytes per group launch
   std::vector<int> corr_group_threads;                   // block size per group launch
   std::vector<char> corr_group_ring;                     // group runs k_corr_rw (one wave per tile)
-  bool corr_ring_on = true;                              // k_corr_rw for the widths it covers (LM_CORR_PK=1: k_corr_pk)
   // device buffers
   DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin;
   DevBuf<unsigned long long> tailmask;  // TAIL_MASK bitmaps, 64 columns per word
@@ -365,7 +364,6 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     throw std::invalid_argument("corr_precision must be LM_CORR_FP32 or LM_CORR_F16.");
 
   c->setup = *su;
-  if (const char* v = getenv("LM_CORR_PK")) c->corr_ring_on = atoi(v) == 0;
   c->params = *P;
   lm_geometry& g = c->geo;
   std::memset(&g, 0, sizeof(g));
@@ -453,7 +451,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     D.oh = out_rel[d].h;
     D.ow = out_rel[d].w;
     const bool f16 = su->corr_precision == LM_CORR_F16;
-    const bool ring = !f16 && c->corr_ring_on && corr_ring(D.kw);
+    const bool ring = !f16 && corr_ring(D.kw);
     D.tile_w = f16 ? LM_F16_TW : LM_TW;
     D.tile_h = f16 ? LM_F16_TH : ring ? LM_RW_TH : LM_TH;
     D.tiles_x = (D.ow + D.tile_w - 1) / D.tile_w;
@@ -588,10 +586,10 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->gscratch_slot = std::max(3 * (int64_t)np, (5 * (int64_t)np + K.ong_nx * K.ong_ny + 2) / 2 + 1);
   c->unfused = su->filter_arith == LM_FILTER_UNFUSED;
   if (const char* v = getenv("LM_KPROF")) c->kprof_on = atoi(v) != 0;
-  // Detectors grouped by correlation kernel: one width-specialised k_corr_pk
+  // Detectors grouped by correlation kernel: one width-specialised k_corr_rw
   // launch per width, every other detector in one k_corr_gen launch.  Each
-  // launch gets exactly the LDS its detectors' windows need, so narrow groups
-  // keep more workgroups per CU.
+  // launch gets exactly the LDS its detectors' rings / windows need, so narrow
+  // groups keep more waves per CU.
   c->corr_groups.clear();
   c->corr_group_lds.clear();
   c->corr_group_threads.clear();
@@ -599,8 +597,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   for (int d = 0; d < 6; ++d) {
     LmDet& D = K.det[d];
     const bool f16 = su->corr_precision == LM_CORR_F16;
-    const bool ring = !f16 && c->corr_ring_on && corr_ring(D.kw);
-    const void* fn = f16 ? corr_kernel_f16(D.kw) : corr_kernel(D.kw, D.kh, c->unfused, ring);
+    const bool ring = !f16 && corr_ring(D.kw);
+    const void* fn = f16 ? corr_kernel_f16(D.kw) : corr_kernel(D.kw, c->unfused);
     size_t need;
     if (f16) {
       D.chunk_rows = D.kh;
@@ -608,9 +606,6 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     } else if (ring) {
       D.chunk_rows = D.kh;
       need = rw_lds_bytes(D.kw);
-    } else if (corr_specialised(D.kw, D.kh)) {
-      D.chunk_rows = D.kh;
-      need = (size_t)(LM_TH + D.kh - 1) * pk_stride(LM_TW + D.kw - 1) * sizeof(float);
     } else {
       const size_t row = (size_t)pk_stride(LM_TW + D.kwp - 1) * sizeof(float);
       D.chunk_rows = std::max(1, std::min(D.kh, (int)(kCorrLdsBudget / row) - (LM_TH - 1)));

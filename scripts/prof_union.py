@@ -34,7 +34,7 @@ def main(path, per_launch=4, skip=0):
     for k in sorted(fam, key=lambda k: -sum(b - a for a, b in fam[k])):
         iv = sorted(fam[k])
         print(f"{k:16s} {len(iv):10d} {sum(b - a for a, b in iv) / len(iv) / 1e3:10.2f} {union(iv) / 1e3:12.1f}")
-    corr = sorted(fam.get("k_corr_pk", []) or fam.get("k_corr", []))[skip * per_launch:]
+    corr = sorted(fam.get("k_corr_rw", []) or fam.get("k_corr_pk", []) or fam.get("k_corr", []))[skip * per_launch:]
     if corr:
         n = len(corr) / per_launch
         print(f"k_corr launches {n:.0f}: union per launch {union(corr) / n / 1e6:.5f} ms, "
