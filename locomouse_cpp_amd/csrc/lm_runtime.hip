@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -1293,7 +1294,23 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     if (device < 0 || device >= ndev) throw HipError("invalid HIP device index");
     c->device = device;
     HIPCHK(hipSetDevice(device));
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // Contexts of a process alternate between the highest and the lowest
+    // stream priority.  With equal priorities, concurrent contexts share the
+    // CUs during their correlation launches, finish them together and then
+    // all run their short post-correlation kernels at once (a convoy: ~19 %
+    // of the time no correlation ran, profiles/r02/rw/).  Unequal priorities
+    // let one context's correlation go first, which keeps the contexts out of
+    // phase: +4-5 % frames/s at 4 contexts per GPU.  LM_STREAM_PRIO=0: one
+    // priority for all.
+    const char* pv = getenv("LM_STREAM_PRIO");
+    if (!pv || atoi(pv) != 0) {
+      static std::atomic<int> n_created{0};
+      int lo = 0, hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, (n_created++ & 1) ? lo : hi));
+    } else {
+      HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    }
     c->max_batch = max_batch;
     c->nslots = max_batch + 1;
     validate_and_build(c, setup, params, model);

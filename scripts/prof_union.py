@@ -39,6 +39,15 @@ def main(path, per_launch=4, skip=0):
         n = len(corr) / per_launch
         print(f"k_corr launches {n:.0f}: union per launch {union(corr) / n / 1e6:.5f} ms, "
               f"mean launch (sum of dispatches) {sum(b - a for a, b in corr) / n / 1e6:.5f} ms")
+        # timeline over the window of the counted k_corr launches: how much of
+        # it any kernel ran, k_corr ran, or the GPU had no kernel at all
+        t0, t1 = corr[0][0], max(b for _, b in corr)
+        clip = lambda iv: [(max(a, t0), min(b, t1)) for a, b in iv if b > t0 and a < t1]
+        allk = clip([x for k, v in fam.items() if k != "k_synth" for x in v])
+        span = t1 - t0
+        u_all, u_corr = union(allk), union(clip(corr))
+        print(f"window {span / 1e6:.3f} ms: any kernel {100 * u_all / span:.1f} %, k_corr {100 * u_corr / span:.1f} %, "
+              f"no kernel {100 * (span - u_all) / span:.1f} %, other kernels only {100 * (u_all - u_corr) / span:.1f} %")
 
 
 if __name__ == "__main__":
