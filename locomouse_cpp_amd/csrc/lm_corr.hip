@@ -126,6 +126,7 @@ struct LmDetGroup {
   int32_t n;
   int32_t ids[LM_NDET];
   int32_t tile_end[LM_NDET];  // cumulative tile counts
+  int32_t ring_floats;        // k_corr_rw_all: LDS floats per wave
 };
 
 // Tile fill: u8 ext-crop window (rows x cols from src, row pitch ew) -> fp32
@@ -196,6 +197,13 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
          (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
 }
 
+// Widths with a width-specialised k_corr_rw (any height); every other
+// detector runs k_corr_gen.
+#define LM_KW_LIST(X)                                                                                             \
+  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
+      X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+#define LM_KW_LIST_RW_ALL LM_KW_LIST
+
 // ---------------------------------------------------------------- k_corr_rw
 // Packed-FP32 correlation.  gfx950 issues one v_fma_f32 (wave64) per 4 cycles
 // per SIMD; v_pk_fma_f32 does two FMAs per lane in the same slot.  Each
@@ -225,20 +233,27 @@ __host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
   return (size_t)LM_RW_WAVES * (LM_RW_SLOTS + 1) * rw_stride(kw) * sizeof(float);
 }
 
-// Wave tile g of a launch (tiles of all slots of the batch flattened, so no
-// wave idles at a slot's end): slot and detector tile.
-DEV CorrTile corr_tile_rw(const LmConst& K, const LmDetGroup& G, int lt) {
-  int gi = 0, tb = 0;
+// Wave g of a launch -> (slot, detector, tile origin).  The batch's tiles
+// are flattened detector-major (all slots of the group's first detector,
+// then the next ...), so no wave idles at a frame's end and the host can
+// put the longest detectors first.  false: past the last tile.
+DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, int& slot, CorrTile& T) {
+  int gi = 0, base = 0;
 #pragma unroll
   for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && lt >= G.tile_end[k]) {
+    if (k + 1 < G.n && g >= nslots * G.tile_end[k]) {
       gi = k + 1;
-      tb = G.tile_end[k];
+      base = nslots * G.tile_end[k];
     }
   const int d = G.ids[gi];
-  lt -= tb;
+  const int nt = G.tile_end[gi] - (gi ? G.tile_end[gi - 1] : 0);
+  const int local = g - base;
+  if (local >= nt * nslots) return false;
+  slot = s0 + local / nt;
+  const int lt = local - (local / nt) * nt;
   const int tx = K.det[d].tiles_x;
-  return CorrTile{d, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
+  T = CorrTile{d, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
+  return true;
 }
 
 // Software pipeline of k_corr_rw's step (PIPE): a detector row's taps in
@@ -339,28 +354,17 @@ struct RwPipe {
   }
 };
 
+// One wave's tile (the body of k_corr_rw and k_corr_rw_all).
 template <int KW, bool UNF>
-__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? 5 : 1, 8))) void k_corr_rw(const LmConst* __restrict__ Kp, const LmDetGroup G,
-                                                           const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
-                                                           const float* __restrict__ weights, int s0, int nslots,
-                                                           unsigned long long* __restrict__ keys,
-                                                           int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin,
-                                                           int64_t tailbin_slot_bytes) {
-  const LmConst& K = *Kp;
-  extern __shared__ uint4 lds_rw[];
+DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D, int slot, int oy0, int ox0,
+                                                float* ring, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                const float* __restrict__ weights,
+                                                unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
+                                                uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
   const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int per_slot = G.tile_end[G.n - 1];
-  const int g = blockIdx.x * LM_RW_WAVES + wave;
-  if (g >= per_slot * nslots) return;
-  const int slot = s0 + g / per_slot;
-  const CorrTile T = corr_tile_rw(K, G, g % per_slot);
-  const LmDet D = K.det[T.d];
-  const int oy0 = T.oy0, ox0 = T.ox0;
   constexpr int STR = rw_stride(KW);
   constexpr int NL = (3 + LM_TW + KW - 1 + 3) / 4;  // lanes that load a window row (4 bytes each)
   static_assert(NL <= 64, "window row wider than a wave's loads");
-  float* ring = reinterpret_cast<float*>(lds_rw) + wave * (LM_RW_SLOTS + 1) * STR;
   const int kh = D.kh, kwp = D.kwp;
   const int nrows = LM_RW_TH + kh - 1;
   const int ew = K.ext_w[D.view];
@@ -508,6 +512,53 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
           kl[off[k]] = ((unsigned long long)(~__float_as_uint(s)) << 32) | (unsigned)(y * D.ow + x);
         }
       }
+}
+
+// One launch per width group (LM_KW_LIST widths).
+template <int KW, bool UNF>
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? 5 : 1, 8))) void k_corr_rw(
+    const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+    const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
+    int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  extern __shared__ uint4 lds_rw[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int slot;
+  CorrTile T;
+  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, slot, T)) return;
+  float* ring = reinterpret_cast<float*>(lds_rw) + wave * (LM_RW_SLOTS + 1) * rw_stride(KW);
+  rw_tile<KW, UNF>(K, K.det[T.d], slot, T.oy0, T.ox0, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin,
+                   tailbin_slot_bytes);
+}
+
+// Every ring detector of the context in ONE launch (longest first), so the
+// widths share the launch's tail instead of each ending its own; each wave
+// branches to its width's body.  G.ring_floats: LDS floats per wave (the
+// widest detector's ring).
+template <bool UNF>
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_corr_rw_all(
+    const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+    const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
+    int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+  const LmConst& K = *Kp;
+  extern __shared__ uint4 lds_rw[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int slot;
+  CorrTile T;
+  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, slot, T)) return;
+  float* ring = reinterpret_cast<float*>(lds_rw) + wave * G.ring_floats;
+  const LmDet D = K.det[T.d];
+  switch (D.kw) {
+#define LM_KW_CASE(n)                                                                                             \
+  case n:                                                                                                         \
+    rw_tile<n, UNF>(K, D, slot, T.oy0, T.ox0, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, \
+                    tailbin_slot_bytes);                                                                          \
+    break;
+    LM_KW_LIST_RW_ALL(LM_KW_CASE)
+#undef LM_KW_CASE
+    default:
+      break;
+  }
 }
 
 // ---------------------------------------------------------------- k_corr_gen
@@ -799,12 +850,6 @@ static inline const void* corr_kernel_f16(int kw) {
 }
 
 // ---------------------------------------------------------------- dispatch
-// Widths with a specialised k_corr_pk (detectors up to 64 rows); every other
-// detector runs k_corr_gen.
-#define LM_KW_LIST(X)                                                                                             \
-  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
-      X(40) X(44) X(48) X(52) X(56) X(60) X(64)
-
 // k_corr_rw's ring does not depend on the detector height: every width of
 // LM_KW_LIST, any kh; other widths run k_corr_gen
 static inline bool corr_ring(int kw) {

@@ -222,10 +222,15 @@ struct lm_ctx {
   int64_t dbg_off[LM_NDET] = {0};
   int64_t gscratch_slot = 0;
   bool unfused = false;                                         // LM_FILTER_UNFUSED
-  std::vector<std::pair<const void*, LmDetGroup>> corr_groups;  // (correlation kernel, its detectors)
-  std::vector<size_t> corr_group_lds;                    // dynamic LDS bytes per group launch
-  std::vector<int> corr_group_threads;                   // block size per group launch
-  std::vector<char> corr_group_ring;                     // group runs k_corr_rw (one wave per tile)
+  // The correlation launches of a batch, two plans: [0] one k_corr_rw launch
+  // per detector width, [1] every ring detector in one k_corr_rw_all launch
+  // (see corr_plan_for)
+  struct CorrPlan {
+    std::vector<std::pair<const void*, LmDetGroup>> groups;  // (correlation kernel, its detectors)
+    std::vector<size_t> lds;                                 // dynamic LDS bytes per group launch
+    std::vector<int> threads;                                // block size per group launch
+    std::vector<char> ring;                                  // group runs k_corr_rw* (one wave per tile)
+  } corr_plan[2];
   // device buffers
   DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin;
   DevBuf<unsigned long long> tailmask;  // TAIL_MASK bitmaps, 64 columns per word
@@ -591,43 +596,52 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   // launch per width, every other detector in one k_corr_gen launch.  Each
   // launch gets exactly the LDS its detectors' rings / windows need, so narrow
   // groups keep more waves per CU.
-  c->corr_groups.clear();
-  c->corr_group_lds.clear();
-  c->corr_group_threads.clear();
-  c->corr_group_ring.clear();
-  for (int d = 0; d < 6; ++d) {
-    LmDet& D = K.det[d];
-    const bool f16 = su->corr_precision == LM_CORR_F16;
-    const bool ring = !f16 && corr_ring(D.kw);
-    const void* fn = f16 ? corr_kernel_f16(D.kw) : corr_kernel(D.kw, c->unfused);
-    size_t need;
-    if (f16) {
-      D.chunk_rows = D.kh;
-      need = f16_lds_bytes(f16_nch(D.kw), D.kh);
-    } else if (ring) {
-      D.chunk_rows = D.kh;
-      need = rw_lds_bytes(D.kw);
-    } else {
-      const size_t row = (size_t)pk_stride(LM_TW + D.kwp - 1) * sizeof(float);
-      D.chunk_rows = std::max(1, std::min(D.kh, (int)(kCorrLdsBudget / row) - (LM_TH - 1)));
-      need = (size_t)(LM_TH + D.chunk_rows - 1) * row;
+  // ring detectors ordered longest waves ((kh + 2) x kw taps) first
+  int order[6] = {0, 1, 2, 3, 4, 5};
+  std::stable_sort(order, order + 6, [&](int x, int y) {
+    return (int64_t)(K.det[x].kh + 2) * K.det[x].kw > (int64_t)(K.det[y].kh + 2) * K.det[y].kw;
+  });
+  for (int m = 0; m < 2; ++m) {
+    lm_ctx::CorrPlan& P = c->corr_plan[m];
+    P = lm_ctx::CorrPlan{};
+    for (int oi = 0; oi < 6; ++oi) {
+      const int d = order[oi];
+      LmDet& D = K.det[d];
+      const bool f16 = su->corr_precision == LM_CORR_F16;
+      const bool ring = !f16 && corr_ring(D.kw);
+      const void* fn = f16 ? corr_kernel_f16(D.kw)
+                       : ring && m == 1 ? (c->unfused ? (const void*)&k_corr_rw_all<true> : (const void*)&k_corr_rw_all<false>)
+                                        : corr_kernel(D.kw, c->unfused);
+      size_t need;
+      if (f16) {
+        D.chunk_rows = D.kh;
+        need = f16_lds_bytes(f16_nch(D.kw), D.kh);
+      } else if (ring) {
+        D.chunk_rows = D.kh;
+        need = rw_lds_bytes(D.kw);
+      } else {
+        const size_t row = (size_t)pk_stride(LM_TW + D.kwp - 1) * sizeof(float);
+        D.chunk_rows = std::max(1, std::min(D.kh, (int)(kCorrLdsBudget / row) - (LM_TH - 1)));
+        need = (size_t)(LM_TH + D.chunk_rows - 1) * row;
+      }
+      size_t gi = 0;
+      while (gi < P.groups.size() && P.groups[gi].first != fn) ++gi;
+      if (gi == P.groups.size()) {
+        LmDetGroup G;
+        std::memset(&G, 0, sizeof(G));
+        P.groups.push_back({fn, G});
+        P.lds.push_back(0);
+        P.threads.push_back(f16 ? LM_F16_THREADS : ring ? LM_RW_THREADS : LM_CORR_THREADS);
+        P.ring.push_back(ring);
+      }
+      LmDetGroup& G = P.groups[gi].second;
+      const int prev = G.n ? G.tile_end[G.n - 1] : 0;
+      G.ids[G.n] = d;
+      G.tile_end[G.n] = prev + D.tiles_x * D.tiles_y;
+      ++G.n;
+      if (ring) G.ring_floats = std::max(G.ring_floats, (LM_RW_SLOTS + 1) * rw_stride(D.kw));
+      P.lds[gi] = std::max(P.lds[gi], need);
     }
-    size_t gi = 0;
-    while (gi < c->corr_groups.size() && c->corr_groups[gi].first != fn) ++gi;
-    if (gi == c->corr_groups.size()) {
-      LmDetGroup G;
-      std::memset(&G, 0, sizeof(G));
-      c->corr_groups.push_back({fn, G});
-      c->corr_group_lds.push_back(0);
-      c->corr_group_threads.push_back(f16 ? LM_F16_THREADS : ring ? LM_RW_THREADS : LM_CORR_THREADS);
-      c->corr_group_ring.push_back(ring);
-    }
-    LmDetGroup& G = c->corr_groups[gi].second;
-    const int prev = G.n ? G.tile_end[G.n - 1] : 0;
-    G.ids[G.n] = d;
-    G.tile_end[G.n] = prev + D.tiles_x * D.tiles_y;
-    ++G.n;
-    c->corr_group_lds[gi] = std::max(c->corr_group_lds[gi], need);
   }
 
   // weights (float, rows zero-padded to kwp) and TM imadjust LUT
@@ -726,9 +740,9 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   for (int a = 0; a < 2; ++a) c->arena[a].alloc(cap, ns);
   c->h_pack.alloc((size_t)c->arena[0].pack_cap);
   HIPCHK(hipFuncSetAttribute((const void*)k_tail, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->tail_lds));
-  for (size_t g = 0; g < c->corr_groups.size(); ++g)
-    HIPCHK(hipFuncSetAttribute(c->corr_groups[g].first, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)c->corr_group_lds[g]));
+  for (const auto& P : c->corr_plan)
+    for (size_t g = 0; g < P.groups.size(); ++g)
+      HIPCHK(hipFuncSetAttribute(P.groups[g].first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds[g]));
 }
 
 
@@ -816,6 +830,23 @@ struct Timer {
 };
 
 // LM_KPROF=1: mean cycles per k_nms / k_tail phase over the batch's blocks (stderr)
+// Live contexts per device.  A context alone on its device runs the merged
+// correlation plan (one k_corr_rw_all launch: the widths share one tail
+// instead of ending four; one context 231k -> 260k frames/s at C3); with
+// several contexts the per-width launches interleave better with the other
+// contexts' post-correlation kernels (4 contexts: 340k vs 322k merged;
+// profiles/r02/merged/).  LM_CORR_PLAN=0 / 1 forces one.
+std::atomic<int> g_live_ctx[64];
+
+int corr_plan_for(const lm_ctx* c) {
+  static const int forced = [] {
+    const char* v = getenv("LM_CORR_PLAN");
+    return v ? atoi(v) : -1;
+  }();
+  if (forced == 0 || forced == 1) return forced;
+  return g_live_ctx[c->device & 63].load(std::memory_order_relaxed) <= 1 ? 1 : 0;
+}
+
 void kprof_report(lm_ctx* c, int n) {
   std::vector<long long> h((size_t)3 * 16 * 2 * c->nslots);
   COPY_SYNC(h.data(), c->kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
@@ -1029,6 +1060,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   // the key of c->graphs (frame pointers and slots reach the kernels through
   // k_prep's copies of mapped host arrays), so the chain is captured once per
   // key into a hipGraph and replayed.
+  const int plan = corr_plan_for(c);
   auto chain = [&](Arena& A, bool do_carry, int part) {  // part: 0 pre, 1 k_corr, 2 post, -1 all
     const int nproc = n + 1 - s_proc0;
     if (part <= 0) {
@@ -1055,12 +1087,12 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
     }
     if (part == 1 || part < 0) {
       T.begin("k_corr");
-      for (size_t gi = 0; gi < c->corr_groups.size(); ++gi) {
-        const auto& grp = c->corr_groups[gi];
+      const lm_ctx::CorrPlan& P = c->corr_plan[plan];
+      for (size_t gi = 0; gi < P.groups.size(); ++gi) {
+        const auto& grp = P.groups[gi];
         const LmDetGroup& G = grp.second;
         const void* w = c->setup.corr_precision == LM_CORR_F16 ? (const void*)c->weights16.p : (const void*)c->weights.p;
-        HIPCHK(launch_corr(grp.first, c->corr_group_ring[gi], dim3(G.tile_end[G.n - 1], nproc), c->corr_group_threads[gi],
-                           c->corr_group_lds[gi], st, dK, G, c->ext.p, c->ext_slot_bytes, w, s_proc0, c->keys.p,
+        HIPCHK(launch_corr(grp.first, P.ring[gi], dim3(G.tile_end[G.n - 1], nproc), P.threads[gi], P.lds[gi], st, dK, G, c->ext.p, c->ext_slot_bytes, w, s_proc0, c->keys.p,
                            c->npos.p, c->tailbin.p, c->tailbin_slot_bytes));
       }
       T.end();
@@ -1133,7 +1165,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       // Three graphs per key (before / k_corr / after), so the timing events
       // of k_corr (the roofline kernel) are recorded on the stream between
       // graph launches; the other kernels are not timed on this path.
-      const std::array<int, 7> key{n, cur, carry ? 1 : 0, carry ? c->last_n : 0, s_lut0, s_proc0, 0};
+      const std::array<int, 7> key{n, cur, carry ? 1 : 0, carry ? c->last_n : 0, s_lut0, s_proc0, plan};
       auto it = c->graphs.find(key);
       if (it == c->graphs.end()) {
         lm_ctx::GraphEntry ent{};
@@ -1319,11 +1351,13 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     delete c;
     return s;
   }
+  g_live_ctx[c->device & 63].fetch_add(1);
   *out = c;
   return LM_OK;
 }
 
 LM_API void lm_ctx_destroy(lm_ctx* ctx) {
+  if (ctx) g_live_ctx[ctx->device & 63].fetch_sub(1);
   delete ctx;
 }
 
