@@ -221,7 +221,9 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
 // operations execute in order, so the ring needs no barrier at all.  LDS per
 // wave is 17 rows (7.9 KB at KW = 30 vs 11.9 KB per wave for k_corr_pk's 48-row
 // window), any kh fits, and no wave waits for another.
+#ifndef LM_RW_WAVES
 #define LM_RW_WAVES 4
+#endif
 #define LM_RW_THREADS (64 * LM_RW_WAVES)
 #define LM_RW_TH 16     // output rows per wave tile
 #define LM_RW_SLOTS 16  // ring rows (+ 1 mirror)
