@@ -241,7 +241,12 @@ const char* lm_last_error(void);
 /* Create a context on HIP device `device`.  Copies background, calibration and
  * model weights to the device.  max_batch bounds n in lm_detect_batch*.
  * Fails with LM_ERR_INVALID_ARGUMENT on the reference's validation errors
- * (:35-249, :486-540, :3097-3140) and on use_provided_bounding_box == 0. */
+ * (:35-249, :486-540, :3097-3140) and on use_provided_bounding_box == 0.
+ * Contexts share no state; several may run concurrently from different host
+ * threads.  Results never depend on how many exist, but two scheduling
+ * choices do: contexts alternate between the highest and the lowest HIP
+ * stream priority, and a context alone on its device runs its correlation
+ * widths in one launch (several contexts: one launch per width). */
 lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_params* params,
                         const lm_model* model, int32_t max_batch, lm_ctx** out);
 void lm_ctx_destroy(lm_ctx* ctx);
