@@ -658,10 +658,13 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
 // Four waves side by side: a 128 x 64 output tile per workgroup.
 // Accumulator layout (32x32 MFMA): column = lane & 31, row = (reg & 3) +
 // 8 (reg >> 2) + 4 (lane >> 5).
-#define LM_F16_TW 128
+#ifndef LM_F16_WAVES
+#define LM_F16_WAVES 4  // waves side by side, 32 output columns each (5: -4 % k_corr at C5 but fewer frames/s; C3 worse)
+#endif
+#define LM_F16_TW (32 * LM_F16_WAVES)
 #define LM_F16_TH 64
 #define LM_F16_T 2      // 32-row accumulator tiles per wave
-#define LM_F16_THREADS 256
+#define LM_F16_THREADS (64 * LM_F16_WAVES)
 #define LM_F16_MAX_NCH 10
 
 typedef _Float16 lm_h8 __attribute__((ext_vector_type(8)));
