@@ -372,6 +372,9 @@ def main():
         "config": {"workload": workload,
                    "batch_frames": B, "streams_per_gpu": NS, "frames_per_rank": args.steps * B * NS,
                    "resident_frames_per_stream": R,
+                   "stream_priorities": "alternating high/low" if os.environ.get("LM_STREAM_PRIO", "1") != "0" else "equal",
+                   "corr_launches": ("one merged launch" if NS == 1 else "one per detector width")
+                   if os.environ.get("LM_CORR_PLAN") not in ("0", "1") else f"LM_CORR_PLAN={os.environ['LM_CORR_PLAN']}",
                    "parallelism": f"frame shards x{world} (no collective)"},
         "hbm_gbs": round(fps * FRAME_BYTES / 1e9, 3),
         "roofline": {"bound": "mfma",
