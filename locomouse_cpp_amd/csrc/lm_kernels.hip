@@ -1230,6 +1230,14 @@ DEV void for_overflow_pairs(int npairs, Pred overflow, Fn fn) {
 // small grid that walks all npairs (slot, feature) pairs — usually none
 // qualifies, so it costs a launch and a few header reads.  One kernel
 // holding both paths ran the common one slower (register allocation).
+// LM_KPROF=1: clock64() of thread 0 per k_post phase (LDS instantiation),
+// 16 per (frame, feature) block; null otherwise
+__device__ long long* g_post_prof;
+#define POST_PROF(k)                                                                           \
+  if (!G && threadIdx.x == 0) {                                                                \
+    long long* pp_ = g_post_prof;                                                              \
+    if (pp_) pp_[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = (k) >= 14 ? wall_clock64() : clock64(); \
+  }
 template <bool GLOB>
 __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
                                                        const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
@@ -1256,35 +1264,59 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
 #define LM_POST_MAXC 512     // candidates per list handled in LDS
 #define LM_POST_MAXOFF 2048  // CSC columns (Ni + Nong) + 1
 
+// checkVelCriterion (:1256-1267): sum(sat_u8(I - I_prev) > 25) >= area*alpha,
+// by one whole wave (called with every lane active, arguments wave-uniform):
+// the rectangle's pixels are shared out over the lanes and counted with a
+// ballot per round, so a check costs a few dependent load chains
+// (calibration -> frame -> LUT) instead of one per pixel.
 template <class FP>
-DEV bool vel_criterion(const LmConst& K, FP Fc, FP Fp, const uint8_t* bkg, const int32_t* cal,
-                       const uint8_t* lutc, const uint8_t* lutp, const LmSlot& slc, const LmSlot& slp, int crop_x,
-                       int crop_y, int crop_w, int crop_h,
-                       int bx, int by, int bwid, int bhei, int area, double alpha, int32_t* err, int tag) {
-  // checkVelCriterion (:1256-1267): sum(sat_u8(I - I_prev) > 25) >= area*alpha
+DEV bool vel_criterion_wave(const LmConst& K, FP Fc, FP Fp, const uint8_t* bkg, const int32_t* cal,
+                            const uint8_t* lutc, const uint8_t* lutp, const LmSlot& slc, const LmSlot& slp, int crop_x,
+                            int crop_y, int crop_w, int crop_h, int bx, int by, int bwid, int bhei, int area,
+                            double alpha, int32_t* err, int tag) {
+  const int lane = threadIdx.x & 63;
   if (bx < 0 || by < 0 || bwid < 0 || bhei < 0 || bx + bwid > crop_w || by + bhei > crop_h) {
-    atomicOr(err, 4);  // cv::Mat ROI assertion in the reference
-    if (atomicCAS(&err[1], 0, 1) == 0) {  // first offender, for the error message
-      err[2] = tag;
-      err[3] = bx;
-      err[4] = by;
-      err[5] = bwid;
-      err[6] = bhei;
-      err[7] = crop_w;
-      err[8] = crop_h;
+    if (lane == 0) {
+      atomicOr(err, 4);  // cv::Mat ROI assertion in the reference
+      if (atomicCAS(&err[1], 0, 1) == 0) {  // first offender, for the error message
+        err[2] = tag;
+        err[3] = bx;
+        err[4] = by;
+        err[5] = bwid;
+        err[6] = bhei;
+        err[7] = crop_w;
+        err[8] = crop_h;
+      }
     }
     return false;
   }
+  const int n = bwid * bhei;
   int sum = 0;
-  for (int r = 0; r < bhei; ++r)
-    for (int c = 0; c < bwid; ++c) {
+  for (int p0 = 0; p0 < n; p0 += 64) {
+    const int p = p0 + lane;
+    bool hit = false;
+    if (p < n) {
+      const int r = p / bwid, c = p - r * bwid;
       const int R = crop_y + by + r, C = crop_x + bx + c;
       const int a = ipad_pixel_t(Fc, bkg, cal, lutc, K, slc, R, C);  // I_*_MOUSE_PAD
       const int b = ipad_pixel_t(Fp, bkg, cal, lutp, K, slp, R, C);  // I_*_MOUSE_PAD_PREV
-      const int s = a > b ? a - b : 0;
-      sum += s > 25;
+      hit = (a > b ? a - b : 0) > 25;
     }
+    sum += __popcll(__ballot(hit));
+  }
   return (double)sum >= ((double)area) * alpha;
+}
+
+// Bump allocation of `amount` entries of arena k from sub-arena g (one
+// thread): the offset, or -1 with the overflow flag set.
+DEV int arena_alloc(LmArenaCtl* __restrict__ ctl, int k, int g, int amount) {
+  const int part = ctl->cap[k] / LM_SUBARENA;
+  const int b = atomicAdd(&ctl->sub[g][k], amount);
+  if (b + amount > part) {
+    atomicOr(&ctl->overflow, 1);
+    return -1;
+  }
+  return g * part + b;
 }
 
 // The body of k_post on its working arrays: candidate copies and per-list
@@ -1300,17 +1332,14 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
                   int cap, int* s_base, int& s_any1, int& s_any0, LmP22D* __restrict__ arena_p22d,
                   int32_t* __restrict__ arena_side_y, double* __restrict__ arena_side_s, double* __restrict__ arena_unary,
                   int32_t* __restrict__ arena_jc, int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
-                  LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err) {
+                  LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err, int sub) {
+  POST_PROF(14)
+  POST_PROF(0)
   // ---------------- unary (unaryCostBox :1909-1952), column-major Nb x nprior
   const int nprior = feat == 0 ? 4 : 1;
   const int p0 = feat == 0 ? 0 : 4;
   if (threadIdx.x == 0) {
-    int b = atomicAdd(&ctl->used[AR_UNARY], Nb * nprior);
-    if (b + Nb * nprior > ctl->cap[AR_UNARY]) {
-      atomicOr(&ctl->overflow, 1);
-      b = -1;
-    }
-    s_base[0] = b;
+    s_base[0] = arena_alloc(ctl, AR_UNARY, sub, Nb * nprior);
   }
   __syncthreads();
   if (s_base[0] >= 0) {
@@ -1335,6 +1364,7 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
     H->unary_cnt[feat] = Nb * nprior;
   }
 
+  POST_PROF(1)
   // ---------------- pairwise (pairwisePotential :1954-2070) when frame > 0
   if (frame > 0) {
     const int Nong = K.ong_nx * K.ong_ny;
@@ -1355,6 +1385,10 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
       double inv = 1 - (dist / maxd);
       return inv * alpha;
     };
+    // each bottom candidate's ONG node once (s_mb is free until the matching)
+    int* s_ong = s_mb;
+    for (int j = threadIdx.x; j < Nb; j += blockDim.x) s_ong[j] = ong_of(sb[j]);
+    __syncthreads();
     // column counts -> Jc
     for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
       int cnt = 0;
@@ -1363,31 +1397,40 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
         cnt += occ != 0.0;
       } else {
         const int q = c - Ni;
-        if (Ni > 0)
-          for (int j = 0; j < Nb; ++j) cnt += (ong_of(sb[j]) == q && occ != 0.0);
+        if (Ni > 0 && occ != 0.0)
+          for (int j = 0; j < Nb; ++j) cnt += s_ong[j] == q;
         cnt += occ != 0.0;
       }
       s_off[c] = cnt;
     }
     __syncthreads();
+    // exclusive scan of the counts by the first wave, 64 columns a round
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      int carry = 0;
+      for (int c0 = 0; c0 < ncols; c0 += 64) {
+        const int c = c0 + lane;
+        const int t = c < ncols ? s_off[c] : 0;
+        int v = t;  // inclusive wave scan
+        for (int o = 1; o < 64; o <<= 1) {
+          const int u = __shfl_up(v, o);
+          if (lane >= o) v += u;
+        }
+        if (c < ncols) s_off[c] = carry + v - t;
+        carry += __shfl(v, 63);
+      }
+      if (lane == 0) s_off[ncols] = carry;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-      int acc = 0;
-      for (int c = 0; c < ncols; ++c) {
-        const int t = s_off[c];
-        s_off[c] = acc;
-        acc += t;
-      }
-      s_off[ncols] = acc;
-      int bj = atomicAdd(&ctl->used[AR_PWJC], ncols + 1);
-      int bn = atomicAdd(&ctl->used[AR_PWNZ], acc);
-      if (bj + ncols + 1 > ctl->cap[AR_PWJC] || bn + acc > ctl->cap[AR_PWNZ]) {
-        atomicOr(&ctl->overflow, 1);
-        bj = -1;
-      }
-      s_base[1] = bj;
+      const int acc = s_off[ncols];
+      const int bj = arena_alloc(ctl, AR_PWJC, sub, ncols + 1);
+      const int bn = arena_alloc(ctl, AR_PWNZ, sub, acc);
+      s_base[1] = bn < 0 ? -1 : bj;
       s_base[2] = bn;
     }
     __syncthreads();
+    POST_PROF(2)
     const int bj = s_base[1], bn = s_base[2];
     if (bj >= 0) {
       for (int c = threadIdx.x; c <= ncols; c += blockDim.x) arena_jc[bj + c] = s_off[c];
@@ -1411,7 +1454,7 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
           const int q = c - Ni;
           if (Ni > 0 && occ != 0.0)
             for (int j = 0; j < Nb; ++j)
-              if (ong_of(sb[j]) == q) {
+              if (s_ong[j] == q) {
                 arena_ir[o] = j;
                 arena_pr[o] = occ;
                 ++o;
@@ -1440,6 +1483,7 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
     H->pw_nz_off[feat] = 0;
   }
 
+  POST_PROF(3)
   // ---------------- matching (:1023-1254)
   const int ovlp = (int)(K.size_b[feat][0] * (1 - K.side_bottom_min_overlap));
   const bool vel_check = frame > 0;
@@ -1473,6 +1517,7 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
     s_tpb[i] = s;
   }
   __syncthreads();
+  POST_PROF(4)
   // motion status where the reference evaluates it
   const LmSlot sl = slots[slot], slp = slots[slot - 1];
   const lm_gu8* Fc = as_global(frame_ptr[slot]);
@@ -1482,25 +1527,42 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
   const int* mbox = K.match_b[feat];
   const int* tbox = K.match_s[feat];
   if (vel_check) {
+    // which candidates the reference tests (-2: pending), then one wave per test
     for (int i = threadIdx.x; i < Nb; i += blockDim.x) {
       bool need = false;
       for (int j = 0; j < Ns; ++j) need |= boolD(i, j) && s_bps[j] > 1;
-      if (need)
-        s_mb[i] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl, slp, sl.crop_x[0], sl.crop_y[0], K.crop_w[0], K.crop_h[0],
-                                mbox[0] + sb[i].x + K.spre_b_w, mbox[1] + sb[i].y + K.spre_b_h, mbox[2], mbox[3],
-                                K.size_b[feat][0] * K.size_b[feat][1], 0.02, err, (slot << 16) | (feat << 12) | i);
+      if (need) s_mb[i] = -2;
     }
     for (int j = threadIdx.x; j < Ns; j += blockDim.x) {
       bool need = false;
       if (s_bps[j] > 1)
         for (int i = 0; i < Nb; ++i) need |= boolD(i, j);
-      if (need)
-        s_mt[j] = vel_criterion(K, Fc, Fp, bkg, cal, lutc, lutp, sl, slp, sl.crop_x[1], sl.crop_y[1], K.crop_w[1], K.crop_h[1],
-                                tbox[0] + st[j].x + K.spre_t_w, tbox[1] + st[j].y + K.spre_t_h, tbox[2], tbox[3],
-                                K.size_s[feat][0] * K.size_s[feat][1], 0.05, err, (slot << 16) | (feat << 12) | 0x800 | j);
+      if (need) s_mt[j] = -2;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int k = wid; k < Nb + Ns; k += nw) {
+      if (k < Nb) {
+        const int i = k;
+        if (s_mb[i] != -2) continue;
+        const bool m = vel_criterion_wave(K, Fc, Fp, bkg, cal, lutc, lutp, sl, slp, sl.crop_x[0], sl.crop_y[0], K.crop_w[0],
+                                          K.crop_h[0], mbox[0] + sb[i].x + K.spre_b_w, mbox[1] + sb[i].y + K.spre_b_h,
+                                          mbox[2], mbox[3], K.size_b[feat][0] * K.size_b[feat][1], 0.02, err,
+                                          (slot << 16) | (feat << 12) | i);
+        if (lane == 0) s_mb[i] = m;
+      } else {
+        const int j = k - Nb;
+        if (s_mt[j] != -2) continue;
+        const bool m = vel_criterion_wave(K, Fc, Fp, bkg, cal, lutc, lutp, sl, slp, sl.crop_x[1], sl.crop_y[1], K.crop_w[1],
+                                          K.crop_h[1], tbox[0] + st[j].x + K.spre_t_w, tbox[1] + st[j].y + K.spre_t_h,
+                                          tbox[2], tbox[3], K.size_s[feat][0] * K.size_s[feat][1], 0.05, err,
+                                          (slot << 16) | (feat << 12) | 0x800 | j);
+        if (lane == 0) s_mt[j] = m;
+      }
     }
   }
   __syncthreads();
+  POST_PROF(5)
   const double walpha = -(1. / (double)ovlp);
   auto matches = [&](int i, int j) {
     if (!boolD(i, j)) return false;
@@ -1523,13 +1585,9 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
       acc += t;
     }
     s_off[Nb] = acc;
-    int bp = atomicAdd(&ctl->used[AR_P22D], Nb);
-    int bs = atomicAdd(&ctl->used[AR_SIDE], acc);
-    if (bp + Nb > ctl->cap[AR_P22D] || bs + acc > ctl->cap[AR_SIDE]) {
-      atomicOr(&ctl->overflow, 1);
-      bp = -1;
-    }
-    s_base[0] = bp;
+    const int bp = arena_alloc(ctl, AR_P22D, sub, Nb);
+    const int bs = arena_alloc(ctl, AR_SIDE, sub, acc);
+    s_base[0] = bs < 0 ? -1 : bp;
     s_base[1] = bs;
   }
   __syncthreads();
@@ -1574,6 +1632,8 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
       arena_p22d[bp + i] = p;
     }
   }
+  POST_PROF(6)
+  POST_PROF(15)
   if (threadIdx.x == 0) {
     H->p22d_off[feat] = bp;
     H->p22d_cnt[feat] = Nb;
@@ -1625,7 +1685,7 @@ DEV void post_block(int bx, int feat, LM_POST_ARGS) {
     __syncthreads();
     post_run<false>(K, slots, frame_ptr, bkg, cal, luts, H, slot, feat, frame, Nb, Ns, Ni, sb, st, sp, s_off, s_mb, s_mt,
                     s_bps, s_tpb, LM_POST_MAXC, s_base, s_any1, s_any0, arena_p22d, arena_side_y, arena_side_s,
-                    arena_unary, arena_jc, arena_ir, arena_pr, ctl, err);
+                    arena_unary, arena_jc, arena_ir, arena_pr, ctl, err, (2 * bx + feat) % LM_SUBARENA);
   } else {  // long lists: k_nms's scratch of this (slot, feature) is free again
     const int big = max(max(Nb, Ns), Ni);
     int* g = reinterpret_cast<int*>(gscratch + (int64_t)(feat + 2 * bx) * gscratch_slot);
@@ -1640,7 +1700,7 @@ DEV void post_block(int bx, int feat, LM_POST_ARGS) {
     }
     post_run<true>(K, slots, frame_ptr, bkg, cal, luts, H, slot, feat, frame, Nb, Ns, Ni, cb, ct, cp, g_off, g_mb, g_mt,
                    g_bps, g_tpb, big, s_base, s_any1, s_any0, arena_p22d, arena_side_y, arena_side_s, arena_unary,
-                   arena_jc, arena_ir, arena_pr, ctl, err);
+                   arena_jc, arena_ir, arena_pr, ctl, err, (2 * bx + feat) % LM_SUBARENA);
   }
 }
 
@@ -1702,7 +1762,12 @@ __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots
   }
   for (int i = threadIdx.x; i < ns * LM_NLIST; i += blockDim.x) npos[i] = 0;
   if (threadIdx.x < 16) err[threadIdx.x] = 0;
-  if (threadIdx.x == 0) *ctl = *h_ctl;
+  if (threadIdx.x < AR_COUNT) {
+    ctl->used[threadIdx.x] = h_ctl->used[threadIdx.x];
+    ctl->cap[threadIdx.x] = h_ctl->cap[threadIdx.x];
+  }
+  if (threadIdx.x == 0) ctl->overflow = h_ctl->overflow;
+  for (int i = threadIdx.x; i < LM_SUBARENA * 32; i += blockDim.x) (&ctl->sub[0][0])[i] = 0;
 }
 
 // k_out: the pack header always, and when the batch succeeded and its packed
@@ -1800,7 +1865,11 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const LmSlotOut* __restrict_
     ph->bytes = L.bytes;
     ph->overflow = (L.bytes > pack_cap ? 1 : 0) | (ctl->overflow ? 2 : 0);
     ph->err = *err;
-    for (int k = 0; k < AR_COUNT; ++k) ph->used[k] = ctl->used[k];
+    for (int k = 0; k < AR_COUNT; ++k) {
+      int m = 0;
+      for (int g = 0; g < LM_SUBARENA; ++g) m = max(m, ctl->sub[g][k]);
+      ph->used[k] = m * LM_SUBARENA;
+    }
   }
 }
 

@@ -848,8 +848,36 @@ int corr_plan_for(const lm_ctx* c) {
 }
 
 void kprof_report(lm_ctx* c, int n) {
-  std::vector<long long> h((size_t)3 * 16 * 2 * c->nslots);
+  std::vector<long long> h((size_t)4 * 16 * 2 * c->nslots);
   COPY_SYNC(h.data(), c->kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
+  {  // k_post (LDS instantiation): region 3, one block per (frame, feature)
+    const long long* base = h.data() + (size_t)3 * 16 * 2 * c->nslots;
+    double acc[8] = {0}, life = 0;
+    int nb = 0;
+    long long t_min = 0, t_max = 0, worst = 0;
+    int wb = -1;
+    for (int b = 0; b < 2 * n; ++b) {
+      const long long* t = base + (size_t)b * 16;
+      if (!t[0] || !t[6]) continue;
+      for (int k = 1; k <= 6; ++k) acc[k] += (double)(t[k] - t[k - 1]);
+      life += (double)(t[6] - t[0]);
+      if (t[6] - t[0] > worst) {
+        worst = t[6] - t[0];
+        wb = b;
+      }
+      t_min = t_min ? std::min(t_min, t[14]) : t[14];
+      t_max = std::max(t_max, t[15]);
+      ++nb;
+    }
+    if (nb) {
+      fprintf(stderr, "kprof k_post: blocks=%d life=%.0f cyc, span=%.1f us:", nb, life / nb, (t_max - t_min) * 0.01);
+      for (int k = 1; k <= 6; ++k) fprintf(stderr, " p%d=%.0f", k, acc[k] / nb);
+      const long long* t = base + (size_t)wb * 16;
+      fprintf(stderr, " | slowest blk %d cyc=%lld:", wb, worst);
+      for (int k = 1; k <= 6; ++k) fprintf(stderr, " %lld", t[k] - t[k - 1]);
+      fprintf(stderr, "\n");
+    }
+  }
   {  // k_tail: region 2, one block per processed slot
     const long long* base = h.data() + (size_t)2 * 16 * 2 * c->nslots;
     double acc[16] = {0}, life = 0, wlife = 0, runs = 0;
@@ -1114,8 +1142,10 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
       }
       long long *kp0 = nullptr, *kp1 = nullptr, *kp2 = nullptr;
       if (c->kprof_on) {
-        if (!c->kprof.p) c->kprof.alloc((size_t)3 * 16 * 2 * c->nslots);
-        HIPCHK(hipMemsetAsync(c->kprof.p, 0, sizeof(long long) * 3 * 16 * 2 * c->nslots, st));
+        if (!c->kprof.p) c->kprof.alloc((size_t)4 * 16 * 2 * c->nslots);
+        HIPCHK(hipMemsetAsync(c->kprof.p, 0, sizeof(long long) * 4 * 16 * 2 * c->nslots, st));
+        long long* pp = c->kprof.p + 3 * 16 * 2 * c->nslots;
+        HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_post_prof), &pp, sizeof(pp), 0, hipMemcpyHostToDevice, st));
         kp0 = c->kprof.p;
         kp1 = c->kprof.p + 16 * 2 * c->nslots;
         kp2 = c->kprof.p + 2 * 16 * 2 * c->nslots;
