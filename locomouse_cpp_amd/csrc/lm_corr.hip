@@ -258,7 +258,7 @@ DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s
   return true;
 }
 
-// Software pipeline of k_corr_rw's step (PIPE): a detector row's taps in
+// Software pipeline of k_corr_rw's step: a detector row's taps in
 // chunks (the first of 8 taps, the others of <= 12); while a chunk's FMAs run,
 // the pixel pairs and weights of the next chunk (the next step's first chunk
 // after the last) are already in flight, so a wave waits on LDS / scalar
