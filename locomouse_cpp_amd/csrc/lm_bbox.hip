@@ -3,7 +3,8 @@
 // (LocoMouse_class.cpp:579-653) with computeMouseBox (:948-997),
 // largestBWAreaObject (:921-946), firstLastOverT (LocoMouse_class.hpp:411-440),
 // computeMouseBoxSize (:1481-1506), medianvec / stdvec / vecmovingaverage
-// (:1516-1608).  Included by lm_runtime.hip (one translation unit).
+// (:1516-1608).  Its own translation unit of liblocomouse_hip.so; k_minmax /
+// k_lut come from lm_kernels.hip through launch_minmax_lut (lm_host.h).
 //
 // Exact reformulation on 0/1 images.  medianBlur is a rank filter and the
 // threshold after it (:955, v > 2.55 <=> v >= 3) is monotone, so
@@ -27,6 +28,20 @@
 //                 has too many runs), row/column counts, firstLastOverT
 // The host turns the limits into computeMouseBox's six values and runs the
 // whole-video post-processing in lm_bb_finish.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "locomouse_hip.h"
+#include "lm_device.h"
+#include "lm_dev_common.h"
+#include "lm_host.h"
+#include "lm_cc.h"
 
 struct LmBBConst {
   int32_t n_rows, n_cols;  // corrected image
@@ -1144,8 +1159,7 @@ void bb_push(lm_bb_ctx* c, const uint8_t* frames, int64_t pitch, int n, bool dev
     }
   }
   const int64_t np = (int64_t)K.n_rows * K.n_cols;
-  k_minmax<<<dim3(LM_MM_SPLIT, n), LM_MM_THREADS, 0, s>>>(c->fptr.d, c->bkg.p, (int)c->npix, 0, c->mm.p);
-  k_lut<<<(n + 3) / 4, 256, 0, s>>>(c->mm.p, 0, n, nullptr, 0, c->luts.p);
+  HIPCHK(launch_minmax_lut(c->fptr.d, c->bkg.p, (int)c->npix, 0, n, c->mm.p, nullptr, 0, c->luts.p, s));
   if (c->method == 2) {
     k_bb_de<<<n, 1024, 4 * K.n_cols, s>>>(K, c->fptr.d, c->bkg.p, c->cal.p, c->luts.p, c->bbx.d);
     HIPCHK(hipGetLastError());

@@ -1,0 +1,91 @@
+// lm_corr.h — the correlation (filter2D) kernels' shared constants and the
+// host-side dispatch that lm_corr.hip (its own translation unit) exports to
+// the runtime (lm_runtime.hip).  See lm_corr.hip for the kernels.
+#ifndef LM_CORR_H
+#define LM_CORR_H
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "lm_device.h"
+
+#define LM_CORR_THREADS 192
+#define PK_C 5  // columns per thread
+#define PK_R 4  // rows per thread (two packed row pairs)
+
+// LDS row stride: == 4 (mod 8) so the two 16-lane row groups of a
+// ds_read2_b32 (4 rows apart) hit disjoint bank halves.
+__host__ __device__ constexpr int pk_stride(int cols) { return cols + ((4 - (cols & 7)) + 8) % 8; }
+
+struct LmDetGroup {
+  int32_t n;
+  int32_t ids[LM_NDET];
+  int32_t tile_end[LM_NDET];  // cumulative tile counts
+  int32_t ring_floats;        // k_corr_rw_all: LDS floats per wave
+};
+
+// Widths with a width-specialised k_corr_rw (any height); every other
+// detector runs k_corr_gen.
+#define LM_KW_LIST(X)                                                                                             \
+  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
+      X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+#define LM_KW_LIST_RW_ALL LM_KW_LIST
+
+// k_corr_rw: one wave per 80 x 16 output tile, LM_RW_WAVES waves per workgroup
+#ifndef LM_RW_WAVES
+#define LM_RW_WAVES 4
+#endif
+#define LM_RW_THREADS (64 * LM_RW_WAVES)
+#define LM_RW_TH 16     // output rows per wave tile
+#define LM_RW_SLOTS 16  // ring rows (+ 1 mirror)
+
+// window row: 80 + KW - 1 columns plus up to 3 before them (the loads start on
+// a 4-byte boundary); stride == 4 (mod 8)
+__host__ __device__ constexpr int rw_stride(int kw) { return pk_stride(LM_TW + kw - 1 + 3); }
+__host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
+  return (size_t)LM_RW_WAVES * (LM_RW_SLOTS + 1) * rw_stride(kw) * sizeof(float);
+}
+
+// k_corr_f16 (non-parity LM_CORR_F16 mode)
+#ifndef LM_F16_WAVES
+#define LM_F16_WAVES 4  // waves side by side, 32 output columns each (5: -4 % k_corr at C5 but fewer frames/s; C3 worse)
+#endif
+#define LM_F16_TW (32 * LM_F16_WAVES)
+#define LM_F16_TH 64
+#define LM_F16_T 2  // 32-row accumulator tiles per wave
+#define LM_F16_THREADS (64 * LM_F16_WAVES)
+#define LM_F16_MAX_NCH 10
+
+__host__ __device__ constexpr int f16_nch(int kw) { return (kw + 31 + 15) / 16; }
+__host__ __device__ constexpr int f16_cols(int nch) { return LM_F16_TW - 32 + 16 * nch; }
+__host__ __device__ constexpr int f16_stride(int cols) { return (cols + 7) / 16 * 16 + 8; }
+__host__ __device__ constexpr size_t f16_lds_bytes(int nch, int kh) {
+  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2 + (size_t)2 * nch * 64 * 16;
+}
+// Host: the B fragment of (row i, chunk c) for lane l, element j (0 off the band).
+static inline float f16_bfrag_weight(const double* w, int kw, int i, int c, int l, int j) {
+  const int r = l & 31, h = l >> 5, jj = 16 * c + 8 * h + j - r;
+  return (jj >= 0 && jj < kw) ? (float)w[(size_t)i * kw + jj] : 0.0f;
+}
+
+// ---- host dispatch (defined in lm_corr.hip)
+// k_corr_rw's ring does not depend on the detector height: every width of
+// LM_KW_LIST, any kh; other widths run k_corr_gen
+bool corr_ring(int kw);
+const void* corr_kernel(int kw, bool unf);     // k_corr_rw<kw> or k_corr_gen
+const void* corr_kernel_rw_all(bool unf);      // every ring width in one launch
+const void* corr_kernel_f16(int kw);           // nullptr when kw is too wide
+// Launch the correlation for one detector group (`weights`: the fp32 rows, or
+// the f16 B fragments for k_corr_f16).  Ring kernels take one wave per tile
+// with the batch's tiles flattened (grid.y = slot count); the others one
+// workgroup per (tile, slot).
+hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t lds, hipStream_t st, const LmConst* K,
+                       const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes, const void* weights, int s0,
+                       unsigned long long* keys, int32_t* n_pos, uint8_t* tailbin, int64_t tailbin_slot_bytes);
+// Diagnostics: raw scores of every detector of slots s0 .. s0 + grid.y - 1.
+hipError_t launch_corr_dbg(bool unf, dim3 grid, hipStream_t st, const LmConst* K, const uint8_t* ext,
+                           int64_t ext_slot_bytes, const float* weights, int s0, float* dbg, const int64_t* dbg_off,
+                           int64_t dbg_slot_floats);
+
+#endif  // LM_CORR_H

@@ -1,4 +1,5 @@
-// lm_corr.hip — the six filter2D detectors (included by lm_kernels.hip).
+// lm_corr.hip — the six filter2D detectors (its own translation unit; the
+// runtime reaches it through the dispatch functions declared in lm_corr.h).
 //
 // cv::filter2D(I_VIEW_PAD, scores, CV_32F, W, Point(-1,-1), -rho, BORDER_CONSTANT)
 // at LocoMouse_class.cpp:845, :860, :2575, :2576, restated as
@@ -22,9 +23,14 @@
 //   k_corr_dbg<UNF>     raw scores straight from the ext crops in global memory
 //                       (diagnostics: lm_debug_scores).
 
-#define LM_CORR_THREADS 192
-#define PK_C 5   // columns per thread
-#define PK_R 4   // rows per thread (two packed row pairs)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "lm_corr.h"
+
+#define DEV __device__ __forceinline__
 
 typedef float lm_f2 __attribute__((ext_vector_type(2)));
 
@@ -118,17 +124,6 @@ DEV void corr_epilogue(const LmConst& K, const LmDet& D, const float (&acc)[R_][
       }
 }
 
-// LDS row stride: == 4 (mod 8) so the two 16-lane row groups of a
-// ds_read2_b32 (4 rows apart) hit disjoint bank halves.
-__host__ __device__ constexpr int pk_stride(int cols) { return cols + ((4 - (cols & 7)) + 8) % 8; }
-
-struct LmDetGroup {
-  int32_t n;
-  int32_t ids[LM_NDET];
-  int32_t tile_end[LM_NDET];  // cumulative tile counts
-  int32_t ring_floats;        // k_corr_rw_all: LDS floats per wave
-};
-
 // Tile fill: u8 ext-crop window (rows x cols from src, row pitch ew) -> fp32
 // LDS (row stride `stride`).  16-byte aligned vector loads, all of a round
 // issued before any is consumed (a workgroup's fill is one or two load
@@ -197,13 +192,6 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
          (int64_t)(D.in_y + oy0) * K.ext_w[D.view] + (D.in_x + ox0);
 }
 
-// Widths with a width-specialised k_corr_rw (any height); every other
-// detector runs k_corr_gen.
-#define LM_KW_LIST(X)                                                                                             \
-  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
-      X(40) X(44) X(48) X(52) X(56) X(60) X(64)
-#define LM_KW_LIST_RW_ALL LM_KW_LIST
-
 // ---------------------------------------------------------------- k_corr_rw
 // Packed-FP32 correlation.  gfx950 issues one v_fma_f32 (wave64) per 4 cycles
 // per SIMD; v_pk_fma_f32 does two FMAs per lane in the same slot.  Each
@@ -221,20 +209,6 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
 // operations execute in order, so the ring needs no barrier at all.  LDS per
 // wave is 17 rows (7.9 KB at KW = 30 vs 11.9 KB per wave for k_corr_pk's 48-row
 // window), any kh fits, and no wave waits for another.
-#ifndef LM_RW_WAVES
-#define LM_RW_WAVES 4
-#endif
-#define LM_RW_THREADS (64 * LM_RW_WAVES)
-#define LM_RW_TH 16     // output rows per wave tile
-#define LM_RW_SLOTS 16  // ring rows (+ 1 mirror)
-
-// window row: 80 + KW - 1 columns plus up to 3 before them (the loads start on
-// a 4-byte boundary); stride == 4 (mod 8) as in k_corr_pk
-__host__ __device__ constexpr int rw_stride(int kw) { return pk_stride(LM_TW + kw - 1 + 3); }
-__host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
-  return (size_t)LM_RW_WAVES * (LM_RW_SLOTS + 1) * rw_stride(kw) * sizeof(float);
-}
-
 // Wave g of a launch -> (slot, detector, tile origin).  The batch's tiles
 // are flattened detector-major (all slots of the group's first detector,
 // then the next ...), so no wave idles at a frame's end and the host can
@@ -658,29 +632,8 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
 // Four waves side by side: a 128 x 64 output tile per workgroup.
 // Accumulator layout (32x32 MFMA): column = lane & 31, row = (reg & 3) +
 // 8 (reg >> 2) + 4 (lane >> 5).
-#ifndef LM_F16_WAVES
-#define LM_F16_WAVES 4  // waves side by side, 32 output columns each (5: -4 % k_corr at C5 but fewer frames/s; C3 worse)
-#endif
-#define LM_F16_TW (32 * LM_F16_WAVES)
-#define LM_F16_TH 64
-#define LM_F16_T 2      // 32-row accumulator tiles per wave
-#define LM_F16_THREADS (64 * LM_F16_WAVES)
-#define LM_F16_MAX_NCH 10
-
 typedef _Float16 lm_h8 __attribute__((ext_vector_type(8)));
 typedef float lm_f32x16 __attribute__((ext_vector_type(16)));
-
-__host__ __device__ constexpr int f16_nch(int kw) { return (kw + 31 + 15) / 16; }
-__host__ __device__ constexpr int f16_cols(int nch) { return LM_F16_TW - 32 + 16 * nch; }
-__host__ __device__ constexpr int f16_stride(int cols) { return (cols + 7) / 16 * 16 + 8; }
-__host__ __device__ constexpr size_t f16_lds_bytes(int nch, int kh) {
-  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2 + (size_t)2 * nch * 64 * 16;
-}
-// Host: the B fragment of (row i, chunk c) for lane l, element j (0 off the band).
-static inline float f16_bfrag_weight(const double* w, int kw, int i, int c, int l, int j) {
-  const int r = l & 31, h = l >> 5, jj = 16 * c + 8 * h + j - r;
-  return (jj >= 0 && jj < kw) ? (float)w[(size_t)i * kw + jj] : 0.0f;
-}
 
 // u8 window -> f16 LDS (same loads as tile_fill_f32, one half per pixel).
 DEV void tile_fill_f16(_Float16* __restrict__ lds, int stride, const uint8_t* __restrict__ src, int ew, int rows,
@@ -839,69 +792,6 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
       }
 }
 
-static inline const void* corr_kernel_f16(int kw) {
-  switch (f16_nch(kw)) {
-    case 2: return (const void*)&k_corr_f16<2>;
-    case 3: return (const void*)&k_corr_f16<3>;
-    case 4: return (const void*)&k_corr_f16<4>;
-    case 5: return (const void*)&k_corr_f16<5>;
-    case 6: return (const void*)&k_corr_f16<6>;
-    case 7: return (const void*)&k_corr_f16<7>;
-    case 8: return (const void*)&k_corr_f16<8>;
-    case 9: return (const void*)&k_corr_f16<9>;
-    case 10: return (const void*)&k_corr_f16<10>;
-    default: return nullptr;
-  }
-}
-
-// ---------------------------------------------------------------- dispatch
-// k_corr_rw's ring does not depend on the detector height: every width of
-// LM_KW_LIST, any kh; other widths run k_corr_gen
-static inline bool corr_ring(int kw) {
-  switch (kw) {
-#define LM_KW_CASE(n) case n:
-    LM_KW_LIST(LM_KW_CASE)
-#undef LM_KW_CASE
-    return true;
-    default:
-      return false;
-  }
-}
-
-static inline const void* corr_kernel(int kw, bool unf) {
-  switch (kw) {
-#define LM_KW_CASE(n) \
-  case n:             \
-    return unf ? (const void*)&k_corr_rw<n, true> : (const void*)&k_corr_rw<n, false>;
-    LM_KW_LIST(LM_KW_CASE)
-#undef LM_KW_CASE
-    default:
-      return unf ? (const void*)&k_corr_gen<true> : (const void*)&k_corr_gen<false>;
-  }
-}
-
-// Launch the correlation for one detector group (all detectors of one width
-// that run the same kernel).
-// `weights`: the fp32 rows (k_corr_rw / k_corr_pk / k_corr_gen) or the f16 rows (k_corr_f16).
-// k_corr_rw takes one wave per tile with the batch's tiles flattened (`grid`
-// is then ignored but for its y = slot count); the others one workgroup per
-// (tile, slot).
-static inline hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t lds, hipStream_t st,
-                                     const LmConst* K, const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes,
-                                     const void* weights, int s0, unsigned long long* keys, int32_t* n_pos,
-                                     uint8_t* tailbin, int64_t tailbin_slot_bytes) {
-  if (ring) {
-    int nslots = (int)grid.y;
-    const unsigned waves = (unsigned)(G.tile_end[G.n - 1] * nslots);
-    void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
-                    (void*)&nslots, (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
-    return hipLaunchKernel(fn, dim3((waves + LM_RW_WAVES - 1) / LM_RW_WAVES), dim3(LM_RW_THREADS), args, lds, st);
-  }
-  void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
-                  (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
-  return hipLaunchKernel(fn, grid, dim3(threads), args, lds, st);
-}
-
 // Debug copy of raw scores (lm_debug_scores): the same chain per output,
 // computed straight from the ext crops in global memory (no LDS, any size).
 template <bool UNF>
@@ -926,4 +816,72 @@ __global__ __launch_bounds__(256) void k_corr_dbg(const LmConst* __restrict__ Kp
       for (int j = 0; j < D.kw; ++j) a = corr_tap1<UNF>(a, W[i * D.kwp + j], (float)src[(int64_t)i * ew + j]);
     dbg[(int64_t)slot * dbg_slot_floats + dbg_off[d] + e] = a;
   }
+}
+
+// ---------------------------------------------------------------- dispatch
+const void* corr_kernel_f16(int kw) {
+  switch (f16_nch(kw)) {
+    case 2: return (const void*)&k_corr_f16<2>;
+    case 3: return (const void*)&k_corr_f16<3>;
+    case 4: return (const void*)&k_corr_f16<4>;
+    case 5: return (const void*)&k_corr_f16<5>;
+    case 6: return (const void*)&k_corr_f16<6>;
+    case 7: return (const void*)&k_corr_f16<7>;
+    case 8: return (const void*)&k_corr_f16<8>;
+    case 9: return (const void*)&k_corr_f16<9>;
+    case 10: return (const void*)&k_corr_f16<10>;
+    default: return nullptr;
+  }
+}
+
+bool corr_ring(int kw) {
+  switch (kw) {
+#define LM_KW_CASE(n) case n:
+    LM_KW_LIST(LM_KW_CASE)
+#undef LM_KW_CASE
+    return true;
+    default:
+      return false;
+  }
+}
+
+const void* corr_kernel(int kw, bool unf) {
+  switch (kw) {
+#define LM_KW_CASE(n) \
+  case n:             \
+    return unf ? (const void*)&k_corr_rw<n, true> : (const void*)&k_corr_rw<n, false>;
+    LM_KW_LIST(LM_KW_CASE)
+#undef LM_KW_CASE
+    default:
+      return unf ? (const void*)&k_corr_gen<true> : (const void*)&k_corr_gen<false>;
+  }
+}
+
+const void* corr_kernel_rw_all(bool unf) {
+  return unf ? (const void*)&k_corr_rw_all<true> : (const void*)&k_corr_rw_all<false>;
+}
+
+hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t lds, hipStream_t st, const LmConst* K,
+                       const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes, const void* weights, int s0,
+                       unsigned long long* keys, int32_t* n_pos, uint8_t* tailbin, int64_t tailbin_slot_bytes) {
+  if (ring) {
+    int nslots = (int)grid.y;
+    const unsigned waves = (unsigned)(G.tile_end[G.n - 1] * nslots);
+    void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
+                    (void*)&nslots, (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
+    return hipLaunchKernel(fn, dim3((waves + LM_RW_WAVES - 1) / LM_RW_WAVES), dim3(LM_RW_THREADS), args, lds, st);
+  }
+  void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
+                  (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
+  return hipLaunchKernel(fn, grid, dim3(threads), args, lds, st);
+}
+
+hipError_t launch_corr_dbg(bool unf, dim3 grid, hipStream_t st, const LmConst* K, const uint8_t* ext,
+                           int64_t ext_slot_bytes, const float* weights, int s0, float* dbg, const int64_t* dbg_off,
+                           int64_t dbg_slot_floats) {
+  if (unf)
+    k_corr_dbg<true><<<grid, 256, 0, st>>>(K, ext, ext_slot_bytes, weights, s0, dbg, dbg_off, dbg_slot_floats);
+  else
+    k_corr_dbg<false><<<grid, 256, 0, st>>>(K, ext, ext_slot_bytes, weights, s0, dbg, dbg_off, dbg_slot_floats);
+  return hipGetLastError();
 }

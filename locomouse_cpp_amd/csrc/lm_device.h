@@ -20,6 +20,10 @@
 #define LM_TH (16 * LM_R)  // 48
 #define LM_JC 4            // tap chunk along a detector row (kw padded to a multiple)
 
+// k_minmax: each frame split over LM_MM_SPLIT workgroups of LM_MM_THREADS
+#define LM_MM_SPLIT 8
+#define LM_MM_THREADS 256
+
 #define LM_NDET 6
 #define LM_NLIST 4
 #define LM_NFEAT 2

@@ -29,17 +29,7 @@
 #include "lm_device.h"
 #include "lm_introsort.h"
 
-#define DEV __device__ __forceinline__
-
-// Frame pointers come from a device array (frame_ptr), so the compiler cannot
-// tell that they point to global memory and would access the frames with FLAT
-// instructions (longer latency, and they hold the LDS counter too); the casts
-// below make those accesses global_load_*.
-typedef __attribute__((address_space(1))) const uint8_t lm_gu8;
-typedef __attribute__((address_space(1))) const uint32_t lm_gu32;
-typedef unsigned lm_u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const lm_u32x4 lm_gu4;
-DEV const lm_gu8* as_global(const uint8_t* p) { return (const lm_gu8*)p; }
+#include "lm_dev_common.h"
 
 // ------------------------------------------------------------------ helpers
 
@@ -63,8 +53,6 @@ DEV uint8_t ipad_pixel(FP __restrict__ F, const uint8_t* __restrict__ bkg,
 // Each frame is split over LM_MM_SPLIT workgroups (16-byte loads of frame and
 // background, wave and block reductions); each workgroup writes its partial
 // min/max pair, and k_lut folds the LM_MM_SPLIT pairs of a slot into its LUT.
-#define LM_MM_SPLIT 8
-#define LM_MM_THREADS 256
 __global__ __launch_bounds__(LM_MM_THREADS) void k_minmax(const uint8_t* const* __restrict__ frame_ptr,
                                                           const uint8_t* __restrict__ bkg, int npix, int s0,
                                                           unsigned* __restrict__ mm) {
@@ -356,7 +344,7 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
   }
 }
 
-#include "lm_corr.hip"
+#include "lm_corr.h"  // the correlation kernels are their own translation unit (lm_corr.hip)
 
 #include "lm_cc.h"
 

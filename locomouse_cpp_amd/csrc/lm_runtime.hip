@@ -21,143 +21,14 @@
 #include <vector>
 
 #include "locomouse_hip.h"
+#include "lm_host.h"
 #include "lm_kernels.hip"
-
-#define LM_API extern "C" __attribute__((visibility("default")))
 
 namespace {
 
-thread_local std::string g_err = "";
-
-struct HipError : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
-
-void hip_check(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
-}
-#define HIPCHK(x) hip_check((x), #x)
-
-// Copies and fills on a context's own (non-blocking) stream, waited for.
-// Never the synchronous hipMemcpy / hipMemset: they run on the legacy stream,
-// which HIP refuses while any other thread's stream is capturing a graph
-// (several contexts, one per host thread).
-#define COPY_SYNC(dst, src, bytes, kind, st) \
-  do {                                              \
-    HIPCHK(hipMemcpyAsync((dst), (src), (bytes), (kind), (st))); \
-    HIPCHK(hipStreamSynchronize(st));                \
-  } while (0)
-#define SET_SYNC(dst, v, bytes, st)                   \
-  do {                                              \
-    HIPCHK(hipMemsetAsync((dst), (v), (bytes), (st))); \
-    HIPCHK(hipStreamSynchronize(st));                \
-  } while (0)
-
-bool dbg_env(const char* name) {  // diagnostics switches (LM_* environment variables)
-  const char* v = getenv(name);
-  return v && atoi(v) != 0;
-}
-
-// Diagnostics (LM_GUARD=1): every device buffer gets 64 KiB guard zones on
-// both sides filled with 0xA5; lm_detect_batch* checks them after each batch
-// and fails with the buffer's address if a kernel wrote outside it.
-constexpr size_t kGuard = 64 * 1024;
 // LDS window of one k_corr_gen workgroup (row chunks are sized to fit it)
 constexpr size_t kCorrLdsBudget = 64 * 1024;
 constexpr size_t kF16LdsMax = 160 * 1024;  // one k_corr_f16 workgroup per CU at most
-bool guard_mode() {
-  static const bool on = [] {
-    const char* v = getenv("LM_GUARD");
-    return v && atoi(v) != 0;
-  }();
-  return on;
-}
-std::mutex g_guard_mu;
-std::map<const void*, size_t> g_guarded;  // user pointer -> user bytes
-
-void guard_check_all() {
-  std::vector<std::pair<const void*, size_t>> bufs;
-  {
-    std::lock_guard<std::mutex> lk(g_guard_mu);
-    bufs.assign(g_guarded.begin(), g_guarded.end());
-  }
-  std::vector<uint8_t> h(kGuard);
-  for (const auto& b : bufs) {
-    const uint8_t* u = static_cast<const uint8_t*>(b.first);
-    for (int side = 0; side < 2; ++side) {
-      const uint8_t* g = side ? u + b.second : u - kGuard;
-      HIPCHK(hipMemcpy(h.data(), g, kGuard, hipMemcpyDeviceToHost));
-      for (size_t i = 0; i < kGuard; ++i)
-        if (h[i] != 0xA5) {
-          char m[256];
-          snprintf(m, sizeof m, "guard: write %s buffer %p (%zu bytes) at offset %lld", side ? "past" : "before",
-                   (const void*)u, b.second,
-                   side ? (long long)(b.second + i) : -(long long)(kGuard - i));
-          throw std::runtime_error(m);
-        }
-    }
-  }
-}
-
-template <class T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  void alloc(size_t count) {
-    release();
-    if (count == 0) count = 1;
-    if (guard_mode()) {
-      uint8_t* base = nullptr;
-      const size_t bytes = count * sizeof(T);
-      HIPCHK(hipMalloc(&base, bytes + 2 * kGuard));
-      HIPCHK(hipMemset(base, 0xA5, kGuard));
-      HIPCHK(hipMemset(base + kGuard + bytes, 0xA5, kGuard));
-      p = reinterpret_cast<T*>(base + kGuard);
-      std::lock_guard<std::mutex> lk(g_guard_mu);
-      g_guarded[p] = bytes;
-    } else {
-      HIPCHK(hipMalloc(&p, count * sizeof(T)));
-    }
-    n = count;
-  }
-  void release() {
-    if (p) {
-      if (guard_mode()) {
-        {
-          std::lock_guard<std::mutex> lk(g_guard_mu);
-          g_guarded.erase(p);
-        }
-        (void)hipFree(reinterpret_cast<uint8_t*>(p) - kGuard);
-      } else {
-        (void)hipFree(p);
-      }
-    }
-    p = nullptr;
-    n = 0;
-  }
-  ~DevBuf() { release(); }
-};
-
-template <class T>
-struct HostBuf {  // pinned, mapped into the device address space (d: device-side pointer)
-  T* p = nullptr;
-  T* d = nullptr;
-  size_t n = 0;
-  void alloc(size_t count) {
-    release();
-    if (count == 0) count = 1;
-    HIPCHK(hipHostMalloc(&p, count * sizeof(T), hipHostMallocMapped));
-    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d), p, 0));
-    n = count;
-  }
-  void release() {
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    d = nullptr;
-    n = 0;
-  }
-  ~HostBuf() { release(); }
-};
 
 struct Rect {
   int x = 0, y = 0, w = 0, h = 0;
@@ -610,7 +481,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       const bool f16 = su->corr_precision == LM_CORR_F16;
       const bool ring = !f16 && corr_ring(D.kw);
       const void* fn = f16 ? corr_kernel_f16(D.kw)
-                       : ring && m == 1 ? (c->unfused ? (const void*)&k_corr_rw_all<true> : (const void*)&k_corr_rw_all<false>)
+                       : ring && m == 1 ? corr_kernel_rw_all(c->unfused)
                                         : corr_kernel(D.kw, c->unfused);
       size_t need;
       if (f16) {
@@ -757,24 +628,6 @@ hipEvent_t epoch_event(const lm_ctx* c) {
   return it == g_epoch.end() ? nullptr : it->second;
 }
 
-lm_status fail(lm_status s, const std::string& m) {
-  g_err = m;
-  return s;
-}
-
-template <class F>
-lm_status guarded(F&& f) {
-  try {
-    f();
-    return LM_OK;
-  } catch (const std::invalid_argument& e) {
-    return fail(LM_ERR_INVALID_ARGUMENT, e.what());
-  } catch (const HipError& e) {
-    return fail(LM_ERR_HIP, e.what());
-  } catch (const std::exception& e) {
-    return fail(LM_ERR_RUNTIME, e.what());
-  }
-}
 
 struct Timer {
   lm_ctx* c;
@@ -1132,13 +985,8 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
           c->dbg_offd.alloc(LM_NDET);
           COPY_SYNC(c->dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice, c->stream);
         }
-        const dim3 dgrid(64, nproc, LM_NDET);
-        if (c->unfused)
-          k_corr_dbg<true><<<dgrid, 256, 0, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->dbg.p,
-                                                  c->dbg_offd.p, c->dbg_slot_floats);
-        else
-          k_corr_dbg<false><<<dgrid, 256, 0, st>>>(dK, c->ext.p, c->ext_slot_bytes, c->weights.p, s_proc0, c->dbg.p,
-                                                   c->dbg_offd.p, c->dbg_slot_floats);
+        HIPCHK(launch_corr_dbg(c->unfused, dim3(64, nproc, LM_NDET), st, dK, c->ext.p, c->ext_slot_bytes, c->weights.p,
+                               s_proc0, c->dbg.p, c->dbg_offd.p, c->dbg_slot_floats));
       }
       long long *kp0 = nullptr, *kp1 = nullptr, *kp2 = nullptr;
       if (c->kprof_on) {
@@ -1525,5 +1373,10 @@ LM_API lm_status lm_synth_frames_device(int32_t device, uint8_t* d_out, int32_t 
   });
 }
 
-// ------------------------------------------------ whole-video BB pass (method 0)
-#include "lm_bbox.hip"
+// k_minmax + k_lut for the whole-video BB pass (lm_bbox.hip, its own translation unit)
+hipError_t launch_minmax_lut(const uint8_t* const* frame_ptr, const uint8_t* bkg, int npix, int s0, int n,
+                             unsigned* mm, const uint8_t* adj, int use_adj, uint8_t* luts, hipStream_t st) {
+  k_minmax<<<dim3(LM_MM_SPLIT, n - s0), LM_MM_THREADS, 0, st>>>(frame_ptr, bkg, npix, s0, mm);
+  k_lut<<<(n - s0 + 3) / 4, 256, 0, st>>>(mm, s0, n, adj, use_adj, luts);
+  return hipGetLastError();
+}

@@ -34,16 +34,57 @@ HOST_LIB_PATH = os.path.join(PKG, "liblocomouse_host.so")
 CLI_PATH = os.path.join(PKG, "bin", "LocoMouse")
 
 
-def build(verbose=False):
+HIP_UNITS = ("lm_runtime.hip", "lm_corr.hip", "lm_bbox.hip")  # translation units of liblocomouse_hip.so
+
+
+def _up_to_date(obj, cmd):
+    """True when obj was built by the same command and is newer than every
+    file its dependency list (hipcc -MMD) names."""
+    try:
+        with open(obj + ".cmd") as fh:
+            if fh.read() != " ".join(cmd):
+                return False
+        with open(obj + ".d") as fh:
+            deps = fh.read().replace("\\\n", " ").split(":", 1)[1].split()
+        t = os.path.getmtime(obj)
+        return all(os.path.getmtime(d) <= t for d in deps)
+    except (OSError, IndexError):
+        return False
+
+
+def build(verbose=False, defines=(), out=None):
     """Compile liblocomouse_hip.so for gfx950 in-tree (hipcc cross-compiles
-    without a GPU), then the host C++ LocoMouse mirror above it."""
-    cmd = ["hipcc", *HIPCC_FLAGS, "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-o", LIB_PATH,
-           os.path.join(CSRC, "lm_runtime.hip")]
+    without a GPU), then the host C++ LocoMouse mirror above it.  The
+    translation units compile in parallel, then link into one library.
+    `defines` / `out`: experiment builds (-D flags, another output path; the
+    host mirror is then not rebuilt)."""
+    objdir = os.path.join(ROOT, "build", "hip" if out is None else "hip_" + os.path.basename(out))
+    os.makedirs(objdir, exist_ok=True)
+    inc = ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC, *["-D" + d for d in defines]]
+    flags = [f for f in HIPCC_FLAGS if f != "-shared"]
+    procs, objs = [], []
+    for u in HIP_UNITS:
+        o = os.path.join(objdir, u.replace(".hip", ".o"))
+        cmd = ["hipcc", *flags, *inc, "-c", "-MMD", "-MF", o + ".d", "-o", o, os.path.join(CSRC, u)]
+        objs.append(o)
+        if _up_to_date(o, cmd):
+            continue
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((subprocess.Popen(cmd), cmd, o))
+    for p, cmd, o in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
+        with open(o + ".cmd", "w") as fh:
+            fh.write(" ".join(cmd))
+    target = out or LIB_PATH
+    cmd = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", target, *objs]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    build_host(verbose)
-    return LIB_PATH
+    if out is None:
+        build_host(verbose)
+    return target
 
 
 def build_host(verbose=False):
