@@ -30,6 +30,7 @@ CONFIGS = {  # BASELINE.json configs with a GPU bench line: (rows, cols, descrip
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
 F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16 MFMA peak (MI355X_MICROARCH.md: ~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03", "pmc_k_corr.json")  # this tree's PMC passes (scripts/gpu_final.sh)
 
 
 def algorithmic_flops_per_frame(ctx):
@@ -57,15 +58,32 @@ def union_ms(iv):
     return tot
 
 
-def cpu_baseline(cfg, seconds=10.0, max_frames=2000):
+def cpu_baseline(cfg, seconds=10.0, max_frames=2000, samples=()):
     """The oracle (CPU restatement, 1 thread, AVX2+FMA) on a bounded sample of
-    the same workload: chunks of 50 consecutive synthetic frames until
-    `seconds` of CPU work."""
+    the same workload.  It first runs the frames of the GPU result samples
+    (`samples`: (first frame, GPU result dict, scene indices of its previous
+    and first frame) per stream; the previous frame is the oracle's frame 0) and compares its outputs with the
+    GPU's bit for bit -- the oracle as the checker of the benchmarked run --
+    then chunks of 50 consecutive synthetic frames until `seconds` of CPU
+    work.  Returns (baseline line, parity-sample line)."""
     from oracle import oracle as O
-    import numpy as np
+    from locomouse_cpp_amd.results import same_results, slice_results
     chunk = 50
-    frames = cfg.frames(0, chunk)
     done, t = 0, 0.0
+    checked, exact, mism = 0, True, []
+    import numpy as np
+    for first, got, prev_scene, first_scene in samples:
+        fr = np.concatenate([cfg.frames(prev_scene, 1), cfg.frames(first_scene, got["n_frames"])])
+        t0 = time.perf_counter()
+        ref = O.OracleRun(cfg, fr).result
+        t += time.perf_counter() - t0
+        done += got["n_frames"] + 1
+        ok = same_results(got, slice_results(ref, 1))
+        exact &= ok
+        checked += got["n_frames"]
+        if not ok:
+            mism.append(int(first))
+    frames = cfg.frames(0, chunk)
     while t < seconds and done < max_frames:
         t0 = time.perf_counter()
         O.OracleRun(cfg, frames)
@@ -80,10 +98,16 @@ def cpu_baseline(cfg, seconds=10.0, max_frames=2000):
                     break
     except OSError:
         pass
-    del np
-    return {"value": done / t, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{done} frames (chunks of {chunk} from frame 0), oracle/lm_oracle.cpp single thread, {t:.1f} s",
-            "cpu": cpu}
+    line = {"value": done / t, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{done} frames (the GPU parity samples, then chunks of {chunk} from frame 0), "
+                      f"oracle/lm_oracle.cpp single thread, {t:.1f} s", "cpu": cpu}
+    parity = None
+    if samples:
+        parity = {"frames": checked, "streams": len(samples), "bit_exact": bool(exact),
+                  "first_frames": [int(smp[0]) for smp in samples][:16], "mismatching_batches": mism,
+                  "compared": "every lm_batch_result array (candidates, P22D, unary, pairwise CSC, tail) against "
+                              "oracle/lm_oracle.cpp on the same synthetic frames"}
+    return line, parity
 
 
 def host_cpu_share():
@@ -95,16 +119,15 @@ def host_cpu_share():
     return max(1, min(n, int(share))) if share and share.isdigit() else n
 
 
-def cpu_baseline_threads(cfg, seconds=8.0, threads=None):
-    """The fair CPU baseline of SURVEY.md §8(d)(ii): the oracle on every host
-    thread of this GPU's CPU share, each on its own contiguous 50-frame chunks
-    (frame-sharded like the multi-GPU path; ctypes releases the GIL inside the
-    oracle call)."""
+def cpu_baseline_threads(cfg, seconds=8.0, threads=None, chunk=50):
+    """The fair CPU baseline of SURVEY.md §8(d)(ii): the oracle on `threads`
+    host threads (default: this GPU's CPU share), each on its own contiguous
+    chunk of frames (frame-sharded like the multi-GPU path; ctypes releases
+    the GIL inside the oracle call)."""
     import threading
     from oracle import oracle as O
     if threads is None:
         threads = host_cpu_share()
-    chunk = 50
     samples = [cfg.frames(chunk * t, chunk) for t in range(threads)]
     counts = [0] * threads
     stop = time.perf_counter() + seconds
@@ -125,39 +148,61 @@ def cpu_baseline_threads(cfg, seconds=8.0, threads=None):
             "sample": f"{sum(counts)} frames, {threads} threads x chunks of {chunk} frames, {el:.1f} s wall"}
 
 
+def cpu_baseline_node(cfg, seconds=8.0):
+    """BASELINE.md §2's `nproc`-thread line: one oracle thread per CPU this
+    process may run on (the whole node where nothing restricts it), each on
+    its own contiguous shard.  On a shared GPU box the per-GPU share
+    (cpu_baseline_threads) is the fair per-GPU comparison; this line is the
+    whole-node CPU figure to set beside an 8-GPU frames/s."""
+    n = len(os.sched_getaffinity(0))
+    line = cpu_baseline_threads(cfg, seconds, threads=n, chunk=8)
+    line["nproc"] = os.cpu_count()
+    return line
+
+
 def gather_results(ctxs, frames, state, vbase, R, B, frame_bytes, world, rank):
     """The host gather of north_star's multi-GPU design, after the timed
     region: every stream of every rank runs its next batch, its compact
     results (the lm_batch_result arrays) go to rank 0 over the host process
-    group, and rank 0 checks that the gathered frame ranges are disjoint and
-    whole.  Returns a summary (rank 0) or None."""
+    group, and rank 0 checks that the gathered frame ranges are whole and
+    disjoint.  Returns (summary on rank 0 or None, this rank's
+    (first frame, result dict, scene index of the previous frame, scene index
+    of the first frame) per stream)."""
     import torch.distributed as dist
 
     from locomouse_cpp_amd.abi import result_to_numpy
-    mine = []
+    mine, local = [], []
     for k, c in enumerate(ctxs):
         f = state[k]["frame"]
         i = (f - vbase[k]) % R + 1
         n = min(B, R + 1 - i)
-        # the context processed frame f - 1 last: it carries that frame's state
+        # the context processed frame f - 1 last: it continues from that frame
         res = result_to_numpy(c.detect_device(frames[k].data_ptr() + i * frame_bytes, frame_bytes, n, f))
-        mine.append({"first": f, "n": res["n_frames"], "cand": res["cand"], "cand_offset": res["cand_offset"],
-                     "tail": res["tail"]})
+        # synthetic-scene indices of the pixels this batch saw: resident frame
+        # i holds scene frame vbase - 1 + i, and the frame before it (the one
+        # the context processed last) is resident frame i - 1, or frame R
+        # when the stream wrapped around
+        local.append((f, res, vbase[k] - 1 + (i - 1 if i > 1 else R), vbase[k] - 1 + i))
+        mine.append({"first": f, "n": res["n_frames"], "want": n, "cand": res["cand"],
+                     "cand_offset": res["cand_offset"], "tail": res["tail"]})
     allr = [None] * world if rank == 0 else None
     if world > 1:
         dist.gather_object(mine, allr, dst=0)
     else:
         allr = [mine]
     if rank != 0:
-        return None
+        return None, local
     parts = sorted((p for r in allr for p in r), key=lambda p: p["first"])
+    for p in parts:
+        if p["n"] != p["want"] or len(p["cand_offset"]) != 4 * p["n"] + 1 or p["tail"].shape[0] != p["n"]:
+            raise RuntimeError(f"gathered batch at frame {p['first']} is not whole")
     for a, b in zip(parts, parts[1:]):
         if a["first"] + a["n"] > b["first"]:
             raise RuntimeError("gathered frame ranges overlap")
     return {"ranks": world, "streams": len(parts), "frames": int(sum(p["n"] for p in parts)),
             "candidates": int(sum(len(p["cand"]) for p in parts)),
-            "first_frames": [int(p["first"]) for p in parts][:16], "transport": "gloo gather_object (host)" if world > 1
-            else "local"}
+            "first_frames": [int(p["first"]) for p in parts][:16], "whole_and_disjoint": True,
+            "transport": "gloo gather_object (host)" if world > 1 else "local"}, local
 
 
 def run_bb(args):
@@ -216,7 +261,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--resident", type=int, default=6400, help="frames resident in HBM per stream (cycled)")
     ap.add_argument("--streams", type=int, default=4,
-                    help="contexts (HIP streams + host threads) per GPU")
+                    help="contexts per GPU (each with its own host thread)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="pipeline lanes per context (lm_setup.pipeline_lanes: batches in flight on their own HIP "
+                         "streams, driven with lm_detect_submit / lm_detect_collect)")
+    ap.add_argument("--check-all-ranks", action="store_true",
+                    help="every rank compares its gathered batches with the oracle (multi-rank rehearsals)")
     ap.add_argument("--round-robin", action="store_true", help="one host thread drives all streams in turn")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -265,7 +315,8 @@ def main():
     # NS contexts per GPU, each with its own HIP stream and host thread, each
     # on its own contiguous range of the video (rank-major): like a shard, its
     # first batch gets the previous frame as a 1-frame halo.
-    ctxs = [Context(cfg, max_batch=B, device=local) for _ in range(NS)]
+    NL = max(1, args.lanes)
+    ctxs = [Context(cfg, max_batch=B, device=local, lanes=NL) for _ in range(NS)]
     frames = torch.empty((NS, R + 1, rows, cols), dtype=torch.uint8, device=f"cuda:{local}")
     vbase = [(rank * NS + k) * R for k in range(NS)]
     for k in range(NS):
@@ -275,6 +326,12 @@ def main():
 
     state = [{"frame": vbase[k]} for k in range(NS)]
 
+    def record(k, timing):
+        if timing:
+            for name, t0, t1 in ctxs[k].kernel_spans():
+                kernel_ms.setdefault(name, []).append(t1 - t0)
+                spans.setdefault(name, []).append((t0, t1))
+
     def step(k, timing):
         st = state[k]
         f = st["frame"]
@@ -283,22 +340,34 @@ def main():
         if i == 1 and f > 0:
             # stream start (vbase > 0) or wrap-around: pass the previous frame
             halo = frames[k].data_ptr() + (0 if f == vbase[k] else R * FRAME_BYTES)
-        ctxs[k].detect_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)
+        c = ctxs[k]
+        if NL == 1:
+            c.detect_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)
+            record(k, timing)
+        else:  # pipelined: keep every lane busy, collect in submission order
+            if c.pending() == NL:
+                c.collect(raw=True)
+                record(k, timing)
+            c.submit_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)
         st["frame"] = f + B
-        if timing:
-            for name, t0, t1 in ctxs[k].kernel_spans():
-                kernel_ms.setdefault(name, []).append(t1 - t0)
-                spans.setdefault(name, []).append((t0, t1))
+
+    def drain(k, timing):
+        while ctxs[k].pending():
+            ctxs[k].collect(raw=True)
+            record(k, timing)
 
     def run(k, n, timing):
         for _ in range(n):
             step(k, timing)
+        drain(k, timing)
 
     def run_all(n, timing):
         if NS == 1 or args.round_robin:
             for _ in range(n):
                 for k in range(NS):
                     step(k, timing)
+            for k in range(NS):
+                drain(k, timing)
             return
         import threading
         errors = []
@@ -337,7 +406,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    gathered = gather_results(ctxs, frames, state, vbase, R, B, FRAME_BYTES, world, rank)
+    gathered, local_samples = gather_results(ctxs, frames, state, vbase, R, B, FRAME_BYTES, world, rank)
     total_frames = args.steps * B * NS * world
     fps = total_frames / elapsed
 
@@ -351,10 +420,9 @@ def main():
     corr_avg_ms = union_ms(corr_spans) / max(1, len(corr_spans))
     achieved_tf = flops * B / (corr_avg_ms * 1e-3) / 1e12
     peak_tf = F16_PEAK_TFLOPS if f16 else FP32_PEAK_TFLOPS
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_k_corr.json")
-    if os.path.exists(pmc):
-        with open(pmc) as fh:
+    traffic = None  # HBM bytes per launch from this tree's PMC passes (scripts/pmc_traffic.py)
+    if os.path.exists(PMC_TRAFFIC):
+        with open(PMC_TRAFFIC) as fh:
             traffic = json.load(fh).get("hbm_bytes_per_launch")
     out = {
         "metric": METRIC,
@@ -371,15 +439,15 @@ def main():
         "data": "synthetic (lm_synth.h scene, resident in HBM)",
         "config": {"workload": workload,
                    "batch_frames": B, "streams_per_gpu": NS, "frames_per_rank": args.steps * B * NS,
-                   "resident_frames_per_stream": R,
+                   "lanes_per_context": NL, "resident_frames_per_stream": R,
                    "stream_priorities": "alternating high/low" if os.environ.get("LM_STREAM_PRIO", "1") != "0" else "equal",
-                   "corr_launches": ("one merged launch" if NS == 1 else "one per detector width")
+                   "corr_launches": ("one merged launch" if NS * NL == 1 else "one per detector width")
                    if os.environ.get("LM_CORR_PLAN") not in ("0", "1") else f"LM_CORR_PLAN={os.environ['LM_CORR_PLAN']}",
                    "parallelism": f"frame shards x{world} (no collective)"},
         "hbm_gbs": round(fps * FRAME_BYTES / 1e9, 3),
-        "roofline": {"bound": "mfma",
+        "roofline": {"bound": "mfma" if f16 else "valu",
                      "compute_roof": "dense f16 MFMA (v_mfma_f32_32x32x16_f16)" if f16 else
-                     "fp32 (v_fma_f32 VALU; equals the f32 MFMA peak)",
+                     "fp32 VALU (v_pk_fma_f32; equals the f32 MFMA peak)",
                      "kernel": "k_corr", "achieved": round(achieved_tf, 3), "peak": peak_tf,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
                      "traffic": traffic if not f16 and args.config == "c3" else None,
@@ -390,9 +458,27 @@ def main():
         "kernel_busy_ms_per_batch": {k: round(union_ms(v) / len(v), 5) for k, v in spans.items()},
     }
     out["gathered"] = gathered
-    if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
-        out["cpu_baseline_threads"] = cpu_baseline_threads(cfg, min(8.0, args.cpu_seconds))
+    if (rank == 0 and world == 1 and not args.no_cpu) or args.check_all_ranks:
+        # the CPU baseline leg: the oracle timed on the same workload, and as
+        # the checker of the GPU batches gathered above
+        base, parity = cpu_baseline(cfg, args.cpu_seconds if world == 1 else 0.0, samples=local_samples)
+        if world > 1:
+            allp = [None] * world if rank == 0 else None
+            dist.gather_object(parity, allp, dst=0)
+            if rank == 0:
+                parity = {"frames": sum(p["frames"] for p in allp), "streams": sum(p["streams"] for p in allp),
+                          "bit_exact": all(p["bit_exact"] for p in allp), "ranks": world,
+                          "first_frames": [f for p in allp for f in p["first_frames"]][:32],
+                          "mismatching_batches": [m for p in allp for m in p["mismatching_batches"]],
+                          "compared": allp[0]["compared"]}
+        out["parity_sample"] = parity
+        if parity is not None and not parity["bit_exact"]:
+            print(f"bench: GPU results differ from the oracle at batches {parity['mismatching_batches']}",
+                  file=sys.stderr, flush=True)
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = base
+            out["cpu_baseline_threads"] = cpu_baseline_threads(cfg, min(8.0, args.cpu_seconds))
+            out["cpu_baseline_node"] = cpu_baseline_node(cfg, min(8.0, args.cpu_seconds))
     if rank == 0:
         print(json.dumps(out), flush=True)
     for c in ctxs:

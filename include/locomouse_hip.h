@@ -12,6 +12,10 @@
  *   lm_ctx_create         LocoMouse::LocoMouse  LocoMouse_class.cpp:307-345 (parameters
  *                         already parsed), LocoMouse_Model ctor :3095-3162 and the
  *                         geometry of LocoMouse::initializeFeatureLoop :655-769.
+ *   lm_detect_submit /    the same, pipelined: up to lm_setup.pipeline_lanes batches of
+ *   lm_detect_collect     consecutive frames in flight on their own HIP streams
+ *                         (main.cpp:54-82 runs the frames one after another; results
+ *                         come back in the same order).
  *   lm_detect_batch       one iteration of the per-frame loop main.cpp:57-80, for n
  *                         consecutive frames:  readFrame :1273-1333 (+ LocoMouse_TM::
  *                         readFrame TM.cpp:243-249), cropBoundingBox :1408-1478,
@@ -30,7 +34,7 @@
  *
  * Threading: one context per (device, host thread); a context is not re-entrant.
  * Results returned through lm_batch_result are owned by the context and stay
- * valid until the next lm_detect_batch* call on it or lm_ctx_destroy.
+ * valid until the next lm_detect_* call on it or lm_ctx_destroy.
  */
 #ifndef LOCOMOUSE_HIP_H
 #define LOCOMOUSE_HIP_H
@@ -42,7 +46,7 @@
 extern "C" {
 #endif
 
-#define LM_ABI_VERSION 3
+#define LM_ABI_VERSION 4
 #define LM_N_PAWS 4          /* LocoMouse_class.hpp:84 */
 #define LM_N_TAIL_POINTS 15  /* LocoMouse_class.hpp:86 */
 #define LM_N_LISTS 4         /* candidate lists per frame */
@@ -146,7 +150,9 @@ typedef struct {
   lm_rect view_box_side, view_box_bottom;
   int32_t filter_arith;           /* LM_FILTER_FUSED (default) or LM_FILTER_UNFUSED, see below */
   int32_t corr_precision;         /* LM_CORR_FP32 (default, bit-exact) or LM_CORR_F16, see below */
+  int32_t pipeline_lanes;         /* batches in flight at once (lm_detect_submit); 0 = 1, at most LM_MAX_LANES */
 } lm_setup;
+#define LM_MAX_LANES 16
 /* filter2D's fp32 tap arithmetic depends on the OpenCV build the reference
  * links (no version is pinned, CMakeLists.txt:3): AVX2 builds of OpenCV
  * >= 3.4.9 fuse each tap (fma), SSE2/scalar builds round the product and then
@@ -243,17 +249,19 @@ const char* lm_last_error(void);
  * Fails with LM_ERR_INVALID_ARGUMENT on the reference's validation errors
  * (:35-249, :486-540, :3097-3140) and on use_provided_bounding_box == 0.
  * Contexts share no state; several may run concurrently from different host
- * threads.  Results never depend on how many exist, but two scheduling
- * choices do: contexts alternate between the highest and the lowest HIP
- * stream priority, and a context alone on its device runs its correlation
- * widths in one launch (several contexts: one launch per width). */
+ * threads.  setup->pipeline_lanes HIP streams are created (each with its own
+ * per-batch buffers, about 0.5 GB at 1024x256 and max_batch 256).  Results
+ * never depend on how many contexts or lanes exist, but two scheduling
+ * choices do: lanes alternate between the highest and the lowest HIP stream
+ * priority, and a lane alone on its device runs its correlation widths in
+ * one launch (several lanes: one launch per width). */
 lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_params* params,
                         const lm_model* model, int32_t max_batch, lm_ctx** out);
 void lm_ctx_destroy(lm_ctx* ctx);
 
 lm_status lm_get_geometry(const lm_ctx* ctx, lm_geometry* out);
 
-/* The ctx's HIP stream (hipStream_t as void*), for event timing by callers. */
+/* The ctx's first lane's HIP stream (hipStream_t as void*), for event timing by callers. */
 void* lm_ctx_stream(lm_ctx* ctx);
 
 /* Run frames [first_frame, first_frame + n) through the per-frame path.
@@ -275,10 +283,35 @@ lm_status lm_detect_batch_device(lm_ctx* ctx, const uint8_t* d_frames, int64_t f
                                  int32_t n, int32_t first_frame, const uint8_t* d_prev_frame,
                                  const int32_t* bb, lm_batch_result* out);
 
+/* Pipelined form of lm_detect_batch*: up to pipeline_lanes batches in flight.
+ * Submit puts batch [first_frame, first_frame + n) on the next free lane and
+ * returns once its inputs are staged (host frames are copied before it
+ * returns, so the caller may reuse its buffer; device frames -- and a device
+ * prev_frame -- must stay unchanged until the batch is collected).  Batches
+ * follow each other as in lm_detect_batch (contiguous frames, or prev_frame at
+ * a shard start).  A batch continuing another lane's batch takes that batch's
+ * last frame as a 1-frame halo copied on the device, so consecutive batches
+ * run concurrently; results are bit-identical to one lane.  Submitting while
+ * every lane holds a batch fails (LM_ERR_INVALID_ARGUMENT): collect first.
+ * Collect waits for the OLDEST submitted batch and returns its results
+ * (valid until the next lm_detect_* call on the context); its errors are
+ * the ones lm_detect_batch would report.  lm_detect_batch* require that no
+ * batch is in flight. */
+lm_status lm_detect_submit(lm_ctx* ctx, const uint8_t* frames, int64_t frame_pitch, int32_t n, int32_t first_frame,
+                           const uint8_t* prev_frame, const int32_t* bb);
+lm_status lm_detect_submit_device(lm_ctx* ctx, const uint8_t* d_frames, int64_t frame_pitch, int32_t n,
+                                  int32_t first_frame, const uint8_t* d_prev_frame, const int32_t* bb);
+lm_status lm_detect_collect(lm_ctx* ctx, lm_batch_result* out);
+/* Lanes of the context / batches submitted and not yet collected. */
+int32_t lm_ctx_lanes(const lm_ctx* ctx);
+int32_t lm_ctx_pending(const lm_ctx* ctx);
+
 /* ---- diagnostics (parity tests and benchmarks; not part of the reference surface) ---- */
 
 /* flags: bit 0 keep raw filter2D score maps of the last batch;
- *        bit 1 record per-kernel HIP event timings. */
+ *        bit 1 record per-kernel HIP event timings;
+ *        bit 4 force one correlation launch per detector width, bit 5 force
+ *        one merged launch (otherwise chosen per batch; results are identical). */
 lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags);
 
 /* Copy the raw correlation scores (before masking) of detector det

@@ -10,6 +10,9 @@ import numpy as np
 LM_OK, LM_ERR_INVALID_ARGUMENT, LM_ERR_RUNTIME, LM_ERR_HIP = 0, 1, 2, 3
 LM_N_TAIL_POINTS = 15
 LM_FILTER_FUSED, LM_FILTER_UNFUSED = 0, 1
+# lm_ctx_set_debug flags
+LM_DEBUG_SCORES, LM_DEBUG_TIMING = 1, 2
+LM_DEBUG_PLAN_PER_WIDTH, LM_DEBUG_PLAN_MERGED = 16, 32
 LM_CORR_FP32, LM_CORR_F16 = 0, 1
 LM_DEPTH_8U, LM_DEPTH_32F, LM_DEPTH_64F = 0, 5, 6
 DETECTORS = ("paw_bottom", "snout_bottom", "tail_bottom", "paw_side", "snout_side", "tail_side")
@@ -72,6 +75,7 @@ class lm_setup(C.Structure):
         ("view_box_bottom", lm_rect),
         ("filter_arith", C.c_int32),
         ("corr_precision", C.c_int32),
+        ("pipeline_lanes", C.c_int32),
     ]
 
 

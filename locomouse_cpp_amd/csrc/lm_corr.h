@@ -27,9 +27,13 @@ struct LmDetGroup {
 
 // Widths with a width-specialised k_corr_rw (any height); every other
 // detector runs k_corr_gen.
+#ifdef LM_KW_ONLY  // experiment builds: one ring width
+#define LM_KW_LIST(X) X(LM_KW_ONLY)
+#else
 #define LM_KW_LIST(X)                                                                                             \
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
       X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+#endif
 #define LM_KW_LIST_RW_ALL LM_KW_LIST
 
 // k_corr_rw: one wave per 80 x 16 output tile, LM_RW_WAVES waves per workgroup

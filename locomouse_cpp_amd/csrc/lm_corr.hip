@@ -233,20 +233,36 @@ DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s
 }
 
 // Software pipeline of k_corr_rw's step: a detector row's taps in
-// chunks (the first of 8 taps, the others of <= 12); while a chunk's FMAs run,
-// the pixel pairs and weights of the next chunk (the next step's first chunk
-// after the last) are already in flight, so a wave waits on LDS / scalar
-// loads only when they are late, and at most 12 + 4 pairs are live.
+// chunks (the first of 8 taps, the others of <= 12, every chunk starting on
+// an even tap); while a chunk's FMAs run, the pixel pairs and weights of the
+// next chunk (the next step's first chunk after the last) are already in
+// flight, so a wave waits on LDS / scalar loads only when they are late, and
+// at most 12 + 4 pairs are live.  Weights are read as 64-bit pairs (taps 2q,
+// 2q + 1 of a row; rows are zero-padded to a multiple of 4) into aligned SGPR
+// pairs, and each tap's v_pk_fma_f32 broadcasts its half of the pair with
+// op_sel (LM_RW_ASMFMA): with single-float weights the compiler copied every
+// odd SGPR into an even one, and the copies of the next step's first chunk
+// forced an lgkmcnt(0) wait right after that chunk's loads were issued.
+#ifndef LM_RW_ASMFMA
+#define LM_RW_ASMFMA 1
+#endif
+#ifndef LM_RW_PMAX
+#define LM_RW_PMAX 4
+#endif
 template <int KW>
 struct RwPlan {
   static_assert(KW >= 10, "k_corr_rw pipeline: at least 10 taps per row");
-  static constexpr int T0 = 8;
-  static constexpr int NR0 = (KW - T0 + 11) / 12;
+  static constexpr int NP = (KW + 1) / 2;  // weight pairs per row (the last one half used when KW is odd)
+  static constexpr int P0 = 4;             // pairs of the first chunk
+  static constexpr int RP = NP - P0;
+  static constexpr int PMAX = LM_RW_PMAX;  // weight pairs per chunk
+  static constexpr int NR0 = (RP + PMAX - 1) / PMAX;
   static constexpr int NR = NR0 < 2 ? 2 : NR0;  // >= 3 chunks: the first chunk's pairs are dead by the last
   static constexpr int N = 1 + NR;
-  static constexpr int WMAX = 12;
-  static constexpr int beg(int c) { return c == 0 ? 0 : T0 + ((c - 1) * (KW - T0)) / NR; }
-  static constexpr int end(int c) { return c == N - 1 ? KW : beg(c + 1); }
+  static constexpr int qb(int c) { return c == 0 ? 0 : P0 + ((c - 1) * RP) / NR; }
+  static constexpr int qe(int c) { return c == N - 1 ? NP : qb(c + 1); }
+  static constexpr int beg(int c) { return 2 * qb(c); }
+  static constexpr int end(int c) { return c == N - 1 ? KW : 2 * qe(c); }
   // pixel pairs a chunk needs that the previous chunk of its step did not load
   static constexpr int pbeg(int c) { return c == 0 ? 0 : beg(c) + PK_C - 1; }
   static constexpr int pend(int c) { return end(c) + PK_C - 1; }
@@ -258,13 +274,38 @@ DEV void lds_pair_nw(lm_f2& dst, unsigned base) {
   asm volatile("ds_read2_b32 %0, %1 offset0:%2 offset1:%3" : "=v"(dst) : "v"(base), "i"(Q), "i"(Q + STRIDE) : "memory");
 }
 
+// One tap on a packed pair of accumulators with weight half H of the SGPR
+// pair w2.  Volatile, like the ds_read2_b32 that produce p: the taps stay
+// behind the chunk's s_waitcnt.
+template <bool UNF, int H>
+DEV lm_f2 corr_tap_h(lm_f2 acc, lm_f2 w2, lm_f2 p) {
+  if constexpr (!LM_RW_ASMFMA) {
+    const float w = H ? w2.y : w2.x;
+    return corr_tap<UNF>(acc, (lm_f2){w, w}, p);
+  } else if constexpr (UNF) {  // rounded product, then rounded sum (OpenCV's scalar / SSE2 build)
+    lm_f2 prod;
+    if constexpr (H == 0)
+      asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(prod) : "s"(w2), "v"(p));
+    else
+      asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(prod) : "s"(w2), "v"(p));
+    asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(acc) : "v"(prod));
+    return acc;
+  } else if constexpr (H == 0) {
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "s"(w2), "v"(p));
+    return acc;
+  } else {
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(w2), "v"(p));
+    return acc;
+  }
+}
+
 template <int KW, bool UNF>
 struct RwPipe {
   using P = RwPlan<KW>;
   static constexpr int STR = rw_stride(KW);
   lm_f2 px[PK_C + KW - 1];
   lm_f2 acc[2][PK_C];
-  float wa[P::WMAX], wb[P::WMAX];  // weights of the chunk being computed (rows t, t - 2)
+  lm_f2 wa[P::PMAX], wb[P::PMAX];  // weight pairs of the chunk being computed (rows t, t - 2)
 
   template <int Q0, int Q1>
   DEV void issue(unsigned base) {
@@ -273,44 +314,43 @@ struct RwPipe {
       issue<Q0 + 1, Q1>(base);
     }
   }
-  // chunk C's weights of rows ra (pair 0) and rb (pair 1) into na / nb
+  // chunk C's weight pairs of rows ra (pair 0) and rb (pair 1) into na / nb
   template <int C>
-  DEV void load_w(float (&na)[P::WMAX], float (&nb)[P::WMAX], const float* __restrict__ ra,
-                  const float* __restrict__ rb) {
+  DEV void load_w(lm_f2 (&na)[P::PMAX], lm_f2 (&nb)[P::PMAX], const lm_f2* __restrict__ ra,
+                  const lm_f2* __restrict__ rb) {
 #pragma unroll
-    for (int j = 0; j < P::end(C) - P::beg(C); ++j) {
-      na[j] = ra[P::beg(C) + j];
-      nb[j] = rb[P::beg(C) + j];
+    for (int q = 0; q < P::qe(C) - P::qb(C); ++q) {
+      na[q] = ra[P::qb(C) + q];
+      nb[q] = rb[P::qb(C) + q];
     }
   }
-  template <int C, bool A, bool B>
-  DEV void compute() {
-#pragma unroll
-    for (int j = P::beg(C); j < P::end(C); ++j) {
+  template <int J, int C, bool A, bool B>
+  DEV void compute_from() {
+    if constexpr (J < P::end(C)) {
+      constexpr int q = J / 2 - P::qb(C), h = J & 1;
       if constexpr (A) {
-        const lm_f2 w2 = (lm_f2){wa[j - P::beg(C)], wa[j - P::beg(C)]};
 #pragma unroll
-        for (int c = 0; c < PK_C; ++c) acc[0][c] = corr_tap<UNF>(acc[0][c], w2, px[c + j]);
+        for (int c = 0; c < PK_C; ++c) acc[0][c] = corr_tap_h<UNF, h>(acc[0][c], wa[q], px[c + J]);
       }
       if constexpr (B) {
-        const lm_f2 w2 = (lm_f2){wb[j - P::beg(C)], wb[j - P::beg(C)]};
 #pragma unroll
-        for (int c = 0; c < PK_C; ++c) acc[1][c] = corr_tap<UNF>(acc[1][c], w2, px[c + j]);
+        for (int c = 0; c < PK_C; ++c) acc[1][c] = corr_tap_h<UNF, h>(acc[1][c], wb[q], px[c + J]);
       }
+      compute_from<J + 1, C, A, B>();
     }
   }
   // step t, chunk C onwards.  On entry chunk C's pairs and weights are in
   // flight; on exit the next step's first chunk is.  `base_n` addresses the
   // next step's pixel rows, rows_n its weight rows.
   template <int C, bool A, bool B, typename F>
-  DEV void chunks(unsigned base, unsigned base_n, const float* __restrict__ ra, const float* __restrict__ rb,
-                  const float* __restrict__ ra_n, const float* __restrict__ rb_n, F&& at_start) {
+  DEV void chunks(unsigned base, unsigned base_n, const lm_f2* __restrict__ ra, const lm_f2* __restrict__ rb,
+                  const lm_f2* __restrict__ ra_n, const lm_f2* __restrict__ rb_n, F&& at_start) {
     // lgkmcnt(0) through the builtin (vmcnt / expcnt left at their maxima), so
     // the compiler's own wait insertion knows the scalar loads are done too
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (C == 0) at_start();
-    float na[P::WMAX], nb[P::WMAX];
+    lm_f2 na[P::PMAX], nb[P::PMAX];
     if constexpr (C + 1 < P::N) {
       load_w<C + 1>(na, nb, ra, rb);
       issue<P::pbeg(C + 1), P::pend(C + 1)>(base);
@@ -319,12 +359,12 @@ struct RwPipe {
       issue<P::pbeg(0), P::pend(0)>(base_n);
     }
     __builtin_amdgcn_sched_barrier(0);
-    compute<C, A, B>();
+    compute_from<P::beg(C), C, A, B>();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < P::WMAX; ++j) {
-      wa[j] = na[j];
-      wb[j] = nb[j];
+    for (int q = 0; q < P::PMAX; ++q) {
+      wa[q] = na[q];
+      wb[q] = nb[q];
     }
     if constexpr (C + 1 < P::N) chunks<C + 1, A, B>(base, base_n, ra, rb, ra_n, rb_n, at_start);
   }
@@ -375,16 +415,16 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     }
   };
   {
-    unsigned v0[LM_RW_SLOTS - 2];
+    unsigned v0[LM_RW_SLOTS];
 #pragma unroll
-    for (int r = 0; r < LM_RW_SLOTS - 2; ++r) v0[r] = load_row(r);
+    for (int r = 0; r < LM_RW_SLOTS; ++r) v0[r] = load_row(r);
 #pragma unroll
-    for (int r = 0; r < LM_RW_SLOTS - 2; ++r) store_row(r, v0[r]);
+    for (int r = 0; r < LM_RW_SLOTS; ++r) store_row(r, v0[r]);
   }
-  unsigned pa = load_row(LM_RW_SLOTS - 2), pb = load_row(LM_RW_SLOTS - 1);
 
   lm_f2 acc[PK_R / 2][PK_C];
-  const float* __restrict__ W = weights + D.w_off;
+  const lm_f2* __restrict__ W = reinterpret_cast<const lm_f2*>(weights + D.w_off);  // kwp is a multiple of 4
+  const int kwp2 = kwp >> 1;
   const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring;
   const unsigned lane_off = (unsigned)((lx * PK_C + mis) * (int)sizeof(float));
   auto row_base = [&](int t) -> unsigned {
@@ -395,19 +435,22 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   for (int p = 0; p < 2; ++p)
 #pragma unroll
     for (int c = 0; c < PK_C; ++c) S.acc[p][c] = (lm_f2){D.delta, D.delta};
-  auto wrow = [&](int i) { return W + min(max(i, 0), kh - 1) * kwp; };
+  auto wrow = [&](int i) { return W + min(max(i, 0), kh - 1) * kwp2; };
   S.template load_w<0>(S.wa, S.wb, wrow(0), wrow(-2));
   S.template issue<RwPlan<KW>::pbeg(0), RwPlan<KW>::pend(0)>(row_base(0));
+  // Step t reads ring rows t .. t + 13 and prefetches step t + 1's rows
+  // t + 1 .. t + 14 in its last chunk; it loads row t + 16 at its start and
+  // stores it at its end into the slot of row t (dead by then: a wave's LDS
+  // operations run in order).  The load has a whole step to land, and no
+  // register carries a row from one step to the next (with rows carried in
+  // rotating registers, each rotation moved a load's destination and so waited
+  // for it).
   auto step = [&](int t, auto A, auto B) {
-    auto at_start = [&]() {
-      // row t + 14 is read from the next step on (its pairs are issued in
-      // this step's last chunk); its slot held row t - 2
-      store_row(t + LM_RW_SLOTS - 2, pa);
-      pa = pb;
-      pb = load_row(t + LM_RW_SLOTS);
-    };
+    unsigned nx = 0;
     S.template chunks<0, decltype(A)::value, decltype(B)::value>(row_base(t), row_base(t + 1), wrow(t), wrow(t - 2),
-                                                                  wrow(t + 1), wrow(t - 1), at_start);
+                                                                  wrow(t + 1), wrow(t - 1),
+                                                                  [&]() { nx = load_row(t + LM_RW_SLOTS); });
+    store_row(t + LM_RW_SLOTS, nx);
   };
   using T1 = std::true_type;
   using F0 = std::false_type;

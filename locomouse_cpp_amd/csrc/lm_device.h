@@ -121,18 +121,19 @@ struct LmSlotOut {
 
 // arena counters (device -> host)
 enum { AR_CAND = 0, AR_P22D, AR_SIDE, AR_UNARY, AR_PWJC, AR_PWNZ, AR_COUNT };
-// Each arena is split into LM_SUBARENA equal parts with their own bump
-// counters (one 128-byte line each), so the blocks of a batch do not all
-// queue on one cache line of atomics; a (slot, feature) block allocates from
-// part (block % LM_SUBARENA).  `used` is filled by k_pack_scan with what the
-// fullest part implies for the whole arena (LM_SUBARENA x its count), which
-// is what the host grows the capacity to after an overflow.
+// Each arena is split into nparts = min(LM_SUBARENA, k_post blocks) equal
+// parts with their own bump counters (one 128-byte line each), so the blocks
+// of a batch do not all queue on one cache line of atomics; a (slot, feature)
+// block allocates from part (block % nparts).  `used` is filled by
+// k_pack_scan with what the fullest part implies for the whole arena
+// (nparts x its count), which is what the host grows the capacity to after
+// an overflow.
 #define LM_SUBARENA 16
 struct LmArenaCtl {
   int32_t used[AR_COUNT];
   int32_t cap[AR_COUNT];
   int32_t overflow;
-  int32_t pad_;
+  int32_t nparts;                  // parts in use this batch (set by the host)
   int32_t sub[LM_SUBARENA][32];  // sub[g][k]: part g's count of arena k (k < AR_COUNT)
 };
 

@@ -1220,10 +1220,9 @@ DEV void for_overflow_pairs(int npairs, Pred overflow, Fn fn) {
 // holding both paths ran the common one slower (register allocation).
 // LM_KPROF=1: clock64() of thread 0 per k_post phase (LDS instantiation),
 // 16 per (frame, feature) block; null otherwise
-__device__ long long* g_post_prof;
 #define POST_PROF(k)                                                                           \
   if (!G && threadIdx.x == 0) {                                                                \
-    long long* pp_ = g_post_prof;                                                              \
+    long long* pp_ = prof;                                                                     \
     if (pp_) pp_[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = (k) >= 14 ? wall_clock64() : clock64(); \
   }
 template <bool GLOB>
@@ -1298,7 +1297,7 @@ DEV bool vel_criterion_wave(const LmConst& K, FP Fc, FP Fp, const uint8_t* bkg, 
 // Bump allocation of `amount` entries of arena k from sub-arena g (one
 // thread): the offset, or -1 with the overflow flag set.
 DEV int arena_alloc(LmArenaCtl* __restrict__ ctl, int k, int g, int amount) {
-  const int part = ctl->cap[k] / LM_SUBARENA;
+  const int part = ctl->cap[k] / ctl->nparts;
   const int b = atomicAdd(&ctl->sub[g][k], amount);
   if (b + amount > part) {
     atomicOr(&ctl->overflow, 1);
@@ -1320,7 +1319,8 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
                   int cap, int* s_base, int& s_any1, int& s_any0, LmP22D* __restrict__ arena_p22d,
                   int32_t* __restrict__ arena_side_y, double* __restrict__ arena_side_s, double* __restrict__ arena_unary,
                   int32_t* __restrict__ arena_jc, int32_t* __restrict__ arena_ir, double* __restrict__ arena_pr,
-                  LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err, int sub) {
+                  LmArenaCtl* __restrict__ ctl, int32_t* __restrict__ err, int sub,
+                  long long* __restrict__ prof) {
   POST_PROF(14)
   POST_PROF(0)
   // ---------------- unary (unaryCostBox :1909-1952), column-major Nb x nprior
@@ -1642,10 +1642,10 @@ DEV void post_run(const LmConst& K, const LmSlot* __restrict__ slots, const uint
       int32_t *__restrict__ arena_side_y, double *__restrict__ arena_side_s, double *__restrict__ arena_unary,      \
       int32_t *__restrict__ arena_jc, int32_t *__restrict__ arena_ir, double *__restrict__ arena_pr,                \
       LmArenaCtl *__restrict__ ctl, int32_t *__restrict__ err, unsigned long long *__restrict__ gscratch,          \
-      int64_t gscratch_slot
+      int64_t gscratch_slot, long long *__restrict__ prof
 #define LM_POST_PASS                                                                                                \
   Kp, slots, frame_ptr, bkg, cal, luts, hdr, keys, arena_p22d, arena_side_y, arena_side_s, arena_unary, arena_jc,    \
-      arena_ir, arena_pr, ctl, err, gscratch, gscratch_slot
+      arena_ir, arena_pr, ctl, err, gscratch, gscratch_slot, prof
 template <bool GLOB>
 DEV void post_block(int bx, int feat, LM_POST_ARGS) {
   const LmConst& K = *Kp;
@@ -1673,7 +1673,7 @@ DEV void post_block(int bx, int feat, LM_POST_ARGS) {
     __syncthreads();
     post_run<false>(K, slots, frame_ptr, bkg, cal, luts, H, slot, feat, frame, Nb, Ns, Ni, sb, st, sp, s_off, s_mb, s_mt,
                     s_bps, s_tpb, LM_POST_MAXC, s_base, s_any1, s_any0, arena_p22d, arena_side_y, arena_side_s,
-                    arena_unary, arena_jc, arena_ir, arena_pr, ctl, err, (2 * bx + feat) % LM_SUBARENA);
+                    arena_unary, arena_jc, arena_ir, arena_pr, ctl, err, (2 * bx + feat) % ctl->nparts, prof);
   } else {  // long lists: k_nms's scratch of this (slot, feature) is free again
     const int big = max(max(Nb, Ns), Ni);
     int* g = reinterpret_cast<int*>(gscratch + (int64_t)(feat + 2 * bx) * gscratch_slot);
@@ -1688,7 +1688,7 @@ DEV void post_block(int bx, int feat, LM_POST_ARGS) {
     }
     post_run<true>(K, slots, frame_ptr, bkg, cal, luts, H, slot, feat, frame, Nb, Ns, Ni, cb, ct, cp, g_off, g_mb, g_mt,
                    g_bps, g_tpb, big, s_base, s_any1, s_any0, arena_p22d, arena_side_y, arena_side_s, arena_unary,
-                   arena_jc, arena_ir, arena_pr, ctl, err, (2 * bx + feat) % LM_SUBARENA);
+                   arena_jc, arena_ir, arena_pr, ctl, err, (2 * bx + feat) % ctl->nparts, prof);
   }
 }
 
@@ -1754,7 +1754,10 @@ __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots
     ctl->used[threadIdx.x] = h_ctl->used[threadIdx.x];
     ctl->cap[threadIdx.x] = h_ctl->cap[threadIdx.x];
   }
-  if (threadIdx.x == 0) ctl->overflow = h_ctl->overflow;
+  if (threadIdx.x == 0) {
+    ctl->overflow = h_ctl->overflow;
+    ctl->nparts = h_ctl->nparts;
+  }
   for (int i = threadIdx.x; i < LM_SUBARENA * 32; i += blockDim.x) (&ctl->sub[0][0])[i] = 0;
 }
 
@@ -1855,8 +1858,8 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const LmSlotOut* __restrict_
     ph->err = *err;
     for (int k = 0; k < AR_COUNT; ++k) {
       int m = 0;
-      for (int g = 0; g < LM_SUBARENA; ++g) m = max(m, ctl->sub[g][k]);
-      ph->used[k] = m * LM_SUBARENA;
+      for (int g = 0; g < ctl->nparts; ++g) m = max(m, ctl->sub[g][k]);
+      ph->used[k] = m * ctl->nparts;
     }
   }
 }

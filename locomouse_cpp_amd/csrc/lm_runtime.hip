@@ -15,6 +15,8 @@
 #include <cstring>
 #include <map>
 #include <atomic>
+#include <deque>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -75,11 +77,83 @@ struct Arena {
   }
 };
 
+// One batch in flight: its HIP stream, the per-batch device buffers and the
+// packed results of its last batch.  A context owns `lanes` of them and
+// submits consecutive batches round-robin, so several batches of one video
+// run concurrently (batch k + 1's correlation overlaps batch k's post-
+// correlation kernels); see submit_batch.
+struct Lane {
+  int index = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevBuf<uint8_t> frames, halo, luts, ext, tailbin;
+  DevBuf<unsigned long long> tailmask;  // TAIL_MASK bitmaps, 64 columns per word
+  DevBuf<int32_t> npos, err;
+  DevBuf<unsigned> mm;        // k_minmax partial (min, max) pairs per slot
+  DevBuf<unsigned> tscratch;  // k_tail run tables beyond its LDS
+  DevBuf<float> dbg;
+  DevBuf<int64_t> dbg_offd;
+  DevBuf<const uint8_t*> frame_ptr;
+  DevBuf<LmSlot> slots;
+  DevBuf<unsigned long long> keys, gscratch;
+  DevBuf<long long> kprof;  // LM_KPROF=1: kernel phase timestamps
+  Arena arena[2];
+  int parity = 0;
+  // host
+  HostBuf<LmSlot> h_slots;
+  HostBuf<const uint8_t*> h_frame_ptr;
+  HostBuf<LmArenaCtl> h_ctl;
+  HostBuf<int32_t> h_err;
+  HostBuf<LmPackHdr> h_ph;
+  HostBuf<uint8_t> h_pack;  // packed results of the lane's last batch (lm_batch_result points here)
+  DevBuf<LmPackHdr> zero_ph;
+  // this lane's last batch: the state a batch continuing it on this lane carries over
+  bool have_state = false;
+  int last_frame = -1, last_n = 0, last_parity = 0;
+  // the submitted batch (collected by finish_batch)
+  struct Pending {
+    bool on = false;
+    int n = 0, first = 0, s_lut0 = 1, s_proc0 = 1, plan = 0, cur = 0, prv = 0, last_n = 0;
+    bool carry = false;
+  } pend;
+  int batch_n = 0, batch_s0 = 1;  // last collected batch
+  // pipelined halos: the batch's last frame copied to the context's handoff
+  // buffer / the predecessor's handoff frame copied into this lane's halo
+  hipEvent_t ev_snap = nullptr, ev_consumed = nullptr;
+  // timing (debug bit 1): events around k_corr on this lane's stream
+  std::vector<std::pair<const char*, int>> t_ev;  // (kernel, index of its begin event in ev_pool)
+  std::vector<const char*> t_names;               // static kernel names
+  std::vector<double> t_ms, t_t0, t_t1;
+  std::vector<hipEvent_t> ev_pool;
+  // captured per-batch kernel chains, keyed by (n, parity, carry, last n, s_lut0, s_proc0, plan)
+  struct GraphEntry {
+    hipGraphExec_t exec[3];  // kernels before k_corr, k_corr, after
+  };
+  std::map<std::array<int, 7>, GraphEntry> graphs;
+  bool use_graphs = true;
+  void drop_graphs() {
+    for (auto& g : graphs)
+      for (hipGraphExec_t x : g.second.exec)
+        if (x) (void)hipGraphExecDestroy(x);
+    graphs.clear();
+  }
+  ~Lane() {
+    drop_graphs();
+    if (stream) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(stream);
+      for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+      if (ev_snap) (void)hipEventDestroy(ev_snap);
+      if (ev_consumed) (void)hipEventDestroy(ev_consumed);
+      (void)hipStreamDestroy(stream);
+    }
+  }
+};
+
 }  // namespace
 
 struct lm_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
   int max_batch = 0, nslots = 0;
   int debug = 0;
   lm_setup setup{};
@@ -87,6 +161,7 @@ struct lm_ctx {
   lm_geometry geo{};
   LmConst K{};
   int npix = 0;
+  int64_t fstride = 0;                 // device frame pitch of the staging slots
   int bb_x = 0, bb_yb = 0, bb_ys = 0;  // provided-box bottom-right corners
   int spost_b_w = 0, spost_b_h = 0, spost_t_w = 0, spost_t_h = 0;
   int64_t ext_slot_bytes = 0, tailbin_slot_bytes = 0, dbg_slot_floats = 0;
@@ -102,64 +177,24 @@ struct lm_ctx {
     std::vector<int> threads;                                // block size per group launch
     std::vector<char> ring;                                  // group runs k_corr_rw* (one wave per tile)
   } corr_plan[2];
-  // device buffers
-  DevBuf<uint8_t> bkg, adj, frames, halo, luts, ext, tailbin;
-  DevBuf<unsigned long long> tailmask;  // TAIL_MASK bitmaps, 64 columns per word
-  DevBuf<int32_t> cal, npos, err;
-  DevBuf<unsigned> mm;  // k_minmax partial (min, max) pairs per slot
-  DevBuf<float> weights, dbg;
+  // frame-invariant device data
+  DevBuf<uint8_t> bkg, adj;
+  DevBuf<int32_t> cal;
+  DevBuf<float> weights;
   DevBuf<_Float16> weights16;  // LM_CORR_F16 rows (LmDet::w16_off)
-  DevBuf<int64_t> dbg_offd;
-  DevBuf<const uint8_t*> frame_ptr;
-  DevBuf<LmSlot> slots;
-  DevBuf<unsigned long long> keys, gscratch;
   DevBuf<LmConst> dK;  // the per-context constants, passed to every kernel by pointer
-  DevBuf<unsigned> tscratch;  // k_tail run tables beyond its LDS
   size_t tail_lds = 0;
-  DevBuf<long long> kprof;  // LM_KPROF=1: k_nms phase timestamps
   bool kprof_on = false;
-  Arena arena[2];
-  int parity = 0;
-  // host
-  HostBuf<LmSlot> h_slots;
-  HostBuf<const uint8_t*> h_frame_ptr;
-  HostBuf<LmArenaCtl> h_ctl;
-  HostBuf<int32_t> h_err;
-  HostBuf<LmPackHdr> h_ph;
-  HostBuf<uint8_t> h_pack;  // packed results of the last batch (lm_batch_result points here)
-  DevBuf<LmPackHdr> zero_ph;
-  // state carried between batches
+  // pipeline
+  std::vector<std::unique_ptr<Lane>> lanes;
+  DevBuf<uint8_t> handoff;     // two frames: the last frame of submitted batch k in slot k & 1
+  std::deque<int> inflight;    // lanes holding a submitted batch, in submission order
+  int next_lane = 0, last_lane = -1, collected_lane = 0;
+  int64_t nsub = 0;            // batches submitted
+  // the video position after the last submitted batch
   bool have_state = false;
-  int last_frame = -1, last_n = 0, last_parity = 0;
+  int last_frame = -1;
   int last_bb[3] = {0, 0, 0};  // bottom-right corners of frame last_frame
-  // last batch info
-  int batch_n = 0, batch_s0 = 1;
-  // timing
-  std::vector<const char*> t_names;  // static kernel names
-  std::vector<double> t_ms, t_t0, t_t1;
-  std::vector<hipEvent_t> ev_pool;
-  // captured per-batch kernel chains, keyed by (n, parity, carry, last n, s_lut0, s_proc0, 0)
-  struct GraphEntry {
-    hipGraphExec_t exec[3];  // kernels before k_corr, k_corr, after
-  };
-  std::map<std::array<int, 7>, GraphEntry> graphs;
-  bool use_graphs = true;
-  void drop_graphs() {
-    for (auto& g : graphs)
-      for (hipGraphExec_t x : g.second.exec)
-        if (x) (void)hipGraphExecDestroy(x);
-    graphs.clear();
-  }
-
-  ~lm_ctx() {
-    drop_graphs();
-    if (stream) {
-      (void)hipSetDevice(device);
-      (void)hipStreamSynchronize(stream);
-      for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-      (void)hipStreamDestroy(stream);
-    }
-  }
 };
 
 namespace {
@@ -560,47 +595,67 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     }
   }
 
-  // ---------------- device allocations
-  const int ns = c->nslots;
+  // ---------------- frame-invariant device data (create-time copies on a
+  // temporary stream: see COPY_SYNC)
+  hipStream_t cs = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  struct StreamGuard {
+    hipStream_t s;
+    ~StreamGuard() { (void)hipStreamDestroy(s); }
+  } cs_guard{cs};
   c->bkg.alloc(nv);
-  COPY_SYNC(c->bkg.p, su->background, nv, hipMemcpyHostToDevice, c->stream);
+  COPY_SYNC(c->bkg.p, su->background, nv, hipMemcpyHostToDevice, cs);
   c->cal.alloc(nc);
-  COPY_SYNC(c->cal.p, su->ind_warp_mapping, nc * sizeof(int32_t), hipMemcpyHostToDevice, c->stream);
+  COPY_SYNC(c->cal.p, su->ind_warp_mapping, nc * sizeof(int32_t), hipMemcpyHostToDevice, cs);
   c->weights.alloc(wts.size());
-  COPY_SYNC(c->weights.p, wts.data(), wts.size() * sizeof(float), hipMemcpyHostToDevice, c->stream);
+  COPY_SYNC(c->weights.p, wts.data(), wts.size() * sizeof(float), hipMemcpyHostToDevice, cs);
   if (!w16.empty()) {
     c->weights16.alloc(w16.size());
-    COPY_SYNC(c->weights16.p, w16.data(), w16.size() * sizeof(_Float16), hipMemcpyHostToDevice, c->stream);
+    COPY_SYNC(c->weights16.p, w16.data(), w16.size() * sizeof(_Float16), hipMemcpyHostToDevice, cs);
   }
   c->adj.alloc(256);
-  COPY_SYNC(c->adj.p, adj, 256, hipMemcpyHostToDevice, c->stream);
+  COPY_SYNC(c->adj.p, adj, 256, hipMemcpyHostToDevice, cs);
   c->dK.alloc(1);
-  COPY_SYNC(c->dK.p, &c->K, sizeof(LmConst), hipMemcpyHostToDevice, c->stream);
-  const int64_t fstride = (nv + 255) / 256 * 256;
-  c->frames.alloc((size_t)fstride * ns);
-  c->halo.alloc(fstride);
-  SET_SYNC(c->halo.p, 0, fstride, c->stream);
-  c->luts.alloc((size_t)256 * ns);
-  c->mm.alloc((size_t)2 * LM_MM_SPLIT * ns);
+  COPY_SYNC(c->dK.p, &c->K, sizeof(LmConst), hipMemcpyHostToDevice, cs);
+  c->fstride = (nv + 255) / 256 * 256;
+  HIPCHK(hipFuncSetAttribute((const void*)k_tail, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->tail_lds));
+  for (const auto& P : c->corr_plan)
+    for (size_t g = 0; g < P.groups.size(); ++g)
+      HIPCHK(hipFuncSetAttribute(P.groups[g].first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds[g]));
+}
+
+
+// The per-batch buffers of one lane (B = max_batch, slots 0..B).
+void lane_alloc(lm_ctx* c, Lane& L) {
+  const LmConst& K = c->K;
+  const lm_geometry& g = c->geo;
+  const int ns = c->nslots;
+  const int64_t fstride = c->fstride;
+  hipStream_t st = L.stream;
+  L.frames.alloc((size_t)fstride * ns);
+  L.halo.alloc(fstride);
+  SET_SYNC(L.halo.p, 0, fstride, st);
+  L.luts.alloc((size_t)256 * ns);
+  L.mm.alloc((size_t)2 * LM_MM_SPLIT * ns);
   // slack: the last tiles' windows (and the fill's 16-byte rounding) read past
   // the last slot's side view; those pixels only feed outputs that are discarded
-  c->ext.alloc((size_t)c->ext_slot_bytes * ns + (size_t)(LM_F16_TH + 16) * std::max(K.ext_w[0], K.ext_w[1]) + 64);
-  c->tailbin.alloc((size_t)c->tailbin_slot_bytes * ns);
-  SET_SYNC(c->tailbin.p, 0, (size_t)c->tailbin_slot_bytes * ns, c->stream);
-  c->tailmask.alloc((size_t)K.tail_hb * ((K.tail_w + 63) / 64) * ns);
-  c->tscratch.alloc((size_t)5 * std::max(K.tail_hb, K.tail_hs) * ((K.tail_w + 1) / 2) * ns);
-  c->keys.alloc((size_t)K.keys_per_slot * ns);
-  c->npos.alloc((size_t)LM_NLIST * ns);
-  c->err.alloc(16);
-  c->frame_ptr.alloc(ns);
-  c->slots.alloc(ns);
-  c->h_slots.alloc(ns);
-  c->h_frame_ptr.alloc(ns);
-  c->h_ctl.alloc(1);
-  c->h_ph.alloc(1);
-  c->zero_ph.alloc(1);  // an all-zero pack header: k_out with it copies only the halo
-  SET_SYNC(c->zero_ph.p, 0, sizeof(LmPackHdr), c->stream);
-  c->h_err.alloc(16);
+  L.ext.alloc((size_t)c->ext_slot_bytes * ns + (size_t)(LM_F16_TH + 16) * std::max(K.ext_w[0], K.ext_w[1]) + 64);
+  L.tailbin.alloc((size_t)c->tailbin_slot_bytes * ns);
+  SET_SYNC(L.tailbin.p, 0, (size_t)c->tailbin_slot_bytes * ns, st);
+  L.tailmask.alloc((size_t)K.tail_hb * ((K.tail_w + 63) / 64) * ns);
+  L.tscratch.alloc((size_t)5 * std::max(K.tail_hb, K.tail_hs) * ((K.tail_w + 1) / 2) * ns);
+  L.keys.alloc((size_t)K.keys_per_slot * ns);
+  L.npos.alloc((size_t)LM_NLIST * ns);
+  L.err.alloc(16);
+  L.frame_ptr.alloc(ns);
+  L.slots.alloc(ns);
+  L.h_slots.alloc(ns);
+  L.h_frame_ptr.alloc(ns);
+  L.h_ctl.alloc(1);
+  L.h_ph.alloc(1);
+  L.zero_ph.alloc(1);  // an all-zero pack header: k_out with it copies only the halo
+  SET_SYNC(L.zero_ph.p, 0, sizeof(LmPackHdr), st);
+  L.h_err.alloc(16);
   int cap[AR_COUNT];
   cap[AR_CAND] = ns * LM_NLIST * 64;
   cap[AR_P22D] = ns * LM_NFEAT * 64;
@@ -608,14 +663,11 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   cap[AR_UNARY] = ns * LM_NFEAT * 64 * 4;
   cap[AR_PWJC] = ns * LM_NFEAT * (64 + g.ong_nx * g.ong_ny + 1);
   cap[AR_PWNZ] = ns * LM_NFEAT * 1024;
-  for (int a = 0; a < 2; ++a) c->arena[a].alloc(cap, ns);
-  c->h_pack.alloc((size_t)c->arena[0].pack_cap);
-  HIPCHK(hipFuncSetAttribute((const void*)k_tail, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->tail_lds));
-  for (const auto& P : c->corr_plan)
-    for (size_t g = 0; g < P.groups.size(); ++g)
-      HIPCHK(hipFuncSetAttribute(P.groups[g].first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds[g]));
+  for (int a = 0; a < 2; ++a) L.arena[a].alloc(cap, ns);
+  L.h_pack.alloc((size_t)L.arena[0].pack_cap);
+  HIPCHK(hipEventCreateWithFlags(&L.ev_snap, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&L.ev_consumed, hipEventDisableTiming));
 }
-
 
 // One epoch event per device (recorded when timing is switched on) that every
 // context's kernel spans are measured against.
@@ -629,67 +681,64 @@ hipEvent_t epoch_event(const lm_ctx* c) {
 }
 
 
-struct Timer {
-  lm_ctx* c;
+struct Timer {  // HIP events around the timed kernels of a lane's batch (debug bit 1)
+  Lane& L;
   bool on;
-  std::vector<std::pair<const char*, int>> ev;  // (kernel, index of its begin event in the ctx pool)
-  explicit Timer(lm_ctx* cc) : c(cc), on(cc->debug & 2) {}
+  Timer(lm_ctx* c, Lane& l) : L(l), on(c->debug & 2) {}
   hipEvent_t pool(size_t i) {
-    while (c->ev_pool.size() <= i) {
+    while (L.ev_pool.size() <= i) {
       hipEvent_t e;
       HIPCHK(hipEventCreate(&e));
-      c->ev_pool.push_back(e);
+      L.ev_pool.push_back(e);
     }
-    return c->ev_pool[i];
+    return L.ev_pool[i];
   }
   bool capturing = false;  // inside a graph capture: a failed record aborts the capture, not the batch
   void record(hipEvent_t e) {
-    const hipError_t r = hipEventRecord(e, c->stream);
+    const hipError_t r = hipEventRecord(e, L.stream);
     if (r != hipSuccess && !capturing) hip_check(r, "hipEventRecord");
   }
   void begin(const char* name) {
     if (!on) return;
-    const int i = (int)ev.size() * 2;
+    const int i = (int)L.t_ev.size() * 2;
     record(pool(i));
-    ev.push_back({name, i});
+    L.t_ev.push_back({name, i});
   }
   void end() {
     if (!on) return;
-    record(pool(ev.back().second + 1));
+    record(pool(L.t_ev.back().second + 1));
   }
   // Durations, plus start/end against the device's epoch event so callers can
-  // take the union of one kernel's spans over several contexts' streams.
-  void collect() {
-    if (!on) return;
-    c->t_names.clear();
-    c->t_ms.clear();
-    c->t_t0.clear();
-    c->t_t1.clear();
+  // take the union of one kernel's spans over several streams.
+  static void collect(lm_ctx* c, Lane& L) {
+    L.t_names.clear();
+    L.t_ms.clear();
+    L.t_t0.clear();
+    L.t_t1.clear();
     const hipEvent_t ep = epoch_event(c);
-    for (auto& e : ev) {
+    for (auto& e : L.t_ev) {
       float ms = 0, t0 = 0, t1 = 0;
-      HIPCHK(hipEventElapsedTime(&ms, c->ev_pool[e.second], c->ev_pool[e.second + 1]));
+      HIPCHK(hipEventElapsedTime(&ms, L.ev_pool[e.second], L.ev_pool[e.second + 1]));
       if (ep) {
-        HIPCHK(hipEventElapsedTime(&t0, ep, c->ev_pool[e.second]));
-        HIPCHK(hipEventElapsedTime(&t1, ep, c->ev_pool[e.second + 1]));
+        HIPCHK(hipEventElapsedTime(&t0, ep, L.ev_pool[e.second]));
+        HIPCHK(hipEventElapsedTime(&t1, ep, L.ev_pool[e.second + 1]));
       }
-      c->t_names.push_back(e.first);
-      c->t_ms.push_back(ms);
-      c->t_t0.push_back(t0);
-      c->t_t1.push_back(t1);
+      L.t_names.push_back(e.first);
+      L.t_ms.push_back(ms);
+      L.t_t0.push_back(t0);
+      L.t_t1.push_back(t1);
     }
-    ev.clear();
+    L.t_ev.clear();
   }
 };
 
-// LM_KPROF=1: mean cycles per k_nms / k_tail phase over the batch's blocks (stderr)
-// Live contexts per device.  A context alone on its device runs the merged
-// correlation plan (one k_corr_rw_all launch: the widths share one tail
-// instead of ending four; one context 231k -> 260k frames/s at C3); with
-// several contexts the per-width launches interleave better with the other
-// contexts' post-correlation kernels (4 contexts: 340k vs 322k merged;
-// profiles/r02/merged/).  LM_CORR_PLAN=0 / 1 forces one.
-std::atomic<int> g_live_ctx[64];
+// Batch streams per device (every lane of every live context).  With one
+// stream on its device a batch runs the merged correlation plan (one
+// k_corr_rw_all launch: the widths share one tail instead of ending four);
+// with several, the per-width launches interleave better with the other
+// streams' post-correlation kernels (4 streams: 340k vs 322k frames/s merged;
+// profiles/r02/merged/).  LM_CORR_PLAN=0 / 1 or debug bits 4 / 5 force one.
+std::atomic<int> g_live_streams[64];
 
 int corr_plan_for(const lm_ctx* c) {
   static const int forced = [] {
@@ -697,12 +746,15 @@ int corr_plan_for(const lm_ctx* c) {
     return v ? atoi(v) : -1;
   }();
   if (forced == 0 || forced == 1) return forced;
-  return g_live_ctx[c->device & 63].load(std::memory_order_relaxed) <= 1 ? 1 : 0;
+  if (c->debug & 16) return 0;
+  if (c->debug & 32) return 1;
+  return g_live_streams[c->device & 63].load(std::memory_order_relaxed) <= 1 ? 1 : 0;
 }
 
-void kprof_report(lm_ctx* c, int n) {
+// LM_KPROF=1: mean cycles per k_nms / k_tail / k_post phase over the batch's blocks (stderr)
+void kprof_report(lm_ctx* c, Lane& L, int n) {
   std::vector<long long> h((size_t)4 * 16 * 2 * c->nslots);
-  COPY_SYNC(h.data(), c->kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream);
+  COPY_SYNC(h.data(), L.kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost, L.stream);
   {  // k_post (LDS instantiation): region 3, one block per (frame, feature)
     const long long* base = h.data() + (size_t)3 * 16 * 2 * c->nslots;
     double acc[8] = {0}, life = 0;
@@ -803,24 +855,16 @@ void kprof_report(lm_ctx* c, int n) {
   }
 }
 
-void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev,
-                    const int32_t* bb, bool device_frames, lm_batch_result* out);
-
-void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev, const int32_t* bb,
-               bool device_frames, lm_batch_result* out) {
-  run_batch_impl(c, frames, pitch, n, first, prev, bb, device_frames, out);
-}
-
 // Diagnostics (LM_DUMP_DIR): one slot's candidate-path state after a failed
 // batch -> <dir>/dump_<frame>.bin: int32 [frame, slot, feat, npos_b, npos_s,
 // hdr.n_pos[4], hdr.cand_cnt[4], hdr.ties[4]] then, per list 0..3, the list's
 // whole key area (u64 x list_cap).
-void dump_slot(lm_ctx* c, const char* dir, int frame, int slot, int feat) {
+void dump_slot(lm_ctx* c, Lane& L, const char* dir, int frame, int slot, int feat) {
   const LmConst& K = c->K;
   std::vector<int32_t> np(LM_NLIST);
-  COPY_SYNC(np.data(), c->npos.p + (int64_t)slot * LM_NLIST, LM_NLIST * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+  COPY_SYNC(np.data(), L.npos.p + (int64_t)slot * LM_NLIST, LM_NLIST * sizeof(int32_t), hipMemcpyDeviceToHost, L.stream);
   LmSlotOut h;
-  COPY_SYNC(&h, c->arena[c->parity].hdr.p + slot, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+  COPY_SYNC(&h, L.arena[L.parity].hdr.p + slot, sizeof(h), hipMemcpyDeviceToHost, L.stream);
   std::string path = std::string(dir) + "/dump_" + std::to_string(frame) + ".bin";
   FILE* f = fopen(path.c_str(), "wb");
   if (!f) return;
@@ -834,30 +878,216 @@ void dump_slot(lm_ctx* c, const char* dir, int frame, int slot, int feat) {
   fwrite(np.data(), sizeof(int32_t), LM_NLIST, f);
   for (int l = 0; l < LM_NLIST; ++l) {
     std::vector<unsigned long long> kv((size_t)K.list_cap[l]);
-    HIPCHK(hipMemcpy(kv.data(), c->keys.p + (int64_t)slot * K.keys_per_slot + K.list_off[l],
+    HIPCHK(hipMemcpy(kv.data(), L.keys.p + (int64_t)slot * K.keys_per_slot + K.list_off[l],
                      kv.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     fwrite(kv.data(), sizeof(unsigned long long), kv.size(), f);
   }
   fclose(f);
 }
 
-void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev,
-                    const int32_t* bb, bool device_frames, lm_batch_result* out) {
+// The kernel chain of one batch attempt on lane L (part: 0 the kernels before
+// k_corr, 1 k_corr, 2 the kernels after, -1 all).  Kernel arguments depend
+// only on the key of L.graphs (frame pointers and slots reach the kernels
+// through k_prep's copies of mapped host arrays), so the chain is captured
+// once per key into hipGraphs and replayed.
+void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& T, bool do_carry, int part) {
+  const LmConst& K = c->K;
+  const LmConst* dK = c->dK.p;
+  hipStream_t st = L.stream;
+  const int n = P.n, s_lut0 = P.s_lut0, s_proc0 = P.s_proc0;
+  const int nproc = n + 1 - s_proc0;
+  if (part <= 0) {
+    k_prep<<<1, 256, 0, st>>>(L.h_slots.d, L.h_frame_ptr.d, L.h_ctl.d, n + 1, L.slots.p, L.frame_ptr.p, A.ctl.p,
+                              L.npos.p, L.err.p);
+    if (do_carry) {  // a rerun keeps slot 0's staged candidates
+      T.begin("k_carry");
+      k_carry<<<1, 256, 0, st>>>(dK, L.keys.p, L.arena[P.prv].hdr.p, P.last_n, A.hdr.p);
+      T.end();
+    }
+    T.begin("k_minmax");
+    k_minmax<<<dim3(LM_MM_SPLIT, n + 1 - s_lut0), LM_MM_THREADS, 0, st>>>(L.frame_ptr.p, c->bkg.p, c->npix, s_lut0,
+                                                                        L.mm.p);
+    k_lut<<<(n + 1 - s_lut0 + 3) / 4, 256, 0, st>>>(L.mm.p, s_lut0, n + 1, c->adj.p, c->setup.method != 0, L.luts.p);
+    T.end();
+    const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
+    T.begin("k_ingest");
+    const unsigned ext_blocks = (unsigned)((etot / LM_INGEST_VEC + 255) / 256);
+    const unsigned zero_blocks = (unsigned)((K.tail_bm_words + 4 * 256 - 1) / (4 * 256));  // the tail bitmaps
+    k_ingest<<<dim3(ext_blocks + zero_blocks, (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)), 256, 0, st>>>(
+        dK, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, L.slots.p, s_proc0, n + 1, L.ext.p, c->ext_slot_bytes,
+        ext_blocks, reinterpret_cast<unsigned*>(L.tailbin.p));
+    T.end();
+  }
+  if (part == 1 || part < 0) {
+    T.begin("k_corr");
+    const lm_ctx::CorrPlan& CP = c->corr_plan[P.plan];
+    for (size_t gi = 0; gi < CP.groups.size(); ++gi) {
+      const auto& grp = CP.groups[gi];
+      const LmDetGroup& G = grp.second;
+      const void* w = c->setup.corr_precision == LM_CORR_F16 ? (const void*)c->weights16.p : (const void*)c->weights.p;
+      HIPCHK(launch_corr(grp.first, CP.ring[gi], dim3(G.tile_end[G.n - 1], nproc), CP.threads[gi], CP.lds[gi], st, dK,
+                         G, L.ext.p, c->ext_slot_bytes, w, s_proc0, L.keys.p, L.npos.p, L.tailbin.p,
+                         c->tailbin_slot_bytes));
+    }
+    T.end();
+  }
+  if (part == 2 || part < 0) {
+    if (c->debug & 1) {
+      if (!L.dbg.p) {
+        L.dbg.alloc((size_t)c->dbg_slot_floats * c->nslots);
+        L.dbg_offd.alloc(LM_NDET);
+        COPY_SYNC(L.dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice, st);
+      }
+      HIPCHK(launch_corr_dbg(c->unfused, dim3(64, nproc, LM_NDET), st, dK, L.ext.p, c->ext_slot_bytes, c->weights.p,
+                             s_proc0, L.dbg.p, L.dbg_offd.p, c->dbg_slot_floats));
+    }
+    long long *kp0 = nullptr, *kp1 = nullptr, *kp2 = nullptr, *kp3 = nullptr;
+    if (c->kprof_on) {
+      if (!L.kprof.p) L.kprof.alloc((size_t)4 * 16 * 2 * c->nslots);
+      HIPCHK(hipMemsetAsync(L.kprof.p, 0, sizeof(long long) * 4 * 16 * 2 * c->nslots, st));
+      kp0 = L.kprof.p;
+      kp1 = L.kprof.p + 16 * 2 * c->nslots;
+      kp2 = L.kprof.p + 2 * 16 * 2 * c->nslots;
+      kp3 = L.kprof.p + 3 * 16 * 2 * c->nslots;
+    }
+    T.begin("k_tail");
+    k_tail<<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes, L.tailmask.p,
+                                                        L.tscratch.p, A.hdr.p, kp2);
+    T.end();
+    T.begin("k_nms_bottom");
+    // each list goes to one of the two instantiations (LDS / global scratch)
+    k_nms<false><<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, L.keys.p, L.npos.p, L.tailmask.p,
+                                                           L.gscratch.p, c->gscratch_slot, A.hdr.p, L.err.p, kp0, 0);
+    k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
+                                              c->gscratch_slot, A.hdr.p, L.err.p, nullptr, 2 * nproc);
+    T.end();
+    T.begin("k_nms_side");
+    k_nms<false><<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(dK, 1, 1, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
+                                                       c->gscratch_slot, A.hdr.p, L.err.p, kp1, 0);
+    k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, 1, 1, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
+                                              c->gscratch_slot, A.hdr.p, L.err.p, nullptr, 2 * n);
+    T.end();
+    T.begin("k_post");
+    k_post<false><<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, L.slots.p, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p,
+                                                         A.hdr.p, L.keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p,
+                                                         A.jc.p, A.ir.p, A.pr.p, A.ctl.p, L.err.p, L.gscratch.p,
+                                                         c->gscratch_slot, kp3, 0);
+    k_post<true><<<16, LM_POST_THREADS, 0, st>>>(dK, L.slots.p, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, A.hdr.p,
+                                                L.keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
+                                                A.pr.p, A.ctl.p, L.err.p, L.gscratch.p, c->gscratch_slot, nullptr,
+                                                2 * n);
+    T.end();
+    T.begin("k_pack");
+    k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, L.err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
+    k_pack_copy<<<dim3(n, 2), 256, 0, st>>>(dK, A.hdr.p, n, L.keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p,
+                                            A.jc.p, A.ir.p, A.pr.p, A.ph.p, A.pack.p, A.side_base.p);
+    T.end();
+    // header + results to host memory, then frame n as the next batch's halo
+    k_out<<<128, 256, 0, st>>>(A.ph.p, L.h_ph.d, A.pack.p, L.h_pack.d, (int64_t)L.h_pack.n, nullptr, L.frame_ptr.p,
+                               n, L.halo.p, c->npix);
+  }
+}
+
+// Launch attempt `attempt` of the lane's pending batch (attempt 0 from the
+// captured graphs; reruns after a result-arena overflow directly).
+void launch_attempt(lm_ctx* c, Lane& L, int attempt) {
+  static const bool graphs_env = [] {
+    const char* v = getenv("LM_GRAPH");
+    return !v || atoi(v) != 0;
+  }();
+  const Lane::Pending& P = L.pend;
+  hipStream_t st = L.stream;
+  Arena& A = L.arena[P.cur];
+  LmArenaCtl& hc = *L.h_ctl.p;
+  std::memset(&hc, 0, sizeof(hc));
+  for (int k = 0; k < AR_COUNT; ++k) hc.cap[k] = A.cap[k];
+  hc.nparts = std::min(LM_SUBARENA, 2 * P.n);  // k_post has 2n blocks: every part gets used
+  Timer T(c, L);
+  const bool graph = graphs_env && L.use_graphs && attempt == 0 && !(c->debug & 1) && !c->kprof_on;
+  if (graph) {
+    // Three graphs per key (before / k_corr / after), so the timing events
+    // of k_corr (the roofline kernel) are recorded on the stream between
+    // graph launches; the other kernels are not timed on this path.
+    const std::array<int, 7> key{P.n, P.cur, P.carry ? 1 : 0, P.carry ? P.last_n : 0, P.s_lut0, P.s_proc0, P.plan};
+    auto it = L.graphs.find(key);
+    if (it == L.graphs.end()) {
+      Lane::GraphEntry ent{};
+      bool ok = true;
+      const bool t_on = T.on;
+      T.on = false;
+      for (int part = 0; part < 3 && ok; ++part) {
+        hipGraph_t g = nullptr;
+        ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
+        if (!ok) break;
+        try {
+          enqueue_chain(c, L, A, P, T, P.carry, part);
+        } catch (const std::exception&) {
+          ok = false;
+        }
+        const hipError_t e = hipStreamEndCapture(st, &g);
+        ok = ok && e == hipSuccess && g;
+        if (ok) ok = hipGraphInstantiate(&ent.exec[part], g, nullptr, nullptr, 0) == hipSuccess;
+        if (g) (void)hipGraphDestroy(g);
+      }
+      T.on = t_on;
+      (void)hipGetLastError();
+      if (ok) {
+        it = L.graphs.emplace(key, ent).first;
+      } else {  // capture unsupported here: run the chain directly from now on
+        for (hipGraphExec_t x : ent.exec)
+          if (x) (void)hipGraphExecDestroy(x);
+        L.use_graphs = false;
+      }
+    }
+    if (it != L.graphs.end()) {
+      HIPCHK(hipGraphLaunch(it->second.exec[0], st));
+      T.begin("k_corr");
+      HIPCHK(hipGraphLaunch(it->second.exec[1], st));
+      T.end();
+      HIPCHK(hipGraphLaunch(it->second.exec[2], st));
+    } else {
+      enqueue_chain(c, L, A, P, T, P.carry, -1);
+    }
+  } else {
+    enqueue_chain(c, L, A, P, T, P.carry && attempt == 0, -1);
+  }
+  HIPCHK(hipGetLastError());
+}
+
+// Submit frames [first, first + n) to the next lane (round-robin).  The lane
+// is idle (its previous batch was collected).  Host frames are copied to the
+// lane's staging slots before this returns; device frames are read in place
+// while the batch runs.  Batch k + 1 continues batch k:
+//  - on the same lane (one lane): slot 0 carries batch k's last frame and
+//    candidates (k_carry; k_out left the frame in the lane's halo);
+//  - on another lane: batch k copied its last frame to handoff[k & 1] at its
+//    start (event ev_snap); batch k + 1 copies it into its own halo (event
+//    ev_consumed) and runs it as a 1-frame halo (its candidates recomputed),
+//    so the two batches' kernels never wait for each other.
+void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev,
+                  const int32_t* bb, bool device_frames) {
   if (n <= 0 || n > c->max_batch) throw std::invalid_argument("n must be in [1, max_batch].");
   if (first < 0) throw std::invalid_argument("first_frame must be >= 0.");
   if (!frames) throw std::invalid_argument("frames is NULL.");
   if (pitch < c->npix) throw std::invalid_argument("frame_pitch smaller than one frame.");
+  if (c->inflight.size() >= c->lanes.size())
+    throw std::invalid_argument("every pipeline lane holds a batch: lm_detect_collect the oldest one first.");
   HIPCHK(hipSetDevice(c->device));
-  const bool halo = prev != nullptr && first > 0;
-  const bool carry = !halo && first > 0;
-  if (carry && !(c->have_state && c->last_frame == first - 1))
+  Lane& L = *c->lanes[c->next_lane];
+  const bool pipelined = c->lanes.size() > 1;
+  const bool given_halo = prev != nullptr && first > 0;
+  const bool cont = !given_halo && first > 0;
+  if (cont && !(c->have_state && c->last_frame == first - 1))
     throw std::invalid_argument("frame first_frame-1 was not processed by this context: pass prev_frame (shard start).");
-  const LmConst& K = c->K;
-  const LmConst* dK = c->dK.p;
+  const bool carry = cont && c->last_lane == L.index && L.have_state && L.last_frame == first - 1;
+  const bool handoff = cont && !carry;
+  if (handoff && !pipelined)
+    throw std::invalid_argument("the previous batch failed: pass prev_frame to continue from frame first_frame.");
+  const bool halo = given_halo || handoff;
   const lm_geometry& g = c->geo;
-  const int64_t fstride = (c->npix + 255) / 256 * 256;
-  hipStream_t st = c->stream;
-  Timer T(c);
+  const LmConst& K = c->K;
+  const int64_t fstride = c->fstride;
+  hipStream_t st = L.stream;
 
   // Device frames are read in place when 16-byte aligned (the kernels load
   // 16 B per lane); otherwise they are first copied into the staging slots.
@@ -866,21 +1096,21 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
   const int s_lut0 = first > 0 ? 0 : 1, s_proc0 = halo ? 0 : 1;
   int new_last_bb[3] = {c->bb_x, c->bb_yb, c->bb_ys};
   for (int s = 0; s <= n; ++s) {
-    LmSlot& S = c->h_slots.p[s];
+    LmSlot& S = L.h_slots.p[s];
     std::memset(&S, 0, sizeof(S));
     const int gframe = first - 1 + s;
     S.frame = gframe;
     S.active = s >= s_lut0;
-    if (s == 0) c->h_frame_ptr.p[0] = c->halo.p;
-    else c->h_frame_ptr.p[s] = direct ? frames + (int64_t)(s - 1) * pitch : c->frames.p + (int64_t)s * fstride;
+    if (s == 0) L.h_frame_ptr.p[0] = L.halo.p;
+    else L.h_frame_ptr.p[s] = direct ? frames + (int64_t)(s - 1) * pitch : L.frames.p + (int64_t)s * fstride;
     if (s < s_lut0) continue;
-    const int bi = halo ? s : s - 1;  // index into bb[]
+    const int bi = given_halo ? s : s - 1;  // index into bb[]
     int bx = c->bb_x, byb = c->bb_yb, bys = c->bb_ys;
-    if (bb && (s > 0 || halo)) {
+    if (bb && (s > 0 || given_halo)) {
       bx = bb[3 * bi];
       byb = bb[3 * bi + 1];
       bys = bb[3 * bi + 2];
-    } else if (s == 0 && carry) {  // the previous batch's last frame
+    } else if (s == 0 && cont) {  // the previous batch's last frame
       bx = c->last_bb[0];
       byb = c->last_bb[1];
       bys = c->last_bb[2];
@@ -909,198 +1139,96 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
                                     "I_PAD's zero padding (not supported).");
     }
   }
-  (void)K;
 
   // ---- inputs.  Host frames (and a host halo frame) are the only runtime
-  // copies; the stream is drained after them, so everything the kernels read
-  // has landed (see k_prep / k_out for why the stream otherwise holds only
-  // kernels).
+  // copies from the caller's memory; the stream is drained after them, so
+  // the caller may reuse its buffer once this returns (see k_prep / k_out for
+  // why the stream otherwise holds only kernels).
   if (!device_frames) {
     // one 2-D transfer for the batch (DMA from page-locked buffers, e.g. lm_host_alloc)
-    HIPCHK(hipMemcpy2DAsync(c->frames.p + fstride, (size_t)fstride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
+    HIPCHK(hipMemcpy2DAsync(L.frames.p + fstride, (size_t)fstride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
                             hipMemcpyHostToDevice, st));
-    if (halo) HIPCHK(hipMemcpyAsync(c->halo.p, prev, c->npix, hipMemcpyHostToDevice, st));
+    if (given_halo) HIPCHK(hipMemcpyAsync(L.halo.p, prev, c->npix, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
   } else {
     if (!direct)
-      HIPCHK(hipMemcpy2DAsync(c->frames.p + fstride, (size_t)fstride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
+      HIPCHK(hipMemcpy2DAsync(L.frames.p + fstride, (size_t)fstride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
                               hipMemcpyDeviceToDevice, st));
-    if (halo && ((uintptr_t)prev & 15) == 0)
-      k_out<<<64, 256, 0, st>>>(c->zero_ph.p, c->h_ph.d, nullptr, nullptr, 0, prev, nullptr, 0, c->halo.p, c->npix);
-    else if (halo)
-      HIPCHK(hipMemcpyAsync(c->halo.p, prev, (size_t)c->npix, hipMemcpyDeviceToDevice, st));
+    if (given_halo && ((uintptr_t)prev & 15) == 0)
+      k_out<<<64, 256, 0, st>>>(L.zero_ph.p, L.h_ph.d, nullptr, nullptr, 0, prev, nullptr, 0, L.halo.p, c->npix);
+    else if (given_halo)
+      HIPCHK(hipMemcpyAsync(L.halo.p, prev, (size_t)c->npix, hipMemcpyDeviceToDevice, st));
   }
+  // ---- pipelined halo hand-off (every batch of a multi-lane context)
+  if (pipelined) {
+    const uint8_t* last = direct ? frames + (int64_t)(n - 1) * pitch : L.frames.p + (int64_t)n * fstride;
+    // handoff[k & 1] was last read by batch k - 1 (it took batch k - 2's frame from there)
+    if (c->last_lane >= 0) HIPCHK(hipStreamWaitEvent(st, c->lanes[c->last_lane]->ev_consumed, 0));
+    HIPCHK(hipMemcpyAsync(c->handoff.p + (c->nsub & 1) * fstride, last, (size_t)c->npix, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipEventRecord(L.ev_snap, st));
+    if (handoff) {
+      HIPCHK(hipStreamWaitEvent(st, c->lanes[c->last_lane]->ev_snap, 0));
+      HIPCHK(hipMemcpyAsync(L.halo.p, c->handoff.p + ((c->nsub - 1) & 1) * fstride, (size_t)c->npix,
+                            hipMemcpyDeviceToDevice, st));
+    }
+    HIPCHK(hipEventRecord(L.ev_consumed, st));
+  }
+  if (!L.gscratch.p) L.gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
 
-  const int cur = c->parity, prv = c->last_parity;
-  if (!c->gscratch.p) c->gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
-  static const bool graphs_env = [] {
-    const char* v = getenv("LM_GRAPH");
-    return !v || atoi(v) != 0;
-  }();
-  // The kernel chain of one batch attempt.  Kernel arguments depend only on
-  // the key of c->graphs (frame pointers and slots reach the kernels through
-  // k_prep's copies of mapped host arrays), so the chain is captured once per
-  // key into a hipGraph and replayed.
-  const int plan = corr_plan_for(c);
-  auto chain = [&](Arena& A, bool do_carry, int part) {  // part: 0 pre, 1 k_corr, 2 post, -1 all
-    const int nproc = n + 1 - s_proc0;
-    if (part <= 0) {
-      k_prep<<<1, 256, 0, st>>>(c->h_slots.d, c->h_frame_ptr.d, c->h_ctl.d, n + 1, c->slots.p, c->frame_ptr.p, A.ctl.p,
-                                c->npos.p, c->err.p);
-      if (do_carry) {  // a rerun keeps slot 0's staged candidates
-        T.begin("k_carry");
-        k_carry<<<1, 256, 0, st>>>(dK, c->keys.p, c->arena[prv].hdr.p, c->last_n, A.hdr.p);
-        T.end();
-      }
-      T.begin("k_minmax");
-      k_minmax<<<dim3(LM_MM_SPLIT, n + 1 - s_lut0), LM_MM_THREADS, 0, st>>>(c->frame_ptr.p, c->bkg.p, c->npix, s_lut0,
-                                                                          c->mm.p);
-      k_lut<<<(n + 1 - s_lut0 + 3) / 4, 256, 0, st>>>(c->mm.p, s_lut0, n + 1, c->adj.p, c->setup.method != 0, c->luts.p);
-      T.end();
-      const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
-      T.begin("k_ingest");
-      const unsigned ext_blocks = (unsigned)((etot / LM_INGEST_VEC + 255) / 256);
-      const unsigned zero_blocks = (unsigned)((K.tail_bm_words + 4 * 256 - 1) / (4 * 256));  // the tail bitmaps
-      k_ingest<<<dim3(ext_blocks + zero_blocks, (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)), 256, 0, st>>>(
-          dK, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, c->slots.p, s_proc0, n + 1, c->ext.p, c->ext_slot_bytes,
-          ext_blocks, reinterpret_cast<unsigned*>(c->tailbin.p));
-      T.end();
-    }
-    if (part == 1 || part < 0) {
-      T.begin("k_corr");
-      const lm_ctx::CorrPlan& P = c->corr_plan[plan];
-      for (size_t gi = 0; gi < P.groups.size(); ++gi) {
-        const auto& grp = P.groups[gi];
-        const LmDetGroup& G = grp.second;
-        const void* w = c->setup.corr_precision == LM_CORR_F16 ? (const void*)c->weights16.p : (const void*)c->weights.p;
-        HIPCHK(launch_corr(grp.first, P.ring[gi], dim3(G.tile_end[G.n - 1], nproc), P.threads[gi], P.lds[gi], st, dK, G, c->ext.p, c->ext_slot_bytes, w, s_proc0, c->keys.p,
-                           c->npos.p, c->tailbin.p, c->tailbin_slot_bytes));
-      }
-      T.end();
-    }
-    if (part == 2 || part < 0) {
-      if (c->debug & 1) {
-        if (!c->dbg.p) {
-          c->dbg.alloc((size_t)c->dbg_slot_floats * c->nslots);
-          c->dbg_offd.alloc(LM_NDET);
-          COPY_SYNC(c->dbg_offd.p, c->dbg_off, sizeof(c->dbg_off), hipMemcpyHostToDevice, c->stream);
-        }
-        HIPCHK(launch_corr_dbg(c->unfused, dim3(64, nproc, LM_NDET), st, dK, c->ext.p, c->ext_slot_bytes, c->weights.p,
-                               s_proc0, c->dbg.p, c->dbg_offd.p, c->dbg_slot_floats));
-      }
-      long long *kp0 = nullptr, *kp1 = nullptr, *kp2 = nullptr;
-      if (c->kprof_on) {
-        if (!c->kprof.p) c->kprof.alloc((size_t)4 * 16 * 2 * c->nslots);
-        HIPCHK(hipMemsetAsync(c->kprof.p, 0, sizeof(long long) * 4 * 16 * 2 * c->nslots, st));
-        long long* pp = c->kprof.p + 3 * 16 * 2 * c->nslots;
-        HIPCHK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_post_prof), &pp, sizeof(pp), 0, hipMemcpyHostToDevice, st));
-        kp0 = c->kprof.p;
-        kp1 = c->kprof.p + 16 * 2 * c->nslots;
-        kp2 = c->kprof.p + 2 * 16 * 2 * c->nslots;
-      }
-      T.begin("k_tail");
-      k_tail<<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, c->tailbin.p, c->tailbin_slot_bytes, c->tailmask.p,
-                                                          c->tscratch.p, A.hdr.p, kp2);
-      T.end();
-      T.begin("k_nms_bottom");
-      // each list goes to one of the two instantiations (LDS / global scratch)
-      k_nms<false><<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p,
-                                                             c->gscratch.p, c->gscratch_slot, A.hdr.p, c->err.p, kp0, 0);
-      k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                c->gscratch_slot, A.hdr.p, c->err.p, nullptr, 2 * nproc);
-      T.end();
-      T.begin("k_nms_side");
-      k_nms<false><<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                         c->gscratch_slot, A.hdr.p, c->err.p, kp1, 0);
-      k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, 1, 1, c->keys.p, c->npos.p, c->tailmask.p, c->gscratch.p,
-                                                c->gscratch_slot, A.hdr.p, c->err.p, nullptr, 2 * n);
-      T.end();
-      T.begin("k_post");
-      k_post<false><<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
-                                                     c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
-                                                     A.pr.p, A.ctl.p, c->err.p, c->gscratch.p, c->gscratch_slot, 0);
-      k_post<true><<<16, LM_POST_THREADS, 0, st>>>(dK, c->slots.p, c->frame_ptr.p, c->bkg.p, c->cal.p, c->luts.p, A.hdr.p,
-                                                     c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
-                                                     A.pr.p, A.ctl.p, c->err.p, c->gscratch.p, c->gscratch_slot, 2 * n);
-      T.end();
-      T.begin("k_pack");
-      k_pack_scan<<<1, 1024, 0, st>>>(A.hdr.p, n, A.ctl.p, c->err.p, A.ph.p, A.pack.p, A.pack_cap, A.side_base.p);
-      k_pack_copy<<<dim3(n, 2), 256, 0, st>>>(dK, A.hdr.p, n, c->keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p,
-                                              A.ir.p, A.pr.p, A.ph.p, A.pack.p, A.side_base.p);
-      T.end();
-      // header + results to host memory, then frame n as the next batch's halo
-      k_out<<<128, 256, 0, st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, nullptr,
-                                 c->frame_ptr.p, n, c->halo.p, c->npix);
-    }
-  };
+  Lane::Pending& P = L.pend;
+  P.on = true;
+  P.n = n;
+  P.first = first;
+  P.s_lut0 = s_lut0;
+  P.s_proc0 = s_proc0;
+  P.plan = corr_plan_for(c);
+  P.cur = L.parity;
+  P.prv = L.last_parity;
+  P.carry = carry;
+  P.last_n = carry ? L.last_n : 0;
+  launch_attempt(c, L, 0);
+
+  // the video position and the lane's carry state advance now; a batch that
+  // fails at collection clears the lane's state (a later batch on another
+  // lane only needs this batch's pixels)
+  c->have_state = true;
+  c->last_frame = first + n - 1;
+  for (int k = 0; k < 3; ++k) c->last_bb[k] = new_last_bb[k];
+  c->last_lane = L.index;
+  ++c->nsub;
+  c->inflight.push_back(L.index);
+  c->next_lane = (L.index + 1) % (int)c->lanes.size();
+  L.have_state = true;
+  L.last_frame = first + n - 1;
+  L.last_n = n;
+  L.last_parity = P.cur;
+  L.parity = 1 - P.cur;
+}
+
+// Wait for the lane's batch, rerun it while its result arena overflows, and
+// point `out` at its packed results (valid until the lane is reused).
+void finish_batch(lm_ctx* c, Lane& L, lm_batch_result* out) {
+  Lane::Pending& P = L.pend;
+  hipStream_t st = L.stream;
+  const int n = P.n, first = P.first;
+  HIPCHK(hipSetDevice(c->device));
   for (int attempt = 0;; ++attempt) {
-    Arena& A = c->arena[cur];
-    LmArenaCtl& hc = *c->h_ctl.p;
-    std::memset(&hc, 0, sizeof(hc));
-    for (int k = 0; k < AR_COUNT; ++k) hc.cap[k] = A.cap[k];
-    const bool graph = graphs_env && c->use_graphs && attempt == 0 && !(c->debug & 1) && !c->kprof_on;
-    if (graph) {
-      // Three graphs per key (before / k_corr / after), so the timing events
-      // of k_corr (the roofline kernel) are recorded on the stream between
-      // graph launches; the other kernels are not timed on this path.
-      const std::array<int, 7> key{n, cur, carry ? 1 : 0, carry ? c->last_n : 0, s_lut0, s_proc0, plan};
-      auto it = c->graphs.find(key);
-      if (it == c->graphs.end()) {
-        lm_ctx::GraphEntry ent{};
-        bool ok = true;
-        const bool t_on = T.on;
-        T.on = false;
-        for (int part = 0; part < 3 && ok; ++part) {
-          hipGraph_t g = nullptr;
-          ok = hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal) == hipSuccess;
-          if (!ok) break;
-          try {
-            chain(A, carry, part);
-          } catch (const std::exception&) {
-            ok = false;
-          }
-          const hipError_t e = hipStreamEndCapture(st, &g);
-          ok = ok && e == hipSuccess && g;
-          if (ok) ok = hipGraphInstantiate(&ent.exec[part], g, nullptr, nullptr, 0) == hipSuccess;
-          if (g) (void)hipGraphDestroy(g);
-        }
-        T.on = t_on;
-        (void)hipGetLastError();
-        if (ok) {
-          it = c->graphs.emplace(key, ent).first;
-        } else {  // capture unsupported here: run the chain directly from now on
-          for (hipGraphExec_t x : ent.exec)
-            if (x) (void)hipGraphExecDestroy(x);
-          c->use_graphs = false;
-        }
-      }
-      if (it != c->graphs.end()) {
-        HIPCHK(hipGraphLaunch(it->second.exec[0], st));
-        T.begin("k_corr");
-        HIPCHK(hipGraphLaunch(it->second.exec[1], st));
-        T.end();
-        HIPCHK(hipGraphLaunch(it->second.exec[2], st));
-      } else {
-        chain(A, carry, -1);
-      }
-    } else {
-      chain(A, carry && attempt == 0, -1);
-    }
-    HIPCHK(hipGetLastError());
+    if (attempt > 0) launch_attempt(c, L, attempt);
     HIPCHK(hipStreamSynchronize(st));
-    const LmPackHdr& ph = *c->h_ph.p;
+    Arena& A = L.arena[P.cur];
+    const LmPackHdr& ph = *L.h_ph.p;
     const int e = (c->debug & 4) ? (ph.err & ~4) : ph.err;  // debug bit 2: report but keep going
     if ((c->debug & 4) && (ph.err & 4)) {
-      COPY_SYNC(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
-      const int32_t* d = c->h_err.p;
+      COPY_SYNC(L.h_err.p, L.err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost, st);
+      const int32_t* d = L.h_err.p;
       fprintf(stderr, "[lm debug] vel box error frame %d tag %x box (%d,%d,%d,%d)\n", first - 1 + (d[2] >> 16), d[2],
               d[3], d[4], d[5], d[6]);
     }
     if (e & 4) {
-      COPY_SYNC(c->h_err.p, c->err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
-      const int32_t* d = c->h_err.p;
+      COPY_SYNC(L.h_err.p, L.err.p, 16 * sizeof(int32_t), hipMemcpyDeviceToHost, st);
+      const int32_t* d = L.h_err.p;
       const int tag = d[2], slot = tag >> 16;
-      if (const char* dir = getenv("LM_DUMP_DIR")) dump_slot(c, dir, first - 1 + slot, slot, (tag >> 12) & 1);
+      if (const char* dir = getenv("LM_DUMP_DIR")) dump_slot(c, L, dir, first - 1 + slot, slot, (tag >> 12) & 1);
       char buf[256];
       snprintf(buf, sizeof buf, " [frame %d, %s %s candidate %d: box (%d,%d,%d,%d) in crop %dx%d]",
                first - 1 + slot, (tag >> 12 & 1) ? "snout" : "paw", (tag & 0x800) ? "side" : "bottom", tag & 0x7FF,
@@ -1114,7 +1242,7 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
     if (e) throw std::runtime_error("device error flags " + std::to_string(e));
     if (!ph.overflow) break;
     if (attempt >= 3) throw std::runtime_error("result arena overflow persists.");
-    c->drop_graphs();  // arena / pack buffers are reallocated below
+    L.drop_graphs();  // arena / pack buffers are reallocated below
     if (ph.overflow & 2) {
       int ncap[AR_COUNT];
       for (int k = 0; k < AR_COUNT; ++k) ncap[k] = std::max(A.cap[k], (int)(ph.used[k] * 1.25) + 1024);
@@ -1122,18 +1250,19 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
     }
     A.alloc_pack(ph.bytes + ph.bytes / 4);
   }
-  T.collect();
-  if (c->kprof_on) kprof_report(c, n);
+  if (c->debug & 2) Timer::collect(c, L);
+  else L.t_ev.clear();
+  if (c->kprof_on) kprof_report(c, L, n);
 
   // ---- the packed results (lm_batch_result layout) are in h_pack unless
   // they outgrew it: then grow it and let k_out copy them (and the halo) again
-  Arena& A = c->arena[cur];
-  const LmPackHdr ph = *c->h_ph.p;
-  if ((int64_t)c->h_pack.n < ph.bytes) {
-    c->drop_graphs();
-    c->h_pack.alloc((size_t)(ph.bytes + ph.bytes / 4));
-    k_out<<<128, 256, 0, st>>>(A.ph.p, c->h_ph.d, A.pack.p, c->h_pack.d, (int64_t)c->h_pack.n, nullptr,
-                               c->frame_ptr.p, n, c->halo.p, c->npix);
+  Arena& A = L.arena[P.cur];
+  const LmPackHdr ph = *L.h_ph.p;
+  if ((int64_t)L.h_pack.n < ph.bytes) {
+    L.drop_graphs();
+    L.h_pack.alloc((size_t)(ph.bytes + ph.bytes / 4));
+    k_out<<<128, 256, 0, st>>>(A.ph.p, L.h_ph.d, A.pack.p, L.h_pack.d, (int64_t)L.h_pack.n, nullptr, L.frame_ptr.p, n,
+                               L.halo.p, c->npix);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
   }
@@ -1146,42 +1275,61 @@ void run_batch_impl(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int 
     std::vector<uint8_t> chk((size_t)ph.bytes);
     HIPCHK(hipMemcpy(chk.data(), A.pack.p, (size_t)ph.bytes, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < ph.bytes; ++i)
-      if (chk[i] != c->h_pack.p[i]) {
+      if (chk[i] != L.h_pack.p[i]) {
         int64_t j = ph.bytes - 1;
-        while (j > i && chk[j] == c->h_pack.p[j]) --j;
+        while (j > i && chk[j] == L.h_pack.p[j]) --j;
         fprintf(stderr, "[lm debug] D2H pack mismatch frames %d..%d: bytes [%ld, %ld] of %ld differ\n", first,
                 first + n - 1, (long)i, (long)j, (long)ph.bytes);
         break;
       }
   }
-  const LmPackLayout L = lm_pack_layout(n, ph.tot);
-  const uint8_t* hp = c->h_pack.p;
-  c->have_state = true;
-  for (int k = 0; k < 3; ++k) c->last_bb[k] = new_last_bb[k];
-  c->last_frame = first + n - 1;
-  c->last_n = n;
-  c->last_parity = cur;
-  c->parity = 1 - cur;
-  c->batch_n = n;
-  c->batch_s0 = s_proc0;
+  const LmPackLayout PL = lm_pack_layout(n, ph.tot);
+  const uint8_t* hp = L.h_pack.p;
+  L.batch_n = n;
+  L.batch_s0 = P.s_proc0;
+  P.on = false;
 
   out->n_frames = n;
   out->first_frame = first;
-  out->cand_offset = reinterpret_cast<const int64_t*>(hp + L.cand_off);
-  out->cand = reinterpret_cast<const lm_candidate*>(hp + L.cand);
-  out->p22d_offset = reinterpret_cast<const int64_t*>(hp + L.p22d_off);
-  out->p22d = reinterpret_cast<const lm_p22d*>(hp + L.p22d);
-  out->side_y = reinterpret_cast<const int32_t*>(hp + L.side_y);
-  out->side_s = reinterpret_cast<const double*>(hp + L.side_s);
-  out->unary_offset = reinterpret_cast<const int64_t*>(hp + L.unary_off);
-  out->unary = reinterpret_cast<const double*>(hp + L.unary);
-  out->pw_dims = reinterpret_cast<const int32_t*>(hp + L.pw_dims);
-  out->pw_jc_offset = reinterpret_cast<const int64_t*>(hp + L.jc_off);
-  out->pw_jc = reinterpret_cast<const int32_t*>(hp + L.jc);
-  out->pw_nz_offset = reinterpret_cast<const int64_t*>(hp + L.nz_off);
-  out->pw_ir = reinterpret_cast<const int32_t*>(hp + L.ir);
-  out->pw_pr = reinterpret_cast<const double*>(hp + L.pr);
-  out->tail = reinterpret_cast<const int32_t*>(hp + L.tail);
+  out->cand_offset = reinterpret_cast<const int64_t*>(hp + PL.cand_off);
+  out->cand = reinterpret_cast<const lm_candidate*>(hp + PL.cand);
+  out->p22d_offset = reinterpret_cast<const int64_t*>(hp + PL.p22d_off);
+  out->p22d = reinterpret_cast<const lm_p22d*>(hp + PL.p22d);
+  out->side_y = reinterpret_cast<const int32_t*>(hp + PL.side_y);
+  out->side_s = reinterpret_cast<const double*>(hp + PL.side_s);
+  out->unary_offset = reinterpret_cast<const int64_t*>(hp + PL.unary_off);
+  out->unary = reinterpret_cast<const double*>(hp + PL.unary);
+  out->pw_dims = reinterpret_cast<const int32_t*>(hp + PL.pw_dims);
+  out->pw_jc_offset = reinterpret_cast<const int64_t*>(hp + PL.jc_off);
+  out->pw_jc = reinterpret_cast<const int32_t*>(hp + PL.jc);
+  out->pw_nz_offset = reinterpret_cast<const int64_t*>(hp + PL.nz_off);
+  out->pw_ir = reinterpret_cast<const int32_t*>(hp + PL.ir);
+  out->pw_pr = reinterpret_cast<const double*>(hp + PL.pr);
+  out->tail = reinterpret_cast<const int32_t*>(hp + PL.tail);
+}
+
+// The oldest submitted batch's results.
+void collect_batch(lm_ctx* c, lm_batch_result* out) {
+  if (c->inflight.empty()) throw std::invalid_argument("no batch in flight: lm_detect_submit one first.");
+  Lane& L = *c->lanes[c->inflight.front()];
+  c->inflight.pop_front();
+  c->collected_lane = L.index;
+  try {
+    finish_batch(c, L, out);
+  } catch (...) {
+    L.pend.on = false;
+    L.have_state = false;
+    throw;
+  }
+}
+
+// One synchronous batch (submit + collect); nothing may be in flight.
+void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev, const int32_t* bb,
+               bool device_frames, lm_batch_result* out) {
+  if (!c->inflight.empty())
+    throw std::invalid_argument("batches are in flight: lm_detect_collect them before lm_detect_batch.");
+  submit_batch(c, frames, pitch, n, first, prev, bb, device_frames);
+  collect_batch(c, out);
 }
 
 }  // namespace
@@ -1197,6 +1345,8 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
   if (!out) return fail(LM_ERR_INVALID_ARGUMENT, "out is NULL");
   *out = nullptr;
   if (max_batch <= 0) return fail(LM_ERR_INVALID_ARGUMENT, "max_batch must be > 0");
+  if (setup && (setup->pipeline_lanes < 0 || setup->pipeline_lanes > LM_MAX_LANES))
+    return fail(LM_ERR_INVALID_ARGUMENT, "pipeline_lanes must be in [0, " + std::to_string(LM_MAX_LANES) + "].");
   lm_ctx* c = new lm_ctx();
   lm_status s = guarded([&] {
     int ndev = 0;
@@ -1204,38 +1354,45 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
     if (device < 0 || device >= ndev) throw HipError("invalid HIP device index");
     c->device = device;
     HIPCHK(hipSetDevice(device));
-    // Contexts of a process alternate between the highest and the lowest
-    // stream priority.  With equal priorities, concurrent contexts share the
-    // CUs during their correlation launches, finish them together and then
-    // all run their short post-correlation kernels at once (a convoy: ~19 %
-    // of the time no correlation ran, profiles/r02/rw/).  Unequal priorities
-    // let one context's correlation go first, which keeps the contexts out of
-    // phase: +4-5 % frames/s at 4 contexts per GPU.  LM_STREAM_PRIO=0: one
-    // priority for all.
-    const char* pv = getenv("LM_STREAM_PRIO");
-    if (!pv || atoi(pv) != 0) {
-      static std::atomic<int> n_created{0};
-      int lo = 0, hi = 0;
-      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, (n_created++ & 1) ? lo : hi));
-    } else {
-      HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    }
     c->max_batch = max_batch;
     c->nslots = max_batch + 1;
     validate_and_build(c, setup, params, model);
+    const int nl = setup->pipeline_lanes > 0 ? setup->pipeline_lanes : 1;
+    // Lanes (of all contexts of the process) alternate between the highest
+    // and the lowest stream priority.  With equal priorities, concurrent
+    // streams share the CUs during their correlation launches, finish them
+    // together and then all run their short post-correlation kernels at once
+    // (a convoy: ~19 % of the time no correlation ran, profiles/r02/rw/).
+    // Unequal priorities let one stream's correlation go first, which keeps
+    // the streams out of phase: +4-5 % frames/s at 4 streams per GPU.
+    // LM_STREAM_PRIO=0: one priority for all.
+    const char* pv = getenv("LM_STREAM_PRIO");
+    const bool prio = !pv || atoi(pv) != 0;
+    static std::atomic<int> n_created{0};
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    for (int i = 0; i < nl; ++i) {
+      c->lanes.emplace_back(new Lane());
+      Lane& L = *c->lanes.back();
+      L.index = i;
+      L.device = device;
+      if (prio) HIPCHK(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, (n_created++ & 1) ? lo : hi));
+      else HIPCHK(hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking));
+      lane_alloc(c, L);
+    }
+    if (nl > 1) c->handoff.alloc((size_t)2 * c->fstride);
   });
   if (s != LM_OK) {
     delete c;
     return s;
   }
-  g_live_ctx[c->device & 63].fetch_add(1);
+  g_live_streams[c->device & 63].fetch_add((int)c->lanes.size());
   *out = c;
   return LM_OK;
 }
 
 LM_API void lm_ctx_destroy(lm_ctx* ctx) {
-  if (ctx) g_live_ctx[ctx->device & 63].fetch_sub(1);
+  if (ctx) g_live_streams[ctx->device & 63].fetch_sub((int)ctx->lanes.size());
   delete ctx;
 }
 
@@ -1245,7 +1402,11 @@ LM_API lm_status lm_get_geometry(const lm_ctx* ctx, lm_geometry* out) {
   return LM_OK;
 }
 
-LM_API void* lm_ctx_stream(lm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+LM_API void* lm_ctx_stream(lm_ctx* ctx) { return ctx && !ctx->lanes.empty() ? (void*)ctx->lanes[0]->stream : nullptr; }
+
+LM_API int32_t lm_ctx_lanes(const lm_ctx* ctx) { return ctx ? (int32_t)ctx->lanes.size() : 0; }
+
+LM_API int32_t lm_ctx_pending(const lm_ctx* ctx) { return ctx ? (int32_t)ctx->inflight.size() : 0; }
 
 LM_API lm_status lm_detect_batch(lm_ctx* ctx, const uint8_t* frames, int64_t frame_pitch, int32_t n, int32_t first_frame,
                                  const uint8_t* prev_frame, const int32_t* bb, lm_batch_result* out) {
@@ -1260,6 +1421,23 @@ LM_API lm_status lm_detect_batch_device(lm_ctx* ctx, const uint8_t* d_frames, in
   return guarded([&] { run_batch(ctx, d_frames, frame_pitch, n, first_frame, d_prev_frame, bb, true, out); });
 }
 
+LM_API lm_status lm_detect_submit(lm_ctx* ctx, const uint8_t* frames, int64_t frame_pitch, int32_t n, int32_t first_frame,
+                                  const uint8_t* prev_frame, const int32_t* bb) {
+  if (!ctx) return fail(LM_ERR_INVALID_ARGUMENT, "null ctx");
+  return guarded([&] { submit_batch(ctx, frames, frame_pitch, n, first_frame, prev_frame, bb, false); });
+}
+
+LM_API lm_status lm_detect_submit_device(lm_ctx* ctx, const uint8_t* d_frames, int64_t frame_pitch, int32_t n,
+                                         int32_t first_frame, const uint8_t* d_prev_frame, const int32_t* bb) {
+  if (!ctx) return fail(LM_ERR_INVALID_ARGUMENT, "null ctx");
+  return guarded([&] { submit_batch(ctx, d_frames, frame_pitch, n, first_frame, d_prev_frame, bb, true); });
+}
+
+LM_API lm_status lm_detect_collect(lm_ctx* ctx, lm_batch_result* out) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  return guarded([&] { collect_batch(ctx, out); });
+}
+
 LM_API lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags) {
   if (!ctx) return fail(LM_ERR_INVALID_ARGUMENT, "null ctx");
   return guarded([&] {
@@ -1269,7 +1447,7 @@ LM_API lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags) {
         HIPCHK(hipSetDevice(ctx->device));
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
-        HIPCHK(hipEventRecord(e, ctx->stream));
+        HIPCHK(hipEventRecord(e, ctx->lanes[0]->stream));
         HIPCHK(hipEventSynchronize(e));
         g_epoch[ctx->device] = e;
       }
@@ -1280,37 +1458,40 @@ LM_API lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags) {
 
 LM_API int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, double* t1, int32_t cap) {
   if (!ctx) return 0;
-  const int32_t n = (int32_t)ctx->t_names.size();
+  const Lane& L = *ctx->lanes[ctx->collected_lane];
+  const int32_t n = (int32_t)L.t_names.size();
   for (int32_t i = 0; i < n && i < cap; ++i) {
-    if (names) names[i] = ctx->t_names[i];
-    if (t0) t0[i] = ctx->t_t0[i];
-    if (t1) t1[i] = ctx->t_t1[i];
+    if (names) names[i] = L.t_names[i];
+    if (t0) t0[i] = L.t_t0[i];
+    if (t1) t1[i] = L.t_t1[i];
   }
   return n;
 }
 
 LM_API lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out, int32_t rows, int32_t cols) {
   if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
-  if (!(ctx->debug & 1) || !ctx->dbg.p) return fail(LM_ERR_INVALID_ARGUMENT, "debug scores not enabled");
-  if (f < 0 || f >= ctx->batch_n || det < 0 || det >= LM_NDET) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
+  const Lane& L = *ctx->lanes[ctx->collected_lane];
+  if (!(ctx->debug & 1) || !L.dbg.p) return fail(LM_ERR_INVALID_ARGUMENT, "debug scores not enabled");
+  if (f < 0 || f >= L.batch_n || det < 0 || det >= LM_NDET) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
   const LmDet& D = ctx->K.det[det];
   if (rows != D.oh || cols != D.ow) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
   return guarded([&] {
     HIPCHK(hipSetDevice(ctx->device));
-    COPY_SYNC(out, ctx->dbg.p + (int64_t)(f + 1) * ctx->dbg_slot_floats + ctx->dbg_off[det], sizeof(float) * rows * cols,
-              hipMemcpyDeviceToHost, ctx->stream);
+    COPY_SYNC(out, L.dbg.p + (int64_t)(f + 1) * ctx->dbg_slot_floats + ctx->dbg_off[det], sizeof(float) * rows * cols,
+              hipMemcpyDeviceToHost, L.stream);
   });
 }
 
 LM_API lm_status lm_debug_tail_mask(lm_ctx* ctx, int32_t f, uint8_t* out, int32_t rows, int32_t cols) {
   if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
-  if (f < 0 || f >= ctx->batch_n) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
+  const Lane& L = *ctx->lanes[ctx->collected_lane];
+  if (f < 0 || f >= L.batch_n) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
   if (rows != ctx->K.tail_hb || cols != ctx->K.tail_w) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
   return guarded([&] {
     HIPCHK(hipSetDevice(ctx->device));
     const int nb = (cols + 63) / 64;
     std::vector<unsigned long long> bits((size_t)rows * nb);
-    COPY_SYNC(bits.data(), ctx->tailmask.p + (int64_t)(f + 1) * rows * nb, bits.size() * 8, hipMemcpyDeviceToHost, ctx->stream);
+    COPY_SYNC(bits.data(), L.tailmask.p + (int64_t)(f + 1) * rows * nb, bits.size() * 8, hipMemcpyDeviceToHost, L.stream);
     for (int r = 0; r < rows; ++r)
       for (int x = 0; x < cols; ++x) out[(size_t)r * cols + x] = ((bits[(size_t)r * nb + (x >> 6)] >> (x & 63)) & 1) ? 255 : 0;
   });
@@ -1318,10 +1499,11 @@ LM_API lm_status lm_debug_tail_mask(lm_ctx* ctx, int32_t f, uint8_t* out, int32_
 
 LM_API int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32_t cap) {
   if (!ctx) return 0;
-  const int32_t n = (int32_t)ctx->t_names.size();
+  const Lane& L = *ctx->lanes[ctx->collected_lane];
+  const int32_t n = (int32_t)L.t_names.size();
   for (int32_t i = 0; i < n && i < cap; ++i) {
-    if (names) names[i] = ctx->t_names[i];
-    if (ms) ms[i] = ctx->t_ms[i];
+    if (names) names[i] = L.t_names[i];
+    if (ms) ms[i] = L.t_ms[i];
   }
   return n;
 }

@@ -322,6 +322,7 @@ int run(int argc, char** argv) {
   li.output_file = in.OUTPUT_PATH + "/output_" + in.FILE_STEM + ".yml";
   if (const char* d = std::getenv("LM_DEVICE")) li.device = std::atoi(d);
   if (const char* b = std::getenv("LM_BATCH")) li.batch = std::max(1, std::atoi(b));
+  if (const char* l = std::getenv("LM_LANES")) li.lanes = std::max(1, std::atoi(l));
   if (std::getenv("LM_PRINT_INPUTS")) {  // diagnostics: the parsed inputs, nothing run on the GPU
     const lm_params& P = li.params;
     std::cout << "method " << method << "\nflip " << li.setup.flip << "\nvideo " << li.setup.video_rows << " "

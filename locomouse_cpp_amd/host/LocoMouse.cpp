@@ -146,8 +146,7 @@ LocoMouse::LocoMouse(const LocoMouse_Inputs& inputs) : IN(inputs), METHOD(0), N_
 }
 
 LocoMouse::~LocoMouse() {
-  if (INFLIGHT.valid()) INFLIGHT.wait();  // its errors die with the object
-  if (CTX) lm_ctx_destroy(CTX);
+  if (CTX) lm_ctx_destroy(CTX);  // waits for the batches in flight; their errors die with the object
 }
 
 // :543-569: with use_provided_bounding_box the bottom-right corners are the
@@ -230,9 +229,9 @@ void LocoMouse::initializeFeatureLoop() {
     DEBUG_TEXT << "===== Preparing Feature Tracking Loop: " << std::endl
                << "BB_SIDE_MOUSE: " << debug_rect(BB_SIDE_MOUSE) << std::endl
                << "BB_BOTTOM_MOUSE: " << debug_rect(BB_BOTTOM_MOUSE) << std::endl;
+  IN.setup.pipeline_lanes = std::max(1, std::min(IN.lanes, LM_MAX_LANES));
   throw_on_error(lm_ctx_create(IN.device, &IN.setup, &IN.params, &IN.model, IN.batch, &CTX));
   PENDING.allocate(FRAME_BYTES * (size_t)IN.batch);
-  SUBMITTED.allocate(FRAME_BYTES * (size_t)IN.batch);
   N_PENDING = 0;
   if (DEBUG_TEXT.is_open()) {  // :700-704, :766
     const lm_geometry g = geometry();
@@ -294,13 +293,19 @@ void LocoMouse::HostBuffer::allocate(size_t bytes) {
 
 void LocoMouse::sync() {
   if (N_PENDING) flush();
-  wait_inflight();
+  while (!INFLIGHT.empty()) collect_oldest();
 }
 
-// Rethrows (once) what the background batch threw: the reference's exception
-// surfaces at the next per-frame call that hands over a batch, or at sync().
-void LocoMouse::wait_inflight() {
-  if (INFLIGHT.valid()) INFLIGHT.get();
+// The oldest batch in flight: its results are appended in frame order.  Its
+// errors (the reference's exceptions) surface here: at the per-frame call
+// that hands over a batch while every lane is busy, or at sync().
+void LocoMouse::collect_oldest() {
+  const std::pair<int, int> b = INFLIGHT.front();
+  INFLIGHT.pop_front();
+  lm_batch_result r{};
+  throw_on_error(lm_detect_collect(CTX, &r));
+  append(r);
+  if (DEBUG_TEXT.is_open()) debug_frames(b.first, b.second);
 }
 
 lm_geometry LocoMouse::geometry() const {
@@ -310,12 +315,11 @@ lm_geometry LocoMouse::geometry() const {
   return g;
 }
 
-// A full batch goes to the device on a helper thread (std::async) while the
-// caller reads the next frames into the other buffer; the context is used by
-// one batch at a time (the previous one is waited for first) and results are
-// appended in frame order before that wait returns.
+// A full batch goes to the device (lm_detect_submit copies the frames and
+// returns); up to IN.lanes batches run on the device at once while the
+// caller reads the next frames.  When every lane is busy the oldest batch is
+// collected first, so results are appended in frame order.
 void LocoMouse::flush() {
-  wait_inflight();
   const int n = N_PENDING, first = CURRENT_FRAME + 1 - n;
   std::vector<int32_t> bb((size_t)3 * n);
   for (int i = 0; i < n; ++i) {
@@ -323,22 +327,18 @@ void LocoMouse::flush() {
     bb[3 * i + 1] = (int32_t)BB_Y_BOTTOM_POS[first + i];
     bb[3 * i + 2] = (int32_t)BB_Y_SIDE_POS[first + i];
   }
-  PENDING.swap(SUBMITTED);
+  while ((int)INFLIGHT.size() >= lm_ctx_lanes(CTX)) collect_oldest();
+  throw_on_error(lm_detect_submit(CTX, PENDING.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data()));
+  INFLIGHT.push_back({first, n});
   // Frames already read ahead past this batch (read_frames fills up to a whole
   // batch; a caller that reads results mid-batch flushes early) move to the
-  // front of the new pending buffer, so the reader's position and the frame
+  // front of the pending buffer, so the reader's position and the frame
   // numbering stay in step.
   const int ahead = std::max(0, N_READ_AHEAD - n);
   if (ahead)
-    std::memcpy(PENDING.data(), SUBMITTED.data() + (size_t)n * FRAME_BYTES, (size_t)ahead * FRAME_BYTES);
+    std::memmove(PENDING.data(), PENDING.data() + (size_t)n * FRAME_BYTES, (size_t)ahead * FRAME_BYTES);
   N_PENDING = 0;
   N_READ_AHEAD = ahead;
-  INFLIGHT = std::async(std::launch::async, [this, n, first, bb = std::move(bb)] {
-    lm_batch_result r{};
-    throw_on_error(lm_detect_batch(CTX, SUBMITTED.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data(), &r));
-    append(r);
-    if (DEBUG_TEXT.is_open()) debug_frames(first, n);
-  });
 }
 
 // After the loop (main.cpp:86-91): the tracker over the containers above.

@@ -29,6 +29,7 @@
 #include <array>
 #include <cstdint>
 #include <fstream>
+#include <deque>
 #include <functional>
 #include <future>
 #include <memory>
@@ -64,7 +65,8 @@ struct LocoMouse_Inputs {
   // early (a result accessor called mid-batch).
   std::function<int(uint8_t* dst, int n)> read_frames;
   int device = 0;      // HIP device of this instance (one per GPU / host thread)
-  int batch = 256;     // frames per lm_detect_batch / lm_bb_push call
+  int batch = 256;     // frames per lm_detect_submit / lm_bb_push call
+  int lanes = 4;       // batches in flight on the device (lm_setup.pipeline_lanes)
   // Whole-video BB pass (use_provided_bounding_box = 0): config.yml's
   // median_filter_size / min_pixel_visible / moving_average_window /
   // conn_comp_connectivity, and V.set(CV_CAP_PROP_POS_FRAMES, 0) (:761-762)
@@ -168,14 +170,13 @@ class LocoMouse : protected FrameResults {
   };
   std::ofstream DEBUG_TEXT;  // verbose_debug log (LocoMouse_class.hpp:180)
   void debug_frames(int first, int n);  // the per-frame stage lines of frames [first, first + n)
-  HostBuffer PENDING;    // raw frames read but not yet processed
-  HostBuffer SUBMITTED;  // the batch being processed by INFLIGHT
-  std::future<void> INFLIGHT;      // lm_detect_batch + append of the previous batch
+  HostBuffer PENDING;    // raw frames read but not yet submitted
+  std::deque<std::pair<int, int>> INFLIGHT;  // (first frame, n) of the submitted batches, oldest first
   int N_PENDING = 0;
   int N_READ_AHEAD = 0;  // frames of PENDING already filled by read_frames
   size_t FRAME_BYTES = 0;
   void flush();
-  void wait_inflight();
+  void collect_oldest();
 };
 
 // LocoMouse_TM (LocoMouse_TM.hpp:30-55): readFrame adds imadjust

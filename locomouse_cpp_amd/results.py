@@ -71,3 +71,18 @@ def slice_results(res, start):
     out["pw_dims"] = res["pw_dims"][start:]
     out["tail"] = res["tail"][start:]
     return out
+
+
+def same_results(a, b):
+    """True when two result dicts hold bit-identical arrays (every KEYS entry;
+    structured arrays field by field, floats compared as stored)."""
+    for k in KEYS:
+        x, y = a[k], b[k]
+        if x.shape != y.shape:
+            return False
+        if x.dtype.names:
+            if not all(np.array_equal(x[n], y[n]) for n in x.dtype.names):
+                return False
+        elif not np.array_equal(x, y):
+            return False
+    return True

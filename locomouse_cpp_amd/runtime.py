@@ -23,6 +23,7 @@ EXPORTED = (
     "lm_debug_kernel_times", "lm_debug_kernel_spans", "lm_synth_frames_device",
     "lm_bb_create", "lm_bb_destroy", "lm_bb_push", "lm_bb_push_device", "lm_bb_finish", "lm_bb_debug_binary",
     "lm_bb_stream", "lm_host_alloc", "lm_host_free",
+    "lm_detect_submit", "lm_detect_submit_device", "lm_detect_collect", "lm_ctx_lanes", "lm_ctx_pending",
 )
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -134,6 +135,12 @@ def lib():
         for fn in (L.lm_detect_batch, L.lm_detect_batch_device):
             fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p,
                            C.POINTER(lm_batch_result)]
+        for fn in (L.lm_detect_submit, L.lm_detect_submit_device):
+            fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.lm_detect_collect.argtypes = [C.c_void_p, C.POINTER(lm_batch_result)]
+        for fn in (L.lm_ctx_lanes, L.lm_ctx_pending):
+            fn.argtypes = [C.c_void_p]
+            fn.restype = C.c_int32
         L.lm_ctx_set_debug.argtypes = [C.c_void_p, C.c_int32]
         L.lm_debug_scores.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
         L.lm_debug_tail_mask.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_int32]
@@ -177,12 +184,46 @@ def synth_frames_device(d_ptr, rows, cols, first, n, pitch, device=0):
 class Context:
     """One lm_ctx on one HIP device (the per-frame loop's state)."""
 
-    def __init__(self, cfg, max_batch=64, device=0):
+    def __init__(self, cfg, max_batch=64, device=0, lanes=None):
+        """lanes: pipeline lanes (lm_setup.pipeline_lanes; None keeps cfg.setup's)."""
         self.cfg = cfg  # keeps the arrays behind the structs alive
         self._h = C.c_void_p()
-        _check(lib().lm_ctx_create(device, C.byref(cfg.setup), C.byref(cfg.params), C.byref(cfg.model), max_batch,
+        setup = cfg.setup
+        if lanes is not None:
+            setup = type(cfg.setup).from_buffer_copy(cfg.setup)
+            setup.pipeline_lanes = lanes
+        self._setup = setup
+        _check(lib().lm_ctx_create(device, C.byref(setup), C.byref(cfg.params), C.byref(cfg.model), max_batch,
                                    C.byref(self._h)))
         self.max_batch = max_batch
+
+    def lanes(self):
+        return lib().lm_ctx_lanes(self._h)
+
+    def pending(self):
+        return lib().lm_ctx_pending(self._h)
+
+    def submit(self, frames, first_frame, prev_frame=None, bb=None):
+        """Pipelined lm_detect_submit of host frames [n, rows, cols] u8."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        pp = None if prev_frame is None else np.ascontiguousarray(prev_frame, dtype=np.uint8)
+        bbp = None if bb is None else np.ascontiguousarray(bb, dtype=np.int32)
+        _check(lib().lm_detect_submit(self._h, frames.ctypes.data, frames.shape[1] * frames.shape[2], frames.shape[0],
+                                      first_frame, None if pp is None else pp.ctypes.data,
+                                      None if bbp is None else bbp.ctypes.data))
+
+    def submit_device(self, d_frames_ptr, pitch, n, first_frame, d_prev_ptr=None, bb=None):
+        """Pipelined lm_detect_submit_device (frames stay in device memory until collected)."""
+        bbp = None if bb is None else np.ascontiguousarray(bb, dtype=np.int32)
+        _check(lib().lm_detect_submit_device(self._h, C.c_void_p(d_frames_ptr), pitch, n, first_frame,
+                                             C.c_void_p(d_prev_ptr) if d_prev_ptr else None,
+                                             None if bbp is None else bbp.ctypes.data))
+
+    def collect(self, raw=False):
+        """Results of the oldest submitted batch (lm_detect_collect)."""
+        res = lm_batch_result()
+        _check(lib().lm_detect_collect(self._h, C.byref(res)))
+        return res if raw else result_to_numpy(res)
 
     def geometry(self):
         g = lm_geometry()

@@ -1,0 +1,96 @@
+"""Per-kernel resource usage of the gfx950 code objects inside a HIP shared
+library: VGPR / SGPR counts, spills and scratch (private segment) bytes, read
+from the code objects' AMDGPU metadata notes.
+
+    python scripts/kernel_resources.py [lib.so] [--filter SUBSTR]
+
+Used by tests/test_kernel_resources.py (no GPU needed)."""
+import os
+import re
+import struct
+import subprocess
+import sys
+import tempfile
+
+READELF = "/opt/rocm/llvm/bin/llvm-readelf"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _section(path, name):
+    """Bytes of ELF section `name` (64-bit little-endian ELF)."""
+    with open(path, "rb") as fh:
+        data = fh.read()
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    def sh(i):
+        return struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize)
+    stro = sh(shstrndx)[4]
+    for i in range(shnum):
+        s = sh(i)
+        nm = data[stro + s[0]:data.index(b"\0", stro + s[0])].decode()
+        if nm == name:
+            return data[s[4]:s[4] + s[5]]
+    raise KeyError(name)
+
+
+def code_objects(lib):
+    """The amdgcn code objects of every offload bundle in lib's .hip_fatbin."""
+    fb = _section(lib, ".hip_fatbin")
+    out = []
+    pos = fb.find(MAGIC)
+    while pos >= 0:
+        n, = struct.unpack_from("<Q", fb, pos + 24)
+        p = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", fb, p)
+            triple = fb[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "amdgcn" in triple and size:
+                out.append(fb[pos + off:pos + off + size])
+        pos = fb.find(MAGIC, pos + 32)
+    return out
+
+
+def kernels(lib):
+    """{kernel symbol: {field: value}} for every kernel of lib."""
+    res = {}
+    for co in code_objects(lib):
+        with tempfile.NamedTemporaryFile(suffix=".co", delete=False) as fh:
+            fh.write(co)
+            name = fh.name
+        try:
+            txt = subprocess.run([READELF, "--notes", name], capture_output=True, text=True, check=True).stdout
+        finally:
+            os.unlink(name)
+        cur = None
+        for line in txt.splitlines():
+            m = re.match(r"\s*-?\s*\.(\w+):\s+(.*)$", line)
+            if not m:
+                continue
+            key, val = m.group(1), m.group(2).strip()
+            if key == "name" and not val.endswith(".kd"):
+                cur = {}
+                res[val] = cur
+                continue
+            if cur is not None and key in ("vgpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count",
+                                           "private_segment_fixed_size", "group_segment_fixed_size", "agpr_count"):
+                cur[key] = int(val)
+    return res
+
+
+def main():
+    lib = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("--") else os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "locomouse_cpp_amd", "liblocomouse_hip.so")
+    flt = sys.argv[sys.argv.index("--filter") + 1] if "--filter" in sys.argv else ""
+    ks = kernels(lib)
+    print(f"{'kernel':70s} {'vgpr':>5s} {'sgpr':>5s} {'vspill':>6s} {'sspill':>6s} {'scratch':>7s}")
+    for k in sorted(ks):
+        if flt not in k:
+            continue
+        r = ks[k]
+        print(f"{k[:70]:70s} {r.get('vgpr_count', -1):5d} {r.get('sgpr_count', -1):5d} {r.get('vgpr_spill_count', -1):6d} "
+              f"{r.get('sgpr_spill_count', -1):6d} {r.get('private_segment_fixed_size', -1):7d}")
+
+
+if __name__ == "__main__":
+    main()

@@ -103,6 +103,16 @@ def odd_size_config():
     return S.SyntheticConfig(weights=w, biases=_bias_for_rate(base, ["snout_bottom", "paw_side"]))
 
 
+def wide_ring_config():
+    """Ring-kernel widths above 32 (k_corr_rw<36..64>): snout_bottom 40x40,
+    paw_side 20 rows x 64 columns, tail_side 16 x 36 and tail_bottom 16 x 48
+    (rows x columns); paw_bottom 24x24 and the default scene otherwise."""
+    w = {"snout_bottom": S.dog_detector(40, 40, 6.0, 31), "paw_side": S.dog_detector(20, 64, 5.0, 32),
+         "tail_side": S.line_detector(16, 36, 1.5, 33), "tail_bottom": S.line_detector(16, 48, 1.5, 34)}
+    base = S.SyntheticConfig(weights=w)
+    return S.SyntheticConfig(weights=w, biases=_bias_for_rate(base, ["snout_bottom", "paw_side"]))
+
+
 def gamma_table(g=0.6):
     return np.round(255.0 * (np.arange(256) / 255.0) ** g)
 

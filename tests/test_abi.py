@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     L = runtime.lib()
     for name in declared_functions():
         assert getattr(L, name) is not None
-    assert L.lm_abi_version() == 3
+    assert L.lm_abi_version() == 4
 
 
 def test_last_error_and_null_arguments_without_gpu():

@@ -105,6 +105,30 @@ def test_detector_sizes_beyond_specialised_kernels():
             assert np.array_equal(s.view(np.uint32), ref.scores(f, det, s.shape).view(np.uint32)), (f, det)
 
 
+@pytest.mark.parametrize("plan", [0, 1])
+@pytest.mark.parametrize("unfused", [False, True])
+def test_wide_ring_widths(plan, unfused):
+    """Ring widths 36-64 (40x40, 20x64, 16x36, 16x48 detectors) through the
+    per-width launches (plan 0) and the single merged launch (plan 1), fused
+    and unfused arithmetic: candidates and raw score maps bit-exact."""
+    cfg = E.wide_ring_config()
+    if unfused:
+        cfg.setup.filter_arith = abi.LM_FILTER_UNFUSED
+    frames = cfg.frames(10, 5)
+    ctx = _ctx(cfg, max_batch=5)
+    ctx.set_debug(1 | (abi.LM_DEBUG_PLAN_MERGED if plan else abi.LM_DEBUG_PLAN_PER_WIDTH))
+    got = ctx.detect(frames, 10, prev_frame=cfg.frames(9, 1)[0])
+    from oracle import oracle as O
+    ref = _oracle(cfg, cfg.frames(9, 6), flags=O.KEEP_DEBUG)
+    from locomouse_cpp_amd.results import slice_results
+    assert_same(got, slice_results(ref.result, 1), f"wide ring plan {plan} unfused {unfused}: ")
+    assert int(got["cand_offset"][-1]) > 0
+    for f in range(5):
+        for det in range(6):
+            s = ctx.debug_scores(f, det)
+            assert np.array_equal(s.view(np.uint32), ref.scores(f + 1, det, s.shape).view(np.uint32)), (f, det)
+
+
 def test_unfused_filter_arithmetic():
     """LM_FILTER_UNFUSED (OpenCV's SSE2/scalar filter2D: rounded product,
     rounded sum) against the oracle's unfused restatement, bit for bit; its

@@ -1,0 +1,110 @@
+"""GPU parity of the pipelined context (lm_setup.pipeline_lanes > 1,
+lm_detect_submit / lm_detect_collect): several batches of one video in flight
+on their own HIP streams, each continuing the previous one through the
+device-side halo hand-off, must give exactly the oracle's per-frame loop
+(main.cpp:54-82) on the whole video -- the same bar as one lane."""
+import pytest
+
+import edge_scenes as E
+from locomouse_cpp_amd import synthetic as S
+from locomouse_cpp_amd.results import concat_results, slice_results
+from test_gpu_parity import _oracle, _quantized_config, assert_same
+
+pytestmark = pytest.mark.gpu
+
+
+def _pctx(cfg, lanes, max_batch):
+    from locomouse_cpp_amd.runtime import Context
+    return Context(cfg, max_batch=max_batch, lanes=lanes)
+
+
+def _pipelined(ctx, frames, B, first=0):
+    """Submit every batch of `frames` (keeping all lanes busy), collect in order."""
+    parts, firsts = [], []
+    lanes = ctx.lanes()
+    for i in range(0, len(frames), B):
+        if ctx.pending() == lanes:
+            r = ctx.collect()
+            firsts.append(r["first_frame"])
+            parts.append(r)
+        ctx.submit(frames[i:i + B], first + i)
+    while ctx.pending():
+        r = ctx.collect()
+        firsts.append(r["first_frame"])
+        parts.append(r)
+    assert firsts == list(range(first, first + len(frames), B)), firsts
+    return concat_results(parts)
+
+
+@pytest.mark.parametrize("lanes,B", [(2, 5), (3, 4), (4, 6)])
+def test_pipelined_video_matches_oracle(lanes, B):
+    """23 frames (a ragged last batch) from frame 0 through 2-4 lanes."""
+    cfg = S.SyntheticConfig()
+    frames = cfg.frames(0, 23)
+    ctx = _pctx(cfg, lanes, B)
+    assert ctx.lanes() == lanes
+    got = _pipelined(ctx, frames, B)
+    assert_same(got, _oracle(cfg, frames).result, f"pipelined L{lanes} B{B}: ")
+
+
+def test_pipelined_shard_start_and_moving_crops():
+    """A shard starting at frame 40 with its previous frame as halo, per-frame
+    crop corners, device frames read in place."""
+    import torch
+    cfg = S.SyntheticConfig()
+    video = cfg.frames(39, 17)
+    bb = E.moving_corners(cfg, 17, first=39)
+    ref = slice_results(_oracle(cfg, video, bb=bb).result, 1)
+    d = torch.from_numpy(video).to("cuda:0")
+    fb = video.shape[1] * video.shape[2]
+    ctx = _pctx(cfg, 3, 4)
+    parts = []
+    for j, i in enumerate(range(1, 17, 4)):
+        if ctx.pending() == 3:
+            parts.append(ctx.collect())
+        n = min(4, 17 - i)
+        ctx.submit_device(d.data_ptr() + i * fb, fb, n, 39 + i, d_prev_ptr=d.data_ptr() if j == 0 else None,
+                          bb=bb[0:n + 1] if j == 0 else bb[i:i + n])
+    while ctx.pending():
+        parts.append(ctx.collect())
+    torch.cuda.synchronize()
+    assert_same(concat_results(parts), ref, "pipelined shard: ")
+
+
+def test_pipelined_tie_heavy_and_blank_frames():
+    """The exact-tie configuration (k_nms's std::sort replica) and the edge
+    video's blank / half-blank frames across the lanes' seams."""
+    c, dups = _quantized_config(1500)
+    assert dups > 20
+    frames = c.frames(200, 12)
+    ref = _oracle(c, frames).result
+    assert_same(_pipelined(_pctx(c, 4, 3), frames, 3), ref, "pipelined ties: ")
+    cfg = S.SyntheticConfig()
+    ev = E.edge_video(cfg)
+    assert_same(_pipelined(_pctx(cfg, 2, 5), ev, 5), _oracle(cfg, ev).result, "pipelined edges: ")
+
+
+def test_pipelined_errors_and_synchronous_mix():
+    from locomouse_cpp_amd.runtime import LMError
+    cfg = S.SyntheticConfig()
+    frames = cfg.frames(0, 12)
+    ctx = _pctx(cfg, 2, 4)
+    ctx.submit(frames[0:4], 0)
+    with pytest.raises(LMError) as e:  # lm_detect_batch while a batch is in flight
+        ctx.detect(frames[4:8], 4)
+    assert e.value.code == 1
+    ctx.submit(frames[4:8], 4)
+    with pytest.raises(LMError) as e:  # every lane busy
+        ctx.submit(frames[8:12], 8)
+    assert e.value.code == 1
+    r0 = ctx.collect()
+    with pytest.raises(LMError) as e:  # a gap in the frame sequence
+        ctx.submit(frames[9:12], 9)
+    assert e.value.code == 1
+    r1 = ctx.collect()
+    assert (r0["first_frame"], r1["first_frame"]) == (0, 4)
+    # a synchronous batch continuing the pipelined ones (hand-off halo)
+    r2 = ctx.detect(frames[8:12], 8)
+    assert_same(concat_results([r0, r1, r2]), _oracle(cfg, frames).result, "mixed: ")
+    with pytest.raises(LMError):
+        ctx.collect()  # nothing in flight
