@@ -484,20 +484,27 @@ DEV void tail_side_moments(const CCRuns<IX> S, int R, const int* rowoff, int H, 
   }
 }
 
+// BIG: tail boxes whose bitmaps and tables do not fit the CU's LDS (the
+// reference has no size limit, LocoMouse_class.cpp:2604-2626): the same code
+// on a per-slot global workspace (`ws`, tail_layout(..., cap 0) bytes per
+// slot), every run table in global scratch.
+template <bool BIG>
 __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restrict__ Kp, int s0,
                                                           const uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
                                                           unsigned long long* __restrict__ tailmask,
                                                           unsigned* __restrict__ scratch, LmSlotOut* __restrict__ hdr,
-                                                          long long* __restrict__ prof) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smt[];
+                                                          long long* __restrict__ prof, uint8_t* __restrict__ ws,
+                                                          int64_t ws_slot) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smt_lds[];
 #define TAIL_PROF(k) \
   if (prof && threadIdx.x == 0) prof[blockIdx.x * 16 + (k)] = clock64();
   TAIL_PROF(0)
   if (prof && threadIdx.x == 0) prof[blockIdx.x * 16 + 14] = wall_clock64();
   const LmConst& K = *Kp;
   const int slot = s0 + blockIdx.x;
+  uint8_t* smt = BIG ? ws + (int64_t)slot * ws_slot : smt_lds;
   const int TW = K.tail_w, HB = K.tail_hb, HS = K.tail_hs, nb64 = (TW + 63) / 64;
-  const int cap = K.tail_cap, ntc = K.tail_ntc, ntrb = (HB + 31) / 32, ntrs = (HS + 31) / 32;
+  const int cap = BIG ? 0 : K.tail_cap, ntc = K.tail_ntc, ntrb = (HB + 31) / 32, ntrs = (HS + 31) / 32;
   const TailLayout L = tail_layout(TW, HB, HS, cap, ntc);
   int* rowoff = reinterpret_cast<int*>(smt + L.rowoff);
   int* colc = reinterpret_cast<int*>(smt + L.colc);

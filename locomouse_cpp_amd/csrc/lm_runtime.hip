@@ -91,6 +91,7 @@ struct Lane {
   DevBuf<int32_t> npos, err;
   DevBuf<unsigned> mm;        // k_minmax partial (min, max) pairs per slot
   DevBuf<unsigned> tscratch;  // k_tail run tables beyond its LDS
+  DevBuf<uint8_t> tail_ws;    // k_tail<true>: per-slot workspace (tail boxes beyond the LDS)
   DevBuf<float> dbg;
   DevBuf<int64_t> dbg_offd;
   DevBuf<const uint8_t*> frame_ptr;
@@ -184,6 +185,8 @@ struct lm_ctx {
   DevBuf<_Float16> weights16;  // LM_CORR_F16 rows (LmDet::w16_off)
   DevBuf<LmConst> dK;  // the per-context constants, passed to every kernel by pointer
   size_t tail_lds = 0;
+  bool tail_big = false;        // k_tail<true>: tail tables in global memory
+  int64_t tail_ws_slot = 0;     // its workspace bytes per slot
   bool kprof_on = false;
   // pipeline
   std::vector<std::unique_ptr<Lane>> lanes;
@@ -426,9 +429,14 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   K.tail_cap = 4096;
   while (K.tail_cap > 64 && tail_layout(tw, ub.height, us.height, K.tail_cap, K.tail_ntc).bytes > 64 * 1024) K.tail_cap -= 64;
   c->tail_lds = (size_t)tail_layout(tw, ub.height, us.height, K.tail_cap, K.tail_ntc).bytes;
-  if (c->tail_lds > 160 * 1024)
-    throw std::invalid_argument("tail box " + std::to_string(tw) + "x" + std::to_string(std::max(ub.height, us.height)) +
-                                " exceeds k_tail's LDS (bitmaps of the tail box).");
+  // a tail box whose bitmaps do not fit the LDS runs k_tail<true> on a
+  // global per-slot workspace instead
+  c->tail_big = c->tail_lds > 160 * 1024;
+  if (c->tail_big) {
+    K.tail_cap = 0;
+    c->tail_lds = 0;
+    c->tail_ws_slot = ((int64_t)tail_layout(tw, ub.height, us.height, 0, K.tail_ntc).bytes + 255) / 256 * 256;
+  }
   int64_t off = 0;
   for (int l = 0; l < LM_NLIST; ++l) {
     const int d = l == 0 ? DET_PAW_B : l == 1 ? DET_SNOUT_B : l == 2 ? DET_PAW_S : DET_SNOUT_S;
@@ -475,7 +483,6 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     const double row[7] = {q.x, q.y, q.max_distance, q.min_x, q.max_x, q.min_y, q.max_y};
     for (int j = 0; j < 7; ++j) K.prior[k][j] = row[j];
   }
-  if (g.ong_nx * g.ong_ny + 1 + 512 > LM_POST_MAXOFF) throw std::invalid_argument("occlusion grid too large.");
   K.gray_lut_on = P->transform_gray_values && !P->use_reference_image_brightness ? 1 : 0;
   for (int i = 0; i < 256; ++i) K.gray_lut[i] = K.gray_lut_on ? (uint8_t)P->gray_value_transformation[i] : (uint8_t)i;
 
@@ -618,7 +625,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->dK.alloc(1);
   COPY_SYNC(c->dK.p, &c->K, sizeof(LmConst), hipMemcpyHostToDevice, cs);
   c->fstride = (nv + 255) / 256 * 256;
-  HIPCHK(hipFuncSetAttribute((const void*)k_tail, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->tail_lds));
+  HIPCHK(hipFuncSetAttribute((const void*)k_tail<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->tail_lds));
   for (const auto& P : c->corr_plan)
     for (size_t g = 0; g < P.groups.size(); ++g)
       HIPCHK(hipFuncSetAttribute(P.groups[g].first, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds[g]));
@@ -644,6 +651,7 @@ void lane_alloc(lm_ctx* c, Lane& L) {
   SET_SYNC(L.tailbin.p, 0, (size_t)c->tailbin_slot_bytes * ns, st);
   L.tailmask.alloc((size_t)K.tail_hb * ((K.tail_w + 63) / 64) * ns);
   L.tscratch.alloc((size_t)5 * std::max(K.tail_hb, K.tail_hs) * ((K.tail_w + 1) / 2) * ns);
+  if (c->tail_big) L.tail_ws.alloc((size_t)c->tail_ws_slot * ns);
   L.keys.alloc((size_t)K.keys_per_slot * ns);
   L.npos.alloc((size_t)LM_NLIST * ns);
   L.err.alloc(16);
@@ -662,7 +670,7 @@ void lane_alloc(lm_ctx* c, Lane& L) {
   cap[AR_SIDE] = ns * LM_NFEAT * 256;
   cap[AR_UNARY] = ns * LM_NFEAT * 64 * 4;
   cap[AR_PWJC] = ns * LM_NFEAT * (64 + g.ong_nx * g.ong_ny + 1);
-  cap[AR_PWNZ] = ns * LM_NFEAT * 1024;
+  cap[AR_PWNZ] = ns * LM_NFEAT * (1024 + g.ong_nx * g.ong_ny);  // an ONG column holds at least its diagonal
   for (int a = 0; a < 2; ++a) L.arena[a].alloc(cap, ns);
   L.h_pack.alloc((size_t)L.arena[0].pack_cap);
   HIPCHK(hipEventCreateWithFlags(&L.ev_snap, hipEventDisableTiming));
@@ -951,8 +959,12 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
       kp3 = L.kprof.p + 3 * 16 * 2 * c->nslots;
     }
     T.begin("k_tail");
-    k_tail<<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes, L.tailmask.p,
-                                                        L.tscratch.p, A.hdr.p, kp2);
+    if (c->tail_big)
+      k_tail<true><<<nproc, LM_TAIL_THREADS, 0, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes, L.tailmask.p,
+                                                      L.tscratch.p, A.hdr.p, kp2, L.tail_ws.p, c->tail_ws_slot);
+    else
+      k_tail<false><<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes,
+                                                                 L.tailmask.p, L.tscratch.p, A.hdr.p, kp2, nullptr, 0);
     T.end();
     T.begin("k_nms_bottom");
     // each list goes to one of the two instantiations (LDS / global scratch)

@@ -113,6 +113,25 @@ def wide_ring_config():
     return S.SyntheticConfig(weights=w, biases=_bias_for_rate(base, ["snout_bottom", "paw_side"]))
 
 
+def big_tail_config():
+    """2048x1024 frames with a 2000-wide, 700-row bottom box and
+    tail_sub_bounding_box = 1: k_tail's bitmaps of the tail box exceed the
+    LDS (k_tail<true> on its global workspace), and the 75 x 35 = 2,625-node
+    occlusion grid exceeds k_post's LDS columns (global-scratch k_post for
+    every block).  9x9 detectors keep the oracle fast."""
+    w = {n: S.dog_detector(9, 9, 2.0, 40 + i) for i, n in enumerate(S.DETECTOR_SPECS) if "tail" not in n}
+    w["tail_bottom"] = S.line_detector(9, 9, 1.5, 50)
+    w["tail_side"] = S.line_detector(9, 9, 1.5, 51)
+    boxes = {"side": (20, 5, 2000, 180), "bottom": (20, 310, 2000, 700)}
+    base = S.SyntheticConfig(rows=1024, cols=2048, weights=w, bounding_boxes=boxes)
+    b = _bias_for_rate(base, ["paw_bottom", "snout_bottom", "paw_side", "snout_side"])
+    b.update({k: v for k, v in _bias_for_rate(base, ["tail_bottom", "tail_side"], rate=0.05).items()
+              if k.startswith("tail")})
+    cfg = S.SyntheticConfig(rows=1024, cols=2048, weights=w, bounding_boxes=boxes, biases=b)
+    cfg.params.tail_sub_bounding_box = 1.0
+    return cfg
+
+
 def gamma_table(g=0.6):
     return np.round(255.0 * (np.arange(256) / 255.0) ** g)
 

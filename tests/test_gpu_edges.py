@@ -129,6 +129,35 @@ def test_wide_ring_widths(plan, unfused):
             assert np.array_equal(s.view(np.uint32), ref.scores(f + 1, det, s.shape).view(np.uint32)), (f, det)
 
 
+@pytest.mark.parametrize("c5", [False, True])
+def test_dense_occlusion_grid(c5):
+    """occlusion_grid_spacing_pixels_bottom = 5: 60 x 28 = 1,680 ONG nodes on
+    the C3 box (k_post's LDS columns while the previous frame has few
+    candidates), 120 x 56 = 6,720 on the C5 box (global-scratch k_post for
+    every block); pairwise CSC bit-exact (pairwisePotential :1954-2070, grid
+    :726-749)."""
+    cfg = S.SyntheticConfig(rows=512, cols=1920) if c5 else S.SyntheticConfig()
+    cfg.params.occlusion_grid_spacing_pixels_bottom = 5
+    frames = cfg.frames(20, 4 if c5 else 7)
+    ctx = _ctx(cfg, max_batch=3)
+    g = ctx.geometry()
+    assert g.ong_nx * g.ong_ny == (6720 if c5 else 1680)
+    ctx.close()
+    ref = _oracle(cfg, frames).result
+    assert int(ref["pw_jc_offset"][-1]) > 1680 * 2
+    assert_same(_batched(cfg, frames, 3), ref, f"ONG spacing 5 c5={c5}: ")
+
+
+def test_tail_box_beyond_lds():
+    """A 2000 x 700 tail box (k_tail on its global workspace) with a
+    2,625-node occlusion grid, against the oracle."""
+    cfg = E.big_tail_config()
+    frames = cfg.frames(0, 4)
+    ref = _oracle(cfg, frames).result
+    assert (ref["tail"][:, 0] >= 0).any()
+    assert_same(_batched(cfg, frames, 2), ref, "big tail box: ")
+
+
 def test_unfused_filter_arithmetic():
     """LM_FILTER_UNFUSED (OpenCV's SSE2/scalar filter2D: rounded product,
     rounded sum) against the oracle's unfused restatement, bit for bit; its
