@@ -181,7 +181,11 @@ constexpr int32_t F0298 = 2446, F0390 = 3196, F0541 = 4433, F0765 = 6270, F0899 
                   F1501 = 12299, F1847 = 15137, F1961 = 16069, F2053 = 16819, F2562 = 20995, F3072 = 25172;
 constexpr int kConstBits = 13, kPass1 = 2;
 
-inline int32_t descale(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+// JLONG arithmetic (64-bit on LP64, as jidctint.c): with 16-bit quantisation
+// tables (SOF1) the products exceed 32 bits.  The column pass's workspace is
+// int, as libjpeg's.
+inline int64_t descale(int64_t x, int n) { return (x + ((int64_t)1 << (n - 1))) >> n; }
+inline int64_t left_shift(int64_t a, int b) { return (int64_t)((uint64_t)a << b); }  // LEFT_SHIFT (jdct.h)
 
 void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, int pitch) {
   int32_t ws[64];
@@ -190,26 +194,26 @@ void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, int pitch)
     const uint16_t* qq = q + c;
     int32_t* w = ws + c;
     if (!(in[8] | in[16] | in[24] | in[32] | in[40] | in[48] | in[56])) {
-      const int32_t dc = ((int32_t)in[0] * qq[0]) * (1 << kPass1);
+      const int32_t dc = (int32_t)left_shift((int32_t)in[0] * (int32_t)qq[0], kPass1);  // int dcval (wraps like libjpeg)
       for (int r = 0; r < 8; ++r) w[8 * r] = dc;
       continue;
     }
-    int32_t z2 = (int32_t)in[16] * qq[16], z3 = (int32_t)in[48] * qq[48];
-    int32_t z1 = (z2 + z3) * F0541;
-    int32_t tmp2 = z1 + z3 * -F1847, tmp3 = z1 + z2 * F0765;
-    z2 = (int32_t)in[0] * qq[0];
-    z3 = (int32_t)in[32] * qq[32];
-    int32_t tmp0 = (z2 + z3) * (1 << kConstBits), tmp1 = (z2 - z3) * (1 << kConstBits);
-    const int32_t t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
-    tmp0 = (int32_t)in[56] * qq[56];
-    tmp1 = (int32_t)in[40] * qq[40];
-    tmp2 = (int32_t)in[24] * qq[24];
-    tmp3 = (int32_t)in[8] * qq[8];
+    int64_t z2 = (int32_t)in[16] * (int32_t)qq[16], z3 = (int32_t)in[48] * (int32_t)qq[48];
+    int64_t z1 = (z2 + z3) * F0541;
+    int64_t tmp2 = z1 + z3 * -F1847, tmp3 = z1 + z2 * F0765;
+    z2 = (int32_t)in[0] * (int32_t)qq[0];
+    z3 = (int32_t)in[32] * (int32_t)qq[32];
+    int64_t tmp0 = left_shift(z2 + z3, kConstBits), tmp1 = left_shift(z2 - z3, kConstBits);
+    const int64_t t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
+    tmp0 = (int32_t)in[56] * (int32_t)qq[56];
+    tmp1 = (int32_t)in[40] * (int32_t)qq[40];
+    tmp2 = (int32_t)in[24] * (int32_t)qq[24];
+    tmp3 = (int32_t)in[8] * (int32_t)qq[8];
     z1 = tmp0 + tmp3;
     z2 = tmp1 + tmp2;
     z3 = tmp0 + tmp2;
-    int32_t z4 = tmp1 + tmp3;
-    const int32_t z5 = (z3 + z4) * F1175;
+    int64_t z4 = tmp1 + tmp3;
+    const int64_t z5 = (z3 + z4) * F1175;
     tmp0 *= F0298;
     tmp1 *= F2053;
     tmp2 *= F3072;
@@ -223,29 +227,29 @@ void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, int pitch)
     tmp2 += z2 + z3;
     tmp3 += z1 + z4;
     constexpr int s = kConstBits - kPass1;
-    w[0] = descale(t10 + tmp3, s);
-    w[56] = descale(t10 - tmp3, s);
-    w[8] = descale(t11 + tmp2, s);
-    w[48] = descale(t11 - tmp2, s);
-    w[16] = descale(t12 + tmp1, s);
-    w[40] = descale(t12 - tmp1, s);
-    w[24] = descale(t13 + tmp0, s);
-    w[32] = descale(t13 - tmp0, s);
+    w[0] = (int32_t)descale(t10 + tmp3, s);
+    w[56] = (int32_t)descale(t10 - tmp3, s);
+    w[8] = (int32_t)descale(t11 + tmp2, s);
+    w[48] = (int32_t)descale(t11 - tmp2, s);
+    w[16] = (int32_t)descale(t12 + tmp1, s);
+    w[40] = (int32_t)descale(t12 - tmp1, s);
+    w[24] = (int32_t)descale(t13 + tmp0, s);
+    w[32] = (int32_t)descale(t13 - tmp0, s);
   }
   constexpr int s2 = kConstBits + kPass1 + 3;
   for (int r = 0; r < 8; ++r) {
     const int32_t* w = ws + 8 * r;
     uint8_t* o = out + (size_t)r * pitch;
     if (!(w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7])) {
-      const uint8_t v = kRange.t[descale(w[0], kPass1 + 3) & 1023];
+      const uint8_t v = kRange.t[(int)descale(w[0], kPass1 + 3) & 1023];
       std::memset(o, v, 8);
       continue;
     }
-    int32_t z2 = w[2], z3 = w[6];
-    int32_t z1 = (z2 + z3) * F0541;
-    int32_t tmp2 = z1 + z3 * -F1847, tmp3 = z1 + z2 * F0765;
-    int32_t tmp0 = (w[0] + w[4]) * (1 << kConstBits), tmp1 = (w[0] - w[4]) * (1 << kConstBits);
-    const int32_t t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
+    int64_t z2 = w[2], z3 = w[6];
+    int64_t z1 = (z2 + z3) * F0541;
+    int64_t tmp2 = z1 + z3 * -F1847, tmp3 = z1 + z2 * F0765;
+    int64_t tmp0 = left_shift((int64_t)w[0] + w[4], kConstBits), tmp1 = left_shift((int64_t)w[0] - w[4], kConstBits);
+    const int64_t t10 = tmp0 + tmp3, t13 = tmp0 - tmp3, t11 = tmp1 + tmp2, t12 = tmp1 - tmp2;
     tmp0 = w[7];
     tmp1 = w[5];
     tmp2 = w[3];
@@ -253,8 +257,8 @@ void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, int pitch)
     z1 = tmp0 + tmp3;
     z2 = tmp1 + tmp2;
     z3 = tmp0 + tmp2;
-    int32_t z4 = tmp1 + tmp3;
-    const int32_t z5 = (z3 + z4) * F1175;
+    int64_t z4 = tmp1 + tmp3;
+    const int64_t z5 = (z3 + z4) * F1175;
     tmp0 *= F0298;
     tmp1 *= F2053;
     tmp2 *= F3072;
@@ -267,14 +271,14 @@ void idct_islow(const int16_t* coef, const uint16_t* q, uint8_t* out, int pitch)
     tmp1 += z2 + z4;
     tmp2 += z2 + z3;
     tmp3 += z1 + z4;
-    o[0] = kRange.t[descale(t10 + tmp3, s2) & 1023];
-    o[7] = kRange.t[descale(t10 - tmp3, s2) & 1023];
-    o[1] = kRange.t[descale(t11 + tmp2, s2) & 1023];
-    o[6] = kRange.t[descale(t11 - tmp2, s2) & 1023];
-    o[2] = kRange.t[descale(t12 + tmp1, s2) & 1023];
-    o[5] = kRange.t[descale(t12 - tmp1, s2) & 1023];
-    o[3] = kRange.t[descale(t13 + tmp0, s2) & 1023];
-    o[4] = kRange.t[descale(t13 - tmp0, s2) & 1023];
+    o[0] = kRange.t[(int)descale(t10 + tmp3, s2) & 1023];
+    o[7] = kRange.t[(int)descale(t10 - tmp3, s2) & 1023];
+    o[1] = kRange.t[(int)descale(t11 + tmp2, s2) & 1023];
+    o[6] = kRange.t[(int)descale(t11 - tmp2, s2) & 1023];
+    o[2] = kRange.t[(int)descale(t12 + tmp1, s2) & 1023];
+    o[5] = kRange.t[(int)descale(t12 - tmp1, s2) & 1023];
+    o[3] = kRange.t[(int)descale(t13 + tmp0, s2) & 1023];
+    o[4] = kRange.t[(int)descale(t13 - tmp0, s2) & 1023];
   }
 }
 

@@ -84,6 +84,22 @@ def test_avi1_frames_without_huffman_tables(tmp_path, mode):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("mode", ["L", "RGB"])
+def test_sixteen_bit_quantisation_tables(tmp_path, mode):
+    """SOF1 with 16-bit (Pq = 1) quantisation tables (entries up to 1,900):
+    parsed and decoded byte-identical to libjpeg-turbo.  The IDCT computes in
+    JLONG as jidctint.c does (no 32-bit overflow for any table); for
+    dequantised products beyond 16 bits libjpeg-turbo's SIMD IDCT wraps its
+    16-bit lanes instead, which is not restated (unpinned: such streams do
+    not come out of an encoder)."""
+    qt = [[257 + 27 * i for i in range(64)], [300 + 25 * i for i in range(64)]]
+    kw = {"qtables": qt[:1]} if mode == "L" else {"qtables": qt, "subsampling": 0}
+    f = _frames(2, 40, 48, 11)
+    js = MW.jpeg_frames(f, mode=mode, **kw)
+    assert all(j.find(b"\xff\xc1") >= 0 for j in js)  # extended sequential (16-bit tables)
+    _check(tmp_path, f, name="q16" + mode, mode=mode, **kw)
+
+
 def test_optimized_huffman_tables(tmp_path):
     _check(tmp_path, _frames(2, 33, 65, 4), mode="RGB", quality=90, optimize=True)
     _check(tmp_path, _frames(2, 33, 65, 5), name="g", mode="L", quality=90, optimize=True)
