@@ -344,8 +344,8 @@ def main():
         if NL == 1:
             c.detect_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)
             record(k, timing)
-        else:  # pipelined: keep every lane busy, collect in submission order
-            if c.pending() == NL:
+        else:  # pipelined: keep every lane busy (finished lanes are reused), collect in submission order
+            if c.pending() == 2 * NL:
                 c.collect(raw=True)
                 record(k, timing)
             c.submit_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)

@@ -291,18 +291,21 @@ lm_status lm_detect_batch_device(lm_ctx* ctx, const uint8_t* d_frames, int64_t f
  * follow each other as in lm_detect_batch (contiguous frames, or prev_frame at
  * a shard start).  A batch continuing another lane's batch takes that batch's
  * last frame as a 1-frame halo copied on the device, so consecutive batches
- * run concurrently; results are bit-identical to one lane.  Submitting while
- * every lane holds a batch fails (LM_ERR_INVALID_ARGUMENT): collect first.
- * Collect waits for the OLDEST submitted batch and returns its results
- * (valid until the next lm_detect_* call on the context); its errors are
- * the ones lm_detect_batch would report.  lm_detect_batch* require that no
- * batch is in flight. */
+ * run concurrently; results are bit-identical to one lane.  When every lane
+ * is busy, submit waits for the first lane whose batch completes and reuses
+ * it (that batch's results are kept until collected); with 2 x
+ * pipeline_lanes batches waiting for collection it fails
+ * (LM_ERR_INVALID_ARGUMENT): collect first.  Collect returns the OLDEST
+ * submitted batch's results (valid until the next lm_detect_* call on the
+ * context), waiting for it if needed; its errors are the ones
+ * lm_detect_batch would report.  lm_detect_batch* require that no batch is
+ * waiting. */
 lm_status lm_detect_submit(lm_ctx* ctx, const uint8_t* frames, int64_t frame_pitch, int32_t n, int32_t first_frame,
                            const uint8_t* prev_frame, const int32_t* bb);
 lm_status lm_detect_submit_device(lm_ctx* ctx, const uint8_t* d_frames, int64_t frame_pitch, int32_t n,
                                   int32_t first_frame, const uint8_t* d_prev_frame, const int32_t* bb);
 lm_status lm_detect_collect(lm_ctx* ctx, lm_batch_result* out);
-/* Lanes of the context / batches submitted and not yet collected. */
+/* Lanes of the context / batches submitted and not yet collected (<= 2 x lanes). */
 int32_t lm_ctx_lanes(const lm_ctx* ctx);
 int32_t lm_ctx_pending(const lm_ctx* ctx);
 

@@ -20,6 +20,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "locomouse_hip.h"
@@ -117,7 +118,8 @@ struct Lane {
     int n = 0, first = 0, s_lut0 = 1, s_proc0 = 1, plan = 0, cur = 0, prv = 0, last_n = 0;
     bool carry = false;
   } pend;
-  int batch_n = 0, batch_s0 = 1;  // last collected batch
+  int64_t seq = -1;               // submission number of the batch running on this lane (-1: idle)
+  int batch_n = 0, batch_s0 = 1;  // last finished batch
   // pipelined halos: the batch's last frame copied to the context's handoff
   // buffer / the predecessor's handoff frame copied into this lane's halo
   hipEvent_t ev_snap = nullptr, ev_consumed = nullptr;
@@ -191,8 +193,25 @@ struct lm_ctx {
   // pipeline
   std::vector<std::unique_ptr<Lane>> lanes;
   DevBuf<uint8_t> handoff;     // two frames: the last frame of submitted batch k in slot k & 1
-  std::deque<int> inflight;    // lanes holding a submitted batch, in submission order
-  int next_lane = 0, last_lane = -1, collected_lane = 0;
+  // Submitted batches not yet returned by lm_detect_collect, in submission
+  // order.  A batch runs on a lane until it is finished: when it is
+  // collected, or earlier when a submission needs its lane (its packed
+  // results are then copied aside, "retired"), so a lane that finishes early
+  // is fed again at once while results still come back in frame order.
+  struct BatchRec {
+    int64_t seq = 0;
+    int lane = -1;  // running there; -1 once retired
+    int first = 0, n = 0;
+    lm_status status = LM_OK;  // a failure found while retiring, reported when collected
+    std::string err;
+    std::vector<uint8_t> pack;  // retired results (lm_batch_result layout)
+    LmPackHdr ph{};
+    std::vector<const char*> t_names;  // kernel timings (debug bit 1)
+    std::vector<double> t_ms, t_t0, t_t1;
+  };
+  std::deque<BatchRec> queue;
+  BatchRec delivered;          // the last collected batch (its arrays back the returned pointers)
+  int last_lane = -1, collected_lane = 0;
   int64_t nsub = 0;            // batches submitted
   // the video position after the last submitted batch
   bool have_state = false;
@@ -1066,12 +1085,71 @@ void launch_attempt(lm_ctx* c, Lane& L, int attempt) {
   HIPCHK(hipGetLastError());
 }
 
-// Submit frames [first, first + n) to the next lane (round-robin).  The lane
-// is idle (its previous batch was collected).  Host frames are copied to the
-// lane's staging slots before this returns; device frames are read in place
-// while the batch runs.  Batch k + 1 continues batch k:
-//  - on the same lane (one lane): slot 0 carries batch k's last frame and
-//    candidates (k_carry; k_out left the frame in the lane's halo);
+void finish_batch(lm_ctx* c, Lane& L);
+
+// The batch running on lane L is complete (or failed): finish it now and
+// keep its packed results (or its error) in its queue record, so the lane
+// can take the next batch while the results wait to be collected in order.
+void retire(lm_ctx* c, Lane& L) {
+  lm_ctx::BatchRec* rec = nullptr;
+  for (auto& r : c->queue)
+    if (r.lane == L.index && r.seq == L.seq) rec = &r;
+  if (!rec) throw std::runtime_error("pipeline: no record of the batch running on lane " + std::to_string(L.index));
+  try {
+    finish_batch(c, L);
+    rec->ph = *L.h_ph.p;
+    rec->pack.assign(L.h_pack.p, L.h_pack.p + rec->ph.bytes);
+  } catch (const std::invalid_argument& e) {
+    rec->status = LM_ERR_INVALID_ARGUMENT;
+    rec->err = e.what();
+  } catch (const HipError& e) {
+    rec->status = LM_ERR_HIP;
+    rec->err = e.what();
+  } catch (const std::exception& e) {
+    rec->status = LM_ERR_RUNTIME;
+    rec->err = e.what();
+  }
+  if (rec->status != LM_OK) L.have_state = false;
+  rec->t_names = L.t_names;
+  rec->t_ms = L.t_ms;
+  rec->t_t0 = L.t_t0;
+  rec->t_t1 = L.t_t1;
+  rec->lane = -1;
+  L.seq = -1;
+}
+
+// A free lane for the next batch: the lane that ran the previous batch when
+// nothing ran there since (it carries that batch's state), else any idle
+// lane; when every lane is busy, the first one whose batch has completed is
+// retired and reused (waiting for one to complete).
+Lane& acquire_lane(lm_ctx* c, int prev_frame) {
+  for (;;) {
+    Lane* pick = nullptr;
+    for (auto& l : c->lanes) {
+      if (l->seq >= 0) continue;
+      if (l->index == c->last_lane && l->have_state && l->last_frame == prev_frame) return *l;
+      if (!pick) pick = l.get();
+    }
+    if (pick) return *pick;
+    for (auto& l : c->lanes) {
+      const hipError_t q = hipStreamQuery(l->stream);
+      if (q != hipErrorNotReady) {
+        (void)hipGetLastError();
+        retire(c, *l);
+        return *l;
+      }
+    }
+    std::this_thread::yield();
+  }
+}
+
+// Submit frames [first, first + n) to a free lane (acquire_lane).  Host
+// frames are copied to the lane's staging slots before this returns; device
+// frames are read in place while the batch runs.  At most 2 x lanes batches
+// may wait for collection.  Batch k + 1 continues batch k:
+//  - on the lane that ran batch k (nothing run there since): slot 0 carries
+//    batch k's last frame and candidates (k_carry; k_out left the frame in
+//    the lane's halo);
 //  - on another lane: batch k copied its last frame to handoff[k & 1] at its
 //    start (event ev_snap); batch k + 1 copies it into its own halo (event
 //    ev_consumed) and runs it as a 1-frame halo (its candidates recomputed),
@@ -1082,15 +1160,15 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   if (first < 0) throw std::invalid_argument("first_frame must be >= 0.");
   if (!frames) throw std::invalid_argument("frames is NULL.");
   if (pitch < c->npix) throw std::invalid_argument("frame_pitch smaller than one frame.");
-  if (c->inflight.size() >= c->lanes.size())
-    throw std::invalid_argument("every pipeline lane holds a batch: lm_detect_collect the oldest one first.");
+  if (c->queue.size() >= 2 * c->lanes.size())
+    throw std::invalid_argument("2 x pipeline_lanes batches wait for collection: lm_detect_collect first.");
   HIPCHK(hipSetDevice(c->device));
-  Lane& L = *c->lanes[c->next_lane];
   const bool pipelined = c->lanes.size() > 1;
   const bool given_halo = prev != nullptr && first > 0;
   const bool cont = !given_halo && first > 0;
   if (cont && !(c->have_state && c->last_frame == first - 1))
     throw std::invalid_argument("frame first_frame-1 was not processed by this context: pass prev_frame (shard start).");
+  Lane& L = acquire_lane(c, cont ? first - 1 : -2);
   const bool carry = cont && c->last_lane == L.index && L.have_state && L.last_frame == first - 1;
   const bool handoff = cont && !carry;
   if (handoff && !pipelined)
@@ -1207,9 +1285,14 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   c->last_frame = first + n - 1;
   for (int k = 0; k < 3; ++k) c->last_bb[k] = new_last_bb[k];
   c->last_lane = L.index;
+  L.seq = c->nsub;
+  lm_ctx::BatchRec rec;
+  rec.seq = c->nsub;
+  rec.lane = L.index;
+  rec.first = first;
+  rec.n = n;
+  c->queue.push_back(std::move(rec));
   ++c->nsub;
-  c->inflight.push_back(L.index);
-  c->next_lane = (L.index + 1) % (int)c->lanes.size();
   L.have_state = true;
   L.last_frame = first + n - 1;
   L.last_n = n;
@@ -1217,9 +1300,9 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   L.parity = 1 - P.cur;
 }
 
-// Wait for the lane's batch, rerun it while its result arena overflows, and
-// point `out` at its packed results (valid until the lane is reused).
-void finish_batch(lm_ctx* c, Lane& L, lm_batch_result* out) {
+// Wait for the lane's batch and rerun it while its result arena overflows;
+// its packed results are then in the lane's h_pack.
+void finish_batch(lm_ctx* c, Lane& L) {
   Lane::Pending& P = L.pend;
   hipStream_t st = L.stream;
   const int n = P.n, first = P.first;
@@ -1295,12 +1378,14 @@ void finish_batch(lm_ctx* c, Lane& L, lm_batch_result* out) {
         break;
       }
   }
-  const LmPackLayout PL = lm_pack_layout(n, ph.tot);
-  const uint8_t* hp = L.h_pack.p;
   L.batch_n = n;
   L.batch_s0 = P.s_proc0;
   P.on = false;
+}
 
+// lm_batch_result pointers into packed results `hp` (lm_pack_layout).
+void fill_result(lm_batch_result* out, const uint8_t* hp, int n, int first, const LmPackHdr& ph) {
+  const LmPackLayout PL = lm_pack_layout(n, ph.tot);
   out->n_frames = n;
   out->first_frame = first;
   out->cand_offset = reinterpret_cast<const int64_t*>(hp + PL.cand_off);
@@ -1320,25 +1405,44 @@ void finish_batch(lm_ctx* c, Lane& L, lm_batch_result* out) {
   out->tail = reinterpret_cast<const int32_t*>(hp + PL.tail);
 }
 
-// The oldest submitted batch's results.
+// The oldest submitted batch's results (valid until the next lm_detect_*
+// call on the context).
 void collect_batch(lm_ctx* c, lm_batch_result* out) {
-  if (c->inflight.empty()) throw std::invalid_argument("no batch in flight: lm_detect_submit one first.");
-  Lane& L = *c->lanes[c->inflight.front()];
-  c->inflight.pop_front();
-  c->collected_lane = L.index;
-  try {
-    finish_batch(c, L, out);
-  } catch (...) {
-    L.pend.on = false;
-    L.have_state = false;
-    throw;
+  if (c->queue.empty()) throw std::invalid_argument("no batch in flight: lm_detect_submit one first.");
+  lm_ctx::BatchRec rec = std::move(c->queue.front());
+  c->queue.pop_front();
+  if (rec.lane >= 0) {  // still on its lane: finish it there
+    Lane& L = *c->lanes[rec.lane];
+    c->collected_lane = L.index;
+    try {
+      finish_batch(c, L);
+    } catch (...) {
+      L.pend.on = false;
+      L.have_state = false;
+      L.seq = -1;
+      throw;
+    }
+    L.seq = -1;
+    rec.t_names = L.t_names;
+    rec.t_ms = L.t_ms;
+    rec.t_t0 = L.t_t0;
+    rec.t_t1 = L.t_t1;
+    const LmPackHdr ph = *L.h_ph.p;
+    c->delivered = std::move(rec);
+    fill_result(out, L.h_pack.p, c->delivered.n, c->delivered.first, ph);
+    return;
   }
+  if (rec.status == LM_ERR_INVALID_ARGUMENT) throw std::invalid_argument(rec.err);
+  if (rec.status == LM_ERR_HIP) throw HipError(rec.err);
+  if (rec.status != LM_OK) throw std::runtime_error(rec.err);
+  c->delivered = std::move(rec);
+  fill_result(out, c->delivered.pack.data(), c->delivered.n, c->delivered.first, c->delivered.ph);
 }
 
 // One synchronous batch (submit + collect); nothing may be in flight.
 void run_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int first, const uint8_t* prev, const int32_t* bb,
                bool device_frames, lm_batch_result* out) {
-  if (!c->inflight.empty())
+  if (!c->queue.empty())
     throw std::invalid_argument("batches are in flight: lm_detect_collect them before lm_detect_batch.");
   submit_batch(c, frames, pitch, n, first, prev, bb, device_frames);
   collect_batch(c, out);
@@ -1418,7 +1522,7 @@ LM_API void* lm_ctx_stream(lm_ctx* ctx) { return ctx && !ctx->lanes.empty() ? (v
 
 LM_API int32_t lm_ctx_lanes(const lm_ctx* ctx) { return ctx ? (int32_t)ctx->lanes.size() : 0; }
 
-LM_API int32_t lm_ctx_pending(const lm_ctx* ctx) { return ctx ? (int32_t)ctx->inflight.size() : 0; }
+LM_API int32_t lm_ctx_pending(const lm_ctx* ctx) { return ctx ? (int32_t)ctx->queue.size() : 0; }
 
 LM_API lm_status lm_detect_batch(lm_ctx* ctx, const uint8_t* frames, int64_t frame_pitch, int32_t n, int32_t first_frame,
                                  const uint8_t* prev_frame, const int32_t* bb, lm_batch_result* out) {
@@ -1470,7 +1574,7 @@ LM_API lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags) {
 
 LM_API int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, double* t1, int32_t cap) {
   if (!ctx) return 0;
-  const Lane& L = *ctx->lanes[ctx->collected_lane];
+  const lm_ctx::BatchRec& L = ctx->delivered;
   const int32_t n = (int32_t)L.t_names.size();
   for (int32_t i = 0; i < n && i < cap; ++i) {
     if (names) names[i] = L.t_names[i];
@@ -1511,7 +1615,7 @@ LM_API lm_status lm_debug_tail_mask(lm_ctx* ctx, int32_t f, uint8_t* out, int32_
 
 LM_API int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32_t cap) {
   if (!ctx) return 0;
-  const Lane& L = *ctx->lanes[ctx->collected_lane];
+  const lm_ctx::BatchRec& L = ctx->delivered;
   const int32_t n = (int32_t)L.t_names.size();
   for (int32_t i = 0; i < n && i < cap; ++i) {
     if (names) names[i] = L.t_names[i];

@@ -317,8 +317,8 @@ lm_geometry LocoMouse::geometry() const {
 
 // A full batch goes to the device (lm_detect_submit copies the frames and
 // returns); up to IN.lanes batches run on the device at once while the
-// caller reads the next frames.  When every lane is busy the oldest batch is
-// collected first, so results are appended in frame order.
+// caller reads the next frames, and up to 2 x IN.lanes wait for their results
+// to be appended (oldest first, so results are appended in frame order).
 void LocoMouse::flush() {
   const int n = N_PENDING, first = CURRENT_FRAME + 1 - n;
   std::vector<int32_t> bb((size_t)3 * n);
@@ -327,7 +327,7 @@ void LocoMouse::flush() {
     bb[3 * i + 1] = (int32_t)BB_Y_BOTTOM_POS[first + i];
     bb[3 * i + 2] = (int32_t)BB_Y_SIDE_POS[first + i];
   }
-  while ((int)INFLIGHT.size() >= lm_ctx_lanes(CTX)) collect_oldest();
+  while ((int)INFLIGHT.size() >= 2 * lm_ctx_lanes(CTX)) collect_oldest();
   throw_on_error(lm_detect_submit(CTX, PENDING.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data()));
   INFLIGHT.push_back({first, n});
   // Frames already read ahead past this batch (read_frames fills up to a whole

@@ -23,7 +23,7 @@ def _pipelined(ctx, frames, B, first=0):
     parts, firsts = [], []
     lanes = ctx.lanes()
     for i in range(0, len(frames), B):
-        if ctx.pending() == lanes:
+        if ctx.pending() == 2 * lanes:
             r = ctx.collect()
             firsts.append(r["first_frame"])
             parts.append(r)
@@ -85,26 +85,34 @@ def test_pipelined_tie_heavy_and_blank_frames():
 
 
 def test_pipelined_errors_and_synchronous_mix():
+    """At most 2 x lanes batches wait for collection (the lanes of finished
+    batches are reused while their results wait); lm_detect_batch needs an
+    empty pipeline; frame gaps are refused; a synchronous batch continues the
+    pipelined ones."""
     from locomouse_cpp_amd.runtime import LMError
     cfg = S.SyntheticConfig()
-    frames = cfg.frames(0, 12)
+    frames = cfg.frames(0, 24)
     ctx = _pctx(cfg, 2, 4)
     ctx.submit(frames[0:4], 0)
     with pytest.raises(LMError) as e:  # lm_detect_batch while a batch is in flight
         ctx.detect(frames[4:8], 4)
     assert e.value.code == 1
-    ctx.submit(frames[4:8], 4)
-    with pytest.raises(LMError) as e:  # every lane busy
-        ctx.submit(frames[8:12], 8)
+    for i in (4, 8, 12):  # four batches in flight on two lanes
+        ctx.submit(frames[i:i + 4], i)
+    assert ctx.pending() == 4
+    with pytest.raises(LMError) as e:  # 2 x lanes waiting
+        ctx.submit(frames[16:20], 16)
     assert e.value.code == 1
-    r0 = ctx.collect()
+    parts = [ctx.collect()]
     with pytest.raises(LMError) as e:  # a gap in the frame sequence
-        ctx.submit(frames[9:12], 9)
+        ctx.submit(frames[17:20], 17)
     assert e.value.code == 1
-    r1 = ctx.collect()
-    assert (r0["first_frame"], r1["first_frame"]) == (0, 4)
+    ctx.submit(frames[16:20], 16)
+    while ctx.pending():
+        parts.append(ctx.collect())
+    assert [p["first_frame"] for p in parts] == [0, 4, 8, 12, 16]
     # a synchronous batch continuing the pipelined ones (hand-off halo)
-    r2 = ctx.detect(frames[8:12], 8)
-    assert_same(concat_results([r0, r1, r2]), _oracle(cfg, frames).result, "mixed: ")
+    parts.append(ctx.detect(frames[20:24], 20))
+    assert_same(concat_results(parts), _oracle(cfg, frames).result, "mixed: ")
     with pytest.raises(LMError):
         ctx.collect()  # nothing in flight
