@@ -45,6 +45,23 @@ def algorithmic_flops_per_frame(ctx):
     return 2 * sum(outs[k] * w[k].size for k in outs)
 
 
+def executed_flops(ctx, work, n):
+    """FLOP the correlation executed for a batch of n frames: the tail
+    detectors over every output, the point detectors over the outputs of their
+    bright tiles only (`work` = Context.corr_work(): dark tiles -- no mouse
+    pixel > 25, all scores zeroed by the reference's mask -- are skipped).
+    None when the batch's work was not recorded."""
+    if work is None:
+        return None
+    g = ctx.geometry()
+    w = ctx.cfg.weights
+    tw = g.tail_box_width
+    hb, hs = g.bb_bottom_mouse.height, g.bb_side_mouse.height
+    ob, os_ = work["outputs"]
+    return 2 * (ob * (w["paw_bottom"].size + w["snout_bottom"].size) + os_ * (w["paw_side"].size + w["snout_side"].size)
+                + n * (hb * tw * w["tail_bottom"].size + hs * tw * w["tail_side"].size))
+
+
 def union_ms(iv):
     """Length of the union of [t0, t1] intervals (ms)."""
     tot, end = 0.0, None
@@ -331,6 +348,7 @@ def main():
             for name, t0, t1 in ctxs[k].kernel_spans():
                 kernel_ms.setdefault(name, []).append(t1 - t0)
                 spans.setdefault(name, []).append((t0, t1))
+            executed.append(executed_flops(ctxs[k], ctxs[k].corr_work(), B))
 
     def step(k, timing):
         st = state[k]
@@ -386,7 +404,7 @@ def main():
         if errors:
             raise errors[0]
 
-    kernel_ms, spans = {}, {}
+    kernel_ms, spans, executed = {}, {}, []
     run_all(args.warmup, False)
     for c in ctxs:
         c.set_debug(2)  # HIP events around every kernel on the ctx stream
@@ -418,7 +436,10 @@ def main():
     # stream this is the plain mean.
     corr_spans = spans.get("k_corr", [])
     corr_avg_ms = union_ms(corr_spans) / max(1, len(corr_spans))
-    achieved_tf = flops * B / (corr_avg_ms * 1e-3) / 1e12
+    algorithmic_tf = flops * B / (corr_avg_ms * 1e-3) / 1e12
+    # the kernel's own rate: the FLOP it executed (dark tiles skipped) per launch
+    exec_per_launch = (sum(executed) / len(executed)) if executed and None not in executed else flops * B
+    achieved_tf = exec_per_launch / (corr_avg_ms * 1e-3) / 1e12
     peak_tf = F16_PEAK_TFLOPS if f16 else FP32_PEAK_TFLOPS
     traffic = None  # HBM bytes per launch from this tree's PMC passes (scripts/pmc_traffic.py)
     if os.path.exists(PMC_TRAFFIC):
@@ -443,6 +464,7 @@ def main():
                    "stream_priorities": "alternating high/low" if os.environ.get("LM_STREAM_PRIO", "1") != "0" else "equal",
                    "corr_launches": ("one merged launch" if NS * NL == 1 else "one per detector width")
                    if os.environ.get("LM_CORR_PLAN") not in ("0", "1") else f"LM_CORR_PLAN={os.environ['LM_CORR_PLAN']}",
+                   "dark_tiles": "skipped" if os.environ.get("LM_CORR_DARK", "1") != "0" else "computed",
                    "parallelism": f"frame shards x{world} (no collective)"},
         "hbm_gbs": round(fps * FRAME_BYTES / 1e9, 3),
         "roofline": {"bound": "mfma" if f16 else "valu",
@@ -451,7 +473,15 @@ def main():
                      "kernel": "k_corr", "achieved": round(achieved_tf, 3), "peak": peak_tf,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
                      "traffic": traffic if not f16 and args.config == "c3" else None,
-                     "algorithmic_flop_per_launch": flops * B, "avg_launch_ms": round(corr_avg_ms, 5),
+                     "executed_flop_per_launch": int(exec_per_launch),
+                     "algorithmic_flop_per_launch": flops * B,
+                     "executed_fraction": round(exec_per_launch / (flops * B), 4),
+                     "algorithmic_tflops": round(algorithmic_tf, 3),
+                     "algorithmic_frac": round(algorithmic_tf / peak_tf, 4),
+                     "flop_note": "achieved/frac: FLOP executed per launch (point detectors' dark tiles, whose scores "
+                                  "the reference zeroes with its brightness mask, are not computed); "
+                                  "algorithmic_*: SURVEY.md 8(d)'s count over every consumed output",
+                     "avg_launch_ms": round(corr_avg_ms, 5),
                      "launches": len(corr_spans),
                      "duration": "union of k_corr HIP-event spans over all streams / launches"},
         "kernel_avg_ms": {k: round(sum(v) / len(v), 5) for k, v in kernel_ms.items()},

@@ -334,6 +334,14 @@ int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32
  * that device), so the spans of several contexts' streams can be merged. */
 int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, double* t1, int32_t cap);
 
+/* Correlation work of the last collected batch when debug bit 1 is set:
+ * out[0], out[1] = bright output tiles (LM_TW x LM_RW_TH = 80 x 16) of the
+ * bottom / side point detectors, out[2], out[3] = the consumed outputs those
+ * tiles hold.  The point detectors' dark tiles (no I_*_MOUSE pixel > 25, so
+ * every score is zeroed by setTo(0, mask), LocoMouse_class.cpp:849, :864)
+ * are not computed.  -1 when not recorded (timing off, LM_CORR_DARK=0). */
+lm_status lm_debug_corr_work(const lm_ctx* ctx, int32_t* out);
+
 /* ---- whole-video bounding-box pass ----
  *
  * Replaces the virtual computeBoundingBox of the three methods:

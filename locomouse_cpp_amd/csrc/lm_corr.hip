@@ -213,22 +213,52 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
 // are flattened detector-major (all slots of the group's first detector,
 // then the next ...), so no wave idles at a frame's end and the host can
 // put the longest detectors first.  false: past the last tile.
-DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, int& slot, CorrTile& T) {
-  int gi = 0, base = 0;
+// With dark-tile lists (tl_cnt != nullptr) a point detector's waves are
+// only its view's bright tiles (k_tilelist), so the group's wave count is
+// known on the device only: the grid is sized for every tile and the waves
+// past the last group's count (whole workgroups at the grid's end) return.
+DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, const int32_t* tl_cnt,
+                        const uint32_t* tl_list, int& slot, CorrTile& T) {
+  int base = 0;
 #pragma unroll
-  for (int k = 0; k < LM_NDET - 1; ++k)
-    if (k + 1 < G.n && g >= nslots * G.tile_end[k]) {
-      gi = k + 1;
-      base = nslots * G.tile_end[k];
+  for (int k = 0; k < LM_NDET; ++k) {
+    if (k >= G.n) return false;
+    const int d = G.ids[k];
+    const LmDet& D = K.det[d];
+    const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
+    const bool listed = tl_cnt != nullptr && D.kind == 0;
+    const int cnt = listed ? tl_cnt[D.view] : nt * nslots;
+    if (g < base + cnt) {
+      const int local = g - base;
+      int lt;
+      if (listed) {
+        const uint32_t e = tl_list[(int64_t)D.view * K.tl_stride + local];
+        slot = (int)(e >> 16);
+        lt = (int)(e & 0xFFFFu);
+      } else {
+        slot = s0 + local / nt;
+        lt = local - (local / nt) * nt;
+      }
+      const int tx = D.tiles_x;
+      T = CorrTile{d, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
+      return true;
     }
-  const int d = G.ids[gi];
-  const int nt = G.tile_end[gi] - (gi ? G.tile_end[gi - 1] : 0);
-  const int local = g - base;
-  if (local >= nt * nslots) return false;
-  slot = s0 + local / nt;
-  const int lt = local - (local / nt) * nt;
-  const int tx = K.det[d].tiles_x;
-  T = CorrTile{d, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
+    base += cnt;
+  }
+  return false;
+}
+
+// A workgroup tile of a point detector (k_corr_gen, k_corr_f16) whose flag
+// tiles are all dark has no output that survives the mask.
+DEV bool corr_tile_dark(const LmConst& K, const LmDet& D, const uint8_t* __restrict__ dark, int slot, int oy0, int ox0) {
+  if (dark == nullptr || D.kind != 0) return false;
+  const int v = D.view;
+  const int ty0 = oy0 / LM_RW_TH, ty1 = min(K.fl_ty[v] - 1, (oy0 + D.tile_h - 1) / LM_RW_TH);
+  const int tx0 = ox0 / LM_TW, tx1 = min(K.fl_tx[v] - 1, (ox0 + D.tile_w - 1) / LM_TW);
+  const uint8_t* __restrict__ f = dark + (int64_t)slot * K.fl_slot + K.fl_off[v];
+  for (int ty = ty0; ty <= ty1; ++ty)
+    for (int tx = tx0; tx <= tx1; ++tx)
+      if (f[ty * K.fl_tx[v] + tx]) return false;
   return true;
 }
 
@@ -538,13 +568,14 @@ template <int KW, bool UNF>
 __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? 5 : 1, 8))) void k_corr_rw(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
-    int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+    int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
+    const int32_t* __restrict__ tl_cnt, const uint32_t* __restrict__ tl_list) {
   const LmConst& K = *Kp;
   extern __shared__ uint4 lds_rw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int slot;
   CorrTile T;
-  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, slot, T)) return;
+  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, tl_cnt, tl_list, slot, T)) return;
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * (LM_RW_SLOTS + 1) * rw_stride(KW);
   rw_tile<KW, UNF>(K, K.det[T.d], slot, T.oy0, T.ox0, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin,
                    tailbin_slot_bytes);
@@ -558,13 +589,14 @@ template <bool UNF>
 __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_corr_rw_all(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
-    int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+    int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
+    const int32_t* __restrict__ tl_cnt, const uint32_t* __restrict__ tl_list) {
   const LmConst& K = *Kp;
   extern __shared__ uint4 lds_rw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int slot;
   CorrTile T;
-  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, slot, T)) return;
+  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, tl_cnt, tl_list, slot, T)) return;
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * G.ring_floats;
   const LmDet D = K.det[T.d];
   switch (D.kw) {
@@ -593,7 +625,8 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
                                                               const float* __restrict__ weights, int s0,
                                                               unsigned long long* __restrict__ keys,
                                                               int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin,
-                                                              int64_t tailbin_slot_bytes) {
+                                                              int64_t tailbin_slot_bytes,
+                                                              const uint8_t* __restrict__ dark) {
   const LmConst& K = *Kp;
   extern __shared__ float lds[];
   __shared__ int s_cnt, s_base;
@@ -601,6 +634,7 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
   const CorrTile T = corr_tile(K, G);
   const LmDet D = K.det[T.d];
   const int oy0 = T.oy0, ox0 = T.ox0;
+  if (corr_tile_dark(K, D, dark, slot, oy0, ox0)) return;
   const int kh = D.kh, kwp = D.kwp, ch = D.chunk_rows;
   const int cols = LM_TW + kwp - 1, stride = pk_stride(cols);
   const int ew = K.ext_w[D.view];
@@ -722,7 +756,8 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
                                                             const uint4* __restrict__ bfrag, int s0,
                                                             unsigned long long* __restrict__ keys,
                                                             int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin,
-                                                            int64_t tailbin_slot_bytes) {
+                                                            int64_t tailbin_slot_bytes,
+                                                            const uint8_t* __restrict__ dark) {
   const LmConst& K = *Kp;
   // uint4: the dynamic area starts 16-byte aligned after the static variables
   // (with a float array it would start 8 bytes in, and every ds_read_b128 of
@@ -733,6 +768,7 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
   const CorrTile T = corr_tile(K, G);
   const LmDet D = K.det[T.d];
   const int oy0 = T.oy0, ox0 = T.ox0, kh = D.kh;
+  if (corr_tile_dark(K, D, dark, slot, oy0, ox0)) return;
   constexpr int cols = f16_cols(NCH), STR = f16_stride(cols);
   constexpr int NB = NCH * 64;  // 16-byte B fragments per detector row
   const int rows = LM_F16_TH + kh - 1;
@@ -906,17 +942,132 @@ const void* corr_kernel_rw_all(bool unf) {
 
 hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t lds, hipStream_t st, const LmConst* K,
                        const LmDetGroup& G, const uint8_t* ext, int64_t ext_slot_bytes, const void* weights, int s0,
-                       unsigned long long* keys, int32_t* n_pos, uint8_t* tailbin, int64_t tailbin_slot_bytes) {
+                       unsigned long long* keys, int32_t* n_pos, uint8_t* tailbin, int64_t tailbin_slot_bytes,
+                       const CorrDark& dk) {
   if (ring) {
     int nslots = (int)grid.y;
     const unsigned waves = (unsigned)(G.tile_end[G.n - 1] * nslots);
-    void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
-                    (void*)&nslots, (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
+    void* args[] = {(void*)&K,       (void*)&G,    (void*)&ext,     (void*)&ext_slot_bytes,
+                    (void*)&weights, (void*)&s0,   (void*)&nslots,  (void*)&keys,
+                    (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes, (void*)&dk.cnt,
+                    (void*)&dk.list};
     return hipLaunchKernel(fn, dim3((waves + LM_RW_WAVES - 1) / LM_RW_WAVES), dim3(LM_RW_THREADS), args, lds, st);
   }
-  void* args[] = {(void*)&K, (void*)&G, (void*)&ext, (void*)&ext_slot_bytes, (void*)&weights, (void*)&s0,
-                  (void*)&keys, (void*)&n_pos, (void*)&tailbin, (void*)&tailbin_slot_bytes};
+  void* args[] = {(void*)&K,     (void*)&G,       (void*)&ext,     (void*)&ext_slot_bytes,           (void*)&weights,
+                  (void*)&s0,    (void*)&keys,    (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes,
+                  (void*)&dk.flags};
   return hipLaunchKernel(fn, grid, dim3(threads), args, lds, st);
+}
+
+// ---------------------------------------------------------------- dark tiles
+// detectBottomCandidates / detectSideCandidates zero every score whose
+// I_*_MOUSE pixel is <= 25 (threshold(25.5, BINARY_INV) + setTo(0, mask),
+// LocoMouse_class.cpp:782, :817, :849, :864), so an output tile of a point
+// detector with no pixel > 25 yields nothing: its filter2D outputs are all
+// discarded by the reference, and the correlation does not compute them.
+// k_tileflag: one wave per (slot, view, LM_TW x LM_RW_TH output tile) writes
+// the tile's flag byte (1: some pixel > 25); the tile's mouse pixels are read
+// from the ext crop k_ingest just wrote (16 rows x 4 lanes of 20 columns).
+__global__ __launch_bounds__(256) void k_tileflag(const LmConst* __restrict__ Kp, const uint8_t* __restrict__ ext,
+                                                  int64_t ext_slot_bytes, int s0, uint8_t* __restrict__ flags) {
+  const LmConst& K = *Kp;
+  const int slot = s0 + blockIdx.y;
+  const int g = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  const int n0 = K.fl_tx[0] * K.fl_ty[0];
+  const int v = g < n0 ? 0 : 1;
+  const int t = v ? g - n0 : g;
+  if (t >= K.fl_tx[v] * K.fl_ty[v]) return;
+  const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
+  const int ty = t / K.fl_tx[v], tx = t - ty * K.fl_tx[v];
+  const int lane = threadIdx.x & 63;
+  const int y = ty * LM_RW_TH + (lane >> 2), x0 = tx * LM_TW + (lane & 3) * (LM_TW / 4);
+  static_assert(LM_RW_TH * 4 == 64 && LM_TW / 4 == 20, "k_tileflag lane map");
+  bool bright = false;
+  if (y < D.oh && x0 < D.ow) {
+    const uint8_t* row = ext + (int64_t)slot * ext_slot_bytes + (v ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
+                         (int64_t)(D.m_y + y) * K.ext_w[v] + (D.m_x + x0);
+    const unsigned mis = (unsigned)((uintptr_t)row & 3);
+    const unsigned* __restrict__ a = reinterpret_cast<const unsigned*>(row - mis);
+    unsigned d[6];
+#pragma unroll
+    for (int u = 0; u < 6; ++u) d[u] = a[u];  // the 20 bytes and <= 3 on either side (inside the ext crop)
+    const int nb = min(LM_TW / 4, D.ow - x0);
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const unsigned w = __builtin_amdgcn_alignbyte(d[j + 1], d[j], mis);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * j + k < nb && ((w >> (8 * k)) & 0xFFu) > 25u) bright = true;
+    }
+  }
+  const bool any = __ballot(bright) != 0ull;
+  if (lane == 0) flags[(int64_t)slot * K.fl_slot + K.fl_off[v] + t] = any ? 1 : 0;
+}
+
+// k_tilelist: one 1024-thread workgroup per view lists the bright tiles of
+// slots s0 .. s0 + nproc - 1 in slot order, (slot << 16) | tile, at
+// view * tl_stride, their count in cnt[view] and the consumed outputs they
+// hold (edge tiles are partial) in cnt[2 + view] (lm_debug_corr_work).
+__global__ __launch_bounds__(1024) void k_tilelist(const LmConst* __restrict__ Kp, int s0, int nproc,
+                                                   const uint8_t* __restrict__ flags, int32_t* __restrict__ cnt,
+                                                   uint32_t* __restrict__ list) {
+  const LmConst& K = *Kp;
+  const int v = blockIdx.x;
+  const int nt = K.fl_tx[v] * K.fl_ty[v];
+  uint32_t* __restrict__ out = list + (int64_t)v * K.tl_stride;
+  const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
+  __shared__ int s_wave[16];
+  __shared__ int s_carry, s_outs;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    s_carry = 0;
+    s_outs = 0;
+  }
+  int outs = 0;
+  for (int c0 = 0; c0 < nproc; c0 += 1024) {
+    const int i = c0 + (int)threadIdx.x;
+    const uint8_t* __restrict__ f = flags + (int64_t)(s0 + i) * K.fl_slot + K.fl_off[v];
+    int n = 0;
+    if (i < nproc)
+      for (int t = 0; t < nt; ++t) n += f[t];
+    // exclusive scan over the workgroup
+    int incl = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
+    }
+    __syncthreads();  // s_carry of the previous chunk is final, s_wave free
+    if (lane == 63) s_wave[wid] = incl;
+    __syncthreads();
+    int before = s_carry;
+    for (int w = 0; w < wid; ++w) before += s_wave[w];
+    int pos = before + incl - n;
+    if (i < nproc)
+      for (int t = 0; t < nt; ++t)
+        if (f[t]) {
+          out[pos++] = ((uint32_t)(s0 + i) << 16) | (uint32_t)t;
+          const int ty = t / K.fl_tx[v], tx = t - ty * K.fl_tx[v];
+          outs += min(LM_RW_TH, D.oh - ty * LM_RW_TH) * min(LM_TW, D.ow - tx * LM_TW);
+        }
+    __syncthreads();
+    if (threadIdx.x == 1023) s_carry = before + incl;
+  }
+  for (int o = 32; o > 0; o >>= 1) outs += __shfl_xor(outs, o);
+  if (lane == 0) atomicAdd(&s_outs, outs);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    cnt[v] = s_carry;
+    cnt[2 + v] = s_outs;
+  }
+}
+
+hipError_t launch_tile_lists(hipStream_t st, const LmConst* dK, const LmConst& K, const uint8_t* ext,
+                             int64_t ext_slot_bytes, int s0, int nproc, const CorrDark& dk) {
+  const int nt = K.fl_tx[0] * K.fl_ty[0] + K.fl_tx[1] * K.fl_ty[1];
+  k_tileflag<<<dim3((unsigned)((nt + 3) / 4), (unsigned)nproc), 256, 0, st>>>(dK, ext, ext_slot_bytes, s0, dk.flags);
+  k_tilelist<<<2, 1024, 0, st>>>(dK, s0, nproc, dk.flags, dk.cnt, dk.list);
+  return hipGetLastError();
 }
 
 hipError_t launch_corr_dbg(bool unf, dim3 grid, hipStream_t st, const LmConst* K, const uint8_t* ext,

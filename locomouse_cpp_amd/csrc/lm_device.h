@@ -74,6 +74,12 @@ struct LmConst {
   // also ceil(tail_w / 64) u64 words); set by k_corr, zeroed by k_ingest
   int32_t tail_nw, tail_bm_words;
   int32_t connectivity;
+  // dark tiles (lm_corr.hip k_tileflag / k_tilelist): per view, the point
+  // detectors' outputs in LM_TW x LM_RW_TH tiles (fl_tx x fl_ty of them); one
+  // flag byte per (slot, view, tile) at slot * fl_slot + fl_off[view] + tile;
+  // the bright tiles of view v listed at v * tl_stride of the tile list
+  int32_t fl_tx[2], fl_ty[2], fl_off[2], fl_slot;
+  int32_t tl_stride;
   // per-list capacities (= output area) and list offsets inside a slot's key area
   int32_t list_cap[LM_NLIST];
   int64_t list_off[LM_NLIST];

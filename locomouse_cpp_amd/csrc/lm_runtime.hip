@@ -98,6 +98,9 @@ struct Lane {
   DevBuf<const uint8_t*> frame_ptr;
   DevBuf<LmSlot> slots;
   DevBuf<unsigned long long> keys, gscratch;
+  DevBuf<uint8_t> dark_flags;  // dark tiles (CorrDark): flag bytes, bright-tile lists and counts
+  DevBuf<uint32_t> dark_list;
+  DevBuf<int32_t> dark_cnt;
   DevBuf<long long> kprof;  // LM_KPROF=1: kernel phase timestamps
   Arena arena[2];
   int parity = 0;
@@ -127,6 +130,7 @@ struct Lane {
   std::vector<std::pair<const char*, int>> t_ev;  // (kernel, index of its begin event in ev_pool)
   std::vector<const char*> t_names;               // static kernel names
   std::vector<double> t_ms, t_t0, t_t1;
+  int32_t t_work[4] = {-1, -1, -1, -1};  // debug bit 1: dark-tile counts of the batch (lm_debug_corr_work)
   std::vector<hipEvent_t> ev_pool;
   // captured per-batch kernel chains, keyed by (n, parity, carry, last n, s_lut0, s_proc0, plan)
   struct GraphEntry {
@@ -190,6 +194,7 @@ struct lm_ctx {
   bool tail_big = false;        // k_tail<true>: tail tables in global memory
   int64_t tail_ws_slot = 0;     // its workspace bytes per slot
   bool kprof_on = false;
+  bool dark_on = true;  // skip the point detectors' dark tiles (LM_CORR_DARK=0: compute every tile)
   // pipeline
   std::vector<std::unique_ptr<Lane>> lanes;
   DevBuf<uint8_t> handoff;     // two frames: the last frame of submitted batch k in slot k & 1
@@ -208,6 +213,7 @@ struct lm_ctx {
     LmPackHdr ph{};
     std::vector<const char*> t_names;  // kernel timings (debug bit 1)
     std::vector<double> t_ms, t_t0, t_t1;
+    int32_t work[4] = {-1, -1, -1, -1};
   };
   std::deque<BatchRec> queue;
   BatchRec delivered;          // the last collected batch (its arrays back the returned pointers)
@@ -442,6 +448,22 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   K.tail_hb = ub.height;
   K.tail_hs = us.height;
   K.connectivity = P->conn_comp_connectivity;
+  // dark-tile flags of the point detectors' outputs (paw and snout of a view
+  // share the output region, out_rel above)
+  {
+    int o = 0;
+    for (int v = 0; v < 2; ++v) {
+      const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
+      K.fl_tx[v] = (D.ow + LM_TW - 1) / LM_TW;
+      K.fl_ty[v] = (D.oh + LM_RW_TH - 1) / LM_RW_TH;
+      K.fl_off[v] = o;
+      o += (K.fl_tx[v] * K.fl_ty[v] + 3) / 4 * 4;
+    }
+    K.fl_slot = o;
+    K.tl_stride = c->nslots * std::max(K.fl_tx[0] * K.fl_ty[0], K.fl_tx[1] * K.fl_ty[1]);
+    if (K.fl_tx[0] * K.fl_ty[0] > 65535 || K.fl_tx[1] * K.fl_ty[1] > 65535 || c->nslots > 65535)
+      throw std::invalid_argument("bounding box or batch too large for the correlation tile lists.");
+  }
   // k_tail's LDS: bitmaps, column tables and moment tiles from the geometry,
   // plus as many runs as fit 64 KiB (more go to global scratch)
   K.tail_ntc = (((tw - 1) / 15 + 1) + 31) / 32;
@@ -524,6 +546,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->gscratch_slot = std::max(3 * (int64_t)np, (5 * (int64_t)np + K.ong_nx * K.ong_ny + 2) / 2 + 1);
   c->unfused = su->filter_arith == LM_FILTER_UNFUSED;
   if (const char* v = getenv("LM_KPROF")) c->kprof_on = atoi(v) != 0;
+  if (const char* v = getenv("LM_CORR_DARK")) c->dark_on = atoi(v) != 0;
   // Detectors grouped by correlation kernel: one width-specialised k_corr_rw
   // launch per width, every other detector in one k_corr_gen launch.  Each
   // launch gets exactly the LDS its detectors' rings / windows need, so narrow
@@ -673,6 +696,11 @@ void lane_alloc(lm_ctx* c, Lane& L) {
   if (c->tail_big) L.tail_ws.alloc((size_t)c->tail_ws_slot * ns);
   L.keys.alloc((size_t)K.keys_per_slot * ns);
   L.npos.alloc((size_t)LM_NLIST * ns);
+  if (c->dark_on) {
+    L.dark_flags.alloc((size_t)K.fl_slot * ns);
+    L.dark_list.alloc((size_t)2 * K.tl_stride);
+    L.dark_cnt.alloc(4);
+  }
   L.err.alloc(16);
   L.frame_ptr.alloc(ns);
   L.slots.alloc(ns);
@@ -756,6 +784,8 @@ struct Timer {  // HIP events around the timed kernels of a lane's batch (debug 
       L.t_t1.push_back(t1);
     }
     L.t_ev.clear();
+    for (int k = 0; k < 4; ++k) L.t_work[k] = -1;
+    if (L.dark_cnt.p) COPY_SYNC(L.t_work, L.dark_cnt.p, sizeof(L.t_work), hipMemcpyDeviceToHost, L.stream);
   }
 };
 
@@ -912,6 +942,16 @@ void dump_slot(lm_ctx* c, Lane& L, const char* dir, int frame, int slot, int fea
   fclose(f);
 }
 
+CorrDark lane_dark(const lm_ctx* c, Lane& L) {
+  CorrDark d;
+  if (c->dark_on) {
+    d.flags = L.dark_flags.p;
+    d.cnt = L.dark_cnt.p;
+    d.list = L.dark_list.p;
+  }
+  return d;
+}
+
 // The kernel chain of one batch attempt on lane L (part: 0 the kernels before
 // k_corr, 1 k_corr, 2 the kernels after, -1 all).  Kernel arguments depend
 // only on the key of L.graphs (frame pointers and slots reach the kernels
@@ -944,6 +984,11 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
         dK, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, L.slots.p, s_proc0, n + 1, L.ext.p, c->ext_slot_bytes,
         ext_blocks, reinterpret_cast<unsigned*>(L.tailbin.p));
     T.end();
+    if (c->dark_on) {
+      T.begin("k_tiles");
+      HIPCHK(launch_tile_lists(st, dK, K, L.ext.p, c->ext_slot_bytes, s_proc0, nproc, lane_dark(c, L)));
+      T.end();
+    }
   }
   if (part == 1 || part < 0) {
     T.begin("k_corr");
@@ -954,7 +999,7 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
       const void* w = c->setup.corr_precision == LM_CORR_F16 ? (const void*)c->weights16.p : (const void*)c->weights.p;
       HIPCHK(launch_corr(grp.first, CP.ring[gi], dim3(G.tile_end[G.n - 1], nproc), CP.threads[gi], CP.lds[gi], st, dK,
                          G, L.ext.p, c->ext_slot_bytes, w, s_proc0, L.keys.p, L.npos.p, L.tailbin.p,
-                         c->tailbin_slot_bytes));
+                         c->tailbin_slot_bytes, lane_dark(c, L)));
     }
     T.end();
   }
@@ -1111,6 +1156,7 @@ void retire(lm_ctx* c, Lane& L) {
   }
   if (rec->status != LM_OK) L.have_state = false;
   rec->t_names = L.t_names;
+  std::copy(L.t_work, L.t_work + 4, rec->work);
   rec->t_ms = L.t_ms;
   rec->t_t0 = L.t_t0;
   rec->t_t1 = L.t_t1;
@@ -1345,8 +1391,12 @@ void finish_batch(lm_ctx* c, Lane& L) {
     }
     A.alloc_pack(ph.bytes + ph.bytes / 4);
   }
-  if (c->debug & 2) Timer::collect(c, L);
-  else L.t_ev.clear();
+  if (c->debug & 2) {
+    Timer::collect(c, L);
+  } else {
+    L.t_ev.clear();
+    for (int k = 0; k < 4; ++k) L.t_work[k] = -1;
+  }
   if (c->kprof_on) kprof_report(c, L, n);
 
   // ---- the packed results (lm_batch_result layout) are in h_pack unless
@@ -1424,6 +1474,7 @@ void collect_batch(lm_ctx* c, lm_batch_result* out) {
     }
     L.seq = -1;
     rec.t_names = L.t_names;
+    std::copy(L.t_work, L.t_work + 4, rec.work);
     rec.t_ms = L.t_ms;
     rec.t_t0 = L.t_t0;
     rec.t_t1 = L.t_t1;
@@ -1582,6 +1633,12 @@ LM_API int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0
     if (t1) t1[i] = L.t_t1[i];
   }
   return n;
+}
+
+LM_API lm_status lm_debug_corr_work(const lm_ctx* ctx, int32_t* out) {
+  if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
+  for (int k = 0; k < 4; ++k) out[k] = ctx->delivered.work[k];
+  return LM_OK;
 }
 
 LM_API lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out, int32_t rows, int32_t cols) {

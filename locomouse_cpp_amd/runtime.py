@@ -24,6 +24,7 @@ EXPORTED = (
     "lm_bb_create", "lm_bb_destroy", "lm_bb_push", "lm_bb_push_device", "lm_bb_finish", "lm_bb_debug_binary",
     "lm_bb_stream", "lm_host_alloc", "lm_host_free",
     "lm_detect_submit", "lm_detect_submit_device", "lm_detect_collect", "lm_ctx_lanes", "lm_ctx_pending",
+    "lm_debug_corr_work",
 )
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -149,6 +150,7 @@ def lib():
         L.lm_debug_kernel_spans.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_double),
                                             C.POINTER(C.c_double), C.c_int32]
         L.lm_debug_kernel_spans.restype = C.c_int32
+        L.lm_debug_corr_work.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
         L.lm_synth_frames_device.argtypes = [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32,
                                              C.c_int64]
         L.lm_bb_create.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
@@ -292,6 +294,13 @@ class Context:
         t1 = (C.c_double * 64)()
         n = lib().lm_debug_kernel_spans(self._h, names, t0, t1, 64)
         return [(names[i].decode(), t0[i], t1[i]) for i in range(min(n, 64))]
+
+    def corr_work(self):
+        """Bright (computed) output tiles and their consumed outputs of the last
+        batch, bottom and side point detectors (lm_debug_corr_work), or None."""
+        out = (C.c_int32 * 4)()
+        _check(lib().lm_debug_corr_work(self._h, out))
+        return None if out[0] < 0 else {"tiles": (out[0], out[1]), "outputs": (out[2], out[3])}
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

@@ -6,11 +6,12 @@ bench.py reports as roofline.traffic.
 Units: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB.  MI355X_MICROARCH.md
 (HBM section, :298): on gfx950 FETCH_SIZE reports exactly 1/2 of the bytes of
 a wide coalesced streaming read (16 B/lane; 128-B requests tallied at 64 B).
-k_corr_gen / k_corr_f16 fill their windows with 16-B/lane uint4 loads
-(tile_fill_f32 / tile_fill_f16), so their FETCH_SIZE is doubled; k_corr_rw
-streams its ring rows with 4-B/lane dword loads, a width the guide leaves
-uncalibrated (:300), so its FETCH_SIZE is taken as reported and labelled so.
-The per-kernel table lists FETCH_SIZE as reported.
+The other widths the kernels use were calibrated on a known byte count
+(scripts/ubench/fetch_calib.hip, profiles/r03/fetch_calib.json): 4-B/lane
+dword loads (k_corr_rw's ring rows), k_ingest's five-dword run gathers and
+byte loads also read 0.50 of their bytes, and WRITE_SIZE is exact for 16-B
+and 4-B stores.  So every FETCH_SIZE is doubled.  The per-kernel table lists
+FETCH_SIZE as reported.
 
 Usage: python scripts/pmc_traffic.py gpurun_out/pmc_<tag> <batch> [out.json]
 """
@@ -34,8 +35,8 @@ def main(root, batch, out=None):
     fetch = per_kernel(os.path.join(root, "FETCH_SIZE", "run_counter_collection.csv"))
     write = per_kernel(os.path.join(root, "WRITE_SIZE", "run_counter_collection.csv"))
     corr = sorted(k for k in fetch if "k_corr" in k)
-    # x2 for the 16-B/lane window loads (MI355X_MICROARCH.md:298); x1 for k_corr_rw's dword loads
-    scale = {k: (1 if "k_corr_rw" in k else 2) for k in corr}
+    # x2 for every read width the kernels use (MI355X_MICROARCH.md:298; profiles/r03/fetch_calib.json)
+    scale = {k: 2 for k in corr}
     f_kib = sum(scale[k] * fetch[k] for k in corr)
     w_kib = sum(write.get(k, 0.0) for k in corr)
     res = {
@@ -46,10 +47,9 @@ def main(root, batch, out=None):
         "write_bytes_per_launch": int(w_kib * 1024),
         "hbm_bytes_per_launch": int((f_kib + w_kib) * 1024),
         "hbm_bytes_per_frame": round((f_kib + w_kib) * 1024 / batch, 1),
-        "correction": {k: ("FETCH_SIZE as reported: 4-B/lane dword ring loads, a width MI355X_MICROARCH.md:300 "
-                           "leaves uncalibrated" if scale[k] == 1 else
-                           "FETCH_SIZE x2: 16-B/lane uint4 window loads, gfx950 tallies 128-B requests at 64 B "
-                           "(MI355X_MICROARCH.md:298)") for k in corr},
+        "correction": {k: "FETCH_SIZE x2: gfx950 tallies 128-B requests at 64 B (MI355X_MICROARCH.md:298); "
+                          "calibrated for the kernel's 4-B/lane and 16-B/lane loads in profiles/r03/fetch_calib.json"
+                       for k in corr},
         "write_correction": "WRITE_SIZE as reported",
         "all_kernels_kib_per_dispatch": {k: {"fetch": round(fetch[k], 1), "write": round(write.get(k, 0.0), 1)}
                                          for k in sorted(fetch)},

@@ -129,6 +129,60 @@ def test_wide_ring_widths(plan, unfused):
             assert np.array_equal(s.view(np.uint32), ref.scores(f + 1, det, s.shape).view(np.uint32)), (f, det)
 
 
+def _bright_tiles(cfg, frames):
+    """Bright 80 x 16 output tiles of the point detectors (some I_*_MOUSE
+    pixel > 25 after readFrame's subtract + NORM_MINMAX, :1304-1310) and the
+    outputs they hold, per view, summed over frames (identity calibration,
+    provided boxes, no flip: the mouse crop ends at the box's bottom-right
+    corner x + width, y + height (getBoundingBox :547-557, cropBoundingBox
+    :1422-1423), one pixel right of and below the box rectangle)."""
+    bk = cfg.background.astype(np.int32)
+    p = cfg.params
+    tiles, outs = [0, 0], [0, 0]
+    for fr in frames:
+        d = np.clip(fr.astype(np.int32) - bk, 0, 255)
+        mn, mx = int(d.min()), int(d.max())
+        scale = 255.0 / (mx - mn) if mx - mn > 2.220446049250313e-16 else 0.0
+        shift = -mn * scale
+        t = d.astype(np.float32) * np.float32(scale) + np.float32(shift)
+        n = np.clip(np.rint(t), 0, 255)
+        for v, r in enumerate((p.bounding_box_bottom, p.bounding_box_side)):
+            crop = n[r.y + 1:r.y + 1 + r.height, r.x + 1:r.x + 1 + r.width] > 25
+            for ty in range(0, r.height, 16):
+                for tx in range(0, r.width, 80):
+                    blk = crop[ty:ty + 16, tx:tx + 80]
+                    if blk.any():
+                        tiles[v] += 1
+                        outs[v] += blk.size
+    return tiles, outs
+
+
+@pytest.mark.parametrize("plan", [0, 1])
+def test_dark_tiles(plan, monkeypatch):
+    """The point detectors' dark output tiles (no mouse pixel > 25: the
+    reference zeroes all their scores, setTo(0, mask) :849, :864) are not
+    computed: results identical to the oracle with the skip on and off, on
+    the default scene and with blank frames (every tile dark), per-width and
+    merged launches; the bright-tile counts equal a numpy count."""
+    cfg = S.SyntheticConfig()
+    frames = np.concatenate([cfg.frames(30, 3), np.zeros_like(cfg.frames(0, 1)), cfg.frames(34, 3)])
+    ref = _oracle(cfg, frames).result
+    for dark in ("1", "0"):
+        monkeypatch.setenv("LM_CORR_DARK", dark)
+        ctx = _ctx(cfg, max_batch=len(frames))
+        ctx.set_debug(2 | (abi.LM_DEBUG_PLAN_MERGED if plan else abi.LM_DEBUG_PLAN_PER_WIDTH))
+        got = ctx.detect(frames, 0)
+        work = ctx.corr_work()
+        ctx.close()
+        assert_same(got, ref, f"dark={dark} plan {plan}: ")
+        if dark == "1":
+            tiles, outs = _bright_tiles(cfg, frames)
+            assert work == {"tiles": tuple(tiles), "outputs": tuple(outs)}, (work, tiles, outs)
+            assert tiles[0] < 45 * len(frames) and tiles[1] < 30 * len(frames)
+        else:
+            assert work is None
+
+
 @pytest.mark.parametrize("c5", [False, True])
 def test_dense_occlusion_grid(c5):
     """occlusion_grid_spacing_pixels_bottom = 5: 60 x 28 = 1,680 ONG nodes on
