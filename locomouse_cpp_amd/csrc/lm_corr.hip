@@ -1027,9 +1027,12 @@ __global__ __launch_bounds__(1024) void k_tilelist(const LmConst* __restrict__ K
   for (int c0 = 0; c0 < nproc; c0 += 1024) {
     const int i = c0 + (int)threadIdx.x;
     const uint8_t* __restrict__ f = flags + (int64_t)(s0 + i) * K.fl_slot + K.fl_off[v];
+    // the slot's flag bytes (0 / 1) as dwords: fl_slot and fl_off are multiples of 4
+    const unsigned* __restrict__ f4 = reinterpret_cast<const unsigned*>(f);
+    const int nw4 = (nt + 3) >> 2;
     int n = 0;
     if (i < nproc)
-      for (int t = 0; t < nt; ++t) n += f[t];
+      for (int w = 0; w < nw4; ++w) n += (int)((f4[w] * 0x01010101u) >> 24);  // k_tileflag writes every byte < nt; the pad stays 0
     // exclusive scan over the workgroup
     int incl = n;
 #pragma unroll
@@ -1044,12 +1047,16 @@ __global__ __launch_bounds__(1024) void k_tilelist(const LmConst* __restrict__ K
     for (int w = 0; w < wid; ++w) before += s_wave[w];
     int pos = before + incl - n;
     if (i < nproc)
-      for (int t = 0; t < nt; ++t)
-        if (f[t]) {
+      for (int w = 0; w < nw4; ++w) {
+        unsigned m = f4[w];
+        while (m) {
+          const int t = 4 * w + (__ffs(m) - 1) / 8;
+          m &= m - 1;
           out[pos++] = ((uint32_t)(s0 + i) << 16) | (uint32_t)t;
           const int ty = t / K.fl_tx[v], tx = t - ty * K.fl_tx[v];
           outs += min(LM_RW_TH, D.oh - ty * LM_RW_TH) * min(LM_TW, D.ow - tx * LM_TW);
         }
+      }
     __syncthreads();
     if (threadIdx.x == 1023) s_carry = before + incl;
   }

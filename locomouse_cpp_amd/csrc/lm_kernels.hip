@@ -192,11 +192,73 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 // is five aligned dword loads instead of sixteen byte loads.
 #define LM_INGEST_FB 8
 #define LM_INGEST_VEC 16
+
+// Gather indices and background bytes of the 16 crop pixels that start at
+// I_PAD (R, C0) (-1 / 0 outside I_UNPAD); returns 1 when idx[k] = idx[0] + k
+// for all k, -1 when idx[k] = idx[0] - k (a flipped translation), else 0, and
+// sets lo to the first source byte of such a run.
+DEV int ingest_locate(const LmConst& K, const int32_t* __restrict__ cal, const uint8_t* __restrict__ bkg, int R, int C0,
+                      int (&idx)[LM_INGEST_VEC], uint8_t (&bv)[LM_INGEST_VEC], int& lo) {
+  const int r = R - K.pad_pre_rows;
+  bool up = true, down = true;
+#pragma unroll
+  for (int k = 0; k < LM_INGEST_VEC; ++k) {
+    int c = C0 + k - K.pad_pre_cols;
+    if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) {
+      idx[k] = -1;
+      bv[k] = 0;
+    } else {
+      if (K.flip) c = K.n_cols - 1 - c;
+      idx[k] = cal[r * K.n_cols + c];
+      bv[k] = bkg[idx[k]];
+    }
+    up = up && idx[k] >= 0 && idx[k] == idx[0] + k;
+    down = down && idx[k] >= 0 && idx[k] == idx[0] - k;
+  }
+  int run = up ? 1 : (down ? -1 : 0);
+  lo = up ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
+  if (run != 0 && (lo & ~3) + 20 > K.video_rows * K.video_cols) run = 0;  // the fifth dword would pass the frame end
+  return run;
+}
+
+// Source map of one view's crop at a fixed position (cx, cy): per 16-byte
+// ext-crop chunk, {first source byte, run} and the 16 background bytes, so
+// k_ingest's batches with their crop there (always, with a provided bounding
+// box) skip the calibration and background gathers (frame-invariant data,
+// LocoMouse_class.cpp:1337-1406).  key[2 v], key[2 v + 1] = the position.
+__global__ __launch_bounds__(256) void k_srcmap(const LmConst* __restrict__ Kp, const int32_t* __restrict__ cal,
+                                                const uint8_t* __restrict__ bkg, int v, int cx, int cy,
+                                                int2* __restrict__ smap, uint4* __restrict__ sbkg,
+                                                int32_t* __restrict__ key) {
+  const LmConst& K = *Kp;
+  const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
+  const int64_t nv = (int64_t)K.ext_h[v] * K.ext_w[v];
+  const int64_t qq = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * LM_INGEST_VEC;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    key[2 * v] = cx;
+    key[2 * v + 1] = cy;
+  }
+  if (qq >= nv) return;
+  const int er = (int)(qq / K.ext_w[v]), ec = (int)(qq % K.ext_w[v]);
+  int idx[LM_INGEST_VEC];
+  uint8_t bv[LM_INGEST_VEC];
+  int lo;
+  const int run = ingest_locate(K, cal, bkg, cy + K.ext_oy[v] + er, cx + K.ext_ox[v] + ec, idx, bv, lo);
+  const int64_t ci = ((v ? e0 : 0) + qq) / LM_INGEST_VEC;
+  smap[ci] = make_int2(lo, run);
+  unsigned w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < LM_INGEST_VEC; ++k) w[k >> 2] |= (unsigned)bv[k] << (8 * (k & 3));
+  sbkg[ci] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
                                                 const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
                                                 const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
                                                 int s0, int s_end, uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
-                                                unsigned ext_blocks, unsigned* __restrict__ tailbm) {
+                                                unsigned ext_blocks, unsigned* __restrict__ tailbm,
+                                                const int2* __restrict__ smap, const uint4* __restrict__ sbkg,
+                                                const int32_t* __restrict__ skey) {
   const LmConst& K = *Kp;
   const int sb = s0 + blockIdx.y * LM_INGEST_FB;
   const int nf = min(LM_INGEST_FB, s_end - sb);
@@ -226,33 +288,17 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
   int idx[LM_INGEST_VEC];
   uint8_t bv[LM_INGEST_VEC];
   int run = 0;  // 1: idx[k] = idx[0] + k, -1: idx[k] = idx[0] - k, 0: gather
+  int lo = 0;   // a run's first source byte
+  bool allv = false;  // every pixel inside I_UNPAD (a run; idx[] not filled on the source-map path)
   // gather indices and background of this thread's 16 pixels for a crop at (cx, cy)
   auto locate = [&](int R, int C0) {
-    const int r = R - K.pad_pre_rows;
-    bool up = true, down = true;
-#pragma unroll
-    for (int k = 0; k < LM_INGEST_VEC; ++k) {
-      int c = C0 + k - K.pad_pre_cols;
-      if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) {
-        idx[k] = -1;
-        bv[k] = 0;
-      } else {
-        if (K.flip) c = K.n_cols - 1 - c;
-        idx[k] = cal[r * K.n_cols + c];
-        bv[k] = bkg[idx[k]];
-      }
-      up = up && idx[k] >= 0 && idx[k] == idx[0] + k;
-      down = down && idx[k] >= 0 && idx[k] == idx[0] - k;
-    }
-    run = up ? 1 : (down ? -1 : 0);
-    const int lo = up ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
-    if (run != 0 && (lo & ~3) + 20 > K.video_rows * K.video_cols) run = 0;  // the fifth dword would pass the frame end
+    run = ingest_locate(K, cal, bkg, R, C0, idx, bv, lo);
+    allv = false;
   };
   // the 16 source bytes of a run span [lo, lo + 16): five aligned dwords cover them
   // (funnel shifts by the byte offset, then a byte reversal for a flipped run:
   // no register array is indexed with a run-time value, so nothing spills)
   auto run_bytes = [&](const uint32_t (&d)[5], uint8_t (&pix)[LM_INGEST_VEC]) {
-    const int lo = run > 0 ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
     const unsigned sh = (unsigned)(lo & 3);
     uint32_t w[4];
 #pragma unroll
@@ -274,7 +320,7 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
 #pragma unroll
     for (int k = 0; k < LM_INGEST_VEC; ++k) {
       uint32_t o = 0;
-      if (idx[k] >= 0) {
+      if (allv || idx[k] >= 0) {
         o = lut[f][pix[k] > bv[k] ? pix[k] - bv[k] : 0];
         if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) o = glut[o];
       } else if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) {
@@ -294,9 +340,20 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
     same = same && slots[sb + f].crop_x[v] == sl0.crop_x[v] && slots[sb + f].crop_y[v] == sl0.crop_y[v];
   {
     const int R = sl0.crop_y[v] + K.ext_oy[v] + er, C0 = sl0.crop_x[v] + K.ext_ox[v] + ec;
-    locate(R, C0);
+    int2 m = make_int2(0, 0);
+    if (same && smap && skey[2 * v] == sl0.crop_x[v] && skey[2 * v + 1] == sl0.crop_y[v]) m = smap[q / LM_INGEST_VEC];
+    if (m.y != 0) {  // the source map holds this crop position: no calibration / background gathers
+      run = m.y;
+      lo = m.x;
+      allv = true;
+      const uint4 b4 = sbkg[q / LM_INGEST_VEC];
+      const unsigned bw[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int k = 0; k < LM_INGEST_VEC; ++k) bv[k] = (uint8_t)(bw[k >> 2] >> (8 * (k & 3)));
+    } else {
+      locate(R, C0);
+    }
     if (same && run != 0) {
-      const int lo = run > 0 ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
       uint32_t d[LM_INGEST_FB][5];
 #pragma unroll
       for (int f = 0; f < LM_INGEST_FB; ++f)
@@ -330,7 +387,6 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
     const lm_gu8* __restrict__ F = as_global(frame_ptr[slot]);
     uint8_t pix[LM_INGEST_VEC];
     if (run != 0) {
-      const int lo = run > 0 ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
       const lm_gu32* w = reinterpret_cast<const lm_gu32*>(F + (lo & ~3));
       uint32_t d[5];
 #pragma unroll
@@ -1025,11 +1081,18 @@ DEV void nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   if (!side) {
     // nmsMax: every point, suppressed or not, suppresses the later points it
     // overlaps (:1677-1720) => j belongs to the first i < j overlapping it;
-    // maxima by pointer jumping.
+    // maxima by pointer jumping.  Most points overlap one of the first few
+    // (the list is sorted by score, so a cluster's members follow its
+    // maximum); the points that do not -- the maxima, few -- would scan every
+    // earlier point alone.  So: (1) every j scans i < min(j, 64) with 4 x 16 B
+    // loads in flight and stops at its first hit; (2) the j still open
+    // (no hit, j > 64) are listed, and one wave per open j scans the rest
+    // 64 points at a time (ballot, first set lane).
+    constexpr int SCAN1 = 64;
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
       const unsigned xj = xy[j];
       int as = j;
-      for (int i0 = 0; i0 < j && as == j; i0 += 16) {  // 4 x 16 B loads in flight
+      for (int i0 = 0; i0 < min(j, SCAN1) && as == j; i0 += 16) {
         unsigned v[16];
         *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(xy + i0);
         *reinterpret_cast<uint4*>(v + 4) = *reinterpret_cast<const uint4*>(xy + i0 + 4);
@@ -1040,7 +1103,26 @@ DEV void nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
         for (int t = 0; t < 16; ++t) hit |= (unsigned)(i0 + t < j && overlaps_xy(v[t], xj, bw, bh)) << t;
         if (hit) as = i0 + __ffs(hit) - 1;
       }
-      assign[j] = as;
+      assign[j] = as == j && j > SCAN1 ? -1 : as;
+    }
+    __syncthreads();
+    {
+      const int nopen = block_compact(n, [&](int j) { return assign[j] < 0; }, mlist, s_wsum);
+      const int lane = threadIdx.x & 63;
+      for (int r = (int)(threadIdx.x >> 6); r < nopen; r += (int)(blockDim.x >> 6)) {
+        const int j = mlist[r];
+        const unsigned xj = xy[j];
+        int first = j;
+        for (int b = SCAN1; b < j; b += 64) {
+          const int i = b + lane;
+          const unsigned long long m = __ballot(i < j && overlaps_xy(xy[i], xj, bw, bh));
+          if (m) {
+            first = b + __ffsll((long long)m) - 1;
+            break;
+          }
+        }
+        if (lane == 0) assign[j] = first;
+      }
     }
     __syncthreads();
     NMS_PROF(4)
@@ -1798,66 +1880,90 @@ __global__ __launch_bounds__(256) void k_out(const LmPackHdr* __restrict__ ph, L
 // buffer: k_pack_scan computes every offset array (exclusive scans over the
 // frames) and the totals, k_pack_copy moves each (frame, feature)'s data.
 // Unit = one batch; a few KB per frame, launch-latency bound.
-template <class F>
-DEV int64_t block_exscan64(int L, F count, int64_t* out, int64_t* s_w) {
-  const int T = blockDim.x, chunk = (L + T - 1) / T;
-  const int i0 = threadIdx.x * chunk, i1 = min(L, i0 + chunk);
-  int64_t c = 0;
-  for (int i = i0; i < i1; ++i) c += count(i);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int64_t v = c;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int64_t u = __shfl_up(v, o);
-    if (lane >= o) v += u;
-  }
-  if (lane == 63) s_w[wid] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int64_t acc = 0;
-    for (int w = 0; w < (T >> 6); ++w) {
-      const int64_t t = s_w[w];
-      s_w[w] = acc;
-      acc += t;
-    }
-    s_w[T >> 6] = acc;
-  }
-  __syncthreads();
-  int64_t r = s_w[wid] + v - c;
-  for (int i = i0; i < i1; ++i) {
-    out[i] = r;
-    r += count(i);
-  }
-  const int64_t total = s_w[T >> 6];
-  if (threadIdx.x == 0) out[L] = total;
-  __syncthreads();
-  return total;
-}
-
+// All six offset arrays in one pass: each thread takes a contiguous run of
+// frames, sums its frames' counts per array, one block-wide exclusive scan of
+// the six sums (one pair of barriers instead of six), then the thread writes
+// its frames' per-list offsets.  (Six scans one after the other cost six
+// dependent load + barrier rounds: ~19 us per batch, launch-latency bound.)
 __global__ __launch_bounds__(1024) void k_pack_scan(const LmSlotOut* __restrict__ hdr, int n,
                                                     const LmArenaCtl* __restrict__ ctl, const int32_t* __restrict__ err,
                                                     LmPackHdr* __restrict__ ph, uint8_t* __restrict__ pack, int64_t pack_cap,
                                                     int64_t* __restrict__ side_base) {
-  __shared__ int64_t s_w[1024 / 64 + 1];
+  constexpr int NA = 6;  // cand, p22d, unary, jc, nz, side
+  __shared__ int64_t s_w[1024 / 64 + 1][NA];
   const int64_t zero[PK_COUNT] = {0, 0, 0, 0, 0, 0};
   const LmPackLayout L0 = lm_pack_layout(n, zero);  // offset arrays do not depend on the totals
   const LmSlotOut* H = hdr + 1;
-  int64_t tot[PK_COUNT];
-  tot[PK_CAND] = block_exscan64(4 * n, [&](int i) { return (int64_t)H[i >> 2].cand_cnt[i & 3]; },
-                                reinterpret_cast<int64_t*>(pack + L0.cand_off), s_w);
-  tot[PK_P22D] = block_exscan64(2 * n, [&](int i) { return (int64_t)H[i >> 1].p22d_cnt[i & 1]; },
-                                reinterpret_cast<int64_t*>(pack + L0.p22d_off), s_w);
-  tot[PK_UNARY] = block_exscan64(2 * n, [&](int i) { return (int64_t)H[i >> 1].unary_cnt[i & 1]; },
-                                 reinterpret_cast<int64_t*>(pack + L0.unary_off), s_w);
-  tot[PK_JC] = block_exscan64(2 * n, [&](int i) {
-    const LmSlotOut& h = H[i >> 1];
-    return h.pw_rows[i & 1] >= 0 ? (int64_t)h.pw_cols[i & 1] + 1 : (int64_t)0;
-  }, reinterpret_cast<int64_t*>(pack + L0.jc_off), s_w);
-  tot[PK_NZ] = block_exscan64(2 * n, [&](int i) {
-    const LmSlotOut& h = H[i >> 1];
-    return h.pw_rows[i & 1] >= 0 ? (int64_t)h.pw_nnz[i & 1] : (int64_t)0;
-  }, reinterpret_cast<int64_t*>(pack + L0.nz_off), s_w);
-  tot[PK_SIDE] = block_exscan64(2 * n, [&](int i) { return (int64_t)H[i >> 1].side_cnt[i & 1]; }, side_base, s_w);
+  int64_t* outs[NA] = {reinterpret_cast<int64_t*>(pack + L0.cand_off), reinterpret_cast<int64_t*>(pack + L0.p22d_off),
+                       reinterpret_cast<int64_t*>(pack + L0.unary_off), reinterpret_cast<int64_t*>(pack + L0.jc_off),
+                       reinterpret_cast<int64_t*>(pack + L0.nz_off), side_base};
+  const int per[NA] = {4, 2, 2, 2, 2, 2};  // entries per frame
+  // count of array a, entry j of frame f
+  auto count = [&](const LmSlotOut& h, int a, int j) -> int64_t {
+    switch (a) {
+      case 0: return h.cand_cnt[j];
+      case 1: return h.p22d_cnt[j];
+      case 2: return h.unary_cnt[j];
+      case 3: return h.pw_rows[j] >= 0 ? (int64_t)h.pw_cols[j] + 1 : 0;
+      case 4: return h.pw_rows[j] >= 0 ? (int64_t)h.pw_nnz[j] : 0;
+      default: return h.side_cnt[j];
+    }
+  };
+  const int T = blockDim.x, chunk = (n + T - 1) / T;
+  const int f0 = threadIdx.x * chunk, f1 = min(n, f0 + chunk);
+  int64_t c[NA] = {0, 0, 0, 0, 0, 0};
+  for (int f = f0; f < f1; ++f) {
+    const LmSlotOut& h = H[f];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      for (int j = 0; j < per[a]; ++j) c[a] += count(h, a, j);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t v[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) {
+    v[a] = c[a];
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t u = __shfl_up(v[a], o);
+      if (lane >= o) v[a] += u;
+    }
+  }
+  if (lane == 63)
+#pragma unroll
+    for (int a = 0; a < NA; ++a) s_w[wid][a] = v[a];
+  __syncthreads();
+  if (threadIdx.x < NA) {
+    const int a = threadIdx.x;
+    int64_t acc = 0;
+    for (int w = 0; w < (T >> 6); ++w) {
+      const int64_t t = s_w[w][a];
+      s_w[w][a] = acc;
+      acc += t;
+    }
+    s_w[T >> 6][a] = acc;
+  }
+  __syncthreads();
+  int64_t r[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) r[a] = s_w[wid][a] + v[a] - c[a];
+  for (int f = f0; f < f1; ++f) {
+    const LmSlotOut& h = H[f];
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      for (int j = 0; j < per[a]; ++j) {
+        outs[a][per[a] * f + j] = r[a];
+        r[a] += count(h, a, j);
+      }
+  }
+  if (threadIdx.x < NA) outs[threadIdx.x][per[threadIdx.x] * n] = s_w[T >> 6][threadIdx.x];
   if (threadIdx.x == 0) {
+    int64_t tot[PK_COUNT];
+    tot[PK_CAND] = s_w[T >> 6][0];
+    tot[PK_P22D] = s_w[T >> 6][1];
+    tot[PK_UNARY] = s_w[T >> 6][2];
+    tot[PK_JC] = s_w[T >> 6][3];
+    tot[PK_NZ] = s_w[T >> 6][4];
+    tot[PK_SIDE] = s_w[T >> 6][5];
     const LmPackLayout L = lm_pack_layout(n, tot);
     for (int k = 0; k < PK_COUNT; ++k) ph->tot[k] = tot[k];
     ph->bytes = L.bytes;

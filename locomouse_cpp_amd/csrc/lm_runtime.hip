@@ -98,6 +98,11 @@ struct Lane {
   DevBuf<const uint8_t*> frame_ptr;
   DevBuf<LmSlot> slots;
   DevBuf<unsigned long long> keys, gscratch;
+  // k_ingest's source map (k_srcmap) for the crop position skey_h (per view)
+  DevBuf<int2> smap;
+  DevBuf<uint4> sbkg;
+  DevBuf<int32_t> skey;
+  int skey_h[4] = {-1, -1, -1, -1};
   DevBuf<uint8_t> dark_flags;  // dark tiles (CorrDark): flag bytes, bright-tile lists and counts
   DevBuf<uint32_t> dark_list;
   DevBuf<int32_t> dark_cnt;
@@ -696,8 +701,16 @@ void lane_alloc(lm_ctx* c, Lane& L) {
   if (c->tail_big) L.tail_ws.alloc((size_t)c->tail_ws_slot * ns);
   L.keys.alloc((size_t)K.keys_per_slot * ns);
   L.npos.alloc((size_t)LM_NLIST * ns);
+  {
+    const int64_t nchunks = ((int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1]) / LM_INGEST_VEC;
+    L.smap.alloc((size_t)nchunks);
+    L.sbkg.alloc((size_t)nchunks);
+    L.skey.alloc(4);
+    SET_SYNC(L.skey.p, 0x80, 4 * sizeof(int32_t), st);  // no position: every k_ingest locates until k_srcmap ran
+  }
   if (c->dark_on) {
     L.dark_flags.alloc((size_t)K.fl_slot * ns);
+    SET_SYNC(L.dark_flags.p, 0, (size_t)K.fl_slot * ns, st);  // the pad bytes after each view's flags stay 0
     L.dark_list.alloc((size_t)2 * K.tl_stride);
     L.dark_cnt.alloc(4);
   }
@@ -982,7 +995,7 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
     const unsigned zero_blocks = (unsigned)((K.tail_bm_words + 4 * 256 - 1) / (4 * 256));  // the tail bitmaps
     k_ingest<<<dim3(ext_blocks + zero_blocks, (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)), 256, 0, st>>>(
         dK, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, L.slots.p, s_proc0, n + 1, L.ext.p, c->ext_slot_bytes,
-        ext_blocks, reinterpret_cast<unsigned*>(L.tailbin.p));
+        ext_blocks, reinterpret_cast<unsigned*>(L.tailbin.p), L.smap.p, L.sbkg.p, L.skey.p);
     T.end();
     if (c->dark_on) {
       T.begin("k_tiles");
@@ -1310,6 +1323,22 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
     HIPCHK(hipEventRecord(L.ev_consumed, st));
   }
   if (!L.gscratch.p) L.gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
+  // k_ingest's source map: rebuilt for a view when every processed slot has
+  // its crop at one position that the lane's map does not hold
+  for (int v = 0; v < 2; ++v) {
+    const LmSlot& S0 = L.h_slots.p[s_proc0];
+    bool uni = true;
+    for (int s = s_proc0 + 1; s <= n && uni; ++s)
+      uni = L.h_slots.p[s].crop_x[v] == S0.crop_x[v] && L.h_slots.p[s].crop_y[v] == S0.crop_y[v];
+    if (uni && (L.skey_h[2 * v] != S0.crop_x[v] || L.skey_h[2 * v + 1] != S0.crop_y[v])) {
+      const int64_t nv = (int64_t)K.ext_h[v] * K.ext_w[v] / LM_INGEST_VEC;
+      k_srcmap<<<(unsigned)((nv + 255) / 256), 256, 0, st>>>(c->dK.p, c->cal.p, c->bkg.p, v, S0.crop_x[v], S0.crop_y[v],
+                                                            L.smap.p, L.sbkg.p, L.skey.p);
+      HIPCHK(hipGetLastError());
+      L.skey_h[2 * v] = S0.crop_x[v];
+      L.skey_h[2 * v + 1] = S0.crop_y[v];
+    }
+  }
 
   Lane::Pending& P = L.pend;
   P.on = true;
