@@ -773,6 +773,48 @@ DEV void rank_sort(unsigned long long* a, unsigned long long* tmp, int n) {
   __syncthreads();
 }
 
+// ascending sort of n <= blockDim.x DISTINCT keys (< ~0): every wave sorts
+// its 64 keys in registers (bitonic network over lane shuffles), the sorted
+// runs go back to a, and each key's position is its index in its run plus,
+// for every other run, the count of smaller keys there (binary searches, the
+// runs' probes interleaved).  A few shuffle and LDS latencies per step instead
+// of rank_sort's n / 8 rounds of loads per key.  tmp holds n keys.
+static_assert(LM_NMS_THREADS == 512, "wave_merge_sort: 8 runs of 64");
+DEV void wave_merge_sort(unsigned long long* a, unsigned long long* tmp, int n) {
+  const int t = threadIdx.x, lane = t & 63, run = t >> 6, nruns = (n + 63) >> 6;
+  unsigned long long v = t < n ? a[t] : ~0ull;
+  if (run < nruns) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const unsigned long long p = __shfl_xor(v, j);
+        const bool keep_min = ((lane & j) == 0) == ((lane & k) == 0);
+        v = keep_min ? (v < p ? v : p) : (v < p ? p : v);
+      }
+  }
+  __syncthreads();  // every key of a has been read
+  if (run < nruns) a[t] = v;  // sorted runs, padded with ~0 past n
+  __syncthreads();
+  if (t < n) {
+    int lo[8], rank = lane;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) lo[r] = 0;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1)
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (r < nruns && r != run && a[r * 64 + lo[r] + s - 1] < v) lo[r] += s;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      if (r < nruns && r != run) rank += lo[r] + (a[r * 64 + lo[r]] < v ? 1 : 0);
+    tmp[rank] = v;
+  }
+  __syncthreads();
+  for (int k = t; k < n; k += blockDim.x) a[k] = tmp[k];
+  __syncthreads();
+}
+
 struct ReplicaLess {  // compareCandidate on (idx << 32 | score bits) words
   DEV bool operator()(unsigned long long a, unsigned long long b) const {
     return __uint_as_float((unsigned)(a & 0xFFFFFFFFu)) > __uint_as_float((unsigned)(b & 0xFFFFFFFFu));
@@ -988,11 +1030,12 @@ DEV double readlane_f64(double v, int lane) {
 #define NMS_PROF(k) \
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = clock64();
 template <bool GLOB>
-DEV void nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int list, int side, int feat, int n_in,
+DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int list, int side, int feat, int n_in,
                  const unsigned long long* __restrict__ src, const unsigned long long* __restrict__ tailmask,
-                 unsigned long long* a, int* assign, int* mlist, unsigned* xy, int* s_tmp, int* s_stk, int* s_wsum,
+                 unsigned long long* a, int* assign, int* mlist, unsigned* xy, int* s_tmp, unsigned long long* stmp,
+                 int qcap, int* s_stk, int* s_wsum,
                  int* s_n_, int* s_flag_, int* s_qcnt, unsigned long long* __restrict__ keys, int32_t* __restrict__ err,
-                 long long* __restrict__ prof) {
+                 long long* __restrict__ prof) -> int {
   int& s_n = *s_n_;
   int& s_flag = *s_flag_;
   constexpr bool glob = GLOB;
@@ -1023,8 +1066,10 @@ DEV void nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 13] = n;
   int np = 1;
   while (np < n) np <<= 1;
-  if (n <= LM_NMS_RANKSORT) {
-    rank_sort(a, reinterpret_cast<unsigned long long*>(s_assign), n);  // s_assign: 8 KB = 1024 keys
+  if (!glob && n <= LM_NMS_THREADS) {
+    wave_merge_sort(a, stmp, n);
+  } else if (n <= LM_NMS_RANKSORT) {
+    rank_sort(a, stmp, n);
   } else {
     for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
     __syncthreads();
@@ -1047,14 +1092,16 @@ DEV void nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
     // garbage candidates in rare tie blocks
     __syncthreads();
     if (!glob) {
-      if (n <= LM_NMS_RANKSORT) {  // back to row-major order
-        rank_sort(a, reinterpret_cast<unsigned long long*>(s_assign), n);
+      if (n <= LM_NMS_THREADS) {  // back to row-major order
+        wave_merge_sort(a, stmp, n);
+      } else if (n <= LM_NMS_RANKSORT) {
+        rank_sort(a, stmp, n);
       } else {
         for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
         __syncthreads();
         bitonic_sort(a, np);
       }
-      std_sort_levels_dev(a, n, s_mlist, LM_NMS_CAP / 6, s_assign, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt);
+      std_sort_levels_dev(a, n, s_mlist, qcap, s_assign, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt);
     } else {  // rare and slow: one thread, explicit stack
       for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
       __syncthreads();
@@ -1229,54 +1276,82 @@ DEV void nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
     H->cand_cnt[list] = fits ? ncand : 0;
     H->ties[list] = tie;
   }
+  return fits ? ncand : 0;
 }
 
-// Two instantiations on the same grid, launched back to back: <false> for
-// lists of at most LM_NMS_CAP positives (LDS), <true> for longer ones.
+// One block per (slot, feature) runs the bottom list (nmsMax) and then, for
+// the batch's frames, the side list (peakClustering), which
+// detectSideCandidates skips when the bottom list came out empty (:820-833):
+// no kernel boundary between the two, so a frame's side list does not wait
+// for the slowest bottom block of the batch.  <false>: lists of at most
+// LM_NMS_CAP positives, in LDS.  <true>: the pairs with a longer bottom list
+// (both lists), or a longer side list behind a non-empty bottom one, in
+// global scratch (for_overflow_pairs, launched after <false>).
 template <bool GLOB>
-DEV void nms_block(int bx, int feat, const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
+DEV void nms_block(int bx, int feat, const LmConst* __restrict__ Kp, int s0, unsigned long long* __restrict__ keys,
                    const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
                    unsigned long long* __restrict__ gscratch, int64_t gscratch_slot, LmSlotOut* __restrict__ hdr,
-                   int32_t* __restrict__ err, long long* __restrict__ prof) {
+                   int32_t* __restrict__ err, long long* __restrict__ prof_b, long long* __restrict__ prof_s) {
+  constexpr int ACAP = GLOB ? 1 : LM_NMS_CAP;  // LDS array sizes
   const LmConst& K = *Kp;
   const int slot = s0 + bx;  // feat: 0 paw, 1 snout
-  NMS_PROF(0)
-  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 14] = wall_clock64();
-  const int list = side ? 2 + feat : feat;
-  const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
-  const LmDet D = K.det[det];
   LmSlotOut* H = hdr + slot;
-  // 16-byte aligned: rank_sort and the nmsMax sweep read them with ds_read_b128
-  __shared__ __attribute__((aligned(16))) unsigned long long s_keys[LM_NMS_CAP];
-  __shared__ __attribute__((aligned(16))) int s_assign[LM_NMS_CAP];
-  __shared__ int s_mlist[LM_NMS_CAP];
-  __shared__ __attribute__((aligned(16))) unsigned s_xy[LM_NMS_CAP + 16];
+  // 16-byte aligned: the sorts and the nmsMax sweep read them with ds_read_b128
+  __shared__ __attribute__((aligned(16))) unsigned long long s_keys[ACAP];
+  __shared__ __attribute__((aligned(16))) int s_assign[ACAP];
+  __shared__ int s_mlist[ACAP];
+  __shared__ __attribute__((aligned(16))) unsigned s_xy[ACAP + 16];
   __shared__ int s_tmp[LM_NMS_CAP];
-  __shared__ int s_stk[lm_sort::kStackInts];
+  __shared__ int s_stk[GLOB ? lm_sort::kStackInts : 1];
   __shared__ int s_wsum[LM_NMS_THREADS / 64 + 1];
   __shared__ int s_n, s_flag, s_qcnt[2];
-
-  if (side && H->cand_cnt[feat] == 0) {  // detectSideCandidates skips (:820-833)
-    if (!GLOB && threadIdx.x == 0) {
-      H->n_pos[list] = 0;
-      H->cand_cnt[list] = 0;
-      H->ties[list] = 0;
+  static_assert(LM_NMS_RANKSORT * 8 <= LM_NMS_CAP * 4, "s_assign holds the sorts' keys");
+  const int64_t npg = gscratch_slot / 3;
+  unsigned long long* ga = gscratch + (int64_t)(feat + 2 * bx) * gscratch_slot;
+  int* gassign = reinterpret_cast<int*>(ga + npg);
+  int* gmlist = gassign + npg;
+  // one list (side 0: bottom, 1: side) of this (slot, feature): returns its candidate count
+  auto run = [&](int side, int n_in, long long* prof) -> int {
+    const int list = side ? 2 + feat : feat;
+    const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
+    const LmDet D = K.det[det];
+    NMS_PROF(0)
+    if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 14] = wall_clock64();
+    const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
+    int c;
+    if constexpr (!GLOB)
+      c = nms_run<false>(K, D, H, slot, list, side, feat, n_in, src, tailmask, s_keys, s_assign, s_mlist, s_xy, s_tmp,
+                         reinterpret_cast<unsigned long long*>(s_assign), LM_NMS_CAP / 6, s_stk, s_wsum, &s_n, &s_flag,
+                         s_qcnt, keys, err, prof);
+    else
+      c = nms_run<true>(K, D, H, slot, list, side, feat, n_in, src, tailmask, ga, gassign, gmlist,
+                        reinterpret_cast<unsigned*>(gmlist + npg), s_tmp, reinterpret_cast<unsigned long long*>(gassign), 0,
+                        s_stk, s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
+    __syncthreads();  // the next list reuses the block's arrays
+    return c;
+  };
+  auto skip_side = [&]() {  // detectSideCandidates not run: an empty side list
+    if (threadIdx.x == 0) {
+      H->n_pos[2 + feat] = 0;
+      H->cand_cnt[2 + feat] = 0;
+      H->ties[2 + feat] = 0;
     }
-    return;
-  }
-  const int n_in = n_pos[slot * LM_NLIST + list];
-  const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
-  if ((n_in > LM_NMS_CAP) != GLOB) return;  // the other instantiation's block
-  if constexpr (!GLOB)
-    nms_run<false>(K, D, H, slot, list, side, feat, n_in, src, tailmask, s_keys, s_assign, s_mlist, s_xy, s_tmp, s_stk,
-                   s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
-  else {  // rare: most of the crop positive; same algorithm in global scratch
-    const int64_t npg = gscratch_slot / 3;
-    unsigned long long* a = gscratch + (int64_t)(feat + 2 * bx) * gscratch_slot;
-    int* assign = reinterpret_cast<int*>(a + npg);
-    int* mlist = assign + npg;
-    nms_run<true>(K, D, H, slot, list, side, feat, n_in, src, tailmask, a, assign, mlist,
-                  reinterpret_cast<unsigned*>(mlist + npg), s_tmp, s_stk, s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
+  };
+  const int n_b = n_pos[slot * LM_NLIST + feat];
+  const int n_s = slot >= 1 ? n_pos[slot * LM_NLIST + 2 + feat] : 0;
+  if constexpr (!GLOB) {
+    if (n_b > LM_NMS_CAP) return;  // both lists go to <true>
+    const int cb = run(0, n_b, prof_b);
+    if (slot < 1) return;  // the previous frame (halo slot): bottom list only
+    if (cb == 0) skip_side();
+    else if (n_s <= LM_NMS_CAP) run(1, n_s, prof_s);
+  } else {
+    int cb;
+    if (n_b > LM_NMS_CAP) cb = run(0, n_b, nullptr);
+    else cb = H->cand_cnt[feat];  // written by <false> (an earlier launch)
+    if (slot < 1) return;
+    if (cb == 0) skip_side();
+    else if (n_b > LM_NMS_CAP || n_s > LM_NMS_CAP) run(1, n_s, nullptr);
   }
 }
 
@@ -1315,22 +1390,26 @@ DEV void for_overflow_pairs(int npairs, Pred overflow, Fn fn) {
     if (pp_) pp_[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = (k) >= 14 ? wall_clock64() : clock64(); \
   }
 template <bool GLOB>
-__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, int side, unsigned long long* __restrict__ keys,
+__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, unsigned long long* __restrict__ keys,
                                                        const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
                                                        unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
                                                        LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
-                                                       long long* __restrict__ prof, int npairs) {
+                                                       long long* __restrict__ prof_b, long long* __restrict__ prof_s,
+                                                       int npairs) {
   if constexpr (!GLOB)
-    nms_block<false>(blockIdx.x, blockIdx.y, Kp, s0, side, keys, n_pos, tailmask, gscratch, gscratch_slot, hdr, err, prof);
+    nms_block<false>(blockIdx.x, blockIdx.y, Kp, s0, keys, n_pos, tailmask, gscratch, gscratch_slot, hdr, err, prof_b,
+                     prof_s);
   else
     for_overflow_pairs(
         npairs,
         [&](int p) {
-          const int slot = s0 + (p >> 1), feat = p & 1, list = side ? 2 + feat : feat;
-          return !(side && hdr[slot].cand_cnt[feat] == 0) && n_pos[slot * LM_NLIST + list] > LM_NMS_CAP;
+          const int slot = s0 + (p >> 1), feat = p & 1;
+          const int n_b = n_pos[slot * LM_NLIST + feat], n_s = n_pos[slot * LM_NLIST + 2 + feat];
+          return n_b > LM_NMS_CAP || (slot >= 1 && n_s > LM_NMS_CAP && hdr[slot].cand_cnt[feat] > 0);
         },
         [&](int p) {
-          nms_block<true>(p >> 1, p & 1, Kp, s0, side, keys, n_pos, tailmask, gscratch, gscratch_slot, hdr, err, nullptr);
+          nms_block<true>(p >> 1, p & 1, Kp, s0, keys, n_pos, tailmask, gscratch, gscratch_slot, hdr, err, nullptr,
+                          nullptr);
         });
 #undef NMS_PROF
 }
@@ -1956,6 +2035,15 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const LmSlotOut* __restrict_
       }
   }
   if (threadIdx.x < NA) outs[threadIdx.x][per[threadIdx.x] * n] = s_w[T >> 6][threadIdx.x];
+  // the sub-arena counts, one load per thread (a serial loop over them by one
+  // thread waited out 6 x 16 dependent L2 round trips)
+  __shared__ int s_sub[AR_COUNT][LM_SUBARENA];
+  const int nparts = ctl->nparts;
+  if (threadIdx.x < AR_COUNT * LM_SUBARENA) {
+    const int k = threadIdx.x / LM_SUBARENA, g = threadIdx.x % LM_SUBARENA;
+    s_sub[k][g] = g < nparts ? ctl->sub[g][k] : 0;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     int64_t tot[PK_COUNT];
     tot[PK_CAND] = s_w[T >> 6][0];
@@ -1971,8 +2059,8 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const LmSlotOut* __restrict_
     ph->err = *err;
     for (int k = 0; k < AR_COUNT; ++k) {
       int m = 0;
-      for (int g = 0; g < ctl->nparts; ++g) m = max(m, ctl->sub[g][k]);
-      ph->used[k] = m * ctl->nparts;
+      for (int g = 0; g < LM_SUBARENA; ++g) m = max(m, s_sub[k][g]);
+      ph->used[k] = m * nparts;
     }
   }
 }

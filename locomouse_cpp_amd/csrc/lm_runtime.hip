@@ -1043,18 +1043,12 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
       k_tail<false><<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes,
                                                                  L.tailmask.p, L.tscratch.p, A.hdr.p, kp2, nullptr, 0);
     T.end();
-    T.begin("k_nms_bottom");
-    // each list goes to one of the two instantiations (LDS / global scratch)
-    k_nms<false><<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, L.keys.p, L.npos.p, L.tailmask.p,
-                                                           L.gscratch.p, c->gscratch_slot, A.hdr.p, L.err.p, kp0, 0);
-    k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, s_proc0, 0, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
-                                              c->gscratch_slot, A.hdr.p, L.err.p, nullptr, 2 * nproc);
-    T.end();
-    T.begin("k_nms_side");
-    k_nms<false><<<dim3(n, 2), LM_NMS_THREADS, 0, st>>>(dK, 1, 1, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
-                                                       c->gscratch_slot, A.hdr.p, L.err.p, kp1, 0);
-    k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, 1, 1, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
-                                              c->gscratch_slot, A.hdr.p, L.err.p, nullptr, 2 * n);
+    T.begin("k_nms");
+    // bottom then side lists per (slot, feature); lists beyond the LDS capacity in global scratch
+    k_nms<false><<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
+                                                           c->gscratch_slot, A.hdr.p, L.err.p, kp0, kp1, 0);
+    k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, s_proc0, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
+                                              c->gscratch_slot, A.hdr.p, L.err.p, nullptr, nullptr, 2 * nproc);
     T.end();
     T.begin("k_post");
     k_post<false><<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, L.slots.p, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p,
