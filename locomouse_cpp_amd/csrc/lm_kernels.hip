@@ -1091,6 +1091,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
     // ranked among new-format ones -- duplicate ranks, unwritten slots, and
     // garbage candidates in rare tie blocks
     __syncthreads();
+    NMS_PROF(8)
     if (!glob) {
       if (n <= LM_NMS_THREADS) {  // back to row-major order
         wave_merge_sort(a, stmp, n);
@@ -1101,7 +1102,9 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
         __syncthreads();
         bitonic_sort(a, np);
       }
+      NMS_PROF(9)
       std_sort_levels_dev(a, n, s_mlist, qcap, s_assign, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt);
+      NMS_PROF(10)
     } else {  // rare and slow: one thread, explicit stack
       for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
       __syncthreads();
@@ -1128,18 +1131,17 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   if (!side) {
     // nmsMax: every point, suppressed or not, suppresses the later points it
     // overlaps (:1677-1720) => j belongs to the first i < j overlapping it;
-    // maxima by pointer jumping.  Most points overlap one of the first few
-    // (the list is sorted by score, so a cluster's members follow its
-    // maximum); the points that do not -- the maxima, few -- would scan every
-    // earlier point alone.  So: (1) every j scans i < min(j, 64) with 4 x 16 B
-    // loads in flight and stops at its first hit; (2) the j still open
-    // (no hit, j > 64) are listed, and one wave per open j scans the rest
-    // 64 points at a time (ballot, first set lane).
-    constexpr int SCAN1 = 64;
+    // maxima by pointer jumping.  Each j scans the earlier points 16 at a
+    // time (4 x 16 B loads in flight) and stops at its first hit: a cluster's
+    // points follow its maximum in score order, so most scans end early.
+    // (Tried and slower on ~300-point lists: a two-stage scan with one wave
+    // per unresolved point, 30k vs 25k cycles; x-window and x-bucket scans
+    // over a second sort, 80k / 36k: the points of the paw clusters share
+    // their x ranges, profiles/r03/h, /i.)
     for (int j = threadIdx.x; j < n; j += blockDim.x) {
       const unsigned xj = xy[j];
       int as = j;
-      for (int i0 = 0; i0 < min(j, SCAN1) && as == j; i0 += 16) {
+      for (int i0 = 0; i0 < j && as == j; i0 += 16) {
         unsigned v[16];
         *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(xy + i0);
         *reinterpret_cast<uint4*>(v + 4) = *reinterpret_cast<const uint4*>(xy + i0 + 4);
@@ -1150,26 +1152,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
         for (int t = 0; t < 16; ++t) hit |= (unsigned)(i0 + t < j && overlaps_xy(v[t], xj, bw, bh)) << t;
         if (hit) as = i0 + __ffs(hit) - 1;
       }
-      assign[j] = as == j && j > SCAN1 ? -1 : as;
-    }
-    __syncthreads();
-    {
-      const int nopen = block_compact(n, [&](int j) { return assign[j] < 0; }, mlist, s_wsum);
-      const int lane = threadIdx.x & 63;
-      for (int r = (int)(threadIdx.x >> 6); r < nopen; r += (int)(blockDim.x >> 6)) {
-        const int j = mlist[r];
-        const unsigned xj = xy[j];
-        int first = j;
-        for (int b = SCAN1; b < j; b += 64) {
-          const int i = b + lane;
-          const unsigned long long m = __ballot(i < j && overlaps_xy(xy[i], xj, bw, bh));
-          if (m) {
-            first = b + __ffsll((long long)m) - 1;
-            break;
-          }
-        }
-        if (lane == 0) assign[j] = first;
-      }
+      assign[j] = as;
     }
     __syncthreads();
     NMS_PROF(4)

@@ -884,7 +884,7 @@ void kprof_report(lm_ctx* c, Lane& L, int n) {
       const long long* t = h.data() + (size_t)side * 16 * 2 * c->nslots + (size_t)b * 16;
       long long last = t[0];
       if (!last) continue;
-      for (int k = 1; k < 13; ++k)
+      for (int k = 1; k < 8; ++k)  // phases 1-7 (8-10: the tie re-sort inside phase 2, in the slowest-block lines)
         if (t[k]) {
           acc[k] += (double)(t[k] - last);
           ++cnt[k];
@@ -912,7 +912,7 @@ void kprof_report(lm_ctx* c, Lane& L, int n) {
       for (size_t i = 0; i < lv.size() && i < 6; ++i) {
         const long long* t = h.data() + (size_t)side * 16 * 2 * c->nslots + (size_t)lv[i].second * 16;
         fprintf(stderr, " [blk %d n=%lld %.1fus cyc=%lld:", lv[i].second, t[13], lv[i].first * 0.01, t[7] - t[0]);
-        for (int k = 1; k <= 7; ++k) fprintf(stderr, " %lld", t[k] ? t[k] - t[0] : -1);
+        for (int k = 1; k <= 10; ++k) fprintf(stderr, " %lld", t[k] ? t[k] - t[0] : -1);
         fprintf(stderr, "]");
       }
       fprintf(stderr, "\n");
