@@ -198,19 +198,20 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 // for all k, -1 when idx[k] = idx[0] - k (a flipped translation), else 0, and
 // sets lo to the first source byte of such a run.
 DEV int ingest_locate(const LmConst& K, const int32_t* __restrict__ cal, const uint8_t* __restrict__ bkg, int R, int C0,
-                      int (&idx)[LM_INGEST_VEC], uint8_t (&bv)[LM_INGEST_VEC], int& lo) {
+                      int (&idx)[LM_INGEST_VEC], uint32_t (&bw)[4], int& lo) {
   const int r = R - K.pad_pre_rows;
   bool up = true, down = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bw[j] = 0u;
 #pragma unroll
   for (int k = 0; k < LM_INGEST_VEC; ++k) {
     int c = C0 + k - K.pad_pre_cols;
     if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) {
       idx[k] = -1;
-      bv[k] = 0;
     } else {
       if (K.flip) c = K.n_cols - 1 - c;
       idx[k] = cal[r * K.n_cols + c];
-      bv[k] = bkg[idx[k]];
+      bw[k >> 2] |= (uint32_t)bkg[idx[k]] << (8 * (k & 3));
     }
     up = up && idx[k] >= 0 && idx[k] == idx[0] + k;
     down = down && idx[k] >= 0 && idx[k] == idx[0] - k;
@@ -241,14 +242,11 @@ __global__ __launch_bounds__(256) void k_srcmap(const LmConst* __restrict__ Kp, 
   if (qq >= nv) return;
   const int er = (int)(qq / K.ext_w[v]), ec = (int)(qq % K.ext_w[v]);
   int idx[LM_INGEST_VEC];
-  uint8_t bv[LM_INGEST_VEC];
+  uint32_t w[4];
   int lo;
-  const int run = ingest_locate(K, cal, bkg, cy + K.ext_oy[v] + er, cx + K.ext_ox[v] + ec, idx, bv, lo);
+  const int run = ingest_locate(K, cal, bkg, cy + K.ext_oy[v] + er, cx + K.ext_ox[v] + ec, idx, w, lo);
   const int64_t ci = ((v ? e0 : 0) + qq) / LM_INGEST_VEC;
   smap[ci] = make_int2(lo, run);
-  unsigned w[4] = {0, 0, 0, 0};
-#pragma unroll
-  for (int k = 0; k < LM_INGEST_VEC; ++k) w[k >> 2] |= (unsigned)bv[k] << (8 * (k & 3));
   sbkg[ci] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
@@ -262,47 +260,78 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
   const LmConst& K = *Kp;
   const int sb = s0 + blockIdx.y * LM_INGEST_FB;
   const int nf = min(LM_INGEST_FB, s_end - sb);
-  if (blockIdx.x >= ext_blocks) {  // zero the group's tail bitmaps (k_corr ORs the tail detectors' bits in)
-    const int w = 4 * ((blockIdx.x - ext_blocks) * blockDim.x + threadIdx.x);
+  {  // this block's share of the group's tail bitmaps is zeroed (k_corr ORs the tail detectors' bits in)
+    const int per = (K.tail_bm_words + (int)ext_blocks - 1) / (int)ext_blocks;
+    const int w0 = (int)blockIdx.x * per, w1 = min(K.tail_bm_words, w0 + per);
     for (int f = 0; f < nf; ++f) {
       unsigned* __restrict__ t = tailbm + (int64_t)(sb + f) * K.tail_bm_words;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (w + u < K.tail_bm_words) t[w + u] = 0u;
+      for (int w = w0 + (int)threadIdx.x; w < w1; w += blockDim.x) t[w] = 0u;
     }
-    return;
   }
-  __shared__ uint8_t lut[LM_INGEST_FB][256];
+  // One round of independent loads (the group's LUTs into registers, the
+  // slots, the source map entry), then the frame loads the map points at, and
+  // only then the LUTs into LDS and the barrier: the group costs two load
+  // latencies, not four (LUT copy, slots, map, frames one after another).
+  __shared__ __attribute__((aligned(16))) uint8_t lut[LM_INGEST_FB][256];
   __shared__ uint8_t glut[256];
-  for (int i = threadIdx.x; i < nf * 256; i += blockDim.x) lut[i >> 8][i & 255] = luts[(sb + (i >> 8)) * 256 + (i & 255)];
-  glut[threadIdx.x] = K.gray_lut[threadIdx.x];
-  __syncthreads();
+  static_assert(LM_INGEST_FB * 256 == 8 * 256, "k_ingest: 8 LUT bytes per thread");
+  const int li = (int)threadIdx.x * 8;
+  uint2 lv = make_uint2(0u, 0u);
+  if (li < nf * 256) lv = *reinterpret_cast<const uint2*>(luts + (int64_t)sb * 256 + li);
+  const uint8_t gl = K.gray_lut[threadIdx.x];
   const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
   const int64_t etot = e0 + (int64_t)K.ext_h[1] * K.ext_w[1];
   const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * LM_INGEST_VEC;
-  if (q >= etot) return;
+  const bool act = q < etot;
   const int v = q < e0 ? 0 : 1;
   const int64_t qq = v == 0 ? q : q - e0;
-  const int er = (int)(qq / K.ext_w[v]);
-  const int ec = (int)(qq % K.ext_w[v]);  // multiple of 16 (ext_w % 16 == 0)
+  const int er = act ? (int)(qq / K.ext_w[v]) : 0;
+  const int ec = act ? (int)(qq % K.ext_w[v]) : 0;  // multiple of 16 (ext_w % 16 == 0)
+  int2 m = make_int2(0, 0);
+  uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
+  if (act && smap) {  // speculative: used when the group's crops all sit at the map's position
+    m = smap[q / LM_INGEST_VEC];
+    b4 = sbkg[q / LM_INGEST_VEC];
+  }
+  const LmSlot sl0 = slots[sb];
+  bool same = true;
+  for (int f = 1; f < nf; ++f)
+    same = same && slots[sb + f].crop_x[v] == sl0.crop_x[v] && slots[sb + f].crop_y[v] == sl0.crop_y[v];
+  const bool fast = act && same && smap && skey[2 * v] == sl0.crop_x[v] && skey[2 * v + 1] == sl0.crop_y[v] && m.y != 0;
   int idx[LM_INGEST_VEC];
-  uint8_t bv[LM_INGEST_VEC];
+  uint32_t bw[4];  // background bytes, packed
   int run = 0;  // 1: idx[k] = idx[0] + k, -1: idx[k] = idx[0] - k, 0: gather
   int lo = 0;   // a run's first source byte
   bool allv = false;  // every pixel inside I_UNPAD (a run; idx[] not filled on the source-map path)
+  uint32_t d[LM_INGEST_FB][5];
+  if (fast) {  // the source map holds this crop position: no calibration / background gathers
+    run = m.y;
+    lo = m.x;
+    allv = true;
+#pragma unroll
+    for (int f = 0; f < LM_INGEST_FB; ++f)
+      if (f < nf) {
+        const lm_gu32* w = reinterpret_cast<const lm_gu32*>(as_global(frame_ptr[sb + f]) + (lo & ~3));
+#pragma unroll
+        for (int u = 0; u < 5; ++u) d[f][u] = w[u];
+      }
+  }
+  if (li < nf * 256) *reinterpret_cast<uint2*>(&lut[0][0] + li) = lv;
+  glut[threadIdx.x] = gl;
+  __syncthreads();
+  if (!act) return;
   // gather indices and background of this thread's 16 pixels for a crop at (cx, cy)
   auto locate = [&](int R, int C0) {
-    run = ingest_locate(K, cal, bkg, R, C0, idx, bv, lo);
+    run = ingest_locate(K, cal, bkg, R, C0, idx, bw, lo);
     allv = false;
   };
   // the 16 source bytes of a run span [lo, lo + 16): five aligned dwords cover them
   // (funnel shifts by the byte offset, then a byte reversal for a flipped run:
   // no register array is indexed with a run-time value, so nothing spills)
-  auto run_bytes = [&](const uint32_t (&d)[5], uint8_t (&pix)[LM_INGEST_VEC]) {
+  auto run_bytes = [&](const uint32_t (&dd)[5], uint32_t (&w)[4]) {
     const unsigned sh = (unsigned)(lo & 3);
-    uint32_t w[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+    for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_alignbyte(dd[j + 1], dd[j], sh);
     if (run < 0) {
       const uint32_t r0 = __builtin_bswap32(w[3]), r1 = __builtin_bswap32(w[2]), r2 = __builtin_bswap32(w[1]),
                      r3 = __builtin_bswap32(w[0]);
@@ -311,17 +340,17 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
       w[2] = r2;
       w[3] = r3;
     }
-#pragma unroll
-    for (int k = 0; k < LM_INGEST_VEC; ++k) pix[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
   };
   // background subtraction, the slot's LUT, the grey LUT and the 16-byte store
-  auto emit = [&](int f, const uint8_t (&pix)[LM_INGEST_VEC], const LmSlot& sl, int R, int C0) {
+  // (pixels and background bytes stay packed four to a register)
+  auto emit = [&](int f, const uint32_t (&pw)[4], const LmSlot& sl, int R, int C0) {
     uint32_t word[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < LM_INGEST_VEC; ++k) {
       uint32_t o = 0;
       if (allv || idx[k] >= 0) {
-        o = lut[f][pix[k] > bv[k] ? pix[k] - bv[k] : 0];
+        const uint32_t pk = (pw[k >> 2] >> (8 * (k & 3))) & 0xFFu, bk = (bw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        o = lut[f][pk > bk ? pk - bk : 0];
         if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) o = glut[o];
       } else if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) {
         o = glut[0];  // only reachable through the pad (rejected on the host)
@@ -331,30 +360,27 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
     *reinterpret_cast<uint4*>(ext + (int64_t)(sb + f) * ext_slot_bytes + q) = make_uint4(word[0], word[1], word[2], word[3]);
   };
 
-  // Common case: every slot of the group has its crop at the same place (a
-  // provided bounding box) and the pixels are a run: all the group's frame
-  // loads are issued before any is used, so the group costs one load latency.
-  const LmSlot sl0 = slots[sb];
-  bool same = true;
-  for (int f = 1; f < nf; ++f)
-    same = same && slots[sb + f].crop_x[v] == sl0.crop_x[v] && slots[sb + f].crop_y[v] == sl0.crop_y[v];
   {
     const int R = sl0.crop_y[v] + K.ext_oy[v] + er, C0 = sl0.crop_x[v] + K.ext_ox[v] + ec;
-    int2 m = make_int2(0, 0);
-    if (same && smap && skey[2 * v] == sl0.crop_x[v] && skey[2 * v + 1] == sl0.crop_y[v]) m = smap[q / LM_INGEST_VEC];
-    if (m.y != 0) {  // the source map holds this crop position: no calibration / background gathers
-      run = m.y;
-      lo = m.x;
-      allv = true;
-      const uint4 b4 = sbkg[q / LM_INGEST_VEC];
-      const unsigned bw[4] = {b4.x, b4.y, b4.z, b4.w};
+    if (fast) {
+      bw[0] = b4.x;
+      bw[1] = b4.y;
+      bw[2] = b4.z;
+      bw[3] = b4.w;
 #pragma unroll
-      for (int k = 0; k < LM_INGEST_VEC; ++k) bv[k] = (uint8_t)(bw[k >> 2] >> (8 * (k & 3)));
-    } else {
-      locate(R, C0);
+      for (int f = 0; f < LM_INGEST_FB; ++f)
+        if (f < nf) {
+          uint32_t pw[4];
+          run_bytes(d[f], pw);
+          emit(f, pw, slots[sb + f], R, C0);
+        }
+      return;
     }
+    // Every slot of the group has its crop at the same place and the pixels
+    // are a run, but the source map does not hold it: all the group's frame
+    // loads are issued before any is used.
+    locate(R, C0);
     if (same && run != 0) {
-      uint32_t d[LM_INGEST_FB][5];
 #pragma unroll
       for (int f = 0; f < LM_INGEST_FB; ++f)
         if (f < nf) {
@@ -365,9 +391,9 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
 #pragma unroll
       for (int f = 0; f < LM_INGEST_FB; ++f)
         if (f < nf) {
-          uint8_t pix[LM_INGEST_VEC];
-          run_bytes(d[f], pix);
-          emit(f, pix, slots[sb + f], R, C0);
+          uint32_t pw[4];
+          run_bytes(d[f], pw);
+          emit(f, pw, slots[sb + f], R, C0);
         }
       return;
     }
@@ -385,18 +411,19 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
       locate(R, C0);
     }
     const lm_gu8* __restrict__ F = as_global(frame_ptr[slot]);
-    uint8_t pix[LM_INGEST_VEC];
+    uint32_t pw[4] = {0, 0, 0, 0};
     if (run != 0) {
       const lm_gu32* w = reinterpret_cast<const lm_gu32*>(F + (lo & ~3));
-      uint32_t d[5];
+      uint32_t d1[5];
 #pragma unroll
-      for (int u = 0; u < 5; ++u) d[u] = w[u];
-      run_bytes(d, pix);
+      for (int u = 0; u < 5; ++u) d1[u] = w[u];
+      run_bytes(d1, pw);
     } else {
 #pragma unroll
-      for (int k = 0; k < LM_INGEST_VEC; ++k) pix[k] = idx[k] >= 0 ? F[idx[k]] : 0;
+      for (int k = 0; k < LM_INGEST_VEC; ++k)
+        if (idx[k] >= 0) pw[k >> 2] |= (uint32_t)F[idx[k]] << (8 * (k & 3));
     }
-    emit(f, pix, sl, R, C0);
+    emit(f, pw, sl, R, C0);
   }
 }
 

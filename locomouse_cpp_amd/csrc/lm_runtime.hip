@@ -992,8 +992,7 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
     const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
     T.begin("k_ingest");
     const unsigned ext_blocks = (unsigned)((etot / LM_INGEST_VEC + 255) / 256);
-    const unsigned zero_blocks = (unsigned)((K.tail_bm_words + 4 * 256 - 1) / (4 * 256));  // the tail bitmaps
-    k_ingest<<<dim3(ext_blocks + zero_blocks, (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)), 256, 0, st>>>(
+    k_ingest<<<dim3(ext_blocks, (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)), 256, 0, st>>>(
         dK, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, L.slots.p, s_proc0, n + 1, L.ext.p, c->ext_slot_bytes,
         ext_blocks, reinterpret_cast<unsigned*>(L.tailbin.p), L.smap.p, L.sbkg.p, L.skey.p);
     T.end();
