@@ -65,7 +65,7 @@ __host__ __device__ constexpr int f16_nch(int kw) { return (kw + 31 + 15) / 16; 
 __host__ __device__ constexpr int f16_cols(int nch) { return LM_F16_TW - 32 + 16 * nch; }
 __host__ __device__ constexpr int f16_stride(int cols) { return (cols + 7) / 16 * 16 + 8; }
 __host__ __device__ constexpr size_t f16_lds_bytes(int nch, int kh) {
-  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2 + (size_t)2 * nch * 64 * 16;
+  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2;  // the f16 window (B fragments come from global)
 }
 // Host: the B fragment of (row i, chunk c) for lane l, element j (0 off the band).
 static inline float f16_bfrag_weight(const double* w, int kw, int i, int c, int l, int j) {

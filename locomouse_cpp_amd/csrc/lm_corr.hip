@@ -702,10 +702,11 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
 // 16-byte reads of the f16 window in LDS (row stride = 8 mod 16 halfs: the
 // 32 rows a read touches fall in distinct bank groups).  B fragments do not
 // depend on the output tile: the host lays them out once per detector in the
-// MFMA's lane order ([i][chunk][lane] x 8 halfs), and each workgroup stages
-// row i + 1's NCH KiB into LDS (double buffer, one barrier per row) while
-// it multiplies with row i's; every wave reads them with one aligned
-// ds_read_b128 per chunk and uses each for its two 32 x 32 output tiles.
+// MFMA's lane order ([i][chunk][lane] x 8 halfs), and every wave loads row
+// i + 1's fragments from global memory (the same NCH KiB for every workgroup:
+// L1 / L2 hits) into registers while it multiplies with row i's, using each
+// for its two 32 x 32 output tiles; the LDS holds only the window, and the
+// row loop has no barrier.
 // Four waves side by side: a 128 x 64 output tile per workgroup.
 // Accumulator layout (32x32 MFMA): column = lane & 31, row = (reg & 3) +
 // 8 (reg >> 2) + 4 (lane >> 5).
@@ -770,32 +771,9 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
   const int oy0 = T.oy0, ox0 = T.ox0, kh = D.kh;
   if (corr_tile_dark(K, D, dark, slot, oy0, ox0)) return;
   constexpr int cols = f16_cols(NCH), STR = f16_stride(cols);
-  constexpr int NB = NCH * 64;  // 16-byte B fragments per detector row
   const int rows = LM_F16_TH + kh - 1;
   _Float16* __restrict__ img = reinterpret_cast<_Float16*>(lds_f16);
-  uint4* __restrict__ bbuf = reinterpret_cast<uint4*>(img + rows * STR);  // [2][NB]
-  const uint4* __restrict__ bsrc = bfrag + D.w16_off;
-  // B staging: each thread moves fragments tid, tid + 256, tid + 512 of a row
-  // (loads clamped into the row, so they need no branch; stores guarded)
-  static_assert(NB <= 3 * LM_F16_THREADS, "B staging");
-  const int e0 = threadIdx.x;
-  uint4 st0, st1, st2;
-  auto stage_load = [&](int row) {
-    const uint4* __restrict__ p = bsrc + (int64_t)row * NB;
-    st0 = p[min(e0, NB - 1)];
-    if constexpr (NB > LM_F16_THREADS) st1 = p[min(e0 + LM_F16_THREADS, NB - 1)];
-    if constexpr (NB > 2 * LM_F16_THREADS) st2 = p[min(e0 + 2 * LM_F16_THREADS, NB - 1)];
-  };
-  auto stage_store = [&](uint4* __restrict__ dst) {
-    if (e0 < NB) dst[e0] = st0;
-    if constexpr (NB > LM_F16_THREADS)
-      if (e0 + LM_F16_THREADS < NB) dst[e0 + LM_F16_THREADS] = st1;
-    if constexpr (NB > 2 * LM_F16_THREADS)
-      if (e0 + 2 * LM_F16_THREADS < NB) dst[e0 + 2 * LM_F16_THREADS] = st2;
-  };
-  stage_load(0);
   tile_fill_f16(img, STR, corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0), K.ext_w[D.view], rows, cols);
-  stage_store(bbuf);
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
 
@@ -807,23 +785,35 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[t][q] = init;
   const _Float16* __restrict__ arow = img + r * STR + 32 * wave + 8 * h;
-  for (int i = 0; i < kh; ++i) {
-    const bool more = i + 1 < kh;
-    if (more) stage_load(i + 1);  // row i + 1's fragments: global -> registers now, -> LDS after this row's MFMAs
-    const lm_h8* __restrict__ bi = reinterpret_cast<const lm_h8*>(bbuf + (i & 1) * NB) + lane;
+  // B fragments straight from global memory (the same NCH KiB per detector
+  // row for every workgroup: L1/L2 hits), one row ahead in registers, so the
+  // row loop has no barrier (round 2 staged them through LDS with one
+  // __syncthreads per row)
+  const lm_h8* __restrict__ bsrc = reinterpret_cast<const lm_h8*>(bfrag + D.w16_off) + lane;
+  lm_h8 b0[NCH], b1[NCH];
+  auto load_b = [&](lm_h8 (&b)[NCH], int i) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) b[c] = bsrc[(int64_t)(i * NCH + c) * 64];
+  };
+  auto mma_row = [&](const lm_h8 (&b)[NCH], int i) {
     const _Float16* __restrict__ ai = arow + i * STR;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const lm_h8 b = bi[64 * c];
+    for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int t = 0; t < LM_F16_T; ++t) {
         const lm_h8 a = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR + 16 * c);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[c], acc[t], 0, 0, 0);
       }
-    }
-    if (more) stage_store(bbuf + ((i + 1) & 1) * NB);
-    __syncthreads();
+  };
+  load_b(b0, 0);
+  int i = 0;
+  for (; i + 1 < kh; i += 2) {
+    load_b(b1, i + 1);
+    mma_row(b0, i);
+    if (i + 2 < kh) load_b(b0, i + 2);
+    mma_row(b1, i + 1);
   }
+  if (i < kh) mma_row(b0, i);
 
   const int x = ox0 + 32 * wave + r;
   if (D.kind != 0) {
