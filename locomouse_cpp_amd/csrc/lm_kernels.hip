@@ -449,7 +449,9 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
 // the component's runs (arithmetic series per run and tile) and turned into
 // doubles in that same tile order, so the tracks are bit-identical.
 // No size limit: run tables beyond the LDS capacity go to global scratch.
+#ifndef LM_TAIL_THREADS
 #define LM_TAIL_THREADS 256
+#endif
 #define LM_TAIL_SEGS 15
 
 struct TailLayout {  // byte offsets into k_tail's dynamic LDS
@@ -1425,7 +1427,9 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
 }
 
 // ------------------------------------------------------------------ k_post
+#ifndef LM_POST_THREADS
 #define LM_POST_THREADS 256
+#endif
 #define LM_POST_MAXC 512     // candidates per list handled in LDS
 #define LM_POST_MAXOFF 2048  // CSC columns (Ni + Nong) + 1
 
@@ -1897,9 +1901,10 @@ __global__ __launch_bounds__(LM_POST_THREADS) void k_post(LM_POST_ARGS, int npai
 // (frame first-1) into slot 0's candidate staging, where k_post reads the
 // previous frame's candidates (pairwisePotential, :896-919).  Runs first in a
 // batch, before k_corr reuses the key areas of slots >= 1.
-__global__ void k_carry(const LmConst* __restrict__ Kp, unsigned long long* __restrict__ keys, const LmSlotOut* __restrict__ prev_hdr,
-                        int prev_slot, LmSlotOut* __restrict__ hdr) {
-  const LmConst& K = *Kp;
+// k_carry (block 1 of k_prep's launch when the batch continues the lane's
+// last one): the previous batch's last frame's bottom candidates into slot 0.
+DEV void carry_block(const LmConst& K, unsigned long long* __restrict__ keys, const LmSlotOut* __restrict__ prev_hdr,
+                     int prev_slot, LmSlotOut* __restrict__ hdr) {
   for (int l = 0; l < LM_NFEAT; ++l) {
     const int cnt = prev_hdr[prev_slot].cand_cnt[l];
     const LmCand* src = LM_CAND_STAGE(K, keys, prev_slot, l);
@@ -1921,7 +1926,14 @@ __global__ void k_carry(const LmConst* __restrict__ Kp, unsigned long long* __re
 __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots, const uint8_t* const* __restrict__ h_fptr,
                                               const LmArenaCtl* __restrict__ h_ctl, int ns, LmSlot* __restrict__ slots,
                                               const uint8_t** __restrict__ fptr, LmArenaCtl* __restrict__ ctl,
-                                              int32_t* __restrict__ npos, int32_t* __restrict__ err) {
+                                              int32_t* __restrict__ npos, int32_t* __restrict__ err,
+                                              const LmConst* __restrict__ Kp, unsigned long long* __restrict__ keys,
+                                              const LmSlotOut* __restrict__ prev_hdr, int prev_slot,
+                                              LmSlotOut* __restrict__ hdr) {
+  if (blockIdx.x == 1) {
+    carry_block(*Kp, keys, prev_hdr, prev_slot, hdr);
+    return;
+  }
   for (int i = threadIdx.x; i < ns; i += blockDim.x) {
     slots[i] = h_slots[i];
     fptr[i] = h_fptr[i];

@@ -977,13 +977,10 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
   const int n = P.n, s_lut0 = P.s_lut0, s_proc0 = P.s_proc0;
   const int nproc = n + 1 - s_proc0;
   if (part <= 0) {
-    k_prep<<<1, 256, 0, st>>>(L.h_slots.d, L.h_frame_ptr.d, L.h_ctl.d, n + 1, L.slots.p, L.frame_ptr.p, A.ctl.p,
-                              L.npos.p, L.err.p);
-    if (do_carry) {  // a rerun keeps slot 0's staged candidates
-      T.begin("k_carry");
-      k_carry<<<1, 256, 0, st>>>(dK, L.keys.p, L.arena[P.prv].hdr.p, P.last_n, A.hdr.p);
-      T.end();
-    }
+    // block 1: k_carry (a rerun keeps slot 0's staged candidates)
+    k_prep<<<do_carry ? 2 : 1, 256, 0, st>>>(L.h_slots.d, L.h_frame_ptr.d, L.h_ctl.d, n + 1, L.slots.p, L.frame_ptr.p,
+                                             A.ctl.p, L.npos.p, L.err.p, dK, L.keys.p, L.arena[P.prv].hdr.p, P.last_n,
+                                             A.hdr.p);
     T.begin("k_minmax");
     k_minmax<<<dim3(LM_MM_SPLIT, n + 1 - s_lut0), LM_MM_THREADS, 0, st>>>(L.frame_ptr.p, c->bkg.p, c->npix, s_lut0,
                                                                         L.mm.p);
