@@ -34,21 +34,32 @@ struct LmDetGroup {
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
       X(40) X(44) X(48) X(52) X(56) X(60) X(64)
 #endif
+// widths of the merged launch (k_corr_rw_all): those whose window row fits
+// half a wave's loads (rw_tile's lane-split loads; wider ones load both halves
+// from every lane and need more registers than the merged kernel's budget)
+#ifdef LM_KW_ONLY
 #define LM_KW_LIST_RW_ALL LM_KW_LIST
+#else
+#define LM_KW_LIST_RW_ALL(X) \
+  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) X(40)
+#endif
+__host__ __device__ constexpr bool rw_all_width(int kw) { return kw >= 16 && (kw <= 32 || kw == 36 || kw == 40); }
 
 // k_corr_rw: one wave per 80 x 16 output tile, LM_RW_WAVES waves per workgroup
 #ifndef LM_RW_WAVES
 #define LM_RW_WAVES 4
 #endif
 #define LM_RW_THREADS (64 * LM_RW_WAVES)
-#define LM_RW_TH 16     // output rows per wave tile
-#define LM_RW_SLOTS 16  // ring rows (+ 1 mirror)
+#define LM_RW_TH 16     // output rows per wave (two half-tiles)
+#define LM_RW_HTH 8     // output rows per half-tile (also the dark-tile flag grid's rows)
+#define LM_RW_HSLOTS 8  // ring rows per half (+ 1 mirror)
 
 // window row: 80 + KW - 1 columns plus up to 3 before them (the loads start on
 // a 4-byte boundary); stride == 4 (mod 8)
 __host__ __device__ constexpr int rw_stride(int kw) { return pk_stride(LM_TW + kw - 1 + 3); }
+__host__ __device__ constexpr int rw_ring_floats(int kw) { return 2 * (LM_RW_HSLOTS + 1) * rw_stride(kw); }
 __host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
-  return (size_t)LM_RW_WAVES * (LM_RW_SLOTS + 1) * rw_stride(kw) * sizeof(float);
+  return (size_t)LM_RW_WAVES * rw_ring_floats(kw) * sizeof(float);
 }
 
 // k_corr_f16 (non-parity LM_CORR_F16 mode)

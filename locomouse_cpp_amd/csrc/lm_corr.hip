@@ -199,48 +199,67 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
 // one column: for tap (i, j) both use weight w[i][j] (SGPR, broadcast) and
 // pixels (t, t+1) of one column, which one ds_read2_b32 loads into an aligned
 // register pair.  A thread owns 5 columns x 4 rows (two row pairs sharing the
-// pixel rows of a step with weight rows t and t - 2); a wave is 16 x 4
-// threads = an independent 80 x 16 output tile that streams its window
-// through a private LDS ring of LM_RW_SLOTS rows (round 1's k_corr_pk held a
-// 48 + kh - 1 row window per 3-wave workgroup instead).  At step t the
-// wave's 4 row groups read window rows t + 4 ly, t + 4 ly + 1 (rows t..t+13),
-// so 16 slots hold them plus the row being written (row t + 14, into the slot
-// of row t - 2); slot 16 mirrors slot 0 so a pair never wraps.  A wave's LDS
-// operations execute in order, so the ring needs no barrier at all.  LDS per
-// wave is 17 rows (7.9 KB at KW = 30 vs 11.9 KB per wave for k_corr_pk's 48-row
-// window), any kh fits, and no wave waits for another.
-// Wave g of a launch -> (slot, detector, tile origin).  The batch's tiles
-// are flattened detector-major (all slots of the group's first detector,
-// then the next ...), so no wave idles at a frame's end and the host can
-// put the longest detectors first.  false: past the last tile.
-// With dark-tile lists (tl_cnt != nullptr) a point detector's waves are
-// only its view's bright tiles (k_tilelist), so the group's wave count is
-// known on the device only: the grid is sized for every tile and the waves
-// past the last group's count (whole workgroups at the grid's end) return.
+// pixel rows of a step with weight rows t and t - 2).  A wave is two
+// independent 80 x 8 half-tiles of 32 lanes (16 x 2 threads) — since round
+// 3, so that the dark-tile skip works at 80 x 8 granularity (72-73 % of the
+// synthetic point tiles bright vs 77-80 % at 80 x 16) — each streaming its
+// own window through a private LDS ring of LM_RW_HSLOTS rows + 1 mirror row:
+// at step t its 2 row groups read window rows t + 4 ly, t + 4 ly + 1 (rows
+// t .. t + 5), so 8 slots hold them plus rows t + 6, t + 7; the mirror slot
+// keeps a pair from wrapping.  LDS per wave is 2 x 9 rows (18 rows vs round
+// 2's 17 for one 80 x 16 tile), any kh fits, no wave waits for another and
+// a wave's LDS operations execute in order, so the rings need no barrier.
+
+// A ring wave's two 80 x 8 half-tiles (see rw_tile).
+struct RwHalves {
+  int slot[2], oy[2], ox[2];
+  int valid1;  // the second half holds a tile
+};
+
+// Wave g of a ring launch -> its detector and half-tiles.  The batch's work
+// is flattened detector-major (all slots of the group's first detector, then
+// the next ...), so no wave idles at a frame's end and the host can put the
+// longest detectors first.  With dark-tile lists (tl_cnt != nullptr) a point
+// detector's waves take its view's bright half-tiles two at a time
+// (k_tilelist), so the group's wave count is known on the device only: the
+// grid is sized for every 80 x 16 tile and the waves past the last group's
+// count (whole workgroups at the grid's end) return.  Otherwise a wave takes
+// the two halves of one 80 x 16 tile.  false: past the last wave.
 DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, const int32_t* tl_cnt,
-                        const uint32_t* tl_list, int& slot, CorrTile& T) {
+                        const uint32_t* tl_list, int& d, RwHalves& H) {
   int base = 0;
 #pragma unroll
   for (int k = 0; k < LM_NDET; ++k) {
     if (k >= G.n) return false;
-    const int d = G.ids[k];
+    d = G.ids[k];
     const LmDet& D = K.det[d];
     const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
     const bool listed = tl_cnt != nullptr && D.kind == 0;
-    const int cnt = listed ? tl_cnt[D.view] : nt * nslots;
+    const int nh = listed ? tl_cnt[D.view] : 0;  // bright half-tiles
+    const int cnt = listed ? (nh + 1) >> 1 : nt * nslots;
     if (g < base + cnt) {
       const int local = g - base;
-      int lt;
-      if (listed) {
-        const uint32_t e = tl_list[(int64_t)D.view * K.tl_stride + local];
-        slot = (int)(e >> 16);
-        lt = (int)(e & 0xFFFFu);
-      } else {
-        slot = s0 + local / nt;
-        lt = local - (local / nt) * nt;
-      }
       const int tx = D.tiles_x;
-      T = CorrTile{d, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
+      if (listed) {
+        const uint32_t* __restrict__ l = tl_list + (int64_t)D.view * K.tl_stride + 2 * local;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const uint32_t e = (q == 0 || 2 * local + 1 < nh) ? l[q] : l[0];
+          const int lt = (int)(e & 0xFFFFu);
+          H.slot[q] = (int)(e >> 16);
+          H.oy[q] = (lt / tx) * LM_RW_HTH;
+          H.ox[q] = (lt % tx) * LM_TW;
+        }
+        H.valid1 = 2 * local + 1 < nh;
+      } else {
+        const int slot = s0 + local / nt;
+        const int lt = local - (local / nt) * nt;
+        H.slot[0] = H.slot[1] = slot;
+        H.oy[0] = (lt / tx) * LM_RW_TH;
+        H.oy[1] = H.oy[0] + LM_RW_HTH;
+        H.ox[0] = H.ox[1] = (lt % tx) * LM_TW;
+        H.valid1 = 1;
+      }
       return true;
     }
     base += cnt;
@@ -253,7 +272,7 @@ DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s
 DEV bool corr_tile_dark(const LmConst& K, const LmDet& D, const uint8_t* __restrict__ dark, int slot, int oy0, int ox0) {
   if (dark == nullptr || D.kind != 0) return false;
   const int v = D.view;
-  const int ty0 = oy0 / LM_RW_TH, ty1 = min(K.fl_ty[v] - 1, (oy0 + D.tile_h - 1) / LM_RW_TH);
+  const int ty0 = oy0 / LM_RW_HTH, ty1 = min(K.fl_ty[v] - 1, (oy0 + D.tile_h - 1) / LM_RW_HTH);
   const int tx0 = ox0 / LM_TW, tx1 = min(K.fl_tx[v] - 1, (ox0 + D.tile_w - 1) / LM_TW);
   const uint8_t* __restrict__ f = dark + (int64_t)slot * K.fl_slot + K.fl_off[v];
   for (int ty = ty0; ty <= ty1; ++ty)
@@ -400,31 +419,58 @@ struct RwPipe {
   }
 };
 
-// One wave's tile (the body of k_corr_rw and k_corr_rw_all).
+// One wave's work (the body of k_corr_rw and k_corr_rw_all): two 80 x 8
+// half-tiles, lanes 0-31 the first, lanes 32-63 the second, each half
+// streaming its own window through its own ring of 8 rows + 1 mirror.  The
+// halves are two bright half-tiles from the dark-tile list (any slots, any
+// places) or the two halves of one 80 x 16 tile (tail detectors, skip off).
+// Per half: lane (ly, lx) = ((lane >> 4) & 1, lane & 15) owns 5 columns x 4
+// rows as two packed row pairs; at step t it reads window rows t + 4 ly and
+// t + 4 ly + 1, so rows t .. t + 5 are live and the ring holds t .. t + 7;
+// row t + 8 is loaded at the step's start and stored into row t's slot at
+// its end.  A wave's LDS operations run in order, so no barrier anywhere.
 template <int KW, bool UNF>
-DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D, int slot, int oy0, int ox0,
-                                                float* ring, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D, const RwHalves& H, float* ring,
+                                                const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
                                                 const float* __restrict__ weights,
                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
   const int lane = threadIdx.x & 63;
   constexpr int STR = rw_stride(KW);
-  constexpr int NL = (3 + LM_TW + KW - 1 + 3) / 4;  // lanes that load a window row (4 bytes each)
-  static_assert(NL <= 64, "window row wider than a wave's loads");
+  constexpr int NLH = (3 + LM_TW + KW - 1 + 3) / 4;  // dwords of a window row
+  constexpr bool DUAL = NLH > 32;                     // a row wider than half a wave: every lane loads both halves
+  static_assert(NLH <= 64, "window row wider than a wave's loads");
+  constexpr int HS = LM_RW_HSLOTS;                    // ring rows per half (+ 1 mirror)
   const int kh = D.kh, kwp = D.kwp;
-  const int nrows = LM_RW_TH + kh - 1;
+  const int nrows = LM_RW_HTH + kh - 1;
   const int ew = K.ext_w[D.view];
+  const int ew4 = ew >> 2;  // ext rows are padded to 16 bytes
+  const int h = lane >> 5, hl = lane & 31;
+  const int ly = hl >> 4, lx = lane & 15;
+  // this lane's half-tile, in VGPRs from here on (the halves' scalars are not
+  // kept live through the tap loop: the merged kernel's SGPRs are full)
+  const int slot = h ? H.slot[1] : H.slot[0];
+  const int oy0 = h ? H.oy[1] : H.oy[0];
+  const int ox0 = h ? H.ox[1] : H.ox[0];
+  const bool valid = h == 0 || H.valid1;
   const uint8_t* src = corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0);
   const int mis = (int)((uintptr_t)src & 3);
-  const unsigned* __restrict__ a = reinterpret_cast<const unsigned*>(src - mis) + lane;
-  const int ew4 = ew >> 2;  // ext rows are padded to 16 bytes
-  const bool ld = lane < NL;
-  const int ly = lane >> 4, lx = lane & 15;
+  // row loads: each lane its own half's dword hl, or (DUAL) dword `lane` of
+  // both halves' rows: lane h' of a DUAL load of half q reads at the half's
+  // base, which lanes of half q hold in `a` (exchanged once, below)
+  const unsigned* __restrict__ a = reinterpret_cast<const unsigned*>(src - mis) + hl;
+  const uint8_t* src0 = corr_src(K, D, ext, ext_slot_bytes, H.slot[0], H.oy[0], H.ox[0]);  // DUAL: wave-uniform bases
+  const uint8_t* src1 = corr_src(K, D, ext, ext_slot_bytes, H.slot[1], H.oy[1], H.ox[1]);
+  const unsigned* __restrict__ a0 = reinterpret_cast<const unsigned*>(src0 - ((uintptr_t)src0 & 3)) + lane;
+  const unsigned* __restrict__ a1 = reinterpret_cast<const unsigned*>(src1 - ((uintptr_t)src1 & 3)) + lane;
+  const bool valid1 = H.valid1 != 0;
+  const bool ld = DUAL ? lane < NLH : (valid && hl < NLH);
+  const bool ld1 = DUAL && lane < NLH && valid1;
 
   // brightness mask of the point detectors' outputs (crop pixel > 25), read
   // from the ext crop now so the loads are long done by the epilogue
   unsigned mbits = 0;
-  if (D.kind == 0) {
+  if (D.kind == 0 && valid) {
     const uint8_t* __restrict__ m = ext + (int64_t)slot * ext_slot_bytes +
                                     (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) + (int64_t)(D.m_y + oy0 + ly * PK_R) * ew +
                                     (D.m_x + ox0 + lx * PK_C);
@@ -434,31 +480,51 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
       for (int c = 0; c < PK_C; ++c) mbits |= (m[(int64_t)r * ew + c] > 25 ? 1u : 0u) << (r * PK_C + c);
   }
 
-  auto load_row = [&](int r) -> unsigned { return (ld && r < nrows) ? a[(int64_t)r * ew4] : 0u; };
-  auto store_row = [&](int r, unsigned v) {
-    if (ld && r < nrows) {
-      const int s = r & (LM_RW_SLOTS - 1);
-      const float4 f = make_float4((float)(v & 0xFFu), (float)((v >> 8) & 0xFFu), (float)((v >> 16) & 0xFFu),
-                                   (float)(v >> 24));
-      *reinterpret_cast<float4*>(ring + s * STR + 4 * lane) = f;
-      if (s == 0) *reinterpret_cast<float4*>(ring + LM_RW_SLOTS * STR + 4 * lane) = f;
+  struct Row {
+    unsigned v, v1;
+  };
+  auto load_row = [&](int r) -> Row {
+    Row w{0u, 0u};
+    if constexpr (DUAL) {
+      if (ld && r < nrows) w.v = a0[(int64_t)r * ew4];
+      if (ld1 && r < nrows) w.v1 = a1[(int64_t)r * ew4];
+    } else {
+      if (ld && r < nrows) w.v = a[(int64_t)r * ew4];
+    }
+    return w;
+  };
+  auto put = [&](float* hr, int s, int col, unsigned v) {
+    const float4 f = make_float4((float)(v & 0xFFu), (float)((v >> 8) & 0xFFu), (float)((v >> 16) & 0xFFu),
+                                 (float)(v >> 24));
+    *reinterpret_cast<float4*>(hr + s * STR + 4 * col) = f;
+    if (s == 0) *reinterpret_cast<float4*>(hr + HS * STR + 4 * col) = f;
+  };
+  auto store_row = [&](int r, Row w) {
+    if (r >= nrows) return;
+    const int s = r & (HS - 1);
+    if constexpr (DUAL) {
+      if (ld) put(ring, s, lane, w.v);
+      if (ld1) put(ring + (HS + 1) * STR, s, lane, w.v1);
+    } else {
+      if (ld) put(ring + h * (HS + 1) * STR, s, hl, w.v);
     }
   };
   {
-    unsigned v0[LM_RW_SLOTS];
+    Row v0[HS];
 #pragma unroll
-    for (int r = 0; r < LM_RW_SLOTS; ++r) v0[r] = load_row(r);
+    for (int r = 0; r < HS; ++r) v0[r] = load_row(r);
 #pragma unroll
-    for (int r = 0; r < LM_RW_SLOTS; ++r) store_row(r, v0[r]);
+    for (int r = 0; r < HS; ++r) store_row(r, v0[r]);
   }
 
   lm_f2 acc[PK_R / 2][PK_C];
   const lm_f2* __restrict__ W = reinterpret_cast<const lm_f2*>(weights + D.w_off);  // kwp is a multiple of 4
   const int kwp2 = kwp >> 1;
-  const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring;
+  const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring +
+                             (unsigned)(h * (HS + 1) * STR * (int)sizeof(float));
   const unsigned lane_off = (unsigned)((lx * PK_C + mis) * (int)sizeof(float));
   auto row_base = [&](int t) -> unsigned {
-    return ring_base + (unsigned)(((t + ly * PK_R) & (LM_RW_SLOTS - 1)) * STR * (int)sizeof(float)) + lane_off;
+    return ring_base + (unsigned)(((t + ly * PK_R) & (HS - 1)) * STR * (int)sizeof(float)) + lane_off;
   };
   RwPipe<KW, UNF> S;
 #pragma unroll
@@ -468,19 +534,17 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   auto wrow = [&](int i) { return W + min(max(i, 0), kh - 1) * kwp2; };
   S.template load_w<0>(S.wa, S.wb, wrow(0), wrow(-2));
   S.template issue<RwPlan<KW>::pbeg(0), RwPlan<KW>::pend(0)>(row_base(0));
-  // Step t reads ring rows t .. t + 13 and prefetches step t + 1's rows
-  // t + 1 .. t + 14 in its last chunk; it loads row t + 16 at its start and
-  // stores it at its end into the slot of row t (dead by then: a wave's LDS
-  // operations run in order).  The load has a whole step to land, and no
-  // register carries a row from one step to the next (with rows carried in
-  // rotating registers, each rotation moved a load's destination and so waited
-  // for it).
+  // Step t reads ring rows t .. t + 5 and prefetches step t + 1's rows in its
+  // last chunk; it loads row t + 8 at its start and stores it at its end into
+  // the slot of row t (dead by then: a wave's LDS operations run in order).
+  // The load has a whole step to land, and no register carries a row from
+  // one step to the next.
   auto step = [&](int t, auto A, auto B) {
-    unsigned nx = 0;
+    Row nx{0u, 0u};
     S.template chunks<0, decltype(A)::value, decltype(B)::value>(row_base(t), row_base(t + 1), wrow(t), wrow(t - 2),
                                                                   wrow(t + 1), wrow(t - 1),
-                                                                  [&]() { nx = load_row(t + LM_RW_SLOTS); });
-    store_row(t + LM_RW_SLOTS, nx);
+                                                                  [&]() { nx = load_row(t + HS); });
+    store_row(t + HS, nx);
   };
   using T1 = std::true_type;
   using F0 = std::false_type;
@@ -497,23 +561,26 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
 #pragma unroll
     for (int c = 0; c < PK_C; ++c) acc[p][c] = S.acc[p][c];
 
-  // epilogue, per wave (the ring is dead: this wave's reads were issued first)
+  // epilogue (the ring is dead: this wave's reads were issued first)
   unsigned bits = 0;
+  if (valid) {
 #pragma unroll
-  for (int p = 0; p < PK_R / 2; ++p)
+    for (int p = 0; p < PK_R / 2; ++p)
 #pragma unroll
-    for (int c = 0; c < PK_C; ++c) {
-      const int x = ox0 + lx * PK_C + c;
-      const int y0 = oy0 + ly * PK_R + 2 * p;
-      if (x < D.ow && y0 < D.oh && acc[p][c].x > 0.0f) bits |= 1u << ((2 * p) * PK_C + c);
-      if (x < D.ow && y0 + 1 < D.oh && acc[p][c].y > 0.0f) bits |= 1u << ((2 * p + 1) * PK_C + c);
-    }
+      for (int c = 0; c < PK_C; ++c) {
+        const int x = ox0 + lx * PK_C + c;
+        const int y0 = oy0 + ly * PK_R + 2 * p;
+        if (x < D.ow && y0 < D.oh && acc[p][c].x > 0.0f) bits |= 1u << ((2 * p) * PK_C + c);
+        if (x < D.ow && y0 + 1 < D.oh && acc[p][c].y > 0.0f) bits |= 1u << ((2 * p + 1) * PK_C + c);
+      }
+  }
   if (D.kind != 0) {
-    // tail map: the tile's 16 rows x <= 4 u32 words (ox0 is a multiple of 80,
-    // so 80 columns touch at most 4 words) = one word per lane, gathered in
-    // the ring, then ORed into the slot's bitmap
+    // tail map (the halves are one 80 x 16 tile: rows 4 (lane >> 4) + r of
+    // it): 16 rows x <= 4 u32 words (ox0 is a multiple of 80, so 80 columns
+    // touch at most 4 words) = one word per lane, gathered in the ring, then
+    // ORed into the slot's bitmap
     unsigned* s_tb = reinterpret_cast<unsigned*>(ring);
-    const int w0 = ox0 >> 5;
+    const int w0 = ox0 >> 5;  // both halves: the tile's columns
     s_tb[lane] = 0u;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -522,43 +589,45 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
       for (int c = 0; c < PK_C; ++c)
         if (bits & (1u << (r * PK_C + c))) {
           const int x = ox0 + lx * PK_C + c;
-          atomicOr(&s_tb[(ly * PK_R + r) * 4 + (x >> 5) - w0], 1u << (x & 31));
+          atomicOr(&s_tb[((lane >> 4) * PK_R + r) * 4 + (x >> 5) - w0], 1u << (x & 31));
         }
     __builtin_amdgcn_wave_barrier();
     const unsigned v = s_tb[lane];
     unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(tailbin + (int64_t)slot * tailbin_slot_bytes) +
                                 (D.list ? (int64_t)K.tail_hb * K.tail_nw : 0);
-    const int y = oy0 + (lane >> 2), gw = w0 + (lane & 3);
+    const int y = oy0 - h * LM_RW_HTH + (lane >> 2), gw = w0 + (lane & 3);  // rows from the tile's top
     if (v && y < D.oh && gw < K.tail_nw) atomicOr(&tb[(int64_t)y * K.tail_nw + gw], v);
     return;
   }
   bits &= mbits;
-  // keys: one slot per set bit, bit position by bit position (ballot + mbcnt),
-  // one global atomic per wave
+  // keys: one slot per set bit, bit position by bit position (ballot + mbcnt
+  // within the half), one global atomic per half
   int off[PK_R * PK_C];
-  int tot = 0;
+  int tot0 = 0, tot1 = 0;
 #pragma unroll
   for (int k = 0; k < PK_R * PK_C; ++k) {
     const unsigned long long m = __ballot((bits >> k) & 1u);
-    off[k] = tot + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-    tot += __popcll(m);
+    const unsigned m0 = (unsigned)m, m1 = (unsigned)(m >> 32);
+    off[k] = h ? tot1 + (int)__builtin_amdgcn_mbcnt_hi(m1, 0u) : tot0 + (int)__builtin_amdgcn_mbcnt_lo(m0, 0u);
+    tot0 += __popc(m0);
+    tot1 += __popc(m1);
   }
-  if (tot == 0) return;
+  if (tot0 + tot1 == 0) return;
   int base_k = 0;
-  if (lane == 0) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
-  base_k = __shfl(base_k, 0);
+  if ((lane == 0 && tot0) || (lane == 32 && tot1)) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], h ? tot1 : tot0);
+  base_k = h ? __shfl(base_k, 32) : __shfl(base_k, 0);
   unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k;
 #pragma unroll
   for (int p = 0; p < PK_R / 2; ++p)
 #pragma unroll
     for (int c = 0; c < PK_C; ++c)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int r = 2 * p + h, k = r * PK_C + c;
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = 2 * p + hh, k = r * PK_C + c;
         if (bits & (1u << k)) {
           const int y = oy0 + ly * PK_R + r, x = ox0 + lx * PK_C + c;
-          const float s = h ? acc[p][c].y : acc[p][c].x;
-          kl[off[k]] = ((unsigned long long)(~__float_as_uint(s)) << 32) | (unsigned)(y * D.ow + x);
+          const float sc = hh ? acc[p][c].y : acc[p][c].x;
+          kl[off[k]] = ((unsigned long long)(~__float_as_uint(sc)) << 32) | (unsigned)(y * D.ow + x);
         }
       }
 }
@@ -573,12 +642,11 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
   const LmConst& K = *Kp;
   extern __shared__ uint4 lds_rw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int slot;
-  CorrTile T;
-  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, tl_cnt, tl_list, slot, T)) return;
-  float* ring = reinterpret_cast<float*>(lds_rw) + wave * (LM_RW_SLOTS + 1) * rw_stride(KW);
-  rw_tile<KW, UNF>(K, K.det[T.d], slot, T.oy0, T.ox0, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin,
-                   tailbin_slot_bytes);
+  int d;
+  RwHalves H;
+  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, tl_cnt, tl_list, d, H)) return;
+  float* ring = reinterpret_cast<float*>(lds_rw) + wave * rw_ring_floats(KW);
+  rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);
 }
 
 // Every ring detector of the context in ONE launch (longest first), so the
@@ -586,7 +654,7 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
 // branches to its width's body.  G.ring_floats: LDS floats per wave (the
 // widest detector's ring).
 template <bool UNF>
-__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_corr_rw_all(
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_corr_rw_all(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
     int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
@@ -594,16 +662,15 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(5
   const LmConst& K = *Kp;
   extern __shared__ uint4 lds_rw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int slot;
-  CorrTile T;
-  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, tl_cnt, tl_list, slot, T)) return;
+  int d;
+  RwHalves H;
+  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, tl_cnt, tl_list, d, H)) return;
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * G.ring_floats;
-  const LmDet D = K.det[T.d];
+  const LmDet D = K.det[d];
   switch (D.kw) {
 #define LM_KW_CASE(n)                                                                                             \
   case n:                                                                                                         \
-    rw_tile<n, UNF>(K, D, slot, T.oy0, T.ox0, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, \
-                    tailbin_slot_bytes);                                                                          \
+    rw_tile<n, UNF>(K, D, H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);       \
     break;
     LM_KW_LIST_RW_ALL(LM_KW_CASE)
 #undef LM_KW_CASE
@@ -713,46 +780,43 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
 typedef _Float16 lm_h8 __attribute__((ext_vector_type(8)));
 typedef float lm_f32x16 __attribute__((ext_vector_type(16)));
 
-// u8 window -> f16 LDS (same loads as tile_fill_f32, one half per pixel).
+// u8 window -> f16 LDS: each thread converts 8 pixels per item (one 8-byte
+// global load at any alignment, one 16-byte LDS store: the row stride is a
+// multiple of 8 halfs); up to 7 columns past `cols` are written (inside the
+// row's stride) and never read.
 DEV void tile_fill_f16(_Float16* __restrict__ lds, int stride, const uint8_t* __restrict__ src, int ew, int rows,
                        int cols) {
-  const int mis = (int)((uintptr_t)src & 15);
-  const uint8_t* __restrict__ a = src - mis;
-  const int nch = (mis + cols + 15) >> 4;
-  const int total = rows * nch;
+  const int ng = (cols + 7) >> 3;
+  const int total = rows * ng;
   for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
-    uint4 v[4];
+    uint2 v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
       if (e < total) {
-        const int r = e / nch, ch = e - r * nch;
-        v[u] = *reinterpret_cast<const uint4*>(a + (int64_t)r * ew + ch * 16);
+        const int r = e / ng, g = e - r * ng;
+        __builtin_memcpy(&v[u], src + (int64_t)r * ew + 8 * g, 8);
       }
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
       if (e < total) {
-        const int r = e / nch, ch = e - r * nch;
-        const int c0 = ch * 16 - mis;
-        _Float16* __restrict__ o = lds + r * stride + c0;
-        const unsigned w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-        if (c0 >= 0 && c0 + 16 <= cols) {  // whole chunk inside the window: straight-line stores
+        const int r = e / ng, g = e - r * ng;
+        lm_h8 h;
 #pragma unroll
-          for (int k = 0; k < 16; ++k) o[k] = (_Float16)(float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-        } else {
-#pragma unroll
-          for (int k = 0; k < 16; ++k)
-            if (c0 + k >= 0 && c0 + k < cols) o[k] = (_Float16)(float)((w[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+        for (int k = 0; k < 4; ++k) {
+          h[k] = (_Float16)(float)((v[u].x >> (8 * k)) & 0xFFu);
+          h[4 + k] = (_Float16)(float)((v[u].y >> (8 * k)) & 0xFFu);
         }
+        *reinterpret_cast<lm_h8*>(lds + r * stride + 8 * g) = h;
       }
     }
   }
 }
 
 template <int NCH>
-__global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __restrict__ Kp, const LmDetGroup G,
+__global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(NCH <= 7 ? 3 : 2))) void k_corr_f16(const LmConst* __restrict__ Kp, const LmDetGroup G,
                                                             const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
                                                             const uint4* __restrict__ bfrag, int s0,
                                                             unsigned long long* __restrict__ keys,
@@ -790,30 +854,51 @@ __global__ __launch_bounds__(LM_F16_THREADS) void k_corr_f16(const LmConst* __re
   // row loop has no barrier (round 2 staged them through LDS with one
   // __syncthreads per row)
   const lm_h8* __restrict__ bsrc = reinterpret_cast<const lm_h8*>(bfrag + D.w16_off) + lane;
-  lm_h8 b0[NCH], b1[NCH];
+  // Detector rows in groups of three, flattened to 3 NCH (row, chunk) steps:
+  // step k's A fragments were read two steps earlier (a 3-deep register
+  // ring), so an MFMA never waits on the LDS read issued right before it; B
+  // fragments of row i + 3 load while rows i + 1, i + 2 multiply (one row's
+  // MFMAs are shorter than an L2 hit under load).  With the group unrolled,
+  // every ring index is static.
+  lm_h8 bf[3][NCH], ar[3][LM_F16_T];
   auto load_b = [&](lm_h8 (&b)[NCH], int i) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) b[c] = bsrc[(int64_t)(i * NCH + c) * 64];
   };
-  auto mma_row = [&](const lm_h8 (&b)[NCH], int i) {
-    const _Float16* __restrict__ ai = arow + i * STR;
+  auto load_a = [&](lm_h8 (&a)[LM_F16_T], int i, int c) {
+    const _Float16* __restrict__ ai = arow + min(i, kh - 1) * STR + 16 * c;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
-#pragma unroll
-      for (int t = 0; t < LM_F16_T; ++t) {
-        const lm_h8 a = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR + 16 * c);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[c], acc[t], 0, 0, 0);
-      }
+    for (int t = 0; t < LM_F16_T; ++t) a[t] = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR);
   };
-  load_b(b0, 0);
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    if (q < kh) load_b(bf[q], q);
+  load_a(ar[0], 0, 0);
+  load_a(ar[1], 1 / NCH, 1 % NCH);
   int i = 0;
-  for (; i + 1 < kh; i += 2) {
-    load_b(b1, i + 1);
-    mma_row(b0, i);
-    if (i + 2 < kh) load_b(b0, i + 2);
-    mma_row(b1, i + 1);
+  for (; i + 2 < kh; i += 3) {
+#pragma unroll
+    for (int k = 0; k < 3 * NCH; ++k) {
+      const int q = k / NCH, c = k % NCH, k2 = k + 2;
+      load_a(ar[k2 % 3], i + k2 / NCH, k2 % NCH);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < LM_F16_T; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[k % 3][t], bf[q][c], acc[t], 0, 0, 0);
+      if (c == NCH - 1 && i + q + 3 < kh) load_b(bf[q], i + q + 3);
+    }
   }
-  if (i < kh) mma_row(b0, i);
+  // the last kh % 3 rows (their B fragments are in bf[0], bf[1])
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+    if (i + q < kh)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        lm_h8 a[LM_F16_T];
+        load_a(a, i + q, c);
+#pragma unroll
+        for (int t = 0; t < LM_F16_T; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[t], bf[q][c], acc[t], 0, 0, 0);
+      }
 
   const int x = ox0 + 32 * wave + r;
   if (D.kind != 0) {
@@ -955,23 +1040,24 @@ hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t
 // LocoMouse_class.cpp:782, :817, :849, :864), so an output tile of a point
 // detector with no pixel > 25 yields nothing: its filter2D outputs are all
 // discarded by the reference, and the correlation does not compute them.
-// k_tileflag: one wave per (slot, view, LM_TW x LM_RW_TH output tile) writes
-// the tile's flag byte (1: some pixel > 25); the tile's mouse pixels are read
-// from the ext crop k_ingest just wrote (16 rows x 4 lanes of 20 columns).
+// k_tileflag: one wave per (slot, view, 80 x 16 output region) writes the
+// flag bytes (1: some pixel > 25) of the region's two 80 x 8 half-tiles; the
+// mouse pixels are read from the ext crop k_ingest just wrote (16 rows x 4
+// lanes of 20 columns: lanes 0-31 the upper half-tile, 32-63 the lower).
 __global__ __launch_bounds__(256) void k_tileflag(const LmConst* __restrict__ Kp, const uint8_t* __restrict__ ext,
                                                   int64_t ext_slot_bytes, int s0, uint8_t* __restrict__ flags) {
   const LmConst& K = *Kp;
   const int slot = s0 + blockIdx.y;
   const int g = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-  const int n0 = K.fl_tx[0] * K.fl_ty[0];
+  const int n0 = K.fl_tx[0] * ((K.fl_ty[0] + 1) >> 1);
   const int v = g < n0 ? 0 : 1;
   const int t = v ? g - n0 : g;
-  if (t >= K.fl_tx[v] * K.fl_ty[v]) return;
+  if (t >= K.fl_tx[v] * ((K.fl_ty[v] + 1) >> 1)) return;
   const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
-  const int ty = t / K.fl_tx[v], tx = t - ty * K.fl_tx[v];
+  const int ry = t / K.fl_tx[v], tx = t - ry * K.fl_tx[v];
   const int lane = threadIdx.x & 63;
-  const int y = ty * LM_RW_TH + (lane >> 2), x0 = tx * LM_TW + (lane & 3) * (LM_TW / 4);
-  static_assert(LM_RW_TH * 4 == 64 && LM_TW / 4 == 20, "k_tileflag lane map");
+  const int y = ry * LM_RW_TH + (lane >> 2), x0 = tx * LM_TW + (lane & 3) * (LM_TW / 4);
+  static_assert(LM_RW_TH * 4 == 64 && LM_RW_HTH * 8 == 64 && LM_TW / 4 == 20, "k_tileflag lane map");
   bool bright = false;
   if (y < D.oh && x0 < D.ow) {
     const uint8_t* row = ext + (int64_t)slot * ext_slot_bytes + (v ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
@@ -990,78 +1076,82 @@ __global__ __launch_bounds__(256) void k_tileflag(const LmConst* __restrict__ Kp
         if (4 * j + k < nb && ((w >> (8 * k)) & 0xFFu) > 25u) bright = true;
     }
   }
-  const bool any = __ballot(bright) != 0ull;
-  if (lane == 0) flags[(int64_t)slot * K.fl_slot + K.fl_off[v] + t] = any ? 1 : 0;
+  const unsigned long long m = __ballot(bright);
+  uint8_t* __restrict__ f = flags + (int64_t)slot * K.fl_slot + K.fl_off[v] + (2 * ry) * K.fl_tx[v] + tx;
+  if (lane == 0) f[0] = (unsigned)m ? 1 : 0;
+  if (lane == 32 && 2 * ry + 1 < K.fl_ty[v]) f[K.fl_tx[v]] = (unsigned)(m >> 32) ? 1 : 0;
 }
 
 // k_tilelist: one 1024-thread workgroup per view lists the bright tiles of
 // slots s0 .. s0 + nproc - 1 in slot order, (slot << 16) | tile, at
 // view * tl_stride, their count in cnt[view] and the consumed outputs they
-// hold (edge tiles are partial) in cnt[2 + view] (lm_debug_corr_work).
+// hold (edge tiles are partial) in cnt[2 + view] (lm_debug_corr_work).  The
+// flattened (slot, flag dword) range is cut into one run of consecutive
+// dwords per thread: count, one workgroup scan, list (the second pass re-reads
+// the dwords from L1/L2).
 __global__ __launch_bounds__(1024) void k_tilelist(const LmConst* __restrict__ Kp, int s0, int nproc,
                                                    const uint8_t* __restrict__ flags, int32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ list) {
   const LmConst& K = *Kp;
   const int v = blockIdx.x;
-  const int nt = K.fl_tx[v] * K.fl_ty[v];
+  const int ftx = K.fl_tx[v], nt = ftx * K.fl_ty[v];
+  const int nw4 = (nt + 3) >> 2;  // flag dwords per slot (fl_slot and fl_off are multiples of 4)
+  const int items = nproc * nw4;
+  const int run = (items + 1023) >> 10;
+  const int i0 = min(items, (int)threadIdx.x * run), i1 = min(items, i0 + run);
   uint32_t* __restrict__ out = list + (int64_t)v * K.tl_stride;
   const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
+  const uint8_t* __restrict__ fv = flags + K.fl_off[v];
+  auto dword = [&](int i) {
+    const int slot = i / nw4;
+    return reinterpret_cast<const unsigned*>(fv + (int64_t)(s0 + slot) * K.fl_slot)[i - slot * nw4];
+  };
   __shared__ int s_wave[16];
-  __shared__ int s_carry, s_outs;
+  __shared__ int s_outs;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) {
-    s_carry = 0;
-    s_outs = 0;
-  }
-  int outs = 0;
-  for (int c0 = 0; c0 < nproc; c0 += 1024) {
-    const int i = c0 + (int)threadIdx.x;
-    const uint8_t* __restrict__ f = flags + (int64_t)(s0 + i) * K.fl_slot + K.fl_off[v];
-    // the slot's flag bytes (0 / 1) as dwords: fl_slot and fl_off are multiples of 4
-    const unsigned* __restrict__ f4 = reinterpret_cast<const unsigned*>(f);
-    const int nw4 = (nt + 3) >> 2;
-    int n = 0;
-    if (i < nproc)
-      for (int w = 0; w < nw4; ++w) n += (int)((f4[w] * 0x01010101u) >> 24);  // k_tileflag writes every byte < nt; the pad stays 0
-    // exclusive scan over the workgroup
-    int incl = n;
+  if (threadIdx.x == 0) s_outs = 0;
+  int n = 0;
+#pragma unroll 8
+  for (int i = i0; i < i1; ++i) n += (int)((dword(i) * 0x01010101u) >> 24);  // k_tileflag writes every byte < nt; the pad stays 0
+  int incl = n;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(incl, o);
-      if (lane >= o) incl += u;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) s_wave[wid] = incl;
+  __syncthreads();
+  int before = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    before += k < wid ? s_wave[k] : 0;
+    total += s_wave[k];
+  }
+  int pos = before + incl - n, outs = 0;
+  for (int i = i0; i < i1 && n; ++i) {
+    unsigned m = dword(i);
+    const int slot = i / nw4, w = i - slot * nw4;
+    while (m) {
+      const int t = 4 * w + (__ffs(m) - 1) / 8;
+      m &= m - 1;
+      --n;
+      out[pos++] = ((uint32_t)(s0 + slot) << 16) | (uint32_t)t;
+      const int ty = t / ftx, tx = t - ty * ftx;
+      outs += min(LM_RW_HTH, D.oh - ty * LM_RW_HTH) * min(LM_TW, D.ow - tx * LM_TW);
     }
-    __syncthreads();  // s_carry of the previous chunk is final, s_wave free
-    if (lane == 63) s_wave[wid] = incl;
-    __syncthreads();
-    int before = s_carry;
-    for (int w = 0; w < wid; ++w) before += s_wave[w];
-    int pos = before + incl - n;
-    if (i < nproc)
-      for (int w = 0; w < nw4; ++w) {
-        unsigned m = f4[w];
-        while (m) {
-          const int t = 4 * w + (__ffs(m) - 1) / 8;
-          m &= m - 1;
-          out[pos++] = ((uint32_t)(s0 + i) << 16) | (uint32_t)t;
-          const int ty = t / K.fl_tx[v], tx = t - ty * K.fl_tx[v];
-          outs += min(LM_RW_TH, D.oh - ty * LM_RW_TH) * min(LM_TW, D.ow - tx * LM_TW);
-        }
-      }
-    __syncthreads();
-    if (threadIdx.x == 1023) s_carry = before + incl;
   }
   for (int o = 32; o > 0; o >>= 1) outs += __shfl_xor(outs, o);
   if (lane == 0) atomicAdd(&s_outs, outs);
   __syncthreads();
   if (threadIdx.x == 0) {
-    cnt[v] = s_carry;
+    cnt[v] = total;
     cnt[2 + v] = s_outs;
   }
 }
 
 hipError_t launch_tile_lists(hipStream_t st, const LmConst* dK, const LmConst& K, const uint8_t* ext,
                              int64_t ext_slot_bytes, int s0, int nproc, const CorrDark& dk) {
-  const int nt = K.fl_tx[0] * K.fl_ty[0] + K.fl_tx[1] * K.fl_ty[1];
+  const int nt = K.fl_tx[0] * ((K.fl_ty[0] + 1) / 2) + K.fl_tx[1] * ((K.fl_ty[1] + 1) / 2);  // 80 x 16 regions
   k_tileflag<<<dim3((unsigned)((nt + 3) / 4), (unsigned)nproc), 256, 0, st>>>(dK, ext, ext_slot_bytes, s0, dk.flags);
   k_tilelist<<<2, 1024, 0, st>>>(dK, s0, nproc, dk.flags, dk.cnt, dk.list);
   return hipGetLastError();

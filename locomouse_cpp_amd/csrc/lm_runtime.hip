@@ -460,7 +460,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     for (int v = 0; v < 2; ++v) {
       const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
       K.fl_tx[v] = (D.ow + LM_TW - 1) / LM_TW;
-      K.fl_ty[v] = (D.oh + LM_RW_TH - 1) / LM_RW_TH;
+      K.fl_ty[v] = (D.oh + LM_RW_HTH - 1) / LM_RW_HTH;
       K.fl_off[v] = o;
       o += (K.fl_tx[v] * K.fl_ty[v] + 3) / 4 * 4;
     }
@@ -570,8 +570,8 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       const bool f16 = su->corr_precision == LM_CORR_F16;
       const bool ring = !f16 && corr_ring(D.kw);
       const void* fn = f16 ? corr_kernel_f16(D.kw)
-                       : ring && m == 1 ? corr_kernel_rw_all(c->unfused)
-                                        : corr_kernel(D.kw, c->unfused);
+                       : ring && m == 1 && rw_all_width(D.kw) ? corr_kernel_rw_all(c->unfused)
+                                                              : corr_kernel(D.kw, c->unfused);
       size_t need;
       if (f16) {
         D.chunk_rows = D.kh;
@@ -599,7 +599,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       G.ids[G.n] = d;
       G.tile_end[G.n] = prev + D.tiles_x * D.tiles_y;
       ++G.n;
-      if (ring) G.ring_floats = std::max(G.ring_floats, (LM_RW_SLOTS + 1) * rw_stride(D.kw));
+      if (ring) G.ring_floats = std::max(G.ring_floats, rw_ring_floats(D.kw));
       P.lds[gi] = std::max(P.lds[gi], need);
     }
   }

@@ -38,5 +38,8 @@ def test_ring_correlation_budget(kernels):
     ring = {k: r for k, r in kernels.items() if re.match(r"_Z9k_corr_rwILi\d+ELb[01]EE", k)}
     assert len(ring) >= 2 * 25, "expected the 25 ring widths x 2 arithmetic modes"
     for k, r in ring.items():
+        kw = int(re.match(r"_Z9k_corr_rwILi(\d+)E", k).group(1))
         assert r["sgpr_spill_count"] == 0, (k, r)
-        assert r["vgpr_count"] <= 96, (k, r)  # 5 waves per SIMD
+        # 5 waves per SIMD up to kw 32; wider rings (>= 8.5 KB of LDS per
+        # wave) run at most 4 waves per SIMD, which 128 VGPRs allow
+        assert r["vgpr_count"] <= (96 if kw <= 32 else 128), (k, r)
