@@ -67,8 +67,10 @@ __host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
 #define LM_F16_WAVES 4  // waves side by side, 32 output columns each (5: -4 % k_corr at C5 but fewer frames/s; C3 worse)
 #endif
 #define LM_F16_TW (32 * LM_F16_WAVES)
-#define LM_F16_TH 64
-#define LM_F16_T 2  // 32-row accumulator tiles per wave
+#ifndef LM_F16_T
+#define LM_F16_T 2  // 32-row accumulator tiles per wave (2 or 4)
+#endif
+#define LM_F16_TH (32 * LM_F16_T)
 #define LM_F16_THREADS (64 * LM_F16_WAVES)
 #define LM_F16_MAX_NCH 10
 

@@ -816,7 +816,7 @@ DEV void tile_fill_f16(_Float16* __restrict__ lds, int stride, const uint8_t* __
 }
 
 template <int NCH>
-__global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(NCH <= 7 ? 3 : 2))) void k_corr_f16(const LmConst* __restrict__ Kp, const LmDetGroup G,
+__global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(NCH <= 7 && LM_F16_T == 2 ? 3 : 2))) void k_corr_f16(const LmConst* __restrict__ Kp, const LmDetGroup G,
                                                             const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
                                                             const uint4* __restrict__ bfrag, int s0,
                                                             unsigned long long* __restrict__ keys,
@@ -837,7 +837,11 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
   constexpr int cols = f16_cols(NCH), STR = f16_stride(cols);
   const int rows = LM_F16_TH + kh - 1;
   _Float16* __restrict__ img = reinterpret_cast<_Float16*>(lds_f16);
-  tile_fill_f16(img, STR, corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0), K.ext_w[D.view], rows, cols);
+#ifndef LM_F16_EXP  // timing experiments (scripts/build_variant.sh): 1 no window fill, 2 no MFMA; both ignore the mask
+#define LM_F16_EXP 0
+#endif
+  if (LM_F16_EXP != 1)
+    tile_fill_f16(img, STR, corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0), K.ext_w[D.view], rows, cols);
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
 
@@ -862,45 +866,86 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
   // every ring index is static.
   lm_h8 bf[3][NCH], ar[3][LM_F16_T];
   auto load_b = [&](lm_h8 (&b)[NCH], int i) {
+    if (LM_F16_EXP == 4 && (i & 1)) return;  // experiment: half the B fragment loads (stale data)
 #pragma unroll
     for (int c = 0; c < NCH; ++c) b[c] = bsrc[(int64_t)(i * NCH + c) * 64];
   };
-  auto load_a = [&](lm_h8 (&a)[LM_F16_T], int i, int c) {
-    const _Float16* __restrict__ ai = arow + min(i, kh - 1) * STR + 16 * c;
+  // A wave's 32 x 32 accumulator tile t runs only when it holds an output
+  // (inside oh x ow) and, for a point detector, some output whose mouse pixel
+  // is > 25 (the rest are zeroed by the reference's mask and produce no key)
+  const int x = ox0 + 32 * wave + r;
+  const _Float16* __restrict__ mrow = img + (D.m_y - D.in_y) * STR + 32 * wave + r + (D.m_x - D.in_x);
+  // skip groups: the wave's upper and lower LM_F16_T / 2 tiles
+  static_assert(LM_F16_T == 2 || LM_F16_T == 4, "2 or 4 accumulator tiles per wave");
+  constexpr int TG = LM_F16_T / 2;
+  bool on[2];
 #pragma unroll
-    for (int t = 0; t < LM_F16_T; ++t) a[t] = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR);
-  };
+  for (int g = 0; g < 2; ++g) {
+    bool any = false;
 #pragma unroll
-  for (int q = 0; q < 3; ++q)
-    if (q < kh) load_b(bf[q], q);
-  load_a(ar[0], 0, 0);
-  load_a(ar[1], 1 / NCH, 1 % NCH);
-  int i = 0;
-  for (; i + 2 < kh; i += 3) {
+    for (int t = g * TG; t < (g + 1) * TG; ++t)
+      if (x < D.ow && oy0 + 32 * t < D.oh) {
+        if (D.kind != 0 || LM_F16_EXP != 0) {
+          any = true;
+        } else {
 #pragma unroll
-    for (int k = 0; k < 3 * NCH; ++k) {
-      const int q = k / NCH, c = k % NCH, k2 = k + 2;
-      load_a(ar[k2 % 3], i + k2 / NCH, k2 % NCH);
-      __builtin_amdgcn_sched_barrier(0);
+          for (int q = 0; q < 16; ++q) {
+            const int ly = 32 * t + 16 * h + q;
+            any |= oy0 + ly < D.oh && (float)mrow[ly * STR] > 25.0f;
+          }
+        }
+      }
+    on[g] = __builtin_amdgcn_readfirstlane(__ballot(any) != 0 ? 1 : 0) != 0;
+  }
+  auto mma_all = [&](auto c0, auto c1) {
+    constexpr bool ONG[2] = {decltype(c0)::value, decltype(c1)::value};
+    auto load_a = [&](lm_h8 (&a)[LM_F16_T], int i, int c) {
+      const _Float16* __restrict__ ai = arow + min(i, kh - 1) * STR + 16 * c;
 #pragma unroll
       for (int t = 0; t < LM_F16_T; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[k % 3][t], bf[q][c], acc[t], 0, 0, 0);
-      if (c == NCH - 1 && i + q + 3 < kh) load_b(bf[q], i + q + 3);
-    }
-  }
-  // the last kh % 3 rows (their B fragments are in bf[0], bf[1])
+        if (ONG[t / TG]) a[t] = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR);
+    };
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
-    if (i + q < kh)
+    for (int q = 0; q < 3; ++q)
+      if (q < kh) load_b(bf[q], q);
+    load_a(ar[0], 0, 0);
+    load_a(ar[1], 1 / NCH, 1 % NCH);
+    int i = 0;
+    for (; i + 2 < kh; i += 3) {
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        lm_h8 a[LM_F16_T];
-        load_a(a, i + q, c);
+      for (int k = 0; k < 3 * NCH; ++k) {
+        const int q = k / NCH, c = k % NCH, k2 = k + 2;
+        load_a(ar[k2 % 3], i + k2 / NCH, k2 % NCH);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int t = 0; t < LM_F16_T; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[t], bf[q][c], acc[t], 0, 0, 0);
+        for (int t = 0; t < LM_F16_T; ++t)
+          if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[k % 3][t], bf[q][c], acc[t], 0, 0, 0);
+        if (c == NCH - 1 && i + q + 3 < kh) load_b(bf[q], i + q + 3);
       }
+    }
+    // the last kh % 3 rows (their B fragments are in bf[0], bf[1])
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (i + q < kh)
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          lm_h8 a[LM_F16_T];
+          load_a(a, i + q, c);
+#pragma unroll
+          for (int t = 0; t < LM_F16_T; ++t)
+            if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[t], bf[q][c], acc[t], 0, 0, 0);
+        }
+  };
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+  if (LM_F16_EXP == 2) {
+  } else if (on[0] && on[1])
+    mma_all(T1{}, T1{});
+  else if (on[0])
+    mma_all(T1{}, F0{});
+  else if (on[1])
+    mma_all(F0{}, T1{});
 
-  const int x = ox0 + 32 * wave + r;
   if (D.kind != 0) {
     // bits straight from a ballot: this wave owns u32 word (ox0 / 32 + wave) of
     // each of its rows (lanes 0-31: row y, lanes 32-63: row y + 4)
@@ -917,8 +962,8 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
       }
     return;
   }
-  unsigned bits = 0;
-  const _Float16* __restrict__ mrow = img + (D.m_y - D.in_y) * STR + 32 * wave + r + (D.m_x - D.in_x);
+  using Bits = std::conditional_t<(LM_F16_T > 2), unsigned long long, unsigned>;
+  Bits bits = 0;
 #pragma unroll
   for (int t = 0; t < LM_F16_T; ++t)
 #pragma unroll
@@ -926,9 +971,9 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
       const int ly = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
       const int y = oy0 + ly;
       const float pix = (float)mrow[ly * STR];
-      if (y < D.oh && x < D.ow && pix > 25.0f && acc[t][q] > 0.0f) bits |= 1u << (16 * t + q);
+      if (y < D.oh && x < D.ow && pix > 25.0f && acc[t][q] > 0.0f) bits |= (Bits)1 << (16 * t + q);
     }
-  const int nk = __popc(bits);
+  const int nk = LM_F16_T > 2 ? __popcll((unsigned long long)bits) : __popc((unsigned)bits);
   const int off = nk ? atomicAdd(&s_cnt, nk) : 0;
   __syncthreads();
   if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
@@ -939,7 +984,7 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
   for (int t = 0; t < LM_F16_T; ++t)
 #pragma unroll
     for (int q = 0; q < 16; ++q)
-      if (bits & (1u << (16 * t + q))) {
+      if (bits & ((Bits)1 << (16 * t + q))) {
         const int y = oy0 + 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
         const float score = acc[t][q] * D.inv_wscale;
         kl[k++] = ((unsigned long long)(~__float_as_uint(score)) << 32) | (unsigned)(y * D.ow + x);
