@@ -1127,14 +1127,18 @@ __global__ __launch_bounds__(256) void k_tileflag(const LmConst* __restrict__ Kp
   if (lane == 32 && 2 * ry + 1 < K.fl_ty[v]) f[K.fl_tx[v]] = (unsigned)(m >> 32) ? 1 : 0;
 }
 
-// k_tilelist: one 1024-thread workgroup per view lists the bright tiles of
+// k_tilelist: one LM_TL_THREADS-thread workgroup per view lists the bright tiles of
 // slots s0 .. s0 + nproc - 1 in slot order, (slot << 16) | tile, at
 // view * tl_stride, their count in cnt[view] and the consumed outputs they
 // hold (edge tiles are partial) in cnt[2 + view] (lm_debug_corr_work).  The
 // flattened (slot, flag dword) range is cut into one run of consecutive
 // dwords per thread: count, one workgroup scan, list (the second pass re-reads
 // the dwords from L1/L2).
-__global__ __launch_bounds__(1024) void k_tilelist(const LmConst* __restrict__ Kp, int s0, int nproc,
+#ifndef LM_TL_THREADS
+#define LM_TL_THREADS 1024  // k_tilelist workgroup size (a multiple of 64, <= 1024)
+#endif
+static_assert(LM_TL_THREADS % 64 == 0 && LM_TL_THREADS <= 1024, "k_tilelist workgroup size");
+__global__ __launch_bounds__(LM_TL_THREADS) void k_tilelist(const LmConst* __restrict__ Kp, int s0, int nproc,
                                                    const uint8_t* __restrict__ flags, int32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ list) {
   const LmConst& K = *Kp;
@@ -1142,7 +1146,7 @@ __global__ __launch_bounds__(1024) void k_tilelist(const LmConst* __restrict__ K
   const int ftx = K.fl_tx[v], nt = ftx * K.fl_ty[v];
   const int nw4 = (nt + 3) >> 2;  // flag dwords per slot (fl_slot and fl_off are multiples of 4)
   const int items = nproc * nw4;
-  const int run = (items + 1023) >> 10;
+  const int run = (items + LM_TL_THREADS - 1) / LM_TL_THREADS;
   const int i0 = min(items, (int)threadIdx.x * run), i1 = min(items, i0 + run);
   uint32_t* __restrict__ out = list + (int64_t)v * K.tl_stride;
   const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
@@ -1151,7 +1155,7 @@ __global__ __launch_bounds__(1024) void k_tilelist(const LmConst* __restrict__ K
     const int slot = i / nw4;
     return reinterpret_cast<const unsigned*>(fv + (int64_t)(s0 + slot) * K.fl_slot)[i - slot * nw4];
   };
-  __shared__ int s_wave[16];
+  __shared__ int s_wave[LM_TL_THREADS / 64];
   __shared__ int s_outs;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_outs = 0;
@@ -1168,7 +1172,7 @@ __global__ __launch_bounds__(1024) void k_tilelist(const LmConst* __restrict__ K
   __syncthreads();
   int before = 0, total = 0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
+  for (int k = 0; k < LM_TL_THREADS / 64; ++k) {
     before += k < wid ? s_wave[k] : 0;
     total += s_wave[k];
   }
@@ -1198,7 +1202,7 @@ hipError_t launch_tile_lists(hipStream_t st, const LmConst* dK, const LmConst& K
                              int64_t ext_slot_bytes, int s0, int nproc, const CorrDark& dk) {
   const int nt = K.fl_tx[0] * ((K.fl_ty[0] + 1) / 2) + K.fl_tx[1] * ((K.fl_ty[1] + 1) / 2);  // 80 x 16 regions
   k_tileflag<<<dim3((unsigned)((nt + 3) / 4), (unsigned)nproc), 256, 0, st>>>(dK, ext, ext_slot_bytes, s0, dk.flags);
-  k_tilelist<<<2, 1024, 0, st>>>(dK, s0, nproc, dk.flags, dk.cnt, dk.list);
+  k_tilelist<<<2, LM_TL_THREADS, 0, st>>>(dK, s0, nproc, dk.flags, dk.cnt, dk.list);
   return hipGetLastError();
 }
 
