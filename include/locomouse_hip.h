@@ -319,7 +319,11 @@ lm_status lm_ctx_set_debug(lm_ctx* ctx, int32_t flags);
 
 /* Copy the raw correlation scores (before masking) of detector det
  * (0 paw_b, 1 snout_b, 2 tail_b, 3 paw_s, 4 snout_s, 5 tail_s) for frame
- * index f of the last batch: UNPAD region, row-major, rows x cols floats. */
+ * index f of the last collected batch: UNPAD region, row-major, rows x cols
+ * floats.  The maps live on the lane that ran the batch: once a newer batch
+ * was submitted to that lane (pipelined contexts reuse a finished lane at
+ * once) they are gone and this fails with LM_ERR_INVALID_ARGUMENT, as does
+ * lm_debug_tail_mask. */
 lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out, int32_t rows, int32_t cols);
 
 /* Copy the bottom TAIL_MASK (0/255, tail_box_width x bottom height) of frame f. */
@@ -341,6 +345,11 @@ int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, doubl
  * every score is zeroed by setTo(0, mask), LocoMouse_class.cpp:849, :864)
  * are not computed.  -1 when not recorded (timing off, LM_CORR_DARK=0). */
 lm_status lm_debug_corr_work(const lm_ctx* ctx, int32_t* out);
+
+/* Frame slots the last collected batch processed: n, or n + 1 when its halo
+ * frame (slot 0: prev_frame, or the pipelined hand-off) was recomputed --
+ * the slots lm_debug_corr_work's counts and the tail detectors cover. */
+int32_t lm_debug_batch_slots(const lm_ctx* ctx);
 
 /* ---- whole-video bounding-box pass ----
  *

@@ -127,10 +127,14 @@ struct Lane {
     bool carry = false;
   } pend;
   int64_t seq = -1;               // submission number of the batch running on this lane (-1: idle)
+  int64_t done_seq = -1;          // submission number of the last batch finished here (its debug data)
   int batch_n = 0, batch_s0 = 1;  // last finished batch
   // pipelined halos: the batch's last frame copied to the context's handoff
   // buffer / the predecessor's handoff frame copied into this lane's halo
   hipEvent_t ev_snap = nullptr, ev_consumed = nullptr;
+  // recorded after the batch's kernels (blocking sync): acquire_lane waits on
+  // it without burning a host core
+  hipEvent_t ev_done = nullptr;
   // timing (debug bit 1): events around k_corr on this lane's stream
   std::vector<std::pair<const char*, int>> t_ev;  // (kernel, index of its begin event in ev_pool)
   std::vector<const char*> t_names;               // static kernel names
@@ -157,6 +161,7 @@ struct Lane {
       for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
       if (ev_snap) (void)hipEventDestroy(ev_snap);
       if (ev_consumed) (void)hipEventDestroy(ev_consumed);
+      if (ev_done) (void)hipEventDestroy(ev_done);
       (void)hipStreamDestroy(stream);
     }
   }
@@ -210,8 +215,10 @@ struct lm_ctx {
   // is fed again at once while results still come back in frame order.
   struct BatchRec {
     int64_t seq = 0;
-    int lane = -1;  // running there; -1 once retired
+    int lane = -1;      // running there; -1 once retired
+    int ran_lane = -1;  // the lane it ran on (its debug score maps / tail mask stay there until reused)
     int first = 0, n = 0;
+    int slots = 0;      // frame slots processed: n, or n + 1 when the halo frame was recomputed
     lm_status status = LM_OK;  // a failure found while retiring, reported when collected
     std::string err;
     std::vector<uint8_t> pack;  // retired results (lm_batch_result layout)
@@ -222,7 +229,7 @@ struct lm_ctx {
   };
   std::deque<BatchRec> queue;
   BatchRec delivered;          // the last collected batch (its arrays back the returned pointers)
-  int last_lane = -1, collected_lane = 0;
+  int last_lane = -1;
   int64_t nsub = 0;            // batches submitted
   // the video position after the last submitted batch
   bool have_state = false;
@@ -735,6 +742,7 @@ void lane_alloc(lm_ctx* c, Lane& L) {
   L.h_pack.alloc((size_t)L.arena[0].pack_cap);
   HIPCHK(hipEventCreateWithFlags(&L.ev_snap, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&L.ev_consumed, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&L.ev_done, hipEventDisableTiming | hipEventBlockingSync));
 }
 
 // One epoch event per device (recorded when timing is switched on) that every
@@ -1163,6 +1171,7 @@ void retire(lm_ctx* c, Lane& L) {
   rec->t_ms = L.t_ms;
   rec->t_t0 = L.t_t0;
   rec->t_t1 = L.t_t1;
+  rec->ran_lane = L.index;
   rec->lane = -1;
   L.seq = -1;
 }
@@ -1170,26 +1179,31 @@ void retire(lm_ctx* c, Lane& L) {
 // A free lane for the next batch: the lane that ran the previous batch when
 // nothing ran there since (it carries that batch's state), else any idle
 // lane; when every lane is busy, the first one whose batch has completed is
-// retired and reused (waiting for one to complete).
+// retired and reused -- or, when none has, the host thread sleeps on the
+// oldest batch's completion event (blocking sync, not a polling loop) and
+// retires that one.
 Lane& acquire_lane(lm_ctx* c, int prev_frame) {
-  for (;;) {
-    Lane* pick = nullptr;
-    for (auto& l : c->lanes) {
-      if (l->seq >= 0) continue;
-      if (l->index == c->last_lane && l->have_state && l->last_frame == prev_frame) return *l;
-      if (!pick) pick = l.get();
-    }
-    if (pick) return *pick;
-    for (auto& l : c->lanes) {
-      const hipError_t q = hipStreamQuery(l->stream);
-      if (q != hipErrorNotReady) {
-        (void)hipGetLastError();
-        retire(c, *l);
-        return *l;
-      }
-    }
-    std::this_thread::yield();
+  Lane* pick = nullptr;
+  for (auto& l : c->lanes) {
+    if (l->seq >= 0) continue;
+    if (l->index == c->last_lane && l->have_state && l->last_frame == prev_frame) return *l;
+    if (!pick) pick = l.get();
   }
+  if (pick) return *pick;
+  Lane* oldest = nullptr;
+  for (auto& l : c->lanes) {
+    const hipError_t q = hipStreamQuery(l->stream);
+    if (q != hipErrorNotReady) {
+      (void)hipGetLastError();
+      retire(c, *l);
+      return *l;
+    }
+    if (!oldest || l->seq < oldest->seq) oldest = l.get();
+  }
+  (void)hipGetLastError();
+  HIPCHK(hipEventSynchronize(oldest->ev_done));
+  retire(c, *oldest);
+  return *oldest;
 }
 
 // Submit frames [first, first + n) to a free lane (acquire_lane).  Host
@@ -1342,6 +1356,7 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   P.carry = carry;
   P.last_n = carry ? L.last_n : 0;
   launch_attempt(c, L, 0);
+  HIPCHK(hipEventRecord(L.ev_done, st));
 
   // the video position and the lane's carry state advance now; a batch that
   // fails at collection clears the lane's state (a later batch on another
@@ -1356,6 +1371,7 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   rec.lane = L.index;
   rec.first = first;
   rec.n = n;
+  rec.slots = n + 1 - s_proc0;
   c->queue.push_back(std::move(rec));
   ++c->nsub;
   L.have_state = true;
@@ -1449,6 +1465,7 @@ void finish_batch(lm_ctx* c, Lane& L) {
   }
   L.batch_n = n;
   L.batch_s0 = P.s_proc0;
+  L.done_seq = L.seq;
   P.on = false;
 }
 
@@ -1482,7 +1499,7 @@ void collect_batch(lm_ctx* c, lm_batch_result* out) {
   c->queue.pop_front();
   if (rec.lane >= 0) {  // still on its lane: finish it there
     Lane& L = *c->lanes[rec.lane];
-    c->collected_lane = L.index;
+    rec.ran_lane = L.index;
     try {
       finish_batch(c, L);
     } catch (...) {
@@ -1578,7 +1595,14 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
 }
 
 LM_API void lm_ctx_destroy(lm_ctx* ctx) {
-  if (ctx) g_live_streams[ctx->device & 63].fetch_sub((int)ctx->lanes.size());
+  if (!ctx) return;
+  g_live_streams[ctx->device & 63].fetch_sub((int)ctx->lanes.size());
+  // batches still in flight may copy to or from the context's buffers (the
+  // hand-off frames, the arenas): every lane stream drains on the context's
+  // device before anything is freed
+  if (hipSetDevice(ctx->device) == hipSuccess)
+    for (auto& l : ctx->lanes)
+      if (l->stream) (void)hipStreamSynchronize(l->stream);
   delete ctx;
 }
 
@@ -1660,9 +1684,28 @@ LM_API lm_status lm_debug_corr_work(const lm_ctx* ctx, int32_t* out) {
   return LM_OK;
 }
 
+LM_API int32_t lm_debug_batch_slots(const lm_ctx* ctx) { return ctx ? ctx->delivered.slots : 0; }
+
+namespace {
+// The lane whose device buffers still hold the last collected batch's debug
+// data (raw score maps, TAIL_MASK), or null: the data is gone once a newer
+// batch was submitted to that lane (a retired batch's lane is reused at once).
+const Lane* delivered_lane(const lm_ctx* ctx) {
+  const lm_ctx::BatchRec& D = ctx->delivered;
+  if (D.ran_lane < 0 || D.ran_lane >= (int)ctx->lanes.size()) return nullptr;
+  const Lane& L = *ctx->lanes[D.ran_lane];
+  return (L.done_seq == D.seq && L.seq < 0) ? &L : nullptr;
+}
+const char* kLaneReused =
+    "the collected batch's lane already runs a newer batch, so its debug data is gone: collect it before submitting "
+    "more batches (or use one pipeline lane)";
+}  // namespace
+
 LM_API lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out, int32_t rows, int32_t cols) {
   if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
-  const Lane& L = *ctx->lanes[ctx->collected_lane];
+  const Lane* Lp = delivered_lane(ctx);
+  if (!Lp) return fail(LM_ERR_INVALID_ARGUMENT, kLaneReused);
+  const Lane& L = *Lp;
   if (!(ctx->debug & 1) || !L.dbg.p) return fail(LM_ERR_INVALID_ARGUMENT, "debug scores not enabled");
   if (f < 0 || f >= L.batch_n || det < 0 || det >= LM_NDET) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
   const LmDet& D = ctx->K.det[det];
@@ -1676,7 +1719,9 @@ LM_API lm_status lm_debug_scores(lm_ctx* ctx, int32_t f, int32_t det, float* out
 
 LM_API lm_status lm_debug_tail_mask(lm_ctx* ctx, int32_t f, uint8_t* out, int32_t rows, int32_t cols) {
   if (!ctx || !out) return fail(LM_ERR_INVALID_ARGUMENT, "null argument");
-  const Lane& L = *ctx->lanes[ctx->collected_lane];
+  const Lane* Lp = delivered_lane(ctx);
+  if (!Lp) return fail(LM_ERR_INVALID_ARGUMENT, kLaneReused);
+  const Lane& L = *Lp;
   if (f < 0 || f >= L.batch_n) return fail(LM_ERR_INVALID_ARGUMENT, "index out of range");
   if (rows != ctx->K.tail_hb || cols != ctx->K.tail_w) return fail(LM_ERR_INVALID_ARGUMENT, "shape mismatch");
   return guarded([&] {

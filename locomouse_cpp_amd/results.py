@@ -73,6 +73,28 @@ def slice_results(res, start):
     return out
 
 
+def head_results(res, m):
+    """The frames [0, m) of a result dict."""
+    n = res["n_frames"]
+    assert 0 <= m <= n
+    if m == n:
+        return res
+    out = {"n_frames": m, "first_frame": res.get("first_frame", 0)}
+    for k, (per, data) in _OFFSETS.items():
+        off = res[k][:per * m + 1]
+        out[k] = off
+        for d in data:
+            out[d] = res[d][:int(off[-1])]
+    p22d = out["p22d"]
+    # side arrays are laid out in frame order, so the kept frames' entries come first
+    n_side = int((p22d["side_offset"] + p22d["side_count"]).max()) if len(p22d) else 0
+    out["side_y"] = res["side_y"][:n_side]
+    out["side_s"] = res["side_s"][:n_side]
+    out["pw_dims"] = res["pw_dims"][:m]
+    out["tail"] = res["tail"][:m]
+    return out
+
+
 def same_results(a, b):
     """True when two result dicts hold bit-identical arrays (every KEYS entry;
     structured arrays field by field, floats compared as stored)."""

@@ -24,7 +24,7 @@ EXPORTED = (
     "lm_bb_create", "lm_bb_destroy", "lm_bb_push", "lm_bb_push_device", "lm_bb_finish", "lm_bb_debug_binary",
     "lm_bb_stream", "lm_host_alloc", "lm_host_free",
     "lm_detect_submit", "lm_detect_submit_device", "lm_detect_collect", "lm_ctx_lanes", "lm_ctx_pending",
-    "lm_debug_corr_work",
+    "lm_debug_corr_work", "lm_debug_batch_slots",
 )
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -151,6 +151,8 @@ def lib():
                                             C.POINTER(C.c_double), C.c_int32]
         L.lm_debug_kernel_spans.restype = C.c_int32
         L.lm_debug_corr_work.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        L.lm_debug_batch_slots.argtypes = [C.c_void_p]
+        L.lm_debug_batch_slots.restype = C.c_int32
         L.lm_synth_frames_device.argtypes = [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32,
                                              C.c_int64]
         L.lm_bb_create.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
@@ -301,6 +303,11 @@ class Context:
         out = (C.c_int32 * 4)()
         _check(lib().lm_debug_corr_work(self._h, out))
         return None if out[0] < 0 else {"tiles": (out[0], out[1]), "outputs": (out[2], out[3])}
+
+    def batch_slots(self):
+        """Frame slots the last collected batch processed (n, or n + 1 with
+        its halo frame recomputed; lm_debug_batch_slots)."""
+        return lib().lm_debug_batch_slots(self._h)
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

@@ -12,7 +12,7 @@ fi
 for rep in $(seq 1 ${REPS:-2}); do
 for v in ${VARIANTS:-default:}; do
   name=${v%%:*}; envs=${v#*:}
-  timeout -k 10 180 env ${envs//,/ } python3 bench.py --no-cpu ${BENCH_ARGS:---steps 40 --warmup 5} > gpurun_out/ab/${TAG}_$name.$rep.json 2> gpurun_out/ab/${TAG}_$name.$rep.err || { echo "$name failed"; tail -5 gpurun_out/ab/${TAG}_$name.$rep.err; exit 1; }
+  timeout -k 10 180 env ${envs//,/ } python3 bench.py --no-cpu --no-check ${BENCH_ARGS:---steps 40 --warmup 5} > gpurun_out/ab/${TAG}_$name.$rep.json 2> gpurun_out/ab/${TAG}_$name.$rep.err || { echo "$name failed"; tail -5 gpurun_out/ab/${TAG}_$name.$rep.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('gpurun_out/ab/${TAG}_$name.$rep.json')); print('$name', '$rep', d['value'], d['roofline']['avg_launch_ms'], d['roofline']['frac'])"
 done
 done

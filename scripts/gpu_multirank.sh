@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export MASTER_ADDR=127.0.0.1
 for N in ${RANKS:-4 8}; do
   timeout -k 10 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-    --master-port $((29500 + N)) bench.py --gpus $N --steps ${STEPS:-6} --warmup 2 --no-cpu --check-all-ranks \
+    --master-port $((29500 + N)) bench.py --gpus $N --steps ${STEPS:-6} --warmup 2 --no-cpu --oversubscribe --check-all-ranks \
     > gpurun_out/multirank_n$N.json 2> gpurun_out/multirank_n$N.err || { echo "ranks $N failed"; tail -30 gpurun_out/multirank_n$N.err; exit 1; }
   python -c "
 import json,sys

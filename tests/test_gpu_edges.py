@@ -183,6 +183,27 @@ def test_dark_tiles(plan, monkeypatch):
             assert work is None
 
 
+def test_dark_tiles_c5():
+    """C5 (1920x512, detectors x2, bench batch shape per frame): dark-tile
+    skipping against the oracle, and the executed-work counts the bench's
+    roofline uses (lm_debug_corr_work) equal the numpy count of bright 80 x 8
+    half-tiles and their outputs."""
+    c5 = S.SyntheticConfig(rows=512, cols=1920)
+    frames = np.concatenate([c5.frames(10, 2), np.zeros_like(c5.frames(0, 1)), c5.frames(13, 2)])
+    ref = _oracle(c5, frames).result
+    ctx = _ctx(c5, max_batch=len(frames))
+    ctx.set_debug(2)
+    got = ctx.detect(frames, 0)
+    work = ctx.corr_work()
+    slots = ctx.batch_slots()
+    ctx.close()
+    assert_same(got, ref, "C5 dark tiles: ")
+    tiles, outs = _bright_tiles(c5, frames)
+    assert work == {"tiles": tuple(tiles), "outputs": tuple(outs)}, (work, tiles, outs)
+    assert slots == len(frames)  # a batch from frame 0 has no halo slot
+    assert 0 < tiles[0] < 350 * len(frames)
+
+
 @pytest.mark.parametrize("c5", [False, True])
 def test_dense_occlusion_grid(c5):
     """occlusion_grid_spacing_pixels_bottom = 5: 60 x 28 = 1,680 ONG nodes on

@@ -116,3 +116,67 @@ def test_pipelined_errors_and_synchronous_mix():
     assert_same(concat_results(parts), _oracle(cfg, frames).result, "mixed: ")
     with pytest.raises(LMError):
         ctx.collect()  # nothing in flight
+
+
+def test_dropin_config_bench_scale():
+    """The drop-in configuration the host mirror and INTEGRATION.md ship: one
+    context x 4 pipeline lanes x B = 256, over 1,024 device frames (a shard
+    start at frame 7000 with its halo), driven like bench.py --lanes 4
+    --streams 1 (submit while lanes are busy, collect in order), against the
+    oracle on the same frames (LocoMouse_class.cpp:771-1267)."""
+    import torch
+    from locomouse_cpp_amd.runtime import synth_frames_device
+    cfg = S.SyntheticConfig()
+    n, B, f0 = 1024, 256, 7000
+    fb = 256 * 1024
+    d = torch.empty((n + 1, 256, 1024), dtype=torch.uint8, device="cuda")
+    synth_frames_device(d.data_ptr(), 256, 1024, f0 - 1, n + 1, fb)
+    torch.cuda.synchronize()
+    host = d.cpu().numpy()
+    ctx = _pctx(cfg, 4, B)
+    parts = []
+    for j, i in enumerate(range(0, n, B)):
+        if ctx.pending() == 8:
+            parts.append(ctx.collect())
+        ctx.submit_device(d.data_ptr() + (1 + i) * fb, fb, B, f0 + i, d_prev_ptr=d.data_ptr() if j == 0 else None)
+    while ctx.pending():
+        parts.append(ctx.collect())
+    ctx.close()
+    assert [p["first_frame"] for p in parts] == [f0 + i for i in range(0, n, B)]
+    ref = slice_results(_oracle(cfg, host).result, 1)
+    assert_same(concat_results(parts), ref, "1 ctx x 4 lanes x 256: ")
+
+
+def test_debug_data_refused_after_lane_reuse():
+    """Debug score maps / TAIL_MASK live on the lane that ran the batch: with
+    2 x lanes batches submitted, the oldest batches were retired and their
+    lanes reused, so asking for their maps must fail (not return another
+    batch's data); the last batch's maps are still there and exact."""
+    import numpy as np
+    from locomouse_cpp_amd.runtime import LMError
+    from oracle import oracle as O
+    cfg = S.SyntheticConfig()
+    frames = cfg.frames(0, 16)
+    ctx = _pctx(cfg, 2, 4)
+    ctx.set_debug(1)
+    for i in range(0, 16, 4):
+        ctx.submit(frames[i:i + 4], i)
+    first = ctx.collect()
+    assert first["first_frame"] == 0
+    with pytest.raises(LMError) as e:
+        ctx.debug_scores(0, 0)
+    assert e.value.code == 1 and "newer batch" in str(e.value)
+    with pytest.raises(LMError):
+        ctx.debug_tail_mask(0)
+    while ctx.pending():
+        last = ctx.collect()
+    assert last["first_frame"] == 12
+    ref = O.OracleRun(cfg, frames, flags=O.KEEP_DEBUG)
+    for det in range(6):
+        got = ctx.debug_scores(2, det)
+        exp = ref.scores(14, det, got.shape)
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), det
+    g = ctx.geometry()
+    assert np.array_equal(ctx.debug_tail_mask(2), ref.tail_mask(14, (g.bb_bottom_mouse.height, g.tail_box_width)))
+    assert ctx.batch_slots() == 5  # handed-off halo frame recomputed in slot 0
+    ctx.close()
