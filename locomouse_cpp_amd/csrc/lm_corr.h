@@ -93,7 +93,7 @@ bool corr_ring(int kw);
 const void* corr_kernel(int kw, bool unf);     // k_corr_rw<kw> or k_corr_gen
 const void* corr_kernel_rw_all(bool unf);      // every ring width in one launch
 const void* corr_kernel_f16(int kw);           // nullptr when kw is too wide
-// Dark tiles of a batch (k_tileflag / k_tilelist, lm_corr.hip): flag bytes
+// Dark tiles of a batch (written by k_ingest, lm_kernels.hip): flag bytes
 // per (slot, view, tile), the bright tiles' list per view and their counts.
 // All null: every tile is computed (LM_CORR_DARK=0).
 struct CorrDark {
@@ -101,9 +101,6 @@ struct CorrDark {
   int32_t* cnt = nullptr;
   uint32_t* list = nullptr;
 };
-// Flag and list the bright tiles of slots s0 .. s0 + nproc - 1 (after k_ingest).
-hipError_t launch_tile_lists(hipStream_t st, const LmConst* dK, const LmConst& K, const uint8_t* ext,
-                             int64_t ext_slot_bytes, int s0, int nproc, const CorrDark& dk);
 // Launch the correlation for one detector group (`weights`: the fp32 rows, or
 // the f16 B fragments for k_corr_f16).  Ring kernels take one wave per tile
 // with the batch's tiles flattened (grid.y = slot count; with dark-tile lists

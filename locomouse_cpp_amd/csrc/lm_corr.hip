@@ -221,7 +221,7 @@ struct RwHalves {
 // the next ...), so no wave idles at a frame's end and the host can put the
 // longest detectors first.  With dark-tile lists (tl_cnt != nullptr) a point
 // detector's waves take its view's bright half-tiles two at a time
-// (k_tilelist), so the group's wave count is known on the device only: the
+// (k_ingest), so the group's wave count is known on the device only: the
 // grid is sized for every 80 x 16 tile and the waves past the last group's
 // count (whole workgroups at the grid's end) return.  Otherwise a wave takes
 // the two halves of one 80 x 16 tile.  false: past the last wave.
@@ -1077,133 +1077,6 @@ hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t
                   (void*)&s0,    (void*)&keys,    (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes,
                   (void*)&dk.flags};
   return hipLaunchKernel(fn, grid, dim3(threads), args, lds, st);
-}
-
-// ---------------------------------------------------------------- dark tiles
-// detectBottomCandidates / detectSideCandidates zero every score whose
-// I_*_MOUSE pixel is <= 25 (threshold(25.5, BINARY_INV) + setTo(0, mask),
-// LocoMouse_class.cpp:782, :817, :849, :864), so an output tile of a point
-// detector with no pixel > 25 yields nothing: its filter2D outputs are all
-// discarded by the reference, and the correlation does not compute them.
-// k_tileflag: one wave per (slot, view, 80 x 16 output region) writes the
-// flag bytes (1: some pixel > 25) of the region's two 80 x 8 half-tiles; the
-// mouse pixels are read from the ext crop k_ingest just wrote (16 rows x 4
-// lanes of 20 columns: lanes 0-31 the upper half-tile, 32-63 the lower).
-__global__ __launch_bounds__(256) void k_tileflag(const LmConst* __restrict__ Kp, const uint8_t* __restrict__ ext,
-                                                  int64_t ext_slot_bytes, int s0, uint8_t* __restrict__ flags) {
-  const LmConst& K = *Kp;
-  const int slot = s0 + blockIdx.y;
-  const int g = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-  const int n0 = K.fl_tx[0] * ((K.fl_ty[0] + 1) >> 1);
-  const int v = g < n0 ? 0 : 1;
-  const int t = v ? g - n0 : g;
-  if (t >= K.fl_tx[v] * ((K.fl_ty[v] + 1) >> 1)) return;
-  const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
-  const int ry = t / K.fl_tx[v], tx = t - ry * K.fl_tx[v];
-  const int lane = threadIdx.x & 63;
-  const int y = ry * LM_RW_TH + (lane >> 2), x0 = tx * LM_TW + (lane & 3) * (LM_TW / 4);
-  static_assert(LM_RW_TH * 4 == 64 && LM_RW_HTH * 8 == 64 && LM_TW / 4 == 20, "k_tileflag lane map");
-  bool bright = false;
-  if (y < D.oh && x0 < D.ow) {
-    const uint8_t* row = ext + (int64_t)slot * ext_slot_bytes + (v ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) +
-                         (int64_t)(D.m_y + y) * K.ext_w[v] + (D.m_x + x0);
-    const unsigned mis = (unsigned)((uintptr_t)row & 3);
-    const unsigned* __restrict__ a = reinterpret_cast<const unsigned*>(row - mis);
-    unsigned d[6];
-#pragma unroll
-    for (int u = 0; u < 6; ++u) d[u] = a[u];  // the 20 bytes and <= 3 on either side (inside the ext crop)
-    const int nb = min(LM_TW / 4, D.ow - x0);
-#pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const unsigned w = __builtin_amdgcn_alignbyte(d[j + 1], d[j], mis);
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (4 * j + k < nb && ((w >> (8 * k)) & 0xFFu) > 25u) bright = true;
-    }
-  }
-  const unsigned long long m = __ballot(bright);
-  uint8_t* __restrict__ f = flags + (int64_t)slot * K.fl_slot + K.fl_off[v] + (2 * ry) * K.fl_tx[v] + tx;
-  if (lane == 0) f[0] = (unsigned)m ? 1 : 0;
-  if (lane == 32 && 2 * ry + 1 < K.fl_ty[v]) f[K.fl_tx[v]] = (unsigned)(m >> 32) ? 1 : 0;
-}
-
-// k_tilelist: one LM_TL_THREADS-thread workgroup per view lists the bright tiles of
-// slots s0 .. s0 + nproc - 1 in slot order, (slot << 16) | tile, at
-// view * tl_stride, their count in cnt[view] and the consumed outputs they
-// hold (edge tiles are partial) in cnt[2 + view] (lm_debug_corr_work).  The
-// flattened (slot, flag dword) range is cut into one run of consecutive
-// dwords per thread: count, one workgroup scan, list (the second pass re-reads
-// the dwords from L1/L2).
-#ifndef LM_TL_THREADS
-#define LM_TL_THREADS 1024  // k_tilelist workgroup size (a multiple of 64, <= 1024)
-#endif
-static_assert(LM_TL_THREADS % 64 == 0 && LM_TL_THREADS <= 1024, "k_tilelist workgroup size");
-__global__ __launch_bounds__(LM_TL_THREADS) void k_tilelist(const LmConst* __restrict__ Kp, int s0, int nproc,
-                                                   const uint8_t* __restrict__ flags, int32_t* __restrict__ cnt,
-                                                   uint32_t* __restrict__ list) {
-  const LmConst& K = *Kp;
-  const int v = blockIdx.x;
-  const int ftx = K.fl_tx[v], nt = ftx * K.fl_ty[v];
-  const int nw4 = (nt + 3) >> 2;  // flag dwords per slot (fl_slot and fl_off are multiples of 4)
-  const int items = nproc * nw4;
-  const int run = (items + LM_TL_THREADS - 1) / LM_TL_THREADS;
-  const int i0 = min(items, (int)threadIdx.x * run), i1 = min(items, i0 + run);
-  uint32_t* __restrict__ out = list + (int64_t)v * K.tl_stride;
-  const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
-  const uint8_t* __restrict__ fv = flags + K.fl_off[v];
-  auto dword = [&](int i) {
-    const int slot = i / nw4;
-    return reinterpret_cast<const unsigned*>(fv + (int64_t)(s0 + slot) * K.fl_slot)[i - slot * nw4];
-  };
-  __shared__ int s_wave[LM_TL_THREADS / 64];
-  __shared__ int s_outs;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_outs = 0;
-  int n = 0;
-#pragma unroll 8
-  for (int i = i0; i < i1; ++i) n += (int)((dword(i) * 0x01010101u) >> 24);  // k_tileflag writes every byte < nt; the pad stays 0
-  int incl = n;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(incl, o);
-    if (lane >= o) incl += u;
-  }
-  if (lane == 63) s_wave[wid] = incl;
-  __syncthreads();
-  int before = 0, total = 0;
-#pragma unroll
-  for (int k = 0; k < LM_TL_THREADS / 64; ++k) {
-    before += k < wid ? s_wave[k] : 0;
-    total += s_wave[k];
-  }
-  int pos = before + incl - n, outs = 0;
-  for (int i = i0; i < i1 && n; ++i) {
-    unsigned m = dword(i);
-    const int slot = i / nw4, w = i - slot * nw4;
-    while (m) {
-      const int t = 4 * w + (__ffs(m) - 1) / 8;
-      m &= m - 1;
-      --n;
-      out[pos++] = ((uint32_t)(s0 + slot) << 16) | (uint32_t)t;
-      const int ty = t / ftx, tx = t - ty * ftx;
-      outs += min(LM_RW_HTH, D.oh - ty * LM_RW_HTH) * min(LM_TW, D.ow - tx * LM_TW);
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) outs += __shfl_xor(outs, o);
-  if (lane == 0) atomicAdd(&s_outs, outs);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    cnt[v] = total;
-    cnt[2 + v] = s_outs;
-  }
-}
-
-hipError_t launch_tile_lists(hipStream_t st, const LmConst* dK, const LmConst& K, const uint8_t* ext,
-                             int64_t ext_slot_bytes, int s0, int nproc, const CorrDark& dk) {
-  const int nt = K.fl_tx[0] * ((K.fl_ty[0] + 1) / 2) + K.fl_tx[1] * ((K.fl_ty[1] + 1) / 2);  // 80 x 16 regions
-  k_tileflag<<<dim3((unsigned)((nt + 3) / 4), (unsigned)nproc), 256, 0, st>>>(dK, ext, ext_slot_bytes, s0, dk.flags);
-  k_tilelist<<<2, LM_TL_THREADS, 0, st>>>(dK, s0, nproc, dk.flags, dk.cnt, dk.list);
-  return hipGetLastError();
 }
 
 hipError_t launch_corr_dbg(bool unf, dim3 grid, hipStream_t st, const LmConst* K, const uint8_t* ext,

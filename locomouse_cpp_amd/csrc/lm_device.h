@@ -74,12 +74,19 @@ struct LmConst {
   // also ceil(tail_w / 64) u64 words); set by k_corr, zeroed by k_ingest
   int32_t tail_nw, tail_bm_words;
   int32_t connectivity;
-  // dark tiles (lm_corr.hip k_tileflag / k_tilelist): per view, the point
+  // dark tiles (flagged and listed by k_ingest): per view, the point
   // detectors' outputs in LM_TW x LM_RW_TH tiles (fl_tx x fl_ty of them); one
   // flag byte per (slot, view, tile) at slot * fl_slot + fl_off[view] + tile;
   // the bright tiles of view v listed at v * tl_stride of the tile list
   int32_t fl_tx[2], fl_ty[2], fl_off[2], fl_slot;
   int32_t tl_stride;
+  // the point detectors' output region per view: output (y, x) has its
+  // I_*_MOUSE pixel at ext (fl_my + y, fl_mx + x); fl_oh x fl_ow outputs
+  int32_t fl_my[2], fl_mx[2], fl_oh[2], fl_ow[2];
+  // k_ingest: 8-row bands of each view's ext crop aligned with the flag grid
+  // (band b = ext rows fl_my + 8b ..), bands ing_b0[v] .. ing_b0[v] +
+  // ing_nb[v] - 1, one workgroup of ing_threads per (band, slot group)
+  int32_t ing_b0[2], ing_nb[2], ing_threads;
   // per-list capacities (= output area) and list offsets inside a slot's key area
   int32_t list_cap[LM_NLIST];
   int64_t list_off[LM_NLIST];

@@ -182,16 +182,23 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 // ---------------------------------------------------------------- k_ingest
 // Builds the extended padded crops of both views for LM_INGEST_FB consecutive
 // slots: every I_PAD pixel any detector tap reads (readFrame's correctImage +
-// flip, :1316-1327 / :1337-1406; cropBoundingBox, :1408-1478).  Each thread
-// owns 16 consecutive crop bytes (one 16-byte store per frame).  The
-// calibration index and background byte of each are loaded once and reused
-// for every slot whose crop sits at the same place (always, with a provided
-// bounding box); per frame only the frame gather, the LUTs and the store
-// remain.  Where the 16 source pixels are consecutive in the frame (a
-// calibration map that is locally a translation, flipped or not) the gather
-// is five aligned dword loads instead of sixteen byte loads.
+// flip, :1316-1327 / :1337-1406; cropBoundingBox, :1408-1478).  One workgroup
+// per (view, 8-row band of the view's ext crop, slot group): the bands are
+// aligned with the dark-tile flag grid (band b holds the point detectors'
+// output rows 8b .. 8b + 7), so the workgroup that writes a tile row's pixels
+// also decides which of its 80 x 8 output tiles are bright (some I_*_MOUSE
+// pixel > 25, LocoMouse_class.cpp:782, :817), writes their flag bytes and
+// appends the bright ones to the view's tile list -- no second pass over the
+// crops.  Each thread owns 16 consecutive crop bytes of the band (one 16-byte
+// store per frame).  The calibration index and background byte of each are
+// loaded once and reused for every slot whose crop sits at the same place
+// (always, with a provided bounding box); per frame only the frame gather, the
+// LUTs and the store remain.  Where the 16 source pixels are consecutive in
+// the frame (a calibration map that is locally a translation, flipped or not)
+// the gather is five aligned dword loads instead of sixteen byte loads.
 #define LM_INGEST_FB 8
 #define LM_INGEST_VEC 16
+#define LM_INGEST_MAXTX 64  // flag-grid columns a band's workgroup can hold (ow <= 5120)
 
 // Gather indices and background bytes of the 16 crop pixels that start at
 // I_PAD (R, C0) (-1 / 0 outside I_UNPAD); returns 1 when idx[k] = idx[0] + k
@@ -250,119 +257,182 @@ __global__ __launch_bounds__(256) void k_srcmap(const LmConst* __restrict__ Kp, 
   sbkg[ci] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
-                                                const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
-                                                const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
-                                                int s0, int s_end, uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
-                                                unsigned ext_blocks, unsigned* __restrict__ tailbm,
-                                                const int2* __restrict__ smap, const uint4* __restrict__ sbkg,
-                                                const int32_t* __restrict__ skey) {
+// Bright bytes (> 25: threshold(25.5, BINARY_INV) leaves them unmasked) of a
+// packed word, as 0x80 in each such byte.
+DEV uint32_t bright_bytes(uint32_t w) {
+  return (((w & 0x7F7F7F7Fu) + 0x66666666u) | w) & 0x80808080u;
+}
+// 0x80 in byte i of the result for bit i of the 4-bit n
+DEV uint32_t byte_mask4(uint32_t n) { return ((n * 0x00204081u) & 0x01010101u) << 7; }
+
+__global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
+                                                 const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
+                                                 const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
+                                                 int s0, int s_end, uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
+                                                 unsigned* __restrict__ tailbm, const int2* __restrict__ smap,
+                                                 const uint4* __restrict__ sbkg, const int32_t* __restrict__ skey,
+                                                 uint8_t* __restrict__ flags, int32_t* __restrict__ tl_cnt,
+                                                 uint32_t* __restrict__ tl_list) {
   const LmConst& K = *Kp;
   const int sb = s0 + blockIdx.y * LM_INGEST_FB;
   const int nf = min(LM_INGEST_FB, s_end - sb);
+  const int T = (int)blockDim.x, tid = (int)threadIdx.x;
   {  // this block's share of the group's tail bitmaps is zeroed (k_corr ORs the tail detectors' bits in)
-    const int per = (K.tail_bm_words + (int)ext_blocks - 1) / (int)ext_blocks;
+    const int per = (K.tail_bm_words + (int)gridDim.x - 1) / (int)gridDim.x;
     const int w0 = (int)blockIdx.x * per, w1 = min(K.tail_bm_words, w0 + per);
     for (int f = 0; f < nf; ++f) {
       unsigned* __restrict__ t = tailbm + (int64_t)(sb + f) * K.tail_bm_words;
-      for (int w = w0 + (int)threadIdx.x; w < w1; w += blockDim.x) t[w] = 0u;
+      for (int w = w0 + tid; w < w1; w += T) t[w] = 0u;
     }
   }
+  // this block's view and band
+  const int v = (int)blockIdx.x < K.ing_nb[0] ? 0 : 1;
+  const int band = K.ing_b0[v] + (int)blockIdx.x - (v ? K.ing_nb[0] : 0);
+  const int ew = K.ext_w[v], cw = ew / LM_INGEST_VEC, nch = 8 * cw;
+  const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
+  const bool fl_band = flags != nullptr && band >= 0 && band < K.fl_ty[v];
+  const int ftx = K.fl_tx[v];
   // One round of independent loads (the group's LUTs into registers, the
-  // slots, the source map entry), then the frame loads the map points at, and
-  // only then the LUTs into LDS and the barrier: the group costs two load
-  // latencies, not four (LUT copy, slots, map, frames one after another).
+  // slots, the first chunk's source map entry), then the frame loads the map
+  // points at, and only then the LUTs into LDS and the barrier: the group
+  // costs two load latencies, not four (LUT copy, slots, map, frames one
+  // after another).
   __shared__ __attribute__((aligned(16))) uint8_t lut[LM_INGEST_FB][256];
   __shared__ uint8_t glut[256];
-  static_assert(LM_INGEST_FB * 256 == 8 * 256, "k_ingest: 8 LUT bytes per thread");
-  const int li = (int)threadIdx.x * 8;
-  uint2 lv = make_uint2(0u, 0u);
-  if (li < nf * 256) lv = *reinterpret_cast<const uint2*>(luts + (int64_t)sb * 256 + li);
-  const uint8_t gl = K.gray_lut[threadIdx.x];
-  const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
-  const int64_t etot = e0 + (int64_t)K.ext_h[1] * K.ext_w[1];
-  const int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * LM_INGEST_VEC;
-  const bool act = q < etot;
-  const int v = q < e0 ? 0 : 1;
-  const int64_t qq = v == 0 ? q : q - e0;
-  const int er = act ? (int)(qq / K.ext_w[v]) : 0;
-  const int ec = act ? (int)(qq % K.ext_w[v]) : 0;  // multiple of 16 (ext_w % 16 == 0)
-  int2 m = make_int2(0, 0);
-  uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
-  if (act && smap) {  // speculative: used when the group's crops all sit at the map's position
-    m = smap[q / LM_INGEST_VEC];
-    b4 = sbkg[q / LM_INGEST_VEC];
+  __shared__ uint8_t s_fl[LM_INGEST_FB][LM_INGEST_MAXTX];  // bright output tiles of the band, per slot
+  __shared__ uint32_t s_ent[LM_INGEST_FB * LM_INGEST_MAXTX];
+  __shared__ int s_n, s_outs, s_base;
+  for (int i = tid; i < LM_INGEST_FB * 256 / 8; i += T) {
+    const int li = i * 8;
+    if (li < nf * 256) *reinterpret_cast<uint2*>(&lut[0][0] + li) = *reinterpret_cast<const uint2*>(luts + (int64_t)sb * 256 + li);
+  }
+  for (int i = tid; i < 256; i += T) glut[i] = K.gray_lut[i];
+  for (int i = tid; i < LM_INGEST_FB * LM_INGEST_MAXTX; i += T) (&s_fl[0][0])[i] = 0;
+  if (tid == 0) {
+    s_n = 0;
+    s_outs = 0;
   }
   const LmSlot sl0 = slots[sb];
   bool same = true;
   for (int f = 1; f < nf; ++f)
     same = same && slots[sb + f].crop_x[v] == sl0.crop_x[v] && slots[sb + f].crop_y[v] == sl0.crop_y[v];
-  const bool fast = act && same && smap && skey[2 * v] == sl0.crop_x[v] && skey[2 * v + 1] == sl0.crop_y[v] && m.y != 0;
-  int idx[LM_INGEST_VEC];
-  uint32_t bw[4];  // background bytes, packed
-  int run = 0;  // 1: idx[k] = idx[0] + k, -1: idx[k] = idx[0] - k, 0: gather
-  int lo = 0;   // a run's first source byte
-  bool allv = false;  // every pixel inside I_UNPAD (a run; idx[] not filled on the source-map path)
+  const bool mapped = same && smap && skey[2 * v] == sl0.crop_x[v] && skey[2 * v + 1] == sl0.crop_y[v];
+  // chunk i of the band: ext row er, byte column ec (a multiple of 16)
+  auto chunk_pos = [&](int i, int& er, int& ec) {
+    const int rr = i / cw;
+    er = K.fl_my[v] + 8 * band + rr;
+    ec = (i - rr * cw) * LM_INGEST_VEC;
+    return i < nch && er >= 0 && er < K.ext_h[v];
+  };
   uint32_t d[LM_INGEST_FB][5];
-  if (fast) {  // the source map holds this crop position: no calibration / background gathers
-    run = m.y;
-    lo = m.x;
-    allv = true;
+  int2 m = make_int2(0, 0);
+  uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
+  // the fast path's loads of chunk i (source map entry, then the run's dwords)
+  auto fast_loads = [&](int i) {
+    int er, ec;
+    const bool act = chunk_pos(i, er, ec);
+    m = make_int2(0, 0);
+    if (act && mapped) {
+      const int64_t ci = ((v ? e0 : 0) + (int64_t)er * ew + ec) / LM_INGEST_VEC;
+      m = smap[ci];
+      b4 = sbkg[ci];
+      if (m.y != 0) {
 #pragma unroll
-    for (int f = 0; f < LM_INGEST_FB; ++f)
-      if (f < nf) {
-        const lm_gu32* w = reinterpret_cast<const lm_gu32*>(as_global(frame_ptr[sb + f]) + (lo & ~3));
+        for (int f = 0; f < LM_INGEST_FB; ++f)
+          if (f < nf) {
+            const lm_gu32* w = reinterpret_cast<const lm_gu32*>(as_global(frame_ptr[sb + f]) + (m.x & ~3));
 #pragma unroll
-        for (int u = 0; u < 5; ++u) d[f][u] = w[u];
+            for (int u = 0; u < 5; ++u) d[f][u] = w[u];
+          }
       }
-  }
-  if (li < nf * 256) *reinterpret_cast<uint2*>(&lut[0][0] + li) = lv;
-  glut[threadIdx.x] = gl;
+    }
+  };
+  fast_loads(tid);
   __syncthreads();
-  if (!act) return;
-  // gather indices and background of this thread's 16 pixels for a crop at (cx, cy)
-  auto locate = [&](int R, int C0) {
-    run = ingest_locate(K, cal, bkg, R, C0, idx, bw, lo);
-    allv = false;
-  };
-  // the 16 source bytes of a run span [lo, lo + 16): five aligned dwords cover them
-  // (funnel shifts by the byte offset, then a byte reversal for a flipped run:
-  // no register array is indexed with a run-time value, so nothing spills)
-  auto run_bytes = [&](const uint32_t (&dd)[5], uint32_t (&w)[4]) {
-    const unsigned sh = (unsigned)(lo & 3);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_alignbyte(dd[j + 1], dd[j], sh);
-    if (run < 0) {
-      const uint32_t r0 = __builtin_bswap32(w[3]), r1 = __builtin_bswap32(w[2]), r2 = __builtin_bswap32(w[1]),
-                     r3 = __builtin_bswap32(w[0]);
-      w[0] = r0;
-      w[1] = r1;
-      w[2] = r2;
-      w[3] = r3;
-    }
-  };
-  // background subtraction, the slot's LUT, the grey LUT and the 16-byte store
-  // (pixels and background bytes stay packed four to a register)
-  auto emit = [&](int f, const uint32_t (&pw)[4], const LmSlot& sl, int R, int C0) {
-    uint32_t word[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < LM_INGEST_VEC; ++k) {
-      uint32_t o = 0;
-      if (allv || idx[k] >= 0) {
-        const uint32_t pk = (pw[k >> 2] >> (8 * (k & 3))) & 0xFFu, bk = (bw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-        o = lut[f][pk > bk ? pk - bk : 0];
-        if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) o = glut[o];
-      } else if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) {
-        o = glut[0];  // only reachable through the pad (rejected on the host)
-      }
-      word[k >> 2] |= o << (8 * (k & 3));
-    }
-    *reinterpret_cast<uint4*>(ext + (int64_t)(sb + f) * ext_slot_bytes + q) = make_uint4(word[0], word[1], word[2], word[3]);
-  };
 
-  {
+  for (int i = tid; i < nch; i += T) {
+    if (i != tid) fast_loads(i);
+    int er, ec;
+    if (!chunk_pos(i, er, ec)) continue;
+    const int64_t q = (v ? e0 : 0) + (int64_t)er * ew + ec;  // byte offset in the slot's ext crops
+    // dark-tile flags: the bytes of this chunk that are point-detector
+    // outputs' I_*_MOUSE pixels (output (y, x) = ext (fl_my + y, fl_mx + x)),
+    // split at the 80-column tile boundary: tile ta and ta + 1
+    uint32_t ma[4] = {0u, 0u, 0u, 0u}, mb[4] = {0u, 0u, 0u, 0u};
+    int ta = 0;
+    const int y = er - K.fl_my[v];
+    if (fl_band && y < K.fl_oh[v]) {
+      const int x0 = ec - K.fl_mx[v];
+      ta = x0 >= 0 ? x0 / LM_TW : -((LM_TW - 1 - x0) / LM_TW);
+      const int lo = max(0, -x0), hi = min(LM_INGEST_VEC, K.fl_ow[v] - x0), ks = (ta + 1) * LM_TW - x0;
+      auto range = [](int a, int b) -> uint32_t {  // bits [a, b) of 16
+        return a < b ? ((b >= 32 ? 0xFFFFFFFFu : (1u << b) - 1u) & ~((1u << a) - 1u)) & 0xFFFFu : 0u;
+      };
+      const uint32_t bits_a = range(lo, min(hi, ks)), bits_b = range(max(lo, ks), hi);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ma[j] = byte_mask4((bits_a >> (4 * j)) & 0xFu);
+        mb[j] = byte_mask4((bits_b >> (4 * j)) & 0xFu);
+      }
+    }
+    const bool flag_chunk = (ma[0] | ma[1] | ma[2] | ma[3] | mb[0] | mb[1] | mb[2] | mb[3]) != 0u;
+    int idx[LM_INGEST_VEC];
+    uint32_t bw[4];  // background bytes, packed
+    int run = 0;  // 1: idx[k] = idx[0] + k, -1: idx[k] = idx[0] - k, 0: gather
+    int lo = 0;   // a run's first source byte
+    bool allv = false;  // every pixel inside I_UNPAD (a run; idx[] not filled on the source-map path)
+    // the 16 source bytes of a run span [lo, lo + 16): five aligned dwords cover them
+    // (funnel shifts by the byte offset, then a byte reversal for a flipped run:
+    // no register array is indexed with a run-time value, so nothing spills)
+    auto run_bytes = [&](const uint32_t (&dd)[5], uint32_t (&w)[4]) {
+      const unsigned sh = (unsigned)(lo & 3);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = __builtin_amdgcn_alignbyte(dd[j + 1], dd[j], sh);
+      if (run < 0) {
+        const uint32_t r0 = __builtin_bswap32(w[3]), r1 = __builtin_bswap32(w[2]), r2 = __builtin_bswap32(w[1]),
+                       r3 = __builtin_bswap32(w[0]);
+        w[0] = r0;
+        w[1] = r1;
+        w[2] = r2;
+        w[3] = r3;
+      }
+    };
+    // background subtraction, the slot's LUT, the grey LUT, the 16-byte store
+    // and the chunk's bright-tile bits (pixels and background bytes stay
+    // packed four to a register)
+    auto emit = [&](int f, const uint32_t (&pw)[4], const LmSlot& sl, int R, int C0) {
+      uint32_t word[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < LM_INGEST_VEC; ++k) {
+        uint32_t o = 0;
+        if (allv || idx[k] >= 0) {
+          const uint32_t pk = (pw[k >> 2] >> (8 * (k & 3))) & 0xFFu, bk = (bw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+          o = lut[f][pk > bk ? pk - bk : 0];
+          if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) o = glut[o];
+        } else if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) {
+          o = glut[0];  // only reachable through the pad (rejected on the host)
+        }
+        word[k >> 2] |= o << (8 * (k & 3));
+      }
+      *reinterpret_cast<uint4*>(ext + (int64_t)(sb + f) * ext_slot_bytes + q) = make_uint4(word[0], word[1], word[2], word[3]);
+      if (flag_chunk) {
+        uint32_t ha = 0u, hb = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t br = bright_bytes(word[j]);
+          ha |= br & ma[j];
+          hb |= br & mb[j];
+        }
+        if (ha) s_fl[f][ta] = 1;
+        if (hb) s_fl[f][ta + 1] = 1;
+      }
+    };
+
     const int R = sl0.crop_y[v] + K.ext_oy[v] + er, C0 = sl0.crop_x[v] + K.ext_ox[v] + ec;
-    if (fast) {
+    if (mapped && m.y != 0) {  // the source map holds this crop position: no calibration / background gathers
+      run = m.y;
+      lo = m.x;
+      allv = true;
       bw[0] = b4.x;
       bw[1] = b4.y;
       bw[2] = b4.z;
@@ -374,13 +444,13 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
           run_bytes(d[f], pw);
           emit(f, pw, slots[sb + f], R, C0);
         }
-      return;
+      continue;
     }
-    // Every slot of the group has its crop at the same place and the pixels
-    // are a run, but the source map does not hold it: all the group's frame
-    // loads are issued before any is used.
-    locate(R, C0);
+    run = ingest_locate(K, cal, bkg, R, C0, idx, bw, lo);
     if (same && run != 0) {
+      // Every slot of the group has its crop at the same place and the pixels
+      // are a run, but the source map does not hold it: all the group's frame
+      // loads are issued before any is used.
 #pragma unroll
       for (int f = 0; f < LM_INGEST_FB; ++f)
         if (f < nf) {
@@ -395,36 +465,61 @@ __global__ __launch_bounds__(256) void k_ingest(const LmConst* __restrict__ Kp, 
           run_bytes(d[f], pw);
           emit(f, pw, slots[sb + f], R, C0);
         }
-      return;
+      continue;
+    }
+    // General case: frame by frame, the indices recomputed whenever the crop moves.
+    int px = sl0.crop_x[v], py = sl0.crop_y[v];
+    for (int f = 0; f < nf; ++f) {
+      const int slot = sb + f;
+      const LmSlot sl = slots[slot];
+      const int Rf = sl.crop_y[v] + K.ext_oy[v] + er;
+      const int Cf = sl.crop_x[v] + K.ext_ox[v] + ec;
+      if (sl.crop_x[v] != px || sl.crop_y[v] != py) {  // crop moved: recompute the gather indices
+        px = sl.crop_x[v];
+        py = sl.crop_y[v];
+        run = ingest_locate(K, cal, bkg, Rf, Cf, idx, bw, lo);
+      }
+      const lm_gu8* __restrict__ F = as_global(frame_ptr[slot]);
+      uint32_t pw[4] = {0, 0, 0, 0};
+      if (run != 0) {
+        const lm_gu32* w = reinterpret_cast<const lm_gu32*>(F + (lo & ~3));
+        uint32_t d1[5];
+#pragma unroll
+        for (int u = 0; u < 5; ++u) d1[u] = w[u];
+        run_bytes(d1, pw);
+      } else {
+#pragma unroll
+        for (int k = 0; k < LM_INGEST_VEC; ++k)
+          if (idx[k] >= 0) pw[k >> 2] |= (uint32_t)F[idx[k]] << (8 * (k & 3));
+      }
+      emit(f, pw, sl, Rf, Cf);
     }
   }
-  // General case: frame by frame, the indices recomputed whenever the crop moves.
-  int px = sl0.crop_x[v], py = sl0.crop_y[v];
-  for (int f = 0; f < nf; ++f) {
-    const int slot = sb + f;
-    const LmSlot sl = slots[slot];
-    const int R = sl.crop_y[v] + K.ext_oy[v] + er;
-    const int C0 = sl.crop_x[v] + K.ext_ox[v] + ec;
-    if (sl.crop_x[v] != px || sl.crop_y[v] != py) {  // crop moved: recompute the gather indices
-      px = sl.crop_x[v];
-      py = sl.crop_y[v];
-      locate(R, C0);
+  if (!fl_band) return;
+  // the band's flag bytes (each written by this block only: no zeroing pass)
+  // and its bright tiles appended to the view's list (any order: the
+  // correlation's waves take them two at a time, and the keys they produce
+  // are sorted by k_nms)
+  __syncthreads();
+  const int ty = band, oh_t = min(8, K.fl_oh[v] - 8 * ty);
+  for (int i = tid; i < nf * ftx; i += T) {
+    const int f = i / ftx, tx = i - f * ftx;
+    const uint8_t b = s_fl[f][tx];
+    flags[(int64_t)(sb + f) * K.fl_slot + K.fl_off[v] + ty * ftx + tx] = b;
+    if (b && tl_list) {
+      s_ent[atomicAdd(&s_n, 1)] = ((uint32_t)(sb + f) << 16) | (uint32_t)(ty * ftx + tx);
+      atomicAdd(&s_outs, oh_t * min(LM_TW, K.fl_ow[v] - tx * LM_TW));
     }
-    const lm_gu8* __restrict__ F = as_global(frame_ptr[slot]);
-    uint32_t pw[4] = {0, 0, 0, 0};
-    if (run != 0) {
-      const lm_gu32* w = reinterpret_cast<const lm_gu32*>(F + (lo & ~3));
-      uint32_t d1[5];
-#pragma unroll
-      for (int u = 0; u < 5; ++u) d1[u] = w[u];
-      run_bytes(d1, pw);
-    } else {
-#pragma unroll
-      for (int k = 0; k < LM_INGEST_VEC; ++k)
-        if (idx[k] >= 0) pw[k >> 2] |= (uint32_t)F[idx[k]] << (8 * (k & 3));
-    }
-    emit(f, pw, sl, R, C0);
   }
+  if (!tl_list) return;
+  __syncthreads();
+  if (tid == 0) {
+    s_base = s_n ? atomicAdd(&tl_cnt[v], s_n) : 0;
+    if (s_outs) atomicAdd(&tl_cnt[2 + v], s_outs);
+  }
+  __syncthreads();
+  uint32_t* __restrict__ out = tl_list + (int64_t)v * K.tl_stride + s_base;
+  for (int p = tid; p < s_n; p += T) out[p] = s_ent[p];
 }
 
 #include "lm_corr.h"  // the correlation kernels are their own translation unit (lm_corr.hip)
@@ -1351,6 +1446,15 @@ DEV void nms_block(int bx, int feat, const LmConst* __restrict__ Kp, int s0, uns
   };
   const int n_b = n_pos[slot * LM_NLIST + feat];
   const int n_s = slot >= 1 ? n_pos[slot * LM_NLIST + 2 + feat] : 0;
+#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 1)
+  if (threadIdx.x == 0)
+    for (int l = feat; l < LM_NLIST; l += 2) {
+      H->n_pos[l] = 0;
+      H->cand_cnt[l] = 0;
+      H->ties[l] = 0;
+    }
+  return;
+#endif
   if constexpr (!GLOB) {
     if (n_b > LM_NMS_CAP) return;  // both lists go to <true>
     const int cb = run(0, n_b, prof_b);
@@ -1929,11 +2033,12 @@ __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots
                                               int32_t* __restrict__ npos, int32_t* __restrict__ err,
                                               const LmConst* __restrict__ Kp, unsigned long long* __restrict__ keys,
                                               const LmSlotOut* __restrict__ prev_hdr, int prev_slot,
-                                              LmSlotOut* __restrict__ hdr) {
+                                              LmSlotOut* __restrict__ hdr, int32_t* __restrict__ dark_cnt) {
   if (blockIdx.x == 1) {
     carry_block(*Kp, keys, prev_hdr, prev_slot, hdr);
     return;
   }
+  if (dark_cnt && threadIdx.x < 4) dark_cnt[threadIdx.x] = 0;  // k_ingest's bright-tile counts
   for (int i = threadIdx.x; i < ns; i += blockDim.x) {
     slots[i] = h_slots[i];
     fptr[i] = h_fptr[i];

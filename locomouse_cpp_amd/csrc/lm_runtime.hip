@@ -29,6 +29,12 @@
 
 namespace {
 
+// Timing experiments only (scripts/build_variant_rt.sh -DLM_EXP_SKIP=...;
+// results are wrong): 1 k_nms writes empty lists, 16 no correlation launch.
+#ifndef LM_EXP_SKIP
+#define LM_EXP_SKIP 0
+#endif
+
 // LDS window of one k_corr_gen workgroup (row chunks are sized to fit it)
 constexpr size_t kCorrLdsBudget = 64 * 1024;
 constexpr size_t kF16LdsMax = 160 * 1024;  // one k_corr_f16 workgroup per CU at most
@@ -473,8 +479,23 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     }
     K.fl_slot = o;
     K.tl_stride = c->nslots * std::max(K.fl_tx[0] * K.fl_ty[0], K.fl_tx[1] * K.fl_ty[1]);
-    if (K.fl_tx[0] * K.fl_ty[0] > 65535 || K.fl_tx[1] * K.fl_ty[1] > 65535 || c->nslots > 65535)
+    if (K.fl_tx[0] * K.fl_ty[0] > 65535 || K.fl_tx[1] * K.fl_ty[1] > 65535 || c->nslots > 65535 ||
+        std::max(K.fl_tx[0], K.fl_tx[1]) > LM_INGEST_MAXTX)
       throw std::invalid_argument("bounding box or batch too large for the correlation tile lists.");
+    // k_ingest's bands: 8 ext rows each, aligned with the flag grid's rows
+    int maxcw = 0;
+    for (int v = 0; v < 2; ++v) {
+      const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
+      K.fl_my[v] = D.m_y;
+      K.fl_mx[v] = D.m_x;
+      K.fl_oh[v] = D.oh;
+      K.fl_ow[v] = D.ow;
+      const int above = (D.m_y + 7) / 8;  // bands above the output rows (m_y >= 0)
+      K.ing_b0[v] = -above;
+      K.ing_nb[v] = above + (K.ext_h[v] - D.m_y + 7) / 8;
+      maxcw = std::max(maxcw, K.ext_w[v] / LM_INGEST_VEC);
+    }
+    K.ing_threads = std::min(1024, (8 * maxcw + 63) / 64 * 64);
   }
   // k_tail's LDS: bitmaps, column tables and moment tiles from the geometry,
   // plus as many runs as fit 64 KiB (more go to global scratch)
@@ -717,7 +738,7 @@ void lane_alloc(lm_ctx* c, Lane& L) {
   }
   if (c->dark_on) {
     L.dark_flags.alloc((size_t)K.fl_slot * ns);
-    SET_SYNC(L.dark_flags.p, 0, (size_t)K.fl_slot * ns, st);  // the pad bytes after each view's flags stay 0
+    SET_SYNC(L.dark_flags.p, 0, (size_t)K.fl_slot * ns, st);
     L.dark_list.alloc((size_t)2 * K.tl_stride);
     L.dark_cnt.alloc(4);
   }
@@ -988,26 +1009,22 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
     // block 1: k_carry (a rerun keeps slot 0's staged candidates)
     k_prep<<<do_carry ? 2 : 1, 256, 0, st>>>(L.h_slots.d, L.h_frame_ptr.d, L.h_ctl.d, n + 1, L.slots.p, L.frame_ptr.p,
                                              A.ctl.p, L.npos.p, L.err.p, dK, L.keys.p, L.arena[P.prv].hdr.p, P.last_n,
-                                             A.hdr.p);
+                                             A.hdr.p, L.dark_cnt.p);
     T.begin("k_minmax");
     k_minmax<<<dim3(LM_MM_SPLIT, n + 1 - s_lut0), LM_MM_THREADS, 0, st>>>(L.frame_ptr.p, c->bkg.p, c->npix, s_lut0,
                                                                         L.mm.p);
     k_lut<<<(n + 1 - s_lut0 + 3) / 4, 256, 0, st>>>(L.mm.p, s_lut0, n + 1, c->adj.p, c->setup.method != 0, L.luts.p);
     T.end();
-    const int64_t etot = (int64_t)K.ext_h[0] * K.ext_w[0] + (int64_t)K.ext_h[1] * K.ext_w[1];
+    // ext crops of both views, and (dark tiles) the bright-tile flags and lists
     T.begin("k_ingest");
-    const unsigned ext_blocks = (unsigned)((etot / LM_INGEST_VEC + 255) / 256);
-    k_ingest<<<dim3(ext_blocks, (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)), 256, 0, st>>>(
-        dK, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, L.slots.p, s_proc0, n + 1, L.ext.p, c->ext_slot_bytes,
-        ext_blocks, reinterpret_cast<unsigned*>(L.tailbin.p), L.smap.p, L.sbkg.p, L.skey.p);
+    const CorrDark dk = lane_dark(c, L);
+    k_ingest<<<dim3((unsigned)(K.ing_nb[0] + K.ing_nb[1]), (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)),
+               K.ing_threads, 0, st>>>(dK, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, L.slots.p, s_proc0, n + 1, L.ext.p,
+                                        c->ext_slot_bytes, reinterpret_cast<unsigned*>(L.tailbin.p), L.smap.p, L.sbkg.p,
+                                        L.skey.p, dk.flags, dk.cnt, dk.list);
     T.end();
-    if (c->dark_on) {
-      T.begin("k_tiles");
-      HIPCHK(launch_tile_lists(st, dK, K, L.ext.p, c->ext_slot_bytes, s_proc0, nproc, lane_dark(c, L)));
-      T.end();
-    }
   }
-  if (part == 1 || part < 0) {
+  if ((part == 1 || part < 0) && !(LM_EXP_SKIP & 16)) {
     T.begin("k_corr");
     const lm_ctx::CorrPlan& CP = c->corr_plan[P.plan];
     for (size_t gi = 0; gi < CP.groups.size(); ++gi) {
