@@ -29,6 +29,8 @@ struct LmDetGroup {
 // detector runs k_corr_gen.
 #ifdef LM_KW_ONLY  // experiment builds: one ring width
 #define LM_KW_LIST(X) X(LM_KW_ONLY)
+#elif defined(LM_KW_C3)  // experiment builds: the synthetic C3 widths only (fast compiles)
+#define LM_KW_LIST(X) X(22) X(24) X(26) X(30)
 #else
 #define LM_KW_LIST(X)                                                                                             \
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
@@ -37,7 +39,7 @@ struct LmDetGroup {
 // widths of the merged launch (k_corr_rw_all): those whose window row fits
 // half a wave's loads (rw_tile's lane-split loads; wider ones load both halves
 // from every lane and need more registers than the merged kernel's budget)
-#ifdef LM_KW_ONLY
+#if defined(LM_KW_ONLY) || defined(LM_KW_C3)
 #define LM_KW_LIST_RW_ALL LM_KW_LIST
 #else
 #define LM_KW_LIST_RW_ALL(X) \
@@ -52,7 +54,14 @@ __host__ __device__ constexpr bool rw_all_width(int kw) { return kw >= 16 && (kw
 #define LM_RW_THREADS (64 * LM_RW_WAVES)
 #define LM_RW_TH 16     // output rows per wave (two half-tiles)
 #define LM_RW_HTH 8     // output rows per half-tile (also the dark-tile flag grid's rows)
-#define LM_RW_HSLOTS 8  // ring rows per half (+ 1 mirror)
+#ifndef LM_RW_HSLOTS
+// ring rows per half (+ 1 mirror): rows t .. t + 5 are read at step t and row
+// t + HSLOTS is stored at its end, so 7 suffice; 7 gives kw 30 five waves per
+// SIMD instead of four but measured 1-2 % slower at C3 (profiles/r04/ring7),
+// so 8 (a power of two: the slot index is a mask)
+#define LM_RW_HSLOTS 8
+#endif
+static_assert(LM_RW_HSLOTS >= 7, "k_corr_rw ring: rows t .. t + 6 are live during step t");
 
 // window row: 80 + KW - 1 columns plus up to 3 before them (the loads start on
 // a 4-byte boundary); stride == 4 (mod 8)

@@ -501,7 +501,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   };
   auto store_row = [&](int r, Row w) {
     if (r >= nrows) return;
-    const int s = r & (HS - 1);
+    const int s = r % HS;  // r is wave-uniform: scalar arithmetic
     if constexpr (DUAL) {
       if (ld) put(ring, s, lane, w.v);
       if (ld1) put(ring + (HS + 1) * STR, s, lane, w.v1);
@@ -523,8 +523,11 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring +
                              (unsigned)(h * (HS + 1) * STR * (int)sizeof(float));
   const unsigned lane_off = (unsigned)((lx * PK_C + mis) * (int)sizeof(float));
+  // ring slot of window row t + 4 ly (t wave-uniform: both candidates are
+  // scalar, the lane picks one)
   auto row_base = [&](int t) -> unsigned {
-    return ring_base + (unsigned)(((t + ly * PK_R) & (HS - 1)) * STR * (int)sizeof(float)) + lane_off;
+    const int a = t % HS, b = a + PK_R >= HS ? a + PK_R - HS : a + PK_R;
+    return ring_base + (unsigned)((ly ? b : a) * STR * (int)sizeof(float)) + lane_off;
   };
   RwPipe<KW, UNF> S;
 #pragma unroll
@@ -600,23 +603,25 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     return;
   }
   bits &= mbits;
-  // keys: one slot per set bit, bit position by bit position (ballot + mbcnt
-  // within the half), one global atomic per half
-  int off[PK_R * PK_C];
-  int tot0 = 0, tot1 = 0;
+  // keys: each lane's set bits at consecutive places after the lanes of its
+  // half before it (popcount, then an inclusive scan over the 32 lanes of the
+  // half), one global atomic per half (keys are sorted later: their order in
+  // the list does not matter)
+  const int cnt = __popc(bits);
+  int incl = cnt;
 #pragma unroll
-  for (int k = 0; k < PK_R * PK_C; ++k) {
-    const unsigned long long m = __ballot((bits >> k) & 1u);
-    const unsigned m0 = (unsigned)m, m1 = (unsigned)(m >> 32);
-    off[k] = h ? tot1 + (int)__builtin_amdgcn_mbcnt_hi(m1, 0u) : tot0 + (int)__builtin_amdgcn_mbcnt_lo(m0, 0u);
-    tot0 += __popc(m0);
-    tot1 += __popc(m1);
+  for (int o = 1; o < 32; o <<= 1) {
+    const int u = __shfl_up(incl, o, 32);
+    if (hl >= o) incl += u;
   }
-  if (tot0 + tot1 == 0) return;
+  const int tot = __shfl(incl, 31, 32);  // the half's count (its last lane's inclusive sum)
+  if (__ballot(tot != 0) == 0) return;
   int base_k = 0;
-  if ((lane == 0 && tot0) || (lane == 32 && tot1)) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], h ? tot1 : tot0);
-  base_k = h ? __shfl(base_k, 32) : __shfl(base_k, 0);
-  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k;
+  if (hl == 31 && tot) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
+  base_k = __shfl(base_k, 31, 32);
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k +
+                                        (incl - cnt);
+  int pos = 0;
 #pragma unroll
   for (int p = 0; p < PK_R / 2; ++p)
 #pragma unroll
@@ -627,7 +632,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
         if (bits & (1u << k)) {
           const int y = oy0 + ly * PK_R + r, x = ox0 + lx * PK_C + c;
           const float sc = hh ? acc[p][c].y : acc[p][c].x;
-          kl[off[k]] = ((unsigned long long)(~__float_as_uint(sc)) << 32) | (unsigned)(y * D.ow + x);
+          kl[pos++] = ((unsigned long long)(~__float_as_uint(sc)) << 32) | (unsigned)(y * D.ow + x);
         }
       }
 }

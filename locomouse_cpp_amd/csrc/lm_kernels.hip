@@ -1477,16 +1477,16 @@ DEV void nms_block(int bx, int feat, const LmConst* __restrict__ Kp, int s0, uns
 // share them out.  fn(pair) runs block-wide.
 template <class Pred, class Fn>
 DEV void for_overflow_pairs(int npairs, Pred overflow, Fn fn) {
-  __shared__ int s_list[1024], s_cnt;
+  // every block must see the same list in the same order (block b takes
+  // entries b, b + gridDim.x, ...): an order-preserving compaction, not
+  // atomics (whose order differs between blocks: pairs were skipped or run
+  // twice when several overflowed)
+  __shared__ int s_list[1024], s_wsum[1024 / 64 + 1];
   for (int c0 = 0; c0 < npairs; c0 += 1024) {
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    for (int p = c0 + threadIdx.x; p < min(npairs, c0 + 1024); p += blockDim.x)
-      if (overflow(p)) s_list[atomicAdd(&s_cnt, 1)] = p;
-    __syncthreads();
-    const int cnt = s_cnt;
+    const int cnt = block_compact(min(npairs - c0, 1024), [&](int j) { return overflow(c0 + j) ? 1 : 0; }, s_list,
+                                  s_wsum);
     for (int i = blockIdx.x; i < cnt; i += gridDim.x) {
-      fn(s_list[i]);
+      fn(c0 + s_list[i]);
       __syncthreads();  // the next pair reuses the block's shared variables
     }
     __syncthreads();

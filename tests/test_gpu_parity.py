@@ -249,3 +249,33 @@ def test_long_stream_device_frames():
     ctx.close()
     ref = slice_results(O.OracleRun(cfg, host).result, 1)
     assert_same(concat_results(parts), ref, "long: ")
+
+
+@pytest.mark.parametrize("rank", [900, 1500])
+def test_nms_long_lists_across_batches(rank):
+    """Lists of 900 / 1,500 positives (k_nms's rank sort / bitonic sort in
+    LDS, ties through the std::sort replica) over three batches of one
+    context, bit-exact against the oracle over the seams."""
+    c, dups = _quantized_config(rank)
+    assert dups > 20
+    frames = c.frames(0, 9)
+    ctx = _ctx(c, max_batch=3)
+    parts = [ctx.detect(frames[i:i + 3], i) for i in range(0, 9, 3)]
+    ctx.close()
+    assert_same(concat_results(parts), _oracle(c, frames).result, f"nms cap rank {rank}: ")
+
+
+def test_global_tier_few_overflowing_pairs():
+    """A few (frame, feature) pairs of a batch with lists beyond the LDS
+    capacity, the rest short (blank frames): every block of the global-scratch
+    tier must walk the same pair list in the same order (an atomics-built list
+    differed between blocks, so some pairs were never processed)."""
+    c, dups = _quantized_config(2500)  # lists beyond k_nms's LDS capacity (LM_NMS_CAP)
+    frames = c.frames(0, 12)
+    frames[[1, 2, 4, 5, 7, 9, 10]] = 0
+    ref = _oracle(c, frames).result
+    for _ in range(3):
+        ctx = _ctx(c, max_batch=12)
+        got = ctx.detect(frames, 0)
+        ctx.close()
+        assert_same(got, ref, "few overflowing pairs: ")
