@@ -47,26 +47,41 @@ struct LmDetGroup {
 #endif
 __host__ __device__ constexpr bool rw_all_width(int kw) { return kw >= 16 && (kw <= 32 || kw == 36 || kw == 40); }
 
-// k_corr_rw: one wave per 80 x 16 output tile, LM_RW_WAVES waves per workgroup
+// k_corr_rw: one wave per LM_RW_NQ sub-tiles of LM_FW x 8 outputs (or one
+// 80 x 16 tile split into them), LM_RW_WAVES waves per workgroup
 #ifndef LM_RW_WAVES
 #define LM_RW_WAVES 4
 #endif
 #define LM_RW_THREADS (64 * LM_RW_WAVES)
-#define LM_RW_TH 16     // output rows per wave (two half-tiles)
-#define LM_RW_HTH 8     // output rows per half-tile (also the dark-tile flag grid's rows)
+#ifndef LM_RW_ITEMS
+#define LM_RW_ITEMS 1  // work items (LM_RW_NQ sub-tiles each) per wave, one after another
+#endif
+#define LM_RW_TH 16     // output rows of a wave's 80 x 16 tile (tail detectors)
+#define LM_RW_HTH 8     // output rows per sub-tile (also the dark-tile flag grid's rows)
 #ifndef LM_RW_HSLOTS
-// ring rows per half (+ 1 mirror): rows t .. t + 5 are read at step t and row
-// t + HSLOTS is stored at its end, so 7 suffice; 7 gives kw 30 five waves per
-// SIMD instead of four but measured 1-2 % slower at C3 (profiles/r04/ring7),
-// so 8 (a power of two: the slot index is a mask)
-#define LM_RW_HSLOTS 8
+// ring rows per sub-tile (+ 1 mirror): rows t .. t + 5 are read at step t
+// and row t + HSLOTS is stored at its end, so 7 suffice.  80-column
+// sub-tiles: 8 (a power of two: the slot index is a mask; 7 gives kw 30 five
+// waves per SIMD instead of four but measured 1-2 % slower at C3,
+// profiles/r04/ring7); 40-column sub-tiles: 7, which keeps four waves per
+// SIMD (8 would leave three)
+#define LM_RW_HSLOTS (LM_RW_NQ == 4 ? 7 : 8)
 #endif
 static_assert(LM_RW_HSLOTS >= 7, "k_corr_rw ring: rows t .. t + 6 are live during step t");
 
-// window row: 80 + KW - 1 columns plus up to 3 before them (the loads start on
-// a 4-byte boundary); stride == 4 (mod 8)
-__host__ __device__ constexpr int rw_stride(int kw) { return pk_stride(LM_TW + kw - 1 + 3); }
-__host__ __device__ constexpr int rw_ring_floats(int kw) { return 2 * (LM_RW_HSLOTS + 1) * rw_stride(kw); }
+// window row of a sub-tile: LM_FW + KW - 1 columns plus up to 3 before them
+// (the loads start on a 4-byte boundary); stride == 4 (mod 8)
+__host__ __device__ constexpr int rw_stride(int kw) { return pk_stride(LM_FW + kw - 1 + 3); }
+// floats per sub-tile ring.  Two 40-column sub-tiles share each 32-lane
+// group of a ds_read2_b32: their rings start 8 (mod 32) floats apart, which
+// puts the second's 16 lanes on the 16 banks the first leaves free (its lanes
+// read columns 5 lx of rows r and r + 4: 5 lx + 16 ly (mod 32)).  Two
+// 80-column halves are in different lane groups.
+__host__ __device__ constexpr int rw_qpitch(int kw) {
+  return LM_RW_NQ == 2 ? (LM_RW_HSLOTS + 1) * rw_stride(kw)
+                       : (LM_RW_HSLOTS + 1) * rw_stride(kw) + (40 - ((LM_RW_HSLOTS + 1) * rw_stride(kw)) % 32) % 32;
+}
+__host__ __device__ constexpr int rw_ring_floats(int kw) { return LM_RW_NQ * rw_qpitch(kw); }
 __host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
   return (size_t)LM_RW_WAVES * rw_ring_floats(kw) * sizeof(float);
 }

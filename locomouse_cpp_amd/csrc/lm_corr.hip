@@ -199,34 +199,55 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
 // one column: for tap (i, j) both use weight w[i][j] (SGPR, broadcast) and
 // pixels (t, t+1) of one column, which one ds_read2_b32 loads into an aligned
 // register pair.  A thread owns 5 columns x 4 rows (two row pairs sharing the
-// pixel rows of a step with weight rows t and t - 2).  A wave is two
-// independent 80 x 8 half-tiles of 32 lanes (16 x 2 threads) — since round
-// 3, so that the dark-tile skip works at 80 x 8 granularity (72-73 % of the
-// synthetic point tiles bright vs 77-80 % at 80 x 16) — each streaming its
-// own window through a private LDS ring of LM_RW_HSLOTS rows + 1 mirror row:
-// at step t its 2 row groups read window rows t + 4 ly, t + 4 ly + 1 (rows
-// t .. t + 5), so 8 slots hold them plus rows t + 6, t + 7; the mirror slot
-// keeps a pair from wrapping.  LDS per wave is 2 x 9 rows (18 rows vs round
-// 2's 17 for one 80 x 16 tile), any kh fits, no wave waits for another and
-// a wave's LDS operations execute in order, so the rings need no barrier.
+// pixel rows of a step with weight rows t and t - 2).  A wave is LM_RW_NQ
+// independent sub-tiles of LM_FW x 8 outputs (round 4: four 40 x 8 quarters
+// of 16 lanes, 8 x 2 threads; round 3: two 80 x 8 halves of 32 lanes), so
+// the dark-tile skip works at LM_FW x 8 granularity (60-62 % of the
+// synthetic point outputs in bright 40 x 8 tiles vs 72-73 % at 80 x 8), each
+// streaming its own window through a private LDS ring of LM_RW_HSLOTS rows +
+// 1 mirror row: at step t its 2 row groups read window rows t + 4 ly,
+// t + 4 ly + 1 (rows t .. t + 5), the ring also holds the rows loaded ahead,
+// and the mirror slot keeps a pair from wrapping.  Any kh fits, no wave waits
+// for another and a wave's LDS operations execute in order, so the rings need
+// no barrier.
 
-// A ring wave's two 80 x 8 half-tiles (see rw_tile).
-struct RwHalves {
-  int slot[2], oy[2], ox[2];
-  int valid1;  // the second half holds a tile
+// A ring wave's sub-tiles (see rw_tile): LM_RW_NQ entries of a bright-tile
+// list, or the parts of one 80 x 16 tile.  Each lane looks up the sub-tiles
+// it needs (get: a vector load of the list entry or arithmetic) -- a
+// per-lane pick out of wave-uniform arrays compiled to a private-memory copy.
+struct RwTiles {
+  const uint32_t* l;  // listed: the wave's first entry; nullptr: one 80 x 16 tile
+  int nvalid;         // sub-tiles 0 .. nvalid - 1 hold a tile
+  int ftx;            // listed: flag-grid columns of the view
+  int slot, oy, ox;   // one tile: its slot and origin
+  DEV void get(int i, int& s, int& y, int& x) const {
+    if (l) {
+      const uint32_t e = l[i < nvalid ? i : 0];
+      const int lt = (int)(e & 0xFFFFu);
+      s = (int)(e >> 16);
+      y = (lt / ftx) * LM_RW_HTH;
+      x = (lt % ftx) * LM_FW;
+    } else {
+      s = slot;
+      y = oy + (i / (LM_RW_NQ / 2)) * LM_RW_HTH;
+      x = ox + (i % (LM_RW_NQ / 2)) * LM_FW;
+    }
+  }
 };
 
-// Wave g of a ring launch -> its detector and half-tiles.  The batch's work
+// Wave g of a ring launch -> its detector and sub-tiles.  The batch's work
 // is flattened detector-major (all slots of the group's first detector, then
 // the next ...), so no wave idles at a frame's end and the host can put the
 // longest detectors first.  With dark-tile lists (tl_cnt != nullptr) a point
-// detector's waves take its view's bright half-tiles two at a time
+// detector's waves take its view's bright LM_FW x 8 tiles LM_RW_NQ at a time
 // (k_ingest), so the group's wave count is known on the device only: the
-// grid is sized for every 80 x 16 tile and the waves past the last group's
-// count (whole workgroups at the grid's end) return.  Otherwise a wave takes
-// the two halves of one 80 x 16 tile.  false: past the last wave.
+// grid is sized for every 80 x 16 tile (as many outputs as a wave's
+// sub-tiles) and the waves past the last group's count (whole workgroups at
+// the grid's end) return.  Otherwise a wave takes the sub-tiles of one
+// 80 x 16 tile (row-major).  false: past the last wave.
 DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, const int32_t* tl_cnt,
-                        const uint32_t* tl_list, int& d, RwHalves& H) {
+                        const uint32_t* tl_list, int& d, RwTiles& H) {
+  constexpr int NQ = LM_RW_NQ;
   int base = 0;
 #pragma unroll
   for (int k = 0; k < LM_NDET; ++k) {
@@ -235,30 +256,24 @@ DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s
     const LmDet& D = K.det[d];
     const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
     const bool listed = tl_cnt != nullptr && D.kind == 0;
-    const int nh = listed ? tl_cnt[D.view] : 0;  // bright half-tiles
-    const int cnt = listed ? (nh + 1) >> 1 : nt * nslots;
+    const int nh = listed ? tl_cnt[D.view] : 0;  // bright tiles
+    const int cnt = listed ? (nh + NQ - 1) / NQ : nt * nslots;
     if (g < base + cnt) {
       const int local = g - base;
-      const int tx = D.tiles_x;
       if (listed) {
-        const uint32_t* __restrict__ l = tl_list + (int64_t)D.view * K.tl_stride + 2 * local;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const uint32_t e = (q == 0 || 2 * local + 1 < nh) ? l[q] : l[0];
-          const int lt = (int)(e & 0xFFFFu);
-          H.slot[q] = (int)(e >> 16);
-          H.oy[q] = (lt / tx) * LM_RW_HTH;
-          H.ox[q] = (lt % tx) * LM_TW;
-        }
-        H.valid1 = 2 * local + 1 < nh;
+        H.l = tl_list + (int64_t)D.view * K.tl_stride + NQ * local;
+        H.nvalid = min(NQ, nh - NQ * local);
+        H.ftx = K.fl_tx[D.view];
+        H.slot = H.oy = H.ox = 0;
       } else {
-        const int slot = s0 + local / nt;
+        const int tx = D.tiles_x;
         const int lt = local - (local / nt) * nt;
-        H.slot[0] = H.slot[1] = slot;
-        H.oy[0] = (lt / tx) * LM_RW_TH;
-        H.oy[1] = H.oy[0] + LM_RW_HTH;
-        H.ox[0] = H.ox[1] = (lt % tx) * LM_TW;
-        H.valid1 = 1;
+        H.l = nullptr;
+        H.nvalid = NQ;
+        H.ftx = 0;
+        H.slot = s0 + local / nt;
+        H.oy = (lt / tx) * LM_RW_TH;
+        H.ox = (lt % tx) * LM_TW;
       }
       return true;
     }
@@ -273,7 +288,7 @@ DEV bool corr_tile_dark(const LmConst& K, const LmDet& D, const uint8_t* __restr
   if (dark == nullptr || D.kind != 0) return false;
   const int v = D.view;
   const int ty0 = oy0 / LM_RW_HTH, ty1 = min(K.fl_ty[v] - 1, (oy0 + D.tile_h - 1) / LM_RW_HTH);
-  const int tx0 = ox0 / LM_TW, tx1 = min(K.fl_tx[v] - 1, (ox0 + D.tile_w - 1) / LM_TW);
+  const int tx0 = ox0 / LM_FW, tx1 = min(K.fl_tx[v] - 1, (ox0 + D.tile_w - 1) / LM_FW);
   const uint8_t* __restrict__ f = dark + (int64_t)slot * K.fl_slot + K.fl_off[v];
   for (int ty = ty0; ty <= ty1; ++ty)
     for (int tx = tx0; tx <= tx1; ++tx)
@@ -419,53 +434,60 @@ struct RwPipe {
   }
 };
 
-// One wave's work (the body of k_corr_rw and k_corr_rw_all): two 80 x 8
-// half-tiles, lanes 0-31 the first, lanes 32-63 the second, each half
-// streaming its own window through its own ring of 8 rows + 1 mirror.  The
-// halves are two bright half-tiles from the dark-tile list (any slots, any
-// places) or the two halves of one 80 x 16 tile (tail detectors, skip off).
-// Per half: lane (ly, lx) = ((lane >> 4) & 1, lane & 15) owns 5 columns x 4
-// rows as two packed row pairs; at step t it reads window rows t + 4 ly and
-// t + 4 ly + 1, so rows t .. t + 5 are live and the ring holds t .. t + 7;
-// row t + 8 is loaded at the step's start and stored into row t's slot at
-// its end.  A wave's LDS operations run in order, so no barrier anywhere.
+// One wave's work (the body of k_corr_rw and k_corr_rw_all): LM_RW_NQ
+// sub-tiles of LM_FW x 8 outputs, 64 / LM_RW_NQ consecutive lanes each, each
+// sub-tile streaming its own window through its own ring of LM_RW_HSLOTS
+// rows + 1 mirror.  The sub-tiles are bright tiles from the dark-tile list
+// (any slots, any places) or the parts of one 80 x 16 tile (tail detectors,
+// skip off).  Per sub-tile: lane (ly, lx) owns 5 columns x 4 rows as two
+// packed row pairs; at step t it reads window rows t + 4 ly and t + 4 ly + 1,
+// so rows t .. t + 5 are live; row t + HS is loaded at the step's start and
+// stored at its end into row t's slot.  A wave's LDS operations run in order,
+// so no barrier anywhere.
 template <int KW, bool UNF>
-DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D, const RwHalves& H, float* ring,
+DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D, const RwTiles& H, float* ring,
                                                 const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
                                                 const float* __restrict__ weights,
                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  const int lane = threadIdx.x & 63;
+  constexpr int NQ = LM_RW_NQ;
+  constexpr int QL = 64 / NQ;  // lanes per sub-tile
+  constexpr int QX = QL / 2;   // lanes across a sub-tile
+  static_assert(QX * PK_C == LM_FW, "sub-tile width");
   constexpr int STR = rw_stride(KW);
-  constexpr int NLH = (3 + LM_TW + KW - 1 + 3) / 4;  // dwords of a window row
-  constexpr bool DUAL = NLH > 32;                     // a row wider than half a wave: every lane loads both halves
-  static_assert(NLH <= 64, "window row wider than a wave's loads");
-  constexpr int HS = LM_RW_HSLOTS;                    // ring rows per half (+ 1 mirror)
+  constexpr int QP = rw_qpitch(KW);
+  constexpr int NL = (3 + LM_FW + KW - 1 + 3) / 4;  // dwords of a sub-tile's window row
+  constexpr int NLD = (NQ * NL + 63) / 64;          // dwords a lane loads per row
+  static_assert(NLD <= 2, "window rows wider than two loads per lane");
+  constexpr int HS = LM_RW_HSLOTS;
+  const int lane = threadIdx.x & 63;
   const int kh = D.kh, kwp = D.kwp;
   const int nrows = LM_RW_HTH + kh - 1;
   const int ew = K.ext_w[D.view];
   const int ew4 = ew >> 2;  // ext rows are padded to 16 bytes
-  const int h = lane >> 5, hl = lane & 31;
-  const int ly = hl >> 4, lx = lane & 15;
-  // this lane's half-tile, in VGPRs from here on (the halves' scalars are not
-  // kept live through the tap loop: the merged kernel's SGPRs are full)
-  const int slot = h ? H.slot[1] : H.slot[0];
-  const int oy0 = h ? H.oy[1] : H.oy[0];
-  const int ox0 = h ? H.ox[1] : H.ox[0];
-  const bool valid = h == 0 || H.valid1;
-  const uint8_t* src = corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0);
-  const int mis = (int)((uintptr_t)src & 3);
-  // row loads: each lane its own half's dword hl, or (DUAL) dword `lane` of
-  // both halves' rows: lane h' of a DUAL load of half q reads at the half's
-  // base, which lanes of half q hold in `a` (exchanged once, below)
-  const unsigned* __restrict__ a = reinterpret_cast<const unsigned*>(src - mis) + hl;
-  const uint8_t* src0 = corr_src(K, D, ext, ext_slot_bytes, H.slot[0], H.oy[0], H.ox[0]);  // DUAL: wave-uniform bases
-  const uint8_t* src1 = corr_src(K, D, ext, ext_slot_bytes, H.slot[1], H.oy[1], H.ox[1]);
-  const unsigned* __restrict__ a0 = reinterpret_cast<const unsigned*>(src0 - ((uintptr_t)src0 & 3)) + lane;
-  const unsigned* __restrict__ a1 = reinterpret_cast<const unsigned*>(src1 - ((uintptr_t)src1 & 3)) + lane;
-  const bool valid1 = H.valid1 != 0;
-  const bool ld = DUAL ? lane < NLH : (valid && hl < NLH);
-  const bool ld1 = DUAL && lane < NLH && valid1;
+  const int q = lane / QL, ql = lane % QL;
+  const int ly = ql / QX, lx = ql % QX;
+  // the lane's sub-tile (in VGPRs from here on: the merged kernel's SGPRs
+  // are full)
+  int slot, oy0, ox0;
+  H.get(q, slot, oy0, ox0);
+  const bool valid = q < H.nvalid;
+  const int mis = (int)((uintptr_t)corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0) & 3);
+  // row loads: load k of a lane is dword dk of sub-tile qk's window row
+  // (e = lane + 64 k = qk NL + dk), stored at float lo[k] of the rings
+  const unsigned* __restrict__ la[NLD];
+  int lo[NLD];
+  bool lk[NLD];
+#pragma unroll
+  for (int k = 0; k < NLD; ++k) {
+    const int e = lane + 64 * k, qk = e / NL, dk = e - qk * NL;
+    lk[k] = qk < H.nvalid;
+    int sk, yk, xk;
+    H.get(qk, sk, yk, xk);
+    const uint8_t* s = corr_src(K, D, ext, ext_slot_bytes, sk, yk, xk);
+    la[k] = reinterpret_cast<const unsigned*>(s - ((uintptr_t)s & 3)) + dk;
+    lo[k] = qk * QP + 4 * dk;
+  }
 
   // brightness mask of the point detectors' outputs (crop pixel > 25), read
   // from the ext crop now so the loads are long done by the epilogue
@@ -481,33 +503,29 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   }
 
   struct Row {
-    unsigned v, v1;
+    unsigned v[NLD];
   };
   auto load_row = [&](int r) -> Row {
-    Row w{0u, 0u};
-    if constexpr (DUAL) {
-      if (ld && r < nrows) w.v = a0[(int64_t)r * ew4];
-      if (ld1 && r < nrows) w.v1 = a1[(int64_t)r * ew4];
-    } else {
-      if (ld && r < nrows) w.v = a[(int64_t)r * ew4];
+    Row w;
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      w.v[k] = 0u;
+      if (lk[k] && r < nrows) w.v[k] = la[k][(int64_t)r * ew4];
     }
     return w;
-  };
-  auto put = [&](float* hr, int s, int col, unsigned v) {
-    const float4 f = make_float4((float)(v & 0xFFu), (float)((v >> 8) & 0xFFu), (float)((v >> 16) & 0xFFu),
-                                 (float)(v >> 24));
-    *reinterpret_cast<float4*>(hr + s * STR + 4 * col) = f;
-    if (s == 0) *reinterpret_cast<float4*>(hr + HS * STR + 4 * col) = f;
   };
   auto store_row = [&](int r, Row w) {
     if (r >= nrows) return;
     const int s = r % HS;  // r is wave-uniform: scalar arithmetic
-    if constexpr (DUAL) {
-      if (ld) put(ring, s, lane, w.v);
-      if (ld1) put(ring + (HS + 1) * STR, s, lane, w.v1);
-    } else {
-      if (ld) put(ring + h * (HS + 1) * STR, s, hl, w.v);
-    }
+#pragma unroll
+    for (int k = 0; k < NLD; ++k)
+      if (lk[k]) {
+        const unsigned v = w.v[k];
+        const float4 f = make_float4((float)(v & 0xFFu), (float)((v >> 8) & 0xFFu), (float)((v >> 16) & 0xFFu),
+                                     (float)(v >> 24));
+        *reinterpret_cast<float4*>(ring + lo[k] + s * STR) = f;
+        if (s == 0) *reinterpret_cast<float4*>(ring + lo[k] + HS * STR) = f;
+      }
   };
   {
     Row v0[HS];
@@ -521,7 +539,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   const lm_f2* __restrict__ W = reinterpret_cast<const lm_f2*>(weights + D.w_off);  // kwp is a multiple of 4
   const int kwp2 = kwp >> 1;
   const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring +
-                             (unsigned)(h * (HS + 1) * STR * (int)sizeof(float));
+                             (unsigned)(q * QP * (int)sizeof(float));
   const unsigned lane_off = (unsigned)((lx * PK_C + mis) * (int)sizeof(float));
   // ring slot of window row t + 4 ly (t wave-uniform: both candidates are
   // scalar, the lane picks one)
@@ -538,12 +556,12 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   S.template load_w<0>(S.wa, S.wb, wrow(0), wrow(-2));
   S.template issue<RwPlan<KW>::pbeg(0), RwPlan<KW>::pend(0)>(row_base(0));
   // Step t reads ring rows t .. t + 5 and prefetches step t + 1's rows in its
-  // last chunk; it loads row t + 8 at its start and stores it at its end into
-  // the slot of row t (dead by then: a wave's LDS operations run in order).
-  // The load has a whole step to land, and no register carries a row from
-  // one step to the next.
+  // last chunk; it loads row t + HS at its start and stores it at its end
+  // into the slot of row t (dead by then: a wave's LDS operations run in
+  // order).  The load has a whole step to land, and no register carries a
+  // row from one step to the next.
   auto step = [&](int t, auto A, auto B) {
-    Row nx{0u, 0u};
+    Row nx;
     S.template chunks<0, decltype(A)::value, decltype(B)::value>(row_base(t), row_base(t + 1), wrow(t), wrow(t - 2),
                                                                   wrow(t + 1), wrow(t - 1),
                                                                   [&]() { nx = load_row(t + HS); });
@@ -578,12 +596,13 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
       }
   }
   if (D.kind != 0) {
-    // tail map (the halves are one 80 x 16 tile: rows 4 (lane >> 4) + r of
-    // it): 16 rows x <= 4 u32 words (ox0 is a multiple of 80, so 80 columns
-    // touch at most 4 words) = one word per lane, gathered in the ring, then
-    // ORed into the slot's bitmap
+    // tail map (the sub-tiles are one 80 x 16 tile with sub-tile 0 at its
+    // top left): 16 rows x <= 4 u32 words (the tile's origin is a multiple of
+    // 80, so 80 columns touch at most 4 words) = one word per lane, gathered
+    // in the ring, then ORed into the slot's bitmap
     unsigned* s_tb = reinterpret_cast<unsigned*>(ring);
-    const int w0 = ox0 >> 5;  // both halves: the tile's columns
+    const int w0 = (ox0 - (q % (NQ / 2)) * LM_FW) >> 5;  // the tile's first word
+    const int ty = (q / (NQ / 2)) * LM_RW_HTH + ly * PK_R;  // the lane's first row in the tile
     s_tb[lane] = 0u;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -592,33 +611,33 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
       for (int c = 0; c < PK_C; ++c)
         if (bits & (1u << (r * PK_C + c))) {
           const int x = ox0 + lx * PK_C + c;
-          atomicOr(&s_tb[((lane >> 4) * PK_R + r) * 4 + (x >> 5) - w0], 1u << (x & 31));
+          atomicOr(&s_tb[(ty + r) * 4 + (x >> 5) - w0], 1u << (x & 31));
         }
     __builtin_amdgcn_wave_barrier();
     const unsigned v = s_tb[lane];
     unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(tailbin + (int64_t)slot * tailbin_slot_bytes) +
                                 (D.list ? (int64_t)K.tail_hb * K.tail_nw : 0);
-    const int y = oy0 - h * LM_RW_HTH + (lane >> 2), gw = w0 + (lane & 3);  // rows from the tile's top
+    const int y = oy0 - (q / (NQ / 2)) * LM_RW_HTH + (lane >> 2), gw = w0 + (lane & 3);  // rows from the tile's top
     if (v && y < D.oh && gw < K.tail_nw) atomicOr(&tb[(int64_t)y * K.tail_nw + gw], v);
     return;
   }
   bits &= mbits;
   // keys: each lane's set bits at consecutive places after the lanes of its
-  // half before it (popcount, then an inclusive scan over the 32 lanes of the
-  // half), one global atomic per half (keys are sorted later: their order in
-  // the list does not matter)
+  // sub-tile before it (popcount, then an inclusive scan over the sub-tile's
+  // lanes), one global atomic per sub-tile (keys are sorted later: their
+  // order in the list does not matter)
   const int cnt = __popc(bits);
   int incl = cnt;
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
-    const int u = __shfl_up(incl, o, 32);
-    if (hl >= o) incl += u;
+  for (int o = 1; o < QL; o <<= 1) {
+    const int u = __shfl_up(incl, o, QL);
+    if (ql >= o) incl += u;
   }
-  const int tot = __shfl(incl, 31, 32);  // the half's count (its last lane's inclusive sum)
+  const int tot = __shfl(incl, QL - 1, QL);  // the sub-tile's count (its last lane's inclusive sum)
   if (__ballot(tot != 0) == 0) return;
   int base_k = 0;
-  if (hl == 31 && tot) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
-  base_k = __shfl(base_k, 31, 32);
+  if (ql == QL - 1 && tot) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
+  base_k = __shfl(base_k, QL - 1, QL);
   unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k +
                                         (incl - cnt);
   int pos = 0;
@@ -639,7 +658,9 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
 
 // One launch per width group (LM_KW_LIST widths).
 template <int KW, bool UNF>
-__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? 5 : 1, 8))) void k_corr_rw(
+// waves per SIMD: LDS allows 5 (80-column sub-tiles, kw <= 32) or 4
+// (40-column); the register budget is set to match
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? (LM_RW_NQ == 4 ? 4 : 5) : 1, 8))) void k_corr_rw(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
     int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
@@ -647,19 +668,27 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
   const LmConst& K = *Kp;
   extern __shared__ uint4 lds_rw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int d;
-  RwHalves H;
-  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, tl_cnt, tl_list, d, H)) return;
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * rw_ring_floats(KW);
-  rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);
+  // LM_RW_ITEMS work items per wave, strided by the launch's wave count (the
+  // host sizes the grid for that many)
+  const int nwaves = gridDim.x * LM_RW_WAVES;
+  for (int g = blockIdx.x * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
+    int d;
+    RwTiles H;
+    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) return;
+    rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);
+  }
 }
 
 // Every ring detector of the context in ONE launch (longest first), so the
 // widths share the launch's tail instead of each ending its own; each wave
 // branches to its width's body.  G.ring_floats: LDS floats per wave (the
 // widest detector's ring).
+// Register budget: with 40-column sub-tiles the widths' bodies together need
+// ~154 VGPRs (each alone <= 99: the dispatch's SGPRs spill into VGPR lanes),
+// so three waves per SIMD instead of four, without spills.
 template <bool UNF>
-__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_corr_rw_all(
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(LM_RW_NQ == 4 ? 3 : 4, 8))) void k_corr_rw_all(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
     int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
@@ -667,20 +696,23 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(4
   const LmConst& K = *Kp;
   extern __shared__ uint4 lds_rw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int d;
-  RwHalves H;
-  if (!corr_locate_rw(K, G, nslots, s0, blockIdx.x * LM_RW_WAVES + wave, tl_cnt, tl_list, d, H)) return;
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * G.ring_floats;
-  const LmDet D = K.det[d];
-  switch (D.kw) {
+  const int nwaves = gridDim.x * LM_RW_WAVES;
+  for (int g = blockIdx.x * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
+    int d;
+    RwTiles H;
+    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) return;
+    const LmDet D = K.det[d];
+    switch (D.kw) {
 #define LM_KW_CASE(n)                                                                                             \
   case n:                                                                                                         \
     rw_tile<n, UNF>(K, D, H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);       \
     break;
-    LM_KW_LIST_RW_ALL(LM_KW_CASE)
+      LM_KW_LIST_RW_ALL(LM_KW_CASE)
 #undef LM_KW_CASE
-    default:
-      break;
+      default:
+        break;
+    }
   }
 }
 
@@ -1076,7 +1108,8 @@ hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t
                     (void*)&weights, (void*)&s0,   (void*)&nslots,  (void*)&keys,
                     (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes, (void*)&dk.cnt,
                     (void*)&dk.list};
-    return hipLaunchKernel(fn, dim3((waves + LM_RW_WAVES - 1) / LM_RW_WAVES), dim3(LM_RW_THREADS), args, lds, st);
+    const unsigned per_block = LM_RW_WAVES * LM_RW_ITEMS;  // work items per workgroup
+    return hipLaunchKernel(fn, dim3((waves + per_block - 1) / per_block), dim3(LM_RW_THREADS), args, lds, st);
   }
   void* args[] = {(void*)&K,     (void*)&G,       (void*)&ext,     (void*)&ext_slot_bytes,           (void*)&weights,
                   (void*)&s0,    (void*)&keys,    (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes,

@@ -19,6 +19,13 @@
 #define LM_TW (16 * LM_C)  // 80
 #define LM_TH (16 * LM_R)  // 48
 #define LM_JC 4            // tap chunk along a detector row (kw padded to a multiple)
+// k_corr_rw's wave computes LM_RW_NQ independent sub-tiles of LM_FW x 8
+// outputs (4: 40 x 8, 2: 80 x 8); LM_FW x 8 is also the dark-tile grid
+#ifndef LM_RW_NQ
+#define LM_RW_NQ 4
+#endif
+static_assert(LM_RW_NQ == 2 || LM_RW_NQ == 4, "k_corr_rw sub-tiles per wave");
+#define LM_FW (2 * LM_TW / LM_RW_NQ)
 
 // k_minmax: each frame split over LM_MM_SPLIT workgroups of LM_MM_THREADS
 #define LM_MM_SPLIT 8
@@ -75,7 +82,7 @@ struct LmConst {
   int32_t tail_nw, tail_bm_words;
   int32_t connectivity;
   // dark tiles (flagged and listed by k_ingest): per view, the point
-  // detectors' outputs in LM_TW x LM_RW_TH tiles (fl_tx x fl_ty of them); one
+  // detectors' outputs in LM_FW x LM_RW_HTH tiles (fl_tx x fl_ty of them); one
   // flag byte per (slot, view, tile) at slot * fl_slot + fl_off[view] + tile;
   // the bright tiles of view v listed at v * tl_stride of the tile list
   int32_t fl_tx[2], fl_ty[2], fl_off[2], fl_slot;

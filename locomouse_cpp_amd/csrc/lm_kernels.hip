@@ -186,7 +186,7 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 // per (view, 8-row band of the view's ext crop, slot group): the bands are
 // aligned with the dark-tile flag grid (band b holds the point detectors'
 // output rows 8b .. 8b + 7), so the workgroup that writes a tile row's pixels
-// also decides which of its 80 x 8 output tiles are bright (some I_*_MOUSE
+// also decides which of its LM_FW x 8 output tiles are bright (some I_*_MOUSE
 // pixel > 25, LocoMouse_class.cpp:782, :817), writes their flag bytes and
 // appends the bright ones to the view's tile list -- no second pass over the
 // crops.  Each thread owns 16 consecutive crop bytes of the band (one 16-byte
@@ -198,7 +198,8 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 // the gather is five aligned dword loads instead of sixteen byte loads.
 #define LM_INGEST_FB 8
 #define LM_INGEST_VEC 16
-#define LM_INGEST_MAXTX 64  // flag-grid columns a band's workgroup can hold (ow <= 5120)
+static_assert(LM_FW >= LM_INGEST_VEC, "a 16-byte chunk spans at most two flag tiles");
+#define LM_INGEST_MAXTX 128  // flag-grid columns a band's workgroup can hold (ow <= 128 LM_FW)
 
 // Gather indices and background bytes of the 16 crop pixels that start at
 // I_PAD (R, C0) (-1 / 0 outside I_UNPAD); returns 1 when idx[k] = idx[0] + k
@@ -357,14 +358,14 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
     const int64_t q = (v ? e0 : 0) + (int64_t)er * ew + ec;  // byte offset in the slot's ext crops
     // dark-tile flags: the bytes of this chunk that are point-detector
     // outputs' I_*_MOUSE pixels (output (y, x) = ext (fl_my + y, fl_mx + x)),
-    // split at the 80-column tile boundary: tile ta and ta + 1
+    // split at the LM_FW-column tile boundary: tile ta and ta + 1
     uint32_t ma[4] = {0u, 0u, 0u, 0u}, mb[4] = {0u, 0u, 0u, 0u};
     int ta = 0;
     const int y = er - K.fl_my[v];
     if (fl_band && y < K.fl_oh[v]) {
       const int x0 = ec - K.fl_mx[v];
-      ta = x0 >= 0 ? x0 / LM_TW : -((LM_TW - 1 - x0) / LM_TW);
-      const int lo = max(0, -x0), hi = min(LM_INGEST_VEC, K.fl_ow[v] - x0), ks = (ta + 1) * LM_TW - x0;
+      ta = x0 >= 0 ? x0 / LM_FW : -((LM_FW - 1 - x0) / LM_FW);
+      const int lo = max(0, -x0), hi = min(LM_INGEST_VEC, K.fl_ow[v] - x0), ks = (ta + 1) * LM_FW - x0;
       auto range = [](int a, int b) -> uint32_t {  // bits [a, b) of 16
         return a < b ? ((b >= 32 ? 0xFFFFFFFFu : (1u << b) - 1u) & ~((1u << a) - 1u)) & 0xFFFFu : 0u;
       };
@@ -508,7 +509,7 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
     flags[(int64_t)(sb + f) * K.fl_slot + K.fl_off[v] + ty * ftx + tx] = b;
     if (b && tl_list) {
       s_ent[atomicAdd(&s_n, 1)] = ((uint32_t)(sb + f) << 16) | (uint32_t)(ty * ftx + tx);
-      atomicAdd(&s_outs, oh_t * min(LM_TW, K.fl_ow[v] - tx * LM_TW));
+      atomicAdd(&s_outs, oh_t * min(LM_FW, K.fl_ow[v] - tx * LM_FW));
     }
   }
   if (!tl_list) return;
@@ -847,8 +848,10 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
 // (lm_introsort.h) — then clustered: nmsMax for the bottom view,
 // peakClustering for the side view.
 #define LM_NMS_THREADS 512
+#define LM_GLOB_BLOCKS 16   // grid of the global-scratch (<true>) k_nms / k_post launches: one scratch region each
 #define LM_NMS_CAP 2048     // entries kept in LDS; larger lists use the global-memory path
 #define LM_NMS_RANKSORT 1024  // up to this many entries: O(n^2/T) rank sort instead of bitonic
+#define LM_NMS_PAIRPAR 1024   // up to this many entries: nmsMax tests every pair, spread over the block
 
 DEV float key_score(unsigned long long k) { return __uint_as_float(~(unsigned)(k >> 32)); }
 DEV unsigned key_lo(unsigned long long k) { return (unsigned)(k & 0xFFFFFFFFu); }
@@ -1152,7 +1155,7 @@ DEV double readlane_f64(double v, int lane) {
 // (FLAT) pointers, which cost several times the latency of LDS accesses.
 // optional phase timestamps (LM_KPROF=1): clock64() of thread 0 per phase
 #define NMS_PROF(k) \
-  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = clock64();
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + (k)] = clock64();
 template <bool GLOB>
 DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int list, int side, int feat, int n_in,
                  const unsigned long long* __restrict__ src, const unsigned long long* __restrict__ tailmask,
@@ -1187,7 +1190,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   __syncthreads();
   NMS_PROF(1)
   const int n = s_n;
-  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 13] = n;
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 13] = n;
   int np = 1;
   while (np < n) np <<= 1;
   if (!glob && n <= LM_NMS_THREADS) {
@@ -1255,28 +1258,56 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   if (!side) {
     // nmsMax: every point, suppressed or not, suppresses the later points it
     // overlaps (:1677-1720) => j belongs to the first i < j overlapping it;
-    // maxima by pointer jumping.  Each j scans the earlier points 16 at a
-    // time (4 x 16 B loads in flight) and stops at its first hit: a cluster's
-    // points follow its maximum in score order, so most scans end early.
-    // (Tried and slower on ~300-point lists: a two-stage scan with one wave
-    // per unresolved point, 30k vs 25k cycles; x-window and x-bucket scans
-    // over a second sort, 80k / 36k: the points of the paw clusters share
-    // their x ranges, profiles/r03/h, /i.)
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      const unsigned xj = xy[j];
-      int as = j;
-      for (int i0 = 0; i0 < j && as == j; i0 += 16) {
+    // maxima by pointer jumping.
+    if (n <= LM_NMS_PAIRPAR) {
+      // Every (i < j) pair tested once, spread evenly over the block: tile
+      // (b, j) holds the pairs i in [16 b, min(16 b + 16, j)), tiles in (b, j)
+      // order, a thread takes every blockDim-th one; its first hit goes to
+      // assign[j] by an LDS atomicMin.  (Each j scanning its earlier points
+      // until its first hit left the block waiting for the last maxima's full
+      // scans: ~25k cycles at ~300 points.)
+      for (int j = threadIdx.x; j < n; j += blockDim.x) assign[j] = j;
+      __syncthreads();
+      int b = 0, j = 1 + threadIdx.x;  // tile index threadIdx.x: row b = 0 holds j = 1 .. n - 1
+      while (true) {
+        while (b * 16 + 1 < n && j >= n) {  // past row b: into row b + 1 (j = 16 (b + 1) + 1 ..)
+          const int over = j - n;
+          ++b;
+          j = 16 * b + 1 + over;
+        }
+        if (j >= n) break;
+        const int i0 = 16 * b;
         unsigned v[16];
         *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(xy + i0);
         *reinterpret_cast<uint4*>(v + 4) = *reinterpret_cast<const uint4*>(xy + i0 + 4);
         *reinterpret_cast<uint4*>(v + 8) = *reinterpret_cast<const uint4*>(xy + i0 + 8);
         *reinterpret_cast<uint4*>(v + 12) = *reinterpret_cast<const uint4*>(xy + i0 + 12);
+        const unsigned xj = xy[j];
         unsigned hit = 0;
 #pragma unroll
         for (int t = 0; t < 16; ++t) hit |= (unsigned)(i0 + t < j && overlaps_xy(v[t], xj, bw, bh)) << t;
-        if (hit) as = i0 + __ffs(hit) - 1;
+        if (hit) atomicMin(&assign[j], i0 + __ffs(hit) - 1);
+        j += blockDim.x;
       }
-      assign[j] = as;
+    } else {
+      // long lists: each j scans the earlier points 16 at a time (4 x 16 B
+      // loads in flight) and stops at its first hit
+      for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        const unsigned xj = xy[j];
+        int as = j;
+        for (int i0 = 0; i0 < j && as == j; i0 += 16) {
+          unsigned v[16];
+          *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(xy + i0);
+          *reinterpret_cast<uint4*>(v + 4) = *reinterpret_cast<const uint4*>(xy + i0 + 4);
+          *reinterpret_cast<uint4*>(v + 8) = *reinterpret_cast<const uint4*>(xy + i0 + 8);
+          *reinterpret_cast<uint4*>(v + 12) = *reinterpret_cast<const uint4*>(xy + i0 + 12);
+          unsigned hit = 0;
+#pragma unroll
+          for (int t = 0; t < 16; ++t) hit |= (unsigned)(i0 + t < j && overlaps_xy(v[t], xj, bw, bh)) << t;
+          if (hit) as = i0 + __ffs(hit) - 1;
+        }
+        assign[j] = as;
+      }
     }
     __syncthreads();
     NMS_PROF(4)
@@ -1377,7 +1408,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
     }
   }
   NMS_PROF(7)
-  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 15] = wall_clock64();
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 15] = wall_clock64();
   if (threadIdx.x == 0) {
     H->n_pos[list] = n;
     H->cand_cnt[list] = fits ? ncand : 0;
@@ -1386,22 +1417,37 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   return fits ? ncand : 0;
 }
 
-// One block per (slot, feature) runs the bottom list (nmsMax) and then, for
-// the batch's frames, the side list (peakClustering), which
-// detectSideCandidates skips when the bottom list came out empty (:820-833):
-// no kernel boundary between the two, so a frame's side list does not wait
-// for the slowest bottom block of the batch.  <false>: lists of at most
-// LM_NMS_CAP positives, in LDS.  <true>: the pairs with a longer bottom list
-// (both lists), or a longer side list behind a non-empty bottom one, in
-// global scratch (for_overflow_pairs, launched after <false>).
+// One block per (slot, list): nmsMax for the bottom lists, peakClustering
+// for the side lists.  detectSideCandidates runs only when the frame's
+// bottom candidate list for the feature is non-empty (:820-833); nmsMax makes
+// at least one candidate from any non-empty point list, so a side block
+// decides that itself -- is any bottom key left after the TAIL_MASK filter --
+// and does not wait for the bottom block.  <false>: lists of at most
+// LM_NMS_CAP positives, in LDS.  <true>: the longer lists, in global scratch
+// (for_overflow_pairs, launched after <false>).
+// Some bottom key of (slot, feature) survives the TAIL_MASK filter (block-wide).
+DEV bool bottom_nonempty(const LmConst& K, const LmDet& D, const unsigned long long* __restrict__ src, int n,
+                         const unsigned long long* __restrict__ tailmask, int slot) {
+  const int tnb = (K.tail_w + 63) / 64;
+  const unsigned long long* __restrict__ tm = tailmask + (int64_t)slot * K.tail_hb * tnb;
+  int keep = 0;
+  for (int k = threadIdx.x; k < n && !keep; k += blockDim.x) {
+    const unsigned idx = key_lo(src[k]);
+    const int y = idx / D.ow, x = idx - y * D.ow;
+    keep = !(x < K.tail_w && y < K.tail_hb && ((tm[y * tnb + (x >> 6)] >> (x & 63)) & 1));
+  }
+  return __syncthreads_or(keep) != 0;
+}
+
 template <bool GLOB>
-DEV void nms_block(int bx, int feat, const LmConst* __restrict__ Kp, int s0, unsigned long long* __restrict__ keys,
+DEV void nms_block(int bx, int list, const LmConst* __restrict__ Kp, int s0, unsigned long long* __restrict__ keys,
                    const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
                    unsigned long long* __restrict__ gscratch, int64_t gscratch_slot, LmSlotOut* __restrict__ hdr,
                    int32_t* __restrict__ err, long long* __restrict__ prof_b, long long* __restrict__ prof_s) {
   constexpr int ACAP = GLOB ? 1 : LM_NMS_CAP;  // LDS array sizes
   const LmConst& K = *Kp;
-  const int slot = s0 + bx;  // feat: 0 paw, 1 snout
+  const int slot = s0 + bx;
+  const int feat = list & 1, side = list >> 1;  // feat: 0 paw, 1 snout
   LmSlotOut* H = hdr + slot;
   // 16-byte aligned: the sorts and the nmsMax sweep read them with ds_read_b128
   __shared__ __attribute__((aligned(16))) unsigned long long s_keys[ACAP];
@@ -1414,61 +1460,47 @@ DEV void nms_block(int bx, int feat, const LmConst* __restrict__ Kp, int s0, uns
   __shared__ int s_n, s_flag, s_qcnt[2];
   static_assert(LM_NMS_RANKSORT * 8 <= LM_NMS_CAP * 4, "s_assign holds the sorts' keys");
   const int64_t npg = gscratch_slot / 3;
-  unsigned long long* ga = gscratch + (int64_t)(feat + 2 * bx) * gscratch_slot;
+  // <true>: the launch's block b works its pairs one after another in scratch region b
+  unsigned long long* ga = gscratch + (int64_t)(GLOB ? blockIdx.x : 0) * gscratch_slot;
   int* gassign = reinterpret_cast<int*>(ga + npg);
   int* gmlist = gassign + npg;
-  // one list (side 0: bottom, 1: side) of this (slot, feature): returns its candidate count
-  auto run = [&](int side, int n_in, long long* prof) -> int {
-    const int list = side ? 2 + feat : feat;
-    const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
-    const LmDet D = K.det[det];
-    NMS_PROF(0)
-    if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + blockIdx.y) * 16 + 14] = wall_clock64();
-    const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
-    int c;
-    if constexpr (!GLOB)
-      c = nms_run<false>(K, D, H, slot, list, side, feat, n_in, src, tailmask, s_keys, s_assign, s_mlist, s_xy, s_tmp,
-                         reinterpret_cast<unsigned long long*>(s_assign), LM_NMS_CAP / 6, s_stk, s_wsum, &s_n, &s_flag,
-                         s_qcnt, keys, err, prof);
-    else
-      c = nms_run<true>(K, D, H, slot, list, side, feat, n_in, src, tailmask, ga, gassign, gmlist,
-                        reinterpret_cast<unsigned*>(gmlist + npg), s_tmp, reinterpret_cast<unsigned long long*>(gassign), 0,
-                        s_stk, s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
-    __syncthreads();  // the next list reuses the block's arrays
-    return c;
-  };
-  auto skip_side = [&]() {  // detectSideCandidates not run: an empty side list
-    if (threadIdx.x == 0) {
-      H->n_pos[2 + feat] = 0;
-      H->cand_cnt[2 + feat] = 0;
-      H->ties[2 + feat] = 0;
-    }
-  };
-  const int n_b = n_pos[slot * LM_NLIST + feat];
-  const int n_s = slot >= 1 ? n_pos[slot * LM_NLIST + 2 + feat] : 0;
+  const int n_in = n_pos[slot * LM_NLIST + list];
+  if (side && slot < 1) return;  // the previous frame (halo slot): bottom lists only
 #if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 1)
-  if (threadIdx.x == 0)
-    for (int l = feat; l < LM_NLIST; l += 2) {
-      H->n_pos[l] = 0;
-      H->cand_cnt[l] = 0;
-      H->ties[l] = 0;
-    }
+  if (threadIdx.x == 0) {
+    H->n_pos[list] = 0;
+    H->cand_cnt[list] = 0;
+    H->ties[list] = 0;
+  }
   return;
 #endif
-  if constexpr (!GLOB) {
-    if (n_b > LM_NMS_CAP) return;  // both lists go to <true>
-    const int cb = run(0, n_b, prof_b);
-    if (slot < 1) return;  // the previous frame (halo slot): bottom list only
-    if (cb == 0) skip_side();
-    else if (n_s <= LM_NMS_CAP) run(1, n_s, prof_s);
-  } else {
-    int cb;
-    if (n_b > LM_NMS_CAP) cb = run(0, n_b, nullptr);
-    else cb = H->cand_cnt[feat];  // written by <false> (an earlier launch)
-    if (slot < 1) return;
-    if (cb == 0) skip_side();
-    else if (n_b > LM_NMS_CAP || n_s > LM_NMS_CAP) run(1, n_s, nullptr);
+  if (GLOB != (n_in > LM_NMS_CAP)) return;  // the other instantiation's list
+  const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
+  const LmDet D = K.det[det];
+  if (side) {
+    const int bdet = feat == 0 ? DET_PAW_B : DET_SNOUT_B;
+    const unsigned long long* __restrict__ bsrc = keys + (int64_t)slot * K.keys_per_slot + K.list_off[feat];
+    if (!bottom_nonempty(K, K.det[bdet], bsrc, n_pos[slot * LM_NLIST + feat], tailmask, slot)) {
+      if (threadIdx.x == 0) {  // detectSideCandidates not run: an empty side list
+        H->n_pos[list] = 0;
+        H->cand_cnt[list] = 0;
+        H->ties[list] = 0;
+      }
+      return;
+    }
   }
+  long long* prof = side ? prof_s : prof_b;
+  NMS_PROF(0)
+  if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 14] = wall_clock64();
+  const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
+  if constexpr (!GLOB)
+    nms_run<false>(K, D, H, slot, list, side, feat, n_in, src, tailmask, s_keys, s_assign, s_mlist, s_xy, s_tmp,
+                   reinterpret_cast<unsigned long long*>(s_assign), LM_NMS_CAP / 6, s_stk, s_wsum, &s_n, &s_flag, s_qcnt,
+                   keys, err, prof);
+  else
+    nms_run<true>(K, D, H, slot, list, side, feat, n_in, src, tailmask, ga, gassign, gmlist,
+                  reinterpret_cast<unsigned*>(gmlist + npg), s_tmp, reinterpret_cast<unsigned long long*>(gassign), 0,
+                  s_stk, s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
 }
 
 // For the <true> (global-scratch) instantiations of k_nms / k_post: a small
@@ -1517,14 +1549,13 @@ __global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restric
                      prof_s);
   else
     for_overflow_pairs(
-        npairs,
+        npairs,  // (slot, list) pairs
         [&](int p) {
-          const int slot = s0 + (p >> 1), feat = p & 1;
-          const int n_b = n_pos[slot * LM_NLIST + feat], n_s = n_pos[slot * LM_NLIST + 2 + feat];
-          return n_b > LM_NMS_CAP || (slot >= 1 && n_s > LM_NMS_CAP && hdr[slot].cand_cnt[feat] > 0);
+          const int slot = s0 + (p >> 2), list = p & 3;
+          return n_pos[slot * LM_NLIST + list] > LM_NMS_CAP && (slot >= 1 || list < 2);
         },
         [&](int p) {
-          nms_block<true>(p >> 1, p & 1, Kp, s0, keys, n_pos, tailmask, gscratch, gscratch_slot, hdr, err, nullptr,
+          nms_block<true>(p >> 2, p & 3, Kp, s0, keys, n_pos, tailmask, gscratch, gscratch_slot, hdr, err, nullptr,
                           nullptr);
         });
 #undef NMS_PROF
@@ -1960,9 +1991,10 @@ DEV void post_block(int bx, int feat, LM_POST_ARGS) {
     post_run<false>(K, slots, frame_ptr, bkg, cal, luts, H, slot, feat, frame, Nb, Ns, Ni, sb, st, sp, s_off, s_mb, s_mt,
                     s_bps, s_tpb, LM_POST_MAXC, s_base, s_any1, s_any0, arena_p22d, arena_side_y, arena_side_s,
                     arena_unary, arena_jc, arena_ir, arena_pr, ctl, err, (2 * bx + feat) % ctl->nparts, prof);
-  } else {  // long lists: k_nms's scratch of this (slot, feature) is free again
+  } else {  // long lists, in the block's global scratch region
     const int big = max(max(Nb, Ns), Ni);
-    int* g = reinterpret_cast<int*>(gscratch + (int64_t)(feat + 2 * bx) * gscratch_slot);
+    // the launch's block b works its pairs one after another in scratch region b
+    int* g = reinterpret_cast<int*>(gscratch + (int64_t)blockIdx.x * gscratch_slot);
     int* g_off = g;                      // max(Ni + Nong, Nb) + 1
     int* g_mb = g_off + max(Ni + Nong, Nb) + 1;
     int* g_mt = g_mb + big;

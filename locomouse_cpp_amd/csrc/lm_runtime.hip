@@ -30,7 +30,7 @@
 namespace {
 
 // Timing experiments only (scripts/build_variant_rt.sh -DLM_EXP_SKIP=...;
-// results are wrong): 1 k_nms writes empty lists, 16 no correlation launch.
+// results are wrong): 1 k_nms writes empty lists, 2 no k_tail, 16 no correlation launch.
 #ifndef LM_EXP_SKIP
 #define LM_EXP_SKIP 0
 #endif
@@ -472,7 +472,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     int o = 0;
     for (int v = 0; v < 2; ++v) {
       const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
-      K.fl_tx[v] = (D.ow + LM_TW - 1) / LM_TW;
+      K.fl_tx[v] = (D.ow + LM_FW - 1) / LM_FW;
       K.fl_ty[v] = (D.oh + LM_RW_HTH - 1) / LM_RW_HTH;
       K.fl_off[v] = o;
       o += (K.fl_tx[v] * K.fl_ty[v] + 3) / 4 * 4;
@@ -573,7 +573,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
   c->dbg_slot_floats = doff;
   int np = 1;
   while (np < std::max(K.list_cap[0], K.list_cap[2])) np <<= 1;
-  // per (slot, feature): k_nms's keys (u64) + assign, cluster list, xy (32-bit)
+  // one region per block of the global-scratch k_nms / k_post launches: k_nms's keys (u64) + assign, cluster list, xy (32-bit)
   // per entry; then reused by k_post for lists beyond its LDS capacity
   // (offsets np + Nong + 1, motion flags 2 np, counts 2 np: 32-bit each)
   c->gscratch_slot = std::max(3 * (int64_t)np, (5 * (int64_t)np + K.ong_nx * K.ong_ny + 2) / 2 + 1);
@@ -1057,7 +1057,8 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
       kp3 = L.kprof.p + 3 * 16 * 2 * c->nslots;
     }
     T.begin("k_tail");
-    if (c->tail_big)
+    if (LM_EXP_SKIP & 2) {
+    } else if (c->tail_big)
       k_tail<true><<<nproc, LM_TAIL_THREADS, 0, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes, L.tailmask.p,
                                                       L.tscratch.p, A.hdr.p, kp2, L.tail_ws.p, c->tail_ws_slot);
     else
@@ -1065,18 +1066,18 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
                                                                  L.tailmask.p, L.tscratch.p, A.hdr.p, kp2, nullptr, 0);
     T.end();
     T.begin("k_nms");
-    // bottom then side lists per (slot, feature); lists beyond the LDS capacity in global scratch
-    k_nms<false><<<dim3(nproc, 2), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
+    // one block per (slot, list); lists beyond the LDS capacity in global scratch
+    k_nms<false><<<dim3(nproc, 4), LM_NMS_THREADS, 0, st>>>(dK, s_proc0, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
                                                            c->gscratch_slot, A.hdr.p, L.err.p, kp0, kp1, 0);
-    k_nms<true><<<16, LM_NMS_THREADS, 0, st>>>(dK, s_proc0, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
-                                              c->gscratch_slot, A.hdr.p, L.err.p, nullptr, nullptr, 2 * nproc);
+    k_nms<true><<<LM_GLOB_BLOCKS, LM_NMS_THREADS, 0, st>>>(dK, s_proc0, L.keys.p, L.npos.p, L.tailmask.p, L.gscratch.p,
+                                              c->gscratch_slot, A.hdr.p, L.err.p, nullptr, nullptr, 4 * nproc);
     T.end();
     T.begin("k_post");
     k_post<false><<<dim3(n, 2), LM_POST_THREADS, 0, st>>>(dK, L.slots.p, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p,
                                                          A.hdr.p, L.keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p,
                                                          A.jc.p, A.ir.p, A.pr.p, A.ctl.p, L.err.p, L.gscratch.p,
                                                          c->gscratch_slot, kp3, 0);
-    k_post<true><<<16, LM_POST_THREADS, 0, st>>>(dK, L.slots.p, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, A.hdr.p,
+    k_post<true><<<LM_GLOB_BLOCKS, LM_POST_THREADS, 0, st>>>(dK, L.slots.p, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, A.hdr.p,
                                                 L.keys.p, A.p22d.p, A.side_y.p, A.side_s.p, A.unary.p, A.jc.p, A.ir.p,
                                                 A.pr.p, A.ctl.p, L.err.p, L.gscratch.p, c->gscratch_slot, nullptr,
                                                 2 * n);
@@ -1343,7 +1344,7 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
     }
     HIPCHK(hipEventRecord(L.ev_consumed, st));
   }
-  if (!L.gscratch.p) L.gscratch.alloc((size_t)c->gscratch_slot * 2 * c->nslots);
+  if (!L.gscratch.p) L.gscratch.alloc((size_t)c->gscratch_slot * LM_GLOB_BLOCKS);  // one region per block of the <true> launches
   // k_ingest's source map: rebuilt for a view when every processed slot has
   // its crop at one position that the lane's map does not hold
   for (int v = 0; v < 2; ++v) {
@@ -1702,6 +1703,8 @@ LM_API lm_status lm_debug_corr_work(const lm_ctx* ctx, int32_t* out) {
 }
 
 LM_API int32_t lm_debug_batch_slots(const lm_ctx* ctx) { return ctx ? ctx->delivered.slots : 0; }
+
+LM_API int32_t lm_debug_dark_tile_width(void) { return LM_FW; }
 
 namespace {
 // The lane whose device buffers still hold the last collected batch's debug

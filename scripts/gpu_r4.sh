@@ -3,14 +3,16 @@
 # oracle checks (C3 default, the drop-in 1 context x 4 lanes, C5 fp32), the
 # C4 strong-scaling mode on one GPU and rehearsed with 4 oversubscribed
 # ranks, and the launcher's refusal of --gpus 2 on a one-GPU box.
-# STEPS=tests,smoke,bench,lanes,c5,video,refuse selects steps.
+# STEPS=tests,smoke,bench,lanes,c5,video,refuse,prof,traffic selects steps
+# (default: all but kprof).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 TAG=${TAG:-r4}
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp MASTER_ADDR=127.0.0.1
-S=",${STEPS:-tests,smoke,bench,lanes,c5,video,refuse},"
+S=",${STEPS:-tests,smoke,bench,lanes,c5,video,refuse,prof,traffic},"
+# kprof: phase cycles of k_nms / k_tail / k_post (LM_KPROF=1, one stream)
 on() { [[ $S == *",$1,"* ]]; }
 if on tests; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread ${PYTEST_ARGS:-} > $O/gpu_tests.log 2>&1
@@ -44,5 +46,25 @@ if on refuse; then
   rc=$?
   echo "bench --gpus 2 on this box: rc=$rc (must be non-zero), stdout lines: $(wc -l < $O/refuse.out)"; tail -2 $O/refuse.err
   [ $rc -ne 0 ] || exit 1
+fi
+if on kprof; then
+  LM_KPROF=1 timeout -k 10 240 python bench.py --streams 1 --steps 3 --warmup 1 --no-cpu --no-check > $O/kprof.json 2> $O/kprof.txt || { tail -5 $O/kprof.txt; exit 1; }
+  grep "kprof k_nms" $O/kprof.txt | tail -2
+fi
+# prof: rocprofv3 kernel trace + stats of the driver's bench command (no CPU
+# legs), and the union of the correlation dispatches' spans
+if on prof; then
+  rm -rf $O/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-check > $O/prof.out 2>&1 || { echo "rocprof failed"; tail -20 $O/prof.out; exit 1; }
+  python3 scripts/prof_union.py $O/prof/run_kernel_trace.csv 4 20 > $O/prof_union.txt && tail -4 $O/prof_union.txt
+fi
+# traffic: FETCH_SIZE and WRITE_SIZE of the correlation, one --pmc pass each
+# -> $O/pmc_k_corr.json (copied to profiles/r04/ for bench.py's traffic)
+if on traffic; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    rm -rf $O/pmc/$c
+    timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -f csv -d $O/pmc/$c -o run -- python3 bench.py --steps 4 --warmup 1 --no-cpu --no-check > $O/pmc_$c.out 2>&1 || { echo "pmc $c failed"; tail -5 $O/pmc_$c.out; exit 1; }
+  done
+  python3 scripts/pmc_traffic.py $O/pmc 256 $O/pmc_k_corr.json > $O/pmc_traffic.txt && tail -3 $O/pmc_traffic.txt
 fi
 echo done

@@ -94,3 +94,75 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+OBJDUMP = "/opt/rocm/llvm/bin/llvm-objdump"
+
+
+def disassemble(lib, symbol_filter):
+    """{function symbol: [instruction text]} of the code objects' functions
+    whose names contain symbol_filter (llvm-objdump, no GPU needed)."""
+    out = {}
+    for co in code_objects(lib):
+        with tempfile.NamedTemporaryFile(suffix=".co", delete=False) as fh:
+            fh.write(co)
+            name = fh.name
+        try:
+            txt = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", name], capture_output=True, text=True,
+                                 check=True).stdout
+        finally:
+            os.unlink(name)
+        cur = None
+        for line in txt.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+            if m:
+                cur = m.group(1) if symbol_filter in m.group(1) else None
+                if cur is not None:
+                    out[cur] = []
+                continue
+            if cur is not None:
+                ins = line.split("//")[0].strip()
+                if ins:
+                    out[cur].append(ins)
+    return out
+
+
+def _vregs(operand):
+    """VGPR numbers an operand names (v7, v[4:5])."""
+    m = re.fullmatch(r"v(\d+)", operand)
+    if m:
+        return {int(m.group(1))}
+    m = re.fullmatch(r"v\[(\d+):(\d+)\]", operand)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    return set()
+
+
+def early_reads_of_lds_pairs(instrs):
+    """Instructions that read a VGPR written by a ds_read2_b32 before an
+    s_waitcnt that drains the LDS counter (lgkmcnt(0)) has executed, in
+    program order.  The ring correlation issues those reads as inline asm
+    the compiler's wait insertion does not see, so a register copy or use
+    before the explicit wait would read stale data."""
+    pending, bad = set(), []
+    for ins in instrs:
+        op, _, rest = ins.partition(" ")
+        ops = [o.strip() for o in rest.split(",")] if rest else []
+        if op.startswith("s_waitcnt") and ("lgkmcnt(0)" in rest or "lgkmcnt" not in rest and "vmcnt" not in rest
+                                           and "expcnt" not in rest):
+            pending.clear()
+            continue
+        srcs = set()
+        for o in ops[1:] if ops else []:
+            srcs |= _vregs(o.split()[0]) if o else set()
+        if op.startswith("ds_write") or op.startswith("ds_read") or op.startswith("global_store"):
+            # stores read their data/address operands; a ds_read2 reads its address (operand 1)
+            srcs = set().union(*[_vregs(o.split()[0]) for o in ops[1:] if o]) if op.startswith(("ds_write", "global_store")) \
+                else (_vregs(ops[1].split()[0]) if len(ops) > 1 else set())
+        if srcs & pending:
+            bad.append(ins)
+        if op == "ds_read2_b32" and ops:
+            pending |= _vregs(ops[0])
+        elif ops and op.startswith("v_"):
+            pending -= _vregs(ops[0])  # overwritten: no longer the load's destination
+    return bad

@@ -58,3 +58,26 @@ def test_world2_hip_shards_match_oracle(tmp_path, batch):
     got = {k: z[k] for k in KEYS}
     got["n_frames"] = N_FRAMES
     assert_same(got, ref, f"world2 b{batch}: ")
+
+
+@pytest.mark.parametrize("ranks,lanes", [(2, 1), (3, 4)])
+def test_bench_video_mode_shards_whole_video(ranks, lanes):
+    """BASELINE config 4's shape through bench.py itself: one video split into
+    contiguous shards over `ranks` processes (spawned by bench.py --gpus,
+    oversubscribed on this box's one GPU), several contexts per rank, batches
+    with a 1-frame halo at every shard start; rank 0 gathers every frame and
+    checks all of them against the oracle (video_check)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(ranks), "--oversubscribe",
+                        "--video-frames", "700", "--batch", "64", "--streams", "2", "--lanes", str(lanes),
+                        "--steps", "1", "--warmup", "1", "--no-cpu"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == ranks and line["scaling"] == "strong"
+    assert line["gathered"]["frames"] == 700 and line["gathered"]["whole_and_disjoint"]
+    assert line["video_check"]["frames"] == 700 and line["video_check"]["bit_exact"], line["video_check"]

@@ -1,12 +1,15 @@
 """Register / scratch budget of every gfx950 kernel in liblocomouse_hip.so,
-read from the code objects' metadata (no GPU needed).
+read from the code objects' metadata, and the ring correlation's LDS-wait
+discipline, read from their disassembly (llvm-objdump; no GPU needed).
 
 The ring correlation (k_corr_rw) loads its pixel pairs with inline-asm
 ds_read2_b32 and waits for them with an explicit s_waitcnt at each chunk
 start; a spill or register copy of those pairs between issue and wait would
 read stale LDS data unnoticed by the compiler.  So no kernel may spill VGPRs
-or use scratch, and the width-specialised ring kernels must hold 5 waves per
-SIMD (<= 96 VGPRs) with no SGPR spills either."""
+or use scratch, the width-specialised ring kernels must hold 5 waves per SIMD
+(<= 96 VGPRs) with no SGPR spills either, and in every ring kernel no
+instruction may read a VGPR a ds_read2_b32 wrote before the next
+s_waitcnt lgkmcnt(0) (test_ring_reads_wait_for_lds)."""
 import os
 import re
 import sys
@@ -40,6 +43,30 @@ def test_ring_correlation_budget(kernels):
     for k, r in ring.items():
         kw = int(re.match(r"_Z9k_corr_rwILi(\d+)E", k).group(1))
         assert r["sgpr_spill_count"] == 0, (k, r)
-        # 5 waves per SIMD up to kw 32; wider rings (>= 8.5 KB of LDS per
-        # wave) run at most 4 waves per SIMD, which 128 VGPRs allow
-        assert r["vgpr_count"] <= (96 if kw <= 32 else 128), (k, r)
+        # four 40 x 8 sub-tiles per wave: the rings (>= 8.6 KB of LDS per
+        # wave) allow at most 4 waves per SIMD, which 128 VGPRs allow
+        assert r["vgpr_count"] <= 128, (k, r)
+
+
+def test_ring_reads_wait_for_lds():
+    import kernel_resources
+    if not os.path.exists(LIB):
+        pytest.skip("liblocomouse_hip.so not built")
+    funcs = kernel_resources.disassemble(LIB, "k_corr_rw")
+    assert len(funcs) >= 2 * 25 + 2, sorted(funcs)[:4]
+    for name, ins in funcs.items():
+        assert sum(1 for i in ins if i.startswith("ds_read2_b32")) > 0, name
+        bad = kernel_resources.early_reads_of_lds_pairs(ins)
+        assert not bad, (name, bad[:4])
+
+
+def test_lds_wait_checker_flags_an_early_read():
+    import kernel_resources
+    ok = ["ds_read2_b32 v[2:3], v9 offset0:1 offset1:117", "s_waitcnt lgkmcnt(0)",
+          "v_pk_fma_f32 v[4:5], s[8:9], v[2:3], v[4:5] op_sel_hi:[0,1,1]"]
+    early = ["ds_read2_b32 v[2:3], v9 offset0:1 offset1:117", "v_mov_b32_e32 v10, v3", "s_waitcnt lgkmcnt(0)"]
+    overwritten = ["ds_read2_b32 v[2:3], v9 offset0:1 offset1:117", "s_waitcnt lgkmcnt(0)", "v_mov_b32_e32 v2, v7",
+                   "v_add_u32_e32 v11, v2, v1"]
+    assert kernel_resources.early_reads_of_lds_pairs(ok) == []
+    assert kernel_resources.early_reads_of_lds_pairs(early) == ["v_mov_b32_e32 v10, v3"]
+    assert kernel_resources.early_reads_of_lds_pairs(overwritten) == []
