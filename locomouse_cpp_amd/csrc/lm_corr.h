@@ -72,14 +72,13 @@ static_assert(LM_RW_HSLOTS >= 7, "k_corr_rw ring: rows t .. t + 6 are live durin
 // window row of a sub-tile: LM_FW + KW - 1 columns plus up to 3 before them
 // (the loads start on a 4-byte boundary); stride == 4 (mod 8)
 __host__ __device__ constexpr int rw_stride(int kw) { return pk_stride(LM_FW + kw - 1 + 3); }
-// floats per sub-tile ring.  Two 40-column sub-tiles share each 32-lane
-// group of a ds_read2_b32: their rings start 8 (mod 32) floats apart, which
-// puts the second's 16 lanes on the 16 banks the first leaves free (its lanes
-// read columns 5 lx of rows r and r + 4: 5 lx + 16 ly (mod 32)).  Two
-// 80-column halves are in different lane groups.
+// floats per sub-tile ring: == 32 / LM_RW_NQ (mod 32).  A ds_read_b32 lane
+// group holds one row group (ly) of every sub-tile; a sub-tile's QX lanes
+// read columns 5 lx (mod 32) of one ring row, and rings that start 32 / NQ
+// floats apart (mod 32) put the group's 32 reads on 32 banks (rw_tile).
 __host__ __device__ constexpr int rw_qpitch(int kw) {
-  return LM_RW_NQ == 2 ? (LM_RW_HSLOTS + 1) * rw_stride(kw)
-                       : (LM_RW_HSLOTS + 1) * rw_stride(kw) + (40 - ((LM_RW_HSLOTS + 1) * rw_stride(kw)) % 32) % 32;
+  return (LM_RW_HSLOTS + 1) * rw_stride(kw) +
+         ((32 / LM_RW_NQ - ((LM_RW_HSLOTS + 1) * rw_stride(kw)) % 32) + 32) % 32;
 }
 __host__ __device__ constexpr int rw_ring_floats(int kw) { return LM_RW_NQ * rw_qpitch(kw); }
 __host__ __device__ constexpr size_t rw_lds_bytes(int kw) {

@@ -435,8 +435,8 @@ struct RwPipe {
 };
 
 // One wave's work (the body of k_corr_rw and k_corr_rw_all): LM_RW_NQ
-// sub-tiles of LM_FW x 8 outputs, 64 / LM_RW_NQ consecutive lanes each, each
-// sub-tile streaming its own window through its own ring of LM_RW_HSLOTS
+// sub-tiles of LM_FW x 8 outputs, 64 / LM_RW_NQ lanes each (lane 32 ly +
+// QX q + lx), each sub-tile streaming its own window through its own ring of LM_RW_HSLOTS
 // rows + 1 mirror.  The sub-tiles are bright tiles from the dark-tile list
 // (any slots, any places) or the parts of one 80 x 16 tile (tail detectors,
 // skip off).  Per sub-tile: lane (ly, lx) owns 5 columns x 4 rows as two
@@ -465,8 +465,13 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   const int nrows = LM_RW_HTH + kh - 1;
   const int ew = K.ext_w[D.view];
   const int ew4 = ew >> 2;  // ext rows are padded to 16 bytes
-  const int q = lane / QL, ql = lane % QL;
-  const int ly = ql / QX, lx = ql % QX;
+  // lane = 32 ly + QX q + lx: the lanes of each ds_read_b32 lane group share
+  // ly (one ring row per sub-tile), and the sub-tiles' rings start 32 / NQ
+  // (mod 32) floats apart, so the group's 32 reads hit 32 banks (rw_qpitch);
+  // with the two ly in one group, rings of 7 rows put them 4 or -3 rows apart
+  // and no pitch avoided conflicts for both
+  const int ly = lane >> 5, q = (lane / QX) % NQ, lx = lane % QX;
+  static_assert(QX * NQ == 32, "one ly per lane group");
   // the lane's sub-tile (in VGPRs from here on: the merged kernel's SGPRs
   // are full)
   int slot, oy0, ox0;
@@ -627,19 +632,23 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   // lanes), one global atomic per sub-tile (keys are sorted later: their
   // order in the list does not matter)
   const int cnt = __popc(bits);
-  int incl = cnt;
+  int incl = cnt;  // inclusive scan over the lane's QX-lane segment (its sub-tile's lanes of one ly)
 #pragma unroll
-  for (int o = 1; o < QL; o <<= 1) {
-    const int u = __shfl_up(incl, o, QL);
-    if (ql >= o) incl += u;
+  for (int o = 1; o < QX; o <<= 1) {
+    const int u = __shfl_up(incl, o, QX);
+    if (lx >= o) incl += u;
   }
-  const int tot = __shfl(incl, QL - 1, QL);  // the sub-tile's count (its last lane's inclusive sum)
+  const int seg = __shfl(incl, QX - 1, QX);  // the segment's count
+  const int seg_lo = __shfl(seg, lane & 31);  // the sub-tile's ly = 0 segment
+  const int tot = seg_lo + __shfl(seg, lane | 32);
   if (__ballot(tot != 0) == 0) return;
+  // one atomic per sub-tile (its last lane), the base to all its lanes
+  const int last = 32 + (lane & 31 & ~(QX - 1)) + QX - 1;
   int base_k = 0;
-  if (ql == QL - 1 && tot) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
-  base_k = __shfl(base_k, QL - 1, QL);
+  if (lane == last && tot) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
+  base_k = __shfl(base_k, last);
   unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k +
-                                        (incl - cnt);
+                                        (ly ? seg_lo : 0) + (incl - cnt);
   int pos = 0;
 #pragma unroll
   for (int p = 0; p < PK_R / 2; ++p)
