@@ -196,7 +196,9 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 // LUTs and the store remain.  Where the 16 source pixels are consecutive in
 // the frame (a calibration map that is locally a translation, flipped or not)
 // the gather is five aligned dword loads instead of sixteen byte loads.
-#define LM_INGEST_FB 8
+#ifndef LM_INGEST_FB
+#define LM_INGEST_FB 8  // frames per workgroup (calibration / background loads reused across them)
+#endif
 #define LM_INGEST_VEC 16
 static_assert(LM_FW >= LM_INGEST_VEC, "a 16-byte chunk spans at most two flag tiles");
 #define LM_INGEST_MAXTX 128  // flag-grid columns a band's workgroup can hold (ow <= 128 LM_FW)
@@ -496,6 +498,9 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
       emit(f, pw, sl, Rf, Cf);
     }
   }
+#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 128)  // timing experiment: no flags, no lists
+  return;
+#endif
   if (!fl_band) return;
   // the band's flag bytes (each written by this block only: no zeroing pass)
   // and its bright tiles appended to the view's list (any order: the
@@ -514,10 +519,14 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
   }
   if (!tl_list) return;
   __syncthreads();
+#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 64)  // timing experiment: no global list atomics (lists come out empty)
+  if (tid == 0) s_base = 0;
+#else
   if (tid == 0) {
     s_base = s_n ? atomicAdd(&tl_cnt[v], s_n) : 0;
     if (s_outs) atomicAdd(&tl_cnt[2 + v], s_outs);
   }
+#endif
   __syncthreads();
   uint32_t* __restrict__ out = tl_list + (int64_t)v * K.tl_stride + s_base;
   for (int p = tid; p < s_n; p += T) out[p] = s_ent[p];

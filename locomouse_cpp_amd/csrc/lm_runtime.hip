@@ -30,7 +30,8 @@
 namespace {
 
 // Timing experiments only (scripts/build_variant_rt.sh -DLM_EXP_SKIP=...;
-// results are wrong): 1 k_nms writes empty lists, 2 no k_tail, 16 no correlation launch.
+// results are wrong): 1 k_nms writes empty lists, 2 no k_tail, 16 no correlation launch,
+// 64 k_ingest without its global list atomics, 128 k_ingest without flags and lists.
 #ifndef LM_EXP_SKIP
 #define LM_EXP_SKIP 0
 #endif
