@@ -240,14 +240,19 @@ struct RwTiles {
 // the next ...), so no wave idles at a frame's end and the host can put the
 // longest detectors first.  With dark-tile lists (tl_cnt != nullptr) a point
 // detector's waves take its view's bright LM_FW x 8 tiles LM_RW_NQ at a time
-// (k_ingest), so the group's wave count is known on the device only: the
-// grid is sized for every 80 x 16 tile (as many outputs as a wave's
-// sub-tiles) and the waves past the last group's count (whole workgroups at
-// the grid's end) return.  Otherwise a wave takes the sub-tiles of one
-// 80 x 16 tile (row-major).  false: past the last wave.
+// from the list segments k_ingest filled (segment c: tl_cnt[view LM_TL_NC +
+// c] tiles, ceil(/ LM_RW_NQ) waves; a wave finds its segment with a scan over
+// the 64 counters, one per lane), so the group's wave count is known on the
+// device only: the grid is sized for every 80 x 16 tile (as many outputs as a
+// wave's sub-tiles, and each segment's waves <= its slots' 80 x 16 tiles) and
+// the waves past the last group's count (whole workgroups at the grid's end)
+// return.  Otherwise a wave takes the sub-tiles of one 80 x 16 tile
+// (row-major).  Called by every lane of the wave; false: past the last wave.
+static_assert(LM_TL_NC == 64, "one list counter per lane");
 DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, const int32_t* tl_cnt,
                         const uint32_t* tl_list, int& d, RwTiles& H) {
   constexpr int NQ = LM_RW_NQ;
+  const int lane = threadIdx.x & 63;
   int base = 0;
 #pragma unroll
   for (int k = 0; k < LM_NDET; ++k) {
@@ -255,17 +260,34 @@ DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s
     d = G.ids[k];
     const LmDet& D = K.det[d];
     const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
-    const bool listed = tl_cnt != nullptr && D.kind == 0;
-    const int nh = listed ? tl_cnt[D.view] : 0;  // bright tiles
-    const int cnt = listed ? (nh + NQ - 1) / NQ : nt * nslots;
-    if (g < base + cnt) {
-      const int local = g - base;
-      if (listed) {
-        H.l = tl_list + (int64_t)D.view * K.tl_stride + NQ * local;
-        H.nvalid = min(NQ, nh - NQ * local);
-        H.ftx = K.fl_tx[D.view];
+    if (tl_cnt != nullptr && D.kind == 0) {
+      const int v = D.view;
+      const int cn = tl_cnt[v * LM_TL_NC + lane];  // segment `lane`'s bright tiles
+      const int wv = (cn + NQ - 1) / NQ;
+      int P = wv;  // inclusive scan: waves of segments 0 .. lane
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(P, o);
+        if (lane >= o) P += u;
+      }
+      const int cnt = __builtin_amdgcn_readlane(P, 63);  // (readlane: wave-uniform values stay scalar)
+      if (g < base + cnt) {
+        const int local = g - base;
+        const int c = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(P > local)) - 1);
+        const int w = local - (__builtin_amdgcn_readlane(P, c) - __builtin_amdgcn_readlane(wv, c));  // place in segment c
+        const int ng = (nslots + LM_INGEST_FB - 1) / LM_INGEST_FB;
+        H.l = tl_list + (int64_t)v * K.tl_stride +
+              (int64_t)lm_tl_y0(c, ng) * LM_INGEST_FB * K.fl_tx[v] * K.fl_ty[v] + NQ * w;
+        H.nvalid = min(NQ, __builtin_amdgcn_readlane(cn, c) - NQ * w);
+        H.ftx = K.fl_tx[v];
         H.slot = H.oy = H.ox = 0;
-      } else {
+        return true;
+      }
+      base += cnt;
+    } else {
+      const int cnt = nt * nslots;
+      if (g < base + cnt) {
+        const int local = g - base;
         const int tx = D.tiles_x;
         const int lt = local - (local / nt) * nt;
         H.l = nullptr;
@@ -274,10 +296,10 @@ DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s
         H.slot = s0 + local / nt;
         H.oy = (lt / tx) * LM_RW_TH;
         H.ox = (lt % tx) * LM_TW;
+        return true;
       }
-      return true;
+      base += cnt;
     }
-    base += cnt;
   }
   return false;
 }

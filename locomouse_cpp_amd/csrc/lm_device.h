@@ -26,6 +26,19 @@
 #endif
 static_assert(LM_RW_NQ == 2 || LM_RW_NQ == 4, "k_corr_rw sub-tiles per wave");
 #define LM_FW (2 * LM_TW / LM_RW_NQ)
+// k_ingest: frames per workgroup (the calibration / background loads are
+// reused across them); its workgroups of slot group y append their bright
+// tiles to list segment (y LM_TL_NC) / G of their view (G slot groups), one
+// counter per segment: ~40 bands per counter instead of every workgroup of
+// the batch on one address (same-address atomics serialise in L2: 52 -> 38 us
+// per batch without them, profiles/r04/ingest/)
+#ifndef LM_INGEST_FB
+#define LM_INGEST_FB 8
+#endif
+#define LM_TL_NC 64
+// first slot group of list segment c (G slot groups): the segment holds the
+// tiles of slot groups y0(c) .. y0(c + 1) - 1
+__host__ __device__ inline int lm_tl_y0(int c, int G) { return (c * G + LM_TL_NC - 1) / LM_TL_NC; }
 
 // k_minmax: each frame split over LM_MM_SPLIT workgroups of LM_MM_THREADS
 #define LM_MM_SPLIT 8
@@ -84,7 +97,8 @@ struct LmConst {
   // dark tiles (flagged and listed by k_ingest): per view, the point
   // detectors' outputs in LM_FW x LM_RW_HTH tiles (fl_tx x fl_ty of them); one
   // flag byte per (slot, view, tile) at slot * fl_slot + fl_off[view] + tile;
-  // the bright tiles of view v listed at v * tl_stride of the tile list
+  // the bright tiles of view v listed at v * tl_stride of the tile list, in
+  // LM_TL_NC segments: segment c at lm_tl_y0(c, G) * LM_INGEST_FB * fl_tx * fl_ty
   int32_t fl_tx[2], fl_ty[2], fl_off[2], fl_slot;
   int32_t tl_stride;
   // the point detectors' output region per view: output (y, x) has its

@@ -196,9 +196,6 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 // LUTs and the store remain.  Where the 16 source pixels are consecutive in
 // the frame (a calibration map that is locally a translation, flipped or not)
 // the gather is five aligned dword loads instead of sixteen byte loads.
-#ifndef LM_INGEST_FB
-#define LM_INGEST_FB 8  // frames per workgroup (calibration / background loads reused across them)
-#endif
 #define LM_INGEST_VEC 16
 static_assert(LM_FW >= LM_INGEST_VEC, "a 16-byte chunk spans at most two flag tiles");
 #define LM_INGEST_MAXTX 128  // flag-grid columns a band's workgroup can hold (ow <= 128 LM_FW)
@@ -504,8 +501,8 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
   if (!fl_band) return;
   // the band's flag bytes (each written by this block only: no zeroing pass)
   // and its bright tiles appended to the view's list (any order: the
-  // correlation's waves take them two at a time, and the keys they produce
-  // are sorted by k_nms)
+  // correlation's waves take them LM_RW_NQ at a time, and the keys they
+  // produce are sorted by k_nms)
   __syncthreads();
   const int ty = band, oh_t = min(8, K.fl_oh[v] - 8 * ty);
   for (int i = tid; i < nf * ftx; i += T) {
@@ -519,16 +516,20 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
   }
   if (!tl_list) return;
   __syncthreads();
+  // this workgroup's list segment and its counter (tl_cnt: bright tiles of
+  // view v at v LM_TL_NC + c, their outputs at (2 + v) LM_TL_NC + c)
+  const int G = (int)gridDim.y, c = (int)blockIdx.y * LM_TL_NC / G;
 #if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 64)  // timing experiment: no global list atomics (lists come out empty)
   if (tid == 0) s_base = 0;
 #else
   if (tid == 0) {
-    s_base = s_n ? atomicAdd(&tl_cnt[v], s_n) : 0;
-    if (s_outs) atomicAdd(&tl_cnt[2 + v], s_outs);
+    s_base = s_n ? atomicAdd(&tl_cnt[v * LM_TL_NC + c], s_n) : 0;
+    if (s_outs) atomicAdd(&tl_cnt[(2 + v) * LM_TL_NC + c], s_outs);
   }
 #endif
   __syncthreads();
-  uint32_t* __restrict__ out = tl_list + (int64_t)v * K.tl_stride + s_base;
+  uint32_t* __restrict__ out = tl_list + (int64_t)v * K.tl_stride +
+                               (int64_t)lm_tl_y0(c, G) * LM_INGEST_FB * K.fl_tx[v] * K.fl_ty[v] + s_base;
   for (int p = tid; p < s_n; p += T) out[p] = s_ent[p];
 }
 
@@ -2068,6 +2069,7 @@ DEV void carry_block(const LmConst& K, unsigned long long* __restrict__ keys, co
 //
 // k_prep: slots, frame pointers and the arena control block from host memory,
 // candidate counters and error flags zeroed.  One block.
+static_assert(4 * LM_TL_NC == 256, "k_prep zeroes the tile-list counters with its 256 threads");
 __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots, const uint8_t* const* __restrict__ h_fptr,
                                               const LmArenaCtl* __restrict__ h_ctl, int ns, LmSlot* __restrict__ slots,
                                               const uint8_t** __restrict__ fptr, LmArenaCtl* __restrict__ ctl,
@@ -2079,7 +2081,7 @@ __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots
     carry_block(*Kp, keys, prev_hdr, prev_slot, hdr);
     return;
   }
-  if (dark_cnt && threadIdx.x < 4) dark_cnt[threadIdx.x] = 0;  // k_ingest's bright-tile counts
+  if (dark_cnt) dark_cnt[threadIdx.x] = 0;  // k_ingest's bright-tile counters (4 LM_TL_NC = blockDim.x)
   for (int i = threadIdx.x; i < ns; i += blockDim.x) {
     slots[i] = h_slots[i];
     fptr[i] = h_fptr[i];

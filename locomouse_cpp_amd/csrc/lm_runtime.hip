@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <numeric>
 #include <atomic>
 #include <deque>
 #include <memory>
@@ -741,7 +742,7 @@ void lane_alloc(lm_ctx* c, Lane& L) {
     L.dark_flags.alloc((size_t)K.fl_slot * ns);
     SET_SYNC(L.dark_flags.p, 0, (size_t)K.fl_slot * ns, st);
     L.dark_list.alloc((size_t)2 * K.tl_stride);
-    L.dark_cnt.alloc(4);
+    L.dark_cnt.alloc(4 * LM_TL_NC);
   }
   L.err.alloc(16);
   L.frame_ptr.alloc(ns);
@@ -828,7 +829,11 @@ struct Timer {  // HIP events around the timed kernels of a lane's batch (debug 
     }
     L.t_ev.clear();
     for (int k = 0; k < 4; ++k) L.t_work[k] = -1;
-    if (L.dark_cnt.p) COPY_SYNC(L.t_work, L.dark_cnt.p, sizeof(L.t_work), hipMemcpyDeviceToHost, L.stream);
+    if (L.dark_cnt.p) {  // the segment counters summed per view
+      int32_t h[4 * LM_TL_NC];
+      COPY_SYNC(h, L.dark_cnt.p, sizeof(h), hipMemcpyDeviceToHost, L.stream);
+      for (int k = 0; k < 4; ++k) L.t_work[k] = std::accumulate(h + k * LM_TL_NC, h + (k + 1) * LM_TL_NC, 0);
+    }
   }
 };
 
