@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define LM_ABI_VERSION 6  /* 6: lm_debug_dark_tile_width (40 x 8 dark tiles); 5: lm_debug_batch_slots */
+#define LM_ABI_VERSION 6  /* 6: lm_debug_dark_tile_width / _height (40 x 4 dark tiles); 5: lm_debug_batch_slots */
 #define LM_N_PAWS 4          /* LocoMouse_class.hpp:84 */
 #define LM_N_TAIL_POINTS 15  /* LocoMouse_class.hpp:86 */
 #define LM_N_LISTS 4         /* candidate lists per frame */
@@ -339,16 +339,18 @@ int32_t lm_debug_kernel_times(lm_ctx* ctx, const char** names, double* ms, int32
 int32_t lm_debug_kernel_spans(lm_ctx* ctx, const char** names, double* t0, double* t1, int32_t cap);
 
 /* Correlation work of the last collected batch when debug bit 1 is set:
- * out[0], out[1] = bright output tiles (lm_debug_dark_tile_width() x 8) of the
+ * out[0], out[1] = bright output tiles (the dark-tile grid's) of the
  * bottom / side point detectors, out[2], out[3] = the consumed outputs those
  * tiles hold.  The point detectors' dark tiles (no I_*_MOUSE pixel > 25, so
  * every score is zeroed by setTo(0, mask), LocoMouse_class.cpp:849, :864)
  * are not computed.  -1 when not recorded (timing off, LM_CORR_DARK=0). */
 lm_status lm_debug_corr_work(const lm_ctx* ctx, int32_t* out);
 
-/* Columns of the dark-tile grid (its tiles are that many outputs wide and 8
- * rows high): 40 in the default build, 80 with -DLM_RW_NQ=2. */
+/* The dark-tile grid: tiles of lm_debug_dark_tile_width() x
+ * lm_debug_dark_tile_height() outputs (40 x 4 in the default build; 40 x 8
+ * and 80 x 8 as build options, -DLM_FH=8 / -DLM_FW=80). */
 int32_t lm_debug_dark_tile_width(void);
+int32_t lm_debug_dark_tile_height(void);
 
 /* Frame slots the last collected batch processed: n, or n + 1 when its halo
  * frame (slot 0: prev_frame, or the pipelined hand-off) was recomputed --

@@ -36,18 +36,21 @@ struct LmDetGroup {
   X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) \
       X(40) X(44) X(48) X(52) X(56) X(60) X(64)
 #endif
-// widths of the merged launch (k_corr_rw_all): those whose window row fits
-// half a wave's loads (rw_tile's lane-split loads; wider ones load both halves
-// from every lane and need more registers than the merged kernel's budget)
+// widths of the merged launch (k_corr_rw_all): the even widths up to 40.  The
+// merged kernel's register need grows with every width it holds (all bodies
+// inlined behind one switch): 16..32 all, 36, 40 took 168 VGPRs and spilled
+// with 40 x 4 sub-tiles; the even ones take 151 (three waves per SIMD, no
+// spill).  Other widths run their per-width kernels in either plan.
 #if defined(LM_KW_ONLY) || defined(LM_KW_C3)
 #define LM_KW_LIST_RW_ALL LM_KW_LIST
 #else
-#define LM_KW_LIST_RW_ALL(X) \
-  X(16) X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) X(36) X(40)
+#define LM_KW_LIST_RW_ALL(X) X(16) X(18) X(20) X(22) X(24) X(26) X(28) X(30) X(32) X(36) X(40)
 #endif
-__host__ __device__ constexpr bool rw_all_width(int kw) { return kw >= 16 && (kw <= 32 || kw == 36 || kw == 40); }
+__host__ __device__ constexpr bool rw_all_width(int kw) {
+  return kw % 2 == 0 && kw >= 16 && (kw <= 32 || kw == 36 || kw == 40);
+}
 
-// k_corr_rw: one wave per LM_RW_NQ sub-tiles of LM_FW x 8 outputs (or one
+// k_corr_rw: one wave per LM_RW_NQ sub-tiles of LM_FW x LM_FH outputs (or one
 // 80 x 16 tile split into them), LM_RW_WAVES waves per workgroup
 #ifndef LM_RW_WAVES
 #define LM_RW_WAVES 4
@@ -57,28 +60,31 @@ __host__ __device__ constexpr bool rw_all_width(int kw) { return kw >= 16 && (kw
 #define LM_RW_ITEMS 1  // work items (LM_RW_NQ sub-tiles each) per wave, one after another
 #endif
 #define LM_RW_TH 16     // output rows of a wave's 80 x 16 tile (tail detectors)
-#define LM_RW_HTH 8     // output rows per sub-tile (also the dark-tile flag grid's rows)
+#define LM_RW_HTH LM_FH  // output rows per sub-tile (the dark-tile grid's rows)
 #ifndef LM_RW_HSLOTS
-// ring rows per sub-tile (+ 1 mirror): rows t .. t + 5 are read at step t
-// and row t + HSLOTS is stored at its end, so 7 suffice.  80-column
-// sub-tiles: 8 (a power of two: the slot index is a mask; 7 gives kw 30 five
-// waves per SIMD instead of four but measured 1-2 % slower at C3,
-// profiles/r04/ring7); 40-column sub-tiles: 7, which keeps four waves per
-// SIMD (8 would leave three)
-#define LM_RW_HSLOTS (LM_RW_NQ == 4 ? 7 : 8)
+// ring rows per sub-tile (+ 1 mirror).  Row t + HSLOTS is loaded at the start
+// of step t and stored at its end into row t's slot, after the step's last
+// chunk has issued step t + 1's first reads: 8-row sub-tiles (two row groups
+// 4 rows apart) read rows t + 1 .. t + 6 then, so 7 suffice (80-column
+// sub-tiles: 8 measured 1-2 % faster, profiles/r04/ring7; 40-column: 7 keeps
+// four waves per SIMD); 4-row sub-tiles read t + 1, t + 2: 3 suffice.
+#define LM_RW_HSLOTS (LM_FH == 4 ? 3 : LM_RW_NQ == 4 ? 7 : 8)
 #endif
-static_assert(LM_RW_HSLOTS >= 7, "k_corr_rw ring: rows t .. t + 6 are live during step t");
+static_assert(LM_RW_HSLOTS >= (LM_FH == 4 ? 3 : 7), "k_corr_rw ring: rows live during a step");
 
 // window row of a sub-tile: LM_FW + KW - 1 columns plus up to 3 before them
-// (the loads start on a 4-byte boundary); stride == 4 (mod 8)
-__host__ __device__ constexpr int rw_stride(int kw) { return pk_stride(LM_FW + kw - 1 + 3); }
-// floats per sub-tile ring: == 32 / LM_RW_NQ (mod 32).  A ds_read_b32 lane
-// group holds one row group (ly) of every sub-tile; a sub-tile's QX lanes
-// read columns 5 lx (mod 32) of one ring row, and rings that start 32 / NQ
-// floats apart (mod 32) put the group's 32 reads on 32 banks (rw_tile).
+// (the loads start on a 4-byte boundary), rounded to float4 stores (a lane
+// group's reads all hit one row of each sub-tile: the stride does not enter
+// the bank mapping)
+__host__ __device__ constexpr int rw_stride(int kw) { return (LM_FW + kw - 1 + 3 + 3) / 4 * 4; }
+// floats per sub-tile ring: == LM_FW / 5 (mod 32).  A ds_read_b32 lane
+// group (32 lanes) holds one row group of 32 / (LM_FW / 5) sub-tiles; a
+// sub-tile's LM_FW / 5 lanes of a row group read columns 5 lx (mod 32) of one
+// ring row, and rings that start LM_FW / 5 floats apart (mod 32) put the
+// group's 32 reads on 32 banks (rw_tile).
 __host__ __device__ constexpr int rw_qpitch(int kw) {
   return (LM_RW_HSLOTS + 1) * rw_stride(kw) +
-         ((32 / LM_RW_NQ - ((LM_RW_HSLOTS + 1) * rw_stride(kw)) % 32) + 32) % 32;
+         ((LM_FW / 5 - ((LM_RW_HSLOTS + 1) * rw_stride(kw)) % 32) + 32) % 32;
 }
 __host__ __device__ constexpr int rw_ring_floats(int kw) { return LM_RW_NQ * rw_qpitch(kw); }
 __host__ __device__ constexpr size_t rw_lds_bytes(int kw) {

@@ -225,12 +225,12 @@ struct RwTiles {
       const uint32_t e = l[i < nvalid ? i : 0];
       const int lt = (int)(e & 0xFFFFu);
       s = (int)(e >> 16);
-      y = (lt / ftx) * LM_RW_HTH;
+      y = (lt / ftx) * LM_FH;
       x = (lt % ftx) * LM_FW;
     } else {
       s = slot;
-      y = oy + (i / (LM_RW_NQ / 2)) * LM_RW_HTH;
-      x = ox + (i % (LM_RW_NQ / 2)) * LM_FW;
+      y = oy + (i / LM_RW_NQX) * LM_FH;
+      x = ox + (i % LM_RW_NQX) * LM_FW;
     }
   }
 };
@@ -309,7 +309,7 @@ DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s
 DEV bool corr_tile_dark(const LmConst& K, const LmDet& D, const uint8_t* __restrict__ dark, int slot, int oy0, int ox0) {
   if (dark == nullptr || D.kind != 0) return false;
   const int v = D.view;
-  const int ty0 = oy0 / LM_RW_HTH, ty1 = min(K.fl_ty[v] - 1, (oy0 + D.tile_h - 1) / LM_RW_HTH);
+  const int ty0 = oy0 / LM_FH, ty1 = min(K.fl_ty[v] - 1, (oy0 + D.tile_h - 1) / LM_FH);
   const int tx0 = ox0 / LM_FW, tx1 = min(K.fl_tx[v] - 1, (ox0 + D.tile_w - 1) / LM_FW);
   const uint8_t* __restrict__ f = dark + (int64_t)slot * K.fl_slot + K.fl_off[v];
   for (int ty = ty0; ty <= ty1; ++ty)
@@ -472,28 +472,28 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
                                                 const float* __restrict__ weights,
                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
                                                 uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
-  constexpr int NQ = LM_RW_NQ;
-  constexpr int QL = 64 / NQ;  // lanes per sub-tile
-  constexpr int QX = QL / 2;   // lanes across a sub-tile
-  static_assert(QX * PK_C == LM_FW, "sub-tile width");
+  constexpr int NQ = LM_RW_NQ, NQX = LM_RW_NQX;
+  constexpr int QX = LM_FW / PK_C;  // lanes across a sub-tile
+  constexpr int QY = LM_FH / PK_R;  // row groups (lanes down) of a sub-tile
+  constexpr int LG = 64 / QY;       // lanes per row group of the wave
+  static_assert(QX * QY * NQ == 64, "sub-tile lanes");
   constexpr int STR = rw_stride(KW);
   constexpr int QP = rw_qpitch(KW);
   constexpr int NL = (3 + LM_FW + KW - 1 + 3) / 4;  // dwords of a sub-tile's window row
   constexpr int NLD = (NQ * NL + 63) / 64;          // dwords a lane loads per row
-  static_assert(NLD <= 2, "window rows wider than two loads per lane");
+  static_assert(NLD <= 4, "window rows wider than four loads per lane");
   constexpr int HS = LM_RW_HSLOTS;
   const int lane = threadIdx.x & 63;
   const int kh = D.kh, kwp = D.kwp;
   const int nrows = LM_RW_HTH + kh - 1;
   const int ew = K.ext_w[D.view];
   const int ew4 = ew >> 2;  // ext rows are padded to 16 bytes
-  // lane = 32 ly + QX q + lx: the lanes of each ds_read_b32 lane group share
-  // ly (one ring row per sub-tile), and the sub-tiles' rings start 32 / NQ
-  // (mod 32) floats apart, so the group's 32 reads hit 32 banks (rw_qpitch);
-  // with the two ly in one group, rings of 7 rows put them 4 or -3 rows apart
-  // and no pitch avoided conflicts for both
-  const int ly = lane >> 5, q = (lane / QX) % NQ, lx = lane % QX;
-  static_assert(QX * NQ == 32, "one ly per lane group");
+  // lane = LG ly + QX q + lx: the lanes of each ds_read_b32 lane group share
+  // ly (one ring row per sub-tile), and the sub-tiles' rings start QX (mod 32)
+  // floats apart, so the group's 32 reads hit 32 banks (rw_qpitch); with the
+  // two ly of 8-row sub-tiles in one group, rings of 7 rows put them 4 or -3
+  // rows apart and no pitch avoided conflicts for both
+  const int ly = lane / LG, q = (lane % LG) / QX, lx = lane % QX;
   // the lane's sub-tile (in VGPRs from here on: the merged kernel's SGPRs
   // are full)
   int slot, oy0, ox0;
@@ -571,8 +571,13 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   // ring slot of window row t + 4 ly (t wave-uniform: both candidates are
   // scalar, the lane picks one)
   auto row_base = [&](int t) -> unsigned {
-    const int a = t % HS, b = a + PK_R >= HS ? a + PK_R - HS : a + PK_R;
-    return ring_base + (unsigned)((ly ? b : a) * STR * (int)sizeof(float)) + lane_off;
+    const int a = t % HS;
+    if constexpr (QY == 1) {
+      return ring_base + (unsigned)(a * STR * (int)sizeof(float)) + lane_off;
+    } else {
+      const int b = a + PK_R >= HS ? a + PK_R - HS : a + PK_R;
+      return ring_base + (unsigned)((ly ? b : a) * STR * (int)sizeof(float)) + lane_off;
+    }
   };
   RwPipe<KW, UNF> S;
 #pragma unroll
@@ -628,8 +633,8 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     // 80, so 80 columns touch at most 4 words) = one word per lane, gathered
     // in the ring, then ORed into the slot's bitmap
     unsigned* s_tb = reinterpret_cast<unsigned*>(ring);
-    const int w0 = (ox0 - (q % (NQ / 2)) * LM_FW) >> 5;  // the tile's first word
-    const int ty = (q / (NQ / 2)) * LM_RW_HTH + ly * PK_R;  // the lane's first row in the tile
+    const int w0 = (ox0 - (q % NQX) * LM_FW) >> 5;  // the tile's first word
+    const int ty = (q / NQX) * LM_FH + ly * PK_R;   // the lane's first row in the tile
     s_tb[lane] = 0u;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -644,7 +649,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     const unsigned v = s_tb[lane];
     unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(tailbin + (int64_t)slot * tailbin_slot_bytes) +
                                 (D.list ? (int64_t)K.tail_hb * K.tail_nw : 0);
-    const int y = oy0 - (q / (NQ / 2)) * LM_RW_HTH + (lane >> 2), gw = w0 + (lane & 3);  // rows from the tile's top
+    const int y = oy0 - (q / NQX) * LM_FH + (lane >> 2), gw = w0 + (lane & 3);  // rows from the tile's top
     if (v && y < D.oh && gw < K.tail_nw) atomicOr(&tb[(int64_t)y * K.tail_nw + gw], v);
     return;
   }
@@ -661,16 +666,19 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     if (lx >= o) incl += u;
   }
   const int seg = __shfl(incl, QX - 1, QX);  // the segment's count
-  const int seg_lo = __shfl(seg, lane & 31);  // the sub-tile's ly = 0 segment
-  const int tot = seg_lo + __shfl(seg, lane | 32);
+  int before = incl - cnt, tot = seg, last = (lane & ~(QX - 1)) + QX - 1;
+  if constexpr (QY == 2) {  // the sub-tile's ly = 0 segment first
+    const int seg_lo = __shfl(seg, lane & 31);
+    tot = seg_lo + __shfl(seg, lane | 32);
+    before += ly ? seg_lo : 0;
+    last |= 32;
+  }
   if (__ballot(tot != 0) == 0) return;
   // one atomic per sub-tile (its last lane), the base to all its lanes
-  const int last = 32 + (lane & 31 & ~(QX - 1)) + QX - 1;
   int base_k = 0;
   if (lane == last && tot) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
   base_k = __shfl(base_k, last);
-  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k +
-                                        (ly ? seg_lo : 0) + (incl - cnt);
+  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k + before;
   int pos = 0;
 #pragma unroll
   for (int p = 0; p < PK_R / 2; ++p)
@@ -691,7 +699,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
 template <int KW, bool UNF>
 // waves per SIMD: LDS allows 5 (80-column sub-tiles, kw <= 32) or 4
 // (40-column); the register budget is set to match
-__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? (LM_RW_NQ == 4 ? 4 : 5) : 1, 8))) void k_corr_rw(
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? (LM_FW == 40 ? 4 : 5) : 1, 8))) void k_corr_rw(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
     int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
@@ -719,7 +727,7 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
 // ~154 VGPRs (each alone <= 99: the dispatch's SGPRs spill into VGPR lanes),
 // so three waves per SIMD instead of four, without spills.
 template <bool UNF>
-__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(LM_RW_NQ == 4 ? 3 : 4, 8))) void k_corr_rw_all(
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(LM_FW == 40 ? 3 : 4, 8))) void k_corr_rw_all(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
     int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,

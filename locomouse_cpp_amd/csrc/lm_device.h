@@ -19,13 +19,21 @@
 #define LM_TW (16 * LM_C)  // 80
 #define LM_TH (16 * LM_R)  // 48
 #define LM_JC 4            // tap chunk along a detector row (kw padded to a multiple)
-// k_corr_rw's wave computes LM_RW_NQ independent sub-tiles of LM_FW x 8
-// outputs (4: 40 x 8, 2: 80 x 8); LM_FW x 8 is also the dark-tile grid
-#ifndef LM_RW_NQ
-#define LM_RW_NQ 4
+// The dark-tile grid: LM_FW x LM_FH output tiles (40 x 4; 40 x 8 and 80 x 8
+// as build options).  k_corr_rw's wave computes LM_RW_NQ independent
+// sub-tiles of that size (the LM_RW_NQX x LM_RW_NQY sub-tiles of an 80 x 16
+// tile, or as many bright tiles from the lists), LM_FW / 5 x LM_FH / 4
+// threads each.
+#ifndef LM_FW
+#define LM_FW 40
 #endif
-static_assert(LM_RW_NQ == 2 || LM_RW_NQ == 4, "k_corr_rw sub-tiles per wave");
-#define LM_FW (2 * LM_TW / LM_RW_NQ)
+#ifndef LM_FH
+#define LM_FH 4
+#endif
+static_assert((LM_FW == 40 || LM_FW == 80) && (LM_FH == 4 || LM_FH == 8), "dark-tile grid");
+#define LM_RW_NQX (LM_TW / LM_FW)
+#define LM_RW_NQY (16 / LM_FH)
+#define LM_RW_NQ (LM_RW_NQX * LM_RW_NQY)
 // k_ingest: frames per workgroup (the calibration / background loads are
 // reused across them); its workgroups of slot group y append their bright
 // tiles to list segment (y LM_TL_NC) / G of their view (G slot groups), one
@@ -95,7 +103,7 @@ struct LmConst {
   int32_t tail_nw, tail_bm_words;
   int32_t connectivity;
   // dark tiles (flagged and listed by k_ingest): per view, the point
-  // detectors' outputs in LM_FW x LM_RW_HTH tiles (fl_tx x fl_ty of them); one
+  // detectors' outputs in LM_FW x LM_FH tiles (fl_tx x fl_ty of them); one
   // flag byte per (slot, view, tile) at slot * fl_slot + fl_off[view] + tile;
   // the bright tiles of view v listed at v * tl_stride of the tile list, in
   // LM_TL_NC segments: segment c at lm_tl_y0(c, G) * LM_INGEST_FB * fl_tx * fl_ty

@@ -186,7 +186,7 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 // per (view, 8-row band of the view's ext crop, slot group): the bands are
 // aligned with the dark-tile flag grid (band b holds the point detectors'
 // output rows 8b .. 8b + 7), so the workgroup that writes a tile row's pixels
-// also decides which of its LM_FW x 8 output tiles are bright (some I_*_MOUSE
+// also decides which of its LM_FW x LM_FH output tiles are bright (some I_*_MOUSE
 // pixel > 25, LocoMouse_class.cpp:782, :817), writes their flag bytes and
 // appends the bright ones to the view's tile list -- no second pass over the
 // crops.  Each thread owns 16 consecutive crop bytes of the band (one 16-byte
@@ -290,7 +290,8 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
   const int band = K.ing_b0[v] + (int)blockIdx.x - (v ? K.ing_nb[0] : 0);
   const int ew = K.ext_w[v], cw = ew / LM_INGEST_VEC, nch = 8 * cw;
   const int64_t e0 = (int64_t)K.ext_h[0] * K.ext_w[0];
-  const bool fl_band = flags != nullptr && band >= 0 && band < K.fl_ty[v];
+  constexpr int FPB = 8 / LM_FH;  // flag rows per band
+  const bool fl_band = flags != nullptr && band >= 0 && band * FPB < K.fl_ty[v];
   const int ftx = K.fl_tx[v];
   // One round of independent loads (the group's LUTs into registers, the
   // slots, the first chunk's source map entry), then the frame loads the map
@@ -299,15 +300,15 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
   // after another).
   __shared__ __attribute__((aligned(16))) uint8_t lut[LM_INGEST_FB][256];
   __shared__ uint8_t glut[256];
-  __shared__ uint8_t s_fl[LM_INGEST_FB][LM_INGEST_MAXTX];  // bright output tiles of the band, per slot
-  __shared__ uint32_t s_ent[LM_INGEST_FB * LM_INGEST_MAXTX];
+  __shared__ uint8_t s_fl[LM_INGEST_FB][8 / LM_FH][LM_INGEST_MAXTX];  // bright output tiles of the band, per slot
+  __shared__ uint32_t s_ent[LM_INGEST_FB * (8 / LM_FH) * LM_INGEST_MAXTX];
   __shared__ int s_n, s_outs, s_base;
   for (int i = tid; i < LM_INGEST_FB * 256 / 8; i += T) {
     const int li = i * 8;
     if (li < nf * 256) *reinterpret_cast<uint2*>(&lut[0][0] + li) = *reinterpret_cast<const uint2*>(luts + (int64_t)sb * 256 + li);
   }
   for (int i = tid; i < 256; i += T) glut[i] = K.gray_lut[i];
-  for (int i = tid; i < LM_INGEST_FB * LM_INGEST_MAXTX; i += T) (&s_fl[0][0])[i] = 0;
+  for (int i = tid; i < LM_INGEST_FB * FPB * LM_INGEST_MAXTX; i += T) (&s_fl[0][0][0])[i] = 0;
   if (tid == 0) {
     s_n = 0;
     s_outs = 0;
@@ -361,6 +362,7 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
     uint32_t ma[4] = {0u, 0u, 0u, 0u}, mb[4] = {0u, 0u, 0u, 0u};
     int ta = 0;
     const int y = er - K.fl_my[v];
+    const int fr = (y - 8 * band) / LM_FH;  // the chunk's flag row in the band (when fl_band)
     if (fl_band && y < K.fl_oh[v]) {
       const int x0 = ec - K.fl_mx[v];
       ta = x0 >= 0 ? x0 / LM_FW : -((LM_FW - 1 - x0) / LM_FW);
@@ -423,8 +425,8 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
           ha |= br & ma[j];
           hb |= br & mb[j];
         }
-        if (ha) s_fl[f][ta] = 1;
-        if (hb) s_fl[f][ta + 1] = 1;
+        if (ha) s_fl[f][fr][ta] = 1;
+        if (hb) s_fl[f][fr][ta + 1] = 1;
       }
     };
 
@@ -504,10 +506,12 @@ __global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp,
   // correlation's waves take them LM_RW_NQ at a time, and the keys they
   // produce are sorted by k_nms)
   __syncthreads();
-  const int ty = band, oh_t = min(8, K.fl_oh[v] - 8 * ty);
-  for (int i = tid; i < nf * ftx; i += T) {
-    const int f = i / ftx, tx = i - f * ftx;
-    const uint8_t b = s_fl[f][tx];
+  for (int i = tid; i < nf * FPB * ftx; i += T) {
+    const int f = i / (FPB * ftx), r = (i / ftx) % FPB, tx = i % ftx;
+    const int ty = band * FPB + r;
+    if (ty >= K.fl_ty[v]) continue;
+    const int oh_t = min(LM_FH, K.fl_oh[v] - LM_FH * ty);
+    const uint8_t b = s_fl[f][r][tx];
     flags[(int64_t)(sb + f) * K.fl_slot + K.fl_off[v] + ty * ftx + tx] = b;
     if (b && tl_list) {
       s_ent[atomicAdd(&s_n, 1)] = ((uint32_t)(sb + f) << 16) | (uint32_t)(ty * ftx + tx);

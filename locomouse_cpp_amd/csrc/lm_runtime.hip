@@ -475,7 +475,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     for (int v = 0; v < 2; ++v) {
       const LmDet& D = K.det[v ? DET_PAW_S : DET_PAW_B];
       K.fl_tx[v] = (D.ow + LM_FW - 1) / LM_FW;
-      K.fl_ty[v] = (D.oh + LM_RW_HTH - 1) / LM_RW_HTH;
+      K.fl_ty[v] = (D.oh + LM_FH - 1) / LM_FH;
       K.fl_off[v] = o;
       o += (K.fl_tx[v] * K.fl_ty[v] + 3) / 4 * 4;
     }
@@ -1711,6 +1711,8 @@ LM_API lm_status lm_debug_corr_work(const lm_ctx* ctx, int32_t* out) {
 LM_API int32_t lm_debug_batch_slots(const lm_ctx* ctx) { return ctx ? ctx->delivered.slots : 0; }
 
 LM_API int32_t lm_debug_dark_tile_width(void) { return LM_FW; }
+
+LM_API int32_t lm_debug_dark_tile_height(void) { return LM_FH; }
 
 namespace {
 // The lane whose device buffers still hold the last collected batch's debug

@@ -25,6 +25,7 @@ EXPORTED = (
     "lm_bb_stream", "lm_host_alloc", "lm_host_free",
     "lm_detect_submit", "lm_detect_submit_device", "lm_detect_collect", "lm_ctx_lanes", "lm_ctx_pending",
     "lm_debug_corr_work", "lm_debug_batch_slots", "lm_debug_dark_tile_width",
+    "lm_debug_dark_tile_height",
 )
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-slp-vectorize",
@@ -153,8 +154,6 @@ def lib():
         L.lm_debug_corr_work.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
         L.lm_debug_batch_slots.argtypes = [C.c_void_p]
         L.lm_debug_batch_slots.restype = C.c_int32
-        L.lm_debug_dark_tile_width.argtypes = []
-        L.lm_debug_dark_tile_width.restype = C.c_int32
         L.lm_synth_frames_device.argtypes = [C.c_int32, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32,
                                              C.c_int64]
         L.lm_bb_create.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_void_p)]
@@ -312,10 +311,11 @@ class Context:
         return lib().lm_debug_batch_slots(self._h)
 
     @staticmethod
-    def dark_tile_width():
-        """Columns of the dark-tile grid (tiles of that many x 8 outputs;
-        lm_debug_dark_tile_width)."""
-        return lib().lm_debug_dark_tile_width()
+    def dark_tile_shape():
+        """(columns, rows) of the dark-tile grid's tiles
+        (lm_debug_dark_tile_width / _height)."""
+        L = lib()  # (bound here, not at load: A/B runs load older libraries)
+        return int(L.lm_debug_dark_tile_width()), int(L.lm_debug_dark_tile_height())
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
@@ -377,10 +377,11 @@ class BBContext:
         return lib().lm_bb_stream(self._h)
 
     @staticmethod
-    def dark_tile_width():
-        """Columns of the dark-tile grid (tiles of that many x 8 outputs;
-        lm_debug_dark_tile_width)."""
-        return lib().lm_debug_dark_tile_width()
+    def dark_tile_shape():
+        """(columns, rows) of the dark-tile grid's tiles
+        (lm_debug_dark_tile_width / _height)."""
+        L = lib()  # (bound here, not at load: A/B runs load older libraries)
+        return int(L.lm_debug_dark_tile_width()), int(L.lm_debug_dark_tile_height())
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

@@ -102,6 +102,12 @@ OBJDUMP = "/opt/rocm/llvm/bin/llvm-objdump"
 def disassemble(lib, symbol_filter):
     """{function symbol: [instruction text]} of the code objects' functions
     whose names contain symbol_filter (llvm-objdump, no GPU needed)."""
+    return {k: [t for _, t, _ in v] for k, v in disassemble_cfg(lib, symbol_filter).items()}
+
+
+def disassemble_cfg(lib, symbol_filter):
+    """{function symbol: [(address, instruction text, branch target address
+    or None)]}, for control-flow aware checks."""
     out = {}
     for co in code_objects(lib):
         with tempfile.NamedTemporaryFile(suffix=".co", delete=False) as fh:
@@ -121,9 +127,18 @@ def disassemble(lib, symbol_filter):
                     out[cur] = []
                 continue
             if cur is not None:
-                ins = line.split("//")[0].strip()
+                ins, _, comment = line.partition("//")
+                ins = ins.strip()
                 if ins:
-                    out[cur].append(ins)
+                    ma = re.match(r"\s*([0-9A-Fa-f]+):", comment)
+                    mt = re.search(r"<[^>+]+\+0x([0-9a-f]+)>", comment)
+                    addr = int(ma.group(1), 16) if ma else None
+                    out[cur].append((addr, ins, mt and int(mt.group(1), 16)))
+    # branch targets are function-relative: make them absolute
+    for k, items in out.items():
+        base = items[0][0] if items and items[0][0] is not None else 0
+        out[k] = [(a, t, None if b is None or not t.startswith("s_") or "branch" not in t else base + b)
+                  for a, t, b in items]
     return out
 
 
@@ -138,31 +153,69 @@ def _vregs(operand):
     return set()
 
 
+def _lds_pair_step(ins, pending, bad):
+    """One instruction of early_reads_of_lds_pairs' scan: returns the pending
+    set after it (appending ins to bad when it reads a pending register)."""
+    op, _, rest = ins.partition(" ")
+    ops = [o.strip() for o in rest.split(",")] if rest else []
+    if op.startswith("s_waitcnt") and ("lgkmcnt(0)" in rest or "lgkmcnt" not in rest and "vmcnt" not in rest
+                                       and "expcnt" not in rest):
+        return frozenset()
+    srcs = set()
+    for o in ops[1:] if ops else []:
+        srcs |= _vregs(o.split()[0]) if o else set()
+    if op.startswith("ds_write") or op.startswith("ds_read") or op.startswith("global_store"):
+        # stores read their data/address operands; a ds_read2 reads its address (operand 1)
+        srcs = set().union(*[_vregs(o.split()[0]) for o in ops[1:] if o]) if op.startswith(("ds_write", "global_store")) \
+            else (_vregs(ops[1].split()[0]) if len(ops) > 1 else set())
+    if srcs & pending and bad is not None:
+        bad.append(ins)
+    if op == "ds_read2_b32" and ops:
+        return pending | _vregs(ops[0])
+    if ops and op.startswith("v_"):
+        return pending - _vregs(ops[0])  # overwritten: no longer the load's destination
+    return pending
+
+
 def early_reads_of_lds_pairs(instrs):
     """Instructions that read a VGPR written by a ds_read2_b32 before an
-    s_waitcnt that drains the LDS counter (lgkmcnt(0)) has executed, in
-    program order.  The ring correlation issues those reads as inline asm
+    s_waitcnt that drains the LDS counter (lgkmcnt(0)) has executed, on some
+    control-flow path.  The ring correlation issues those reads as inline asm
     the compiler's wait insertion does not see, so a register copy or use
-    before the explicit wait would read stale data."""
-    pending, bad = set(), []
-    for ins in instrs:
-        op, _, rest = ins.partition(" ")
-        ops = [o.strip() for o in rest.split(",")] if rest else []
-        if op.startswith("s_waitcnt") and ("lgkmcnt(0)" in rest or "lgkmcnt" not in rest and "vmcnt" not in rest
-                                           and "expcnt" not in rest):
-            pending.clear()
-            continue
-        srcs = set()
-        for o in ops[1:] if ops else []:
-            srcs |= _vregs(o.split()[0]) if o else set()
-        if op.startswith("ds_write") or op.startswith("ds_read") or op.startswith("global_store"):
-            # stores read their data/address operands; a ds_read2 reads its address (operand 1)
-            srcs = set().union(*[_vregs(o.split()[0]) for o in ops[1:] if o]) if op.startswith(("ds_write", "global_store")) \
-                else (_vregs(ops[1].split()[0]) if len(ops) > 1 else set())
-        if srcs & pending:
-            bad.append(ins)
-        if op == "ds_read2_b32" and ops:
-            pending |= _vregs(ops[0])
-        elif ops and op.startswith("v_"):
-            pending -= _vregs(ops[0])  # overwritten: no longer the load's destination
+    before the explicit wait would read stale data.  instrs: disassemble_cfg
+    items (address, text, branch target) -- a forward may-analysis over the
+    branches -- or plain instruction texts (scanned in program order)."""
+    if not instrs or isinstance(instrs[0], str):
+        pending, bad = frozenset(), []
+        for ins in instrs:
+            pending = _lds_pair_step(ins, pending, bad)
+        return bad
+    idx = {a: i for i, (a, _, _) in enumerate(instrs)}
+    n = len(instrs)
+
+    def succs(i):
+        _, t, tgt = instrs[i]
+        op = t.split(" ")[0]
+        if op in ("s_endpgm", "s_setpc_b64", "s_trap"):
+            return []
+        nxt = [i + 1] if i + 1 < n else []
+        if tgt is not None and tgt in idx:
+            return [idx[tgt]] if op == "s_branch" else [idx[tgt]] + nxt
+        return nxt
+
+    state = [None] * n  # pending set on entry
+    state[0] = frozenset()
+    work = [0]
+    while work:
+        i = work.pop()
+        out = _lds_pair_step(instrs[i][1], state[i], None)
+        for j in succs(i):
+            merged = out if state[j] is None else state[j] | out
+            if merged != state[j]:
+                state[j] = merged
+                work.append(j)
+    bad = []
+    for i in range(n):
+        if state[i] is not None:
+            _lds_pair_step(instrs[i][1], state[i], bad)
     return bad

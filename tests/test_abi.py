@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert getattr(L, name) is not None
     assert L.lm_abi_version() == 6
-    assert L.lm_debug_dark_tile_width() in (40, 80)
+    assert L.lm_debug_dark_tile_width() in (40, 80) and L.lm_debug_dark_tile_height() in (4, 8)
 
 
 def test_last_error_and_null_arguments_without_gpu():

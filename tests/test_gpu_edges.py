@@ -130,15 +130,15 @@ def test_wide_ring_widths(plan, unfused):
             assert np.array_equal(s.view(np.uint32), ref.scores(f + 1, det, s.shape).view(np.uint32)), (f, det)
 
 
-def _bright_tiles(cfg, frames, tw=None):
-    """Bright tw x 8 output tiles (the library's dark-tile grid: 40 x 8) of
-    the point detectors (some I_*_MOUSE
+def _bright_tiles(cfg, frames):
+    """Bright output tiles of the library's dark-tile grid (40 x 4) of the
+    point detectors (some I_*_MOUSE
     pixel > 25 after readFrame's subtract + NORM_MINMAX, :1304-1310) and the
     outputs they hold, per view, summed over frames (identity calibration,
     provided boxes, no flip: the mouse crop ends at the box's bottom-right
     corner x + width, y + height (getBoundingBox :547-557, cropBoundingBox
     :1422-1423), one pixel right of and below the box rectangle)."""
-    tw = tw or rt.Context.dark_tile_width()
+    tw, th = rt.Context.dark_tile_shape()
     bk = cfg.background.astype(np.int32)
     p = cfg.params
     tiles, outs = [0, 0], [0, 0]
@@ -151,9 +151,9 @@ def _bright_tiles(cfg, frames, tw=None):
         n = np.clip(np.rint(t), 0, 255)
         for v, r in enumerate((p.bounding_box_bottom, p.bounding_box_side)):
             crop = n[r.y + 1:r.y + 1 + r.height, r.x + 1:r.x + 1 + r.width] > 25
-            for ty in range(0, r.height, 8):
+            for ty in range(0, r.height, th):
                 for tx in range(0, r.width, tw):
-                    blk = crop[ty:ty + 8, tx:tx + tw]
+                    blk = crop[ty:ty + th, tx:tx + tw]
                     if blk.any():
                         tiles[v] += 1
                         outs[v] += blk.size
@@ -181,7 +181,7 @@ def test_dark_tiles(plan, monkeypatch):
         if dark == "1":
             tiles, outs = _bright_tiles(cfg, frames)
             assert work == {"tiles": tuple(tiles), "outputs": tuple(outs)}, (work, tiles, outs)
-            assert tiles[0] < 180 * len(frames) and tiles[1] < 120 * len(frames)
+            assert tiles[0] < 360 * len(frames) and tiles[1] < 240 * len(frames)
         else:
             assert work is None
 
@@ -189,7 +189,7 @@ def test_dark_tiles(plan, monkeypatch):
 def test_dark_tiles_c5():
     """C5 (1920x512, detectors x2, bench batch shape per frame): dark-tile
     skipping against the oracle, and the executed-work counts the bench's
-    roofline uses (lm_debug_corr_work) equal the numpy count of bright 40 x 8
+    roofline uses (lm_debug_corr_work) equal the numpy count of bright 40 x 4
     tiles and their outputs."""
     c5 = S.SyntheticConfig(rows=512, cols=1920)
     frames = np.concatenate([c5.frames(10, 2), np.zeros_like(c5.frames(0, 1)), c5.frames(13, 2)])
@@ -204,7 +204,7 @@ def test_dark_tiles_c5():
     tiles, outs = _bright_tiles(c5, frames)
     assert work == {"tiles": tuple(tiles), "outputs": tuple(outs)}, (work, tiles, outs)
     assert slots == len(frames)  # a batch from frame 0 has no halo slot
-    assert 0 < tiles[0] < 700 * len(frames)
+    assert 0 < tiles[0] < 1400 * len(frames)
 
 
 @pytest.mark.parametrize("c5", [False, True])

@@ -52,10 +52,11 @@ def test_ring_reads_wait_for_lds():
     import kernel_resources
     if not os.path.exists(LIB):
         pytest.skip("liblocomouse_hip.so not built")
-    funcs = kernel_resources.disassemble(LIB, "k_corr_rw")
+    funcs = kernel_resources.disassemble_cfg(LIB, "k_corr_rw")
     assert len(funcs) >= 2 * 25 + 2, sorted(funcs)[:4]
     for name, ins in funcs.items():
-        assert sum(1 for i in ins if i.startswith("ds_read2_b32")) > 0, name
+        assert sum(1 for _, i, _ in ins if i.startswith("ds_read2_b32")) > 0, name
+        assert any(t is not None for _, _, t in ins), name  # branch targets parsed
         bad = kernel_resources.early_reads_of_lds_pairs(ins)
         assert not bad, (name, bad[:4])
 
@@ -70,3 +71,19 @@ def test_lds_wait_checker_flags_an_early_read():
     assert kernel_resources.early_reads_of_lds_pairs(ok) == []
     assert kernel_resources.early_reads_of_lds_pairs(early) == ["v_mov_b32_e32 v10, v3"]
     assert kernel_resources.early_reads_of_lds_pairs(overwritten) == []
+
+
+def test_lds_wait_checker_follows_branches():
+    import kernel_resources
+    # a use reached by a branch around the ds_read2 is fine; a path through it
+    # without a wait is not, wherever the blocks are laid out
+    ok = [(0, "s_cbranch_scc1 2", 12), (4, "ds_read2_b32 v[2:3], v9 offset0:1 offset1:117", None),
+          (8, "s_waitcnt lgkmcnt(0)", None), (12, "v_mov_b32_e32 v10, v3", None), (16, "s_endpgm", None)]
+    bad = [(0, "s_cbranch_scc1 2", 12), (4, "ds_read2_b32 v[2:3], v9 offset0:1 offset1:117", None),
+           (8, "s_nop 0", None), (12, "v_mov_b32_e32 v10, v3", None), (16, "s_endpgm", None)]
+    laid_out = [(0, "s_branch 3", 16), (4, "ds_read2_b32 v[2:3], v9 offset0:1 offset1:117", None),
+                (8, "s_nop 0", None), (12, "s_endpgm", None), (16, "v_mov_b32_e32 v10, v3", None),
+                (20, "s_endpgm", None)]
+    assert kernel_resources.early_reads_of_lds_pairs(ok) == []
+    assert kernel_resources.early_reads_of_lds_pairs(bad) == ["v_mov_b32_e32 v10, v3"]
+    assert kernel_resources.early_reads_of_lds_pairs(laid_out) == []  # program order alone would flag it
