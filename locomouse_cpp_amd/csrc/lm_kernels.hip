@@ -863,8 +863,19 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
 // peakClustering for the side view.
 #define LM_NMS_THREADS 512
 #define LM_GLOB_BLOCKS 16   // grid of the global-scratch (<true>) k_nms / k_post launches: one scratch region each
-#define LM_NMS_CAP 2048     // entries kept in LDS; larger lists use the global-memory path
-#define LM_NMS_RANKSORT 1024  // up to this many entries: O(n^2/T) rank sort instead of bitonic
+// The LDS instantiation at 36 KB and <= 64 VGPRs (8 waves per SIMD): four
+// 512-thread blocks per CU, so a batch's 1,024 (slot, list) blocks are one
+// round (at 2,048 entries / 48 KB and 75 VGPRs, three per CU): 67 -> 61 us per
+// batch alone, +1 % frames/s with four contexts (profiles/r04/nms/)
+#ifndef LM_NMS_CAP
+#define LM_NMS_CAP 1536     // entries kept in LDS; larger lists use the global-memory path
+#endif
+#ifndef LM_NMS_RANKSORT
+#define LM_NMS_RANKSORT 768  // up to this many entries: O(n^2/T) rank sort instead of bitonic
+#endif
+#ifndef LM_NMS_WPE
+#define LM_NMS_WPE 8  // amdgpu_waves_per_eu minimum of the LDS instantiation
+#endif
 #define LM_NMS_PAIRPAR 1024   // up to this many entries: nmsMax tests every pair, spread over the block
 
 DEV float key_score(unsigned long long k) { return __uint_as_float(~(unsigned)(k >> 32)); }
@@ -1552,7 +1563,7 @@ DEV void for_overflow_pairs(int npairs, Pred overflow, Fn fn) {
     if (pp_) pp_[(blockIdx.x * 2 + blockIdx.y) * 16 + (k)] = (k) >= 14 ? wall_clock64() : clock64(); \
   }
 template <bool GLOB>
-__global__ __launch_bounds__(LM_NMS_THREADS) void k_nms(const LmConst* __restrict__ Kp, int s0, unsigned long long* __restrict__ keys,
+__global__ __launch_bounds__(LM_NMS_THREADS) __attribute__((amdgpu_waves_per_eu(GLOB ? 1 : LM_NMS_WPE, 8))) void k_nms(const LmConst* __restrict__ Kp, int s0, unsigned long long* __restrict__ keys,
                                                        const int32_t* __restrict__ n_pos, const unsigned long long* __restrict__ tailmask,
                                                        unsigned long long* __restrict__ gscratch, int64_t gscratch_slot,
                                                        LmSlotOut* __restrict__ hdr, int32_t* __restrict__ err,
