@@ -220,15 +220,38 @@ def cpu_baseline_threads(cfg, seconds=8.0, threads=None, chunk=50, pin=False):
                       f"frames, {el:.1f} s wall"}
 
 
+def cgroup_cpus():
+    """CPUs' worth of time the process's cgroup may use (cpu.max /
+    cpu.cfs_quota_us), or None when unlimited or unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            return None if q == "max" else max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            per = int(fh.read())
+        return None if q <= 0 else max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline_node(cfg, seconds=8.0):
     """BASELINE.md §2's `nproc`-thread line: one oracle thread per CPU this
-    process may run on, each pinned to its CPU, on its own contiguous chunks
-    of 50 frames.  On a shared GPU box the other GPUs' jobs use the same
-    CPUs, so this is the whole-node figure as measured there; the per-GPU
-    share (cpu_baseline_threads) is the fair per-GPU comparison."""
+    process may run on (capped by the cgroup's CPU quota: threads beyond it
+    only time-slice), each pinned to its CPU, on its own contiguous chunks of
+    50 frames.  On a shared GPU box the other GPUs' jobs use the same CPUs,
+    so this is the whole-node figure as measured there; the per-GPU share
+    (cpu_baseline_threads) is the fair per-GPU comparison."""
     n = len(os.sched_getaffinity(0))
-    line = cpu_baseline_threads(cfg, seconds, threads=n, chunk=50, pin=True)
+    quota = cgroup_cpus()
+    line = cpu_baseline_threads(cfg, seconds, threads=min(n, quota or n), chunk=50, pin=True)
     line["nproc"] = os.cpu_count()
+    line["affinity_cpus"] = n
+    line["cgroup_cpu_quota"] = quota
     return line
 
 

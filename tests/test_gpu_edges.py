@@ -207,6 +207,25 @@ def test_dark_tiles_c5():
     assert 0 < tiles[0] < 1400 * len(frames)
 
 
+def test_dark_tiles_batch_over_512():
+    """A batch of more than 512 frames: k_ingest's 65 slot groups share the 64
+    list-segment counters of a view (segment c holds groups y0(c) .. y0(c+1)-1,
+    lm_tl_y0), so some segments gather two groups' bright tiles; the
+    correlation's segment lookup must find every one.  Against the oracle,
+    with the work counts equal to the numpy count."""
+    cfg = S.SyntheticConfig()
+    frames = np.concatenate([cfg.frames(200, 260), np.zeros_like(cfg.frames(0, 1)), cfg.frames(461, 259)])
+    ref = _oracle(cfg, frames).result
+    ctx = _ctx(cfg, max_batch=len(frames))
+    ctx.set_debug(2)
+    got = ctx.detect(frames, 0)
+    work = ctx.corr_work()
+    ctx.close()
+    assert_same(got, ref, "520-frame batch: ")
+    tiles, outs = _bright_tiles(cfg, frames)
+    assert work == {"tiles": tuple(tiles), "outputs": tuple(outs)}, (work, tiles, outs)
+
+
 @pytest.mark.parametrize("c5", [False, True])
 def test_dense_occlusion_grid(c5):
     """occlusion_grid_spacing_pixels_bottom = 5: 60 x 28 = 1,680 ONG nodes on
