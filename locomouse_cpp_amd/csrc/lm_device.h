@@ -176,6 +176,8 @@ struct LmArenaCtl {
   int32_t cap[AR_COUNT];
   int32_t overflow;
   int32_t nparts;                  // parts in use this batch (set by the host)
+  uint8_t* pack_dst;               // the batch's pinned result buffer (device view) and its size:
+  int64_t pack_cap;                //   k_out reads them here, so a captured graph takes any buffer
   int32_t sub[LM_SUBARENA][32];  // sub[g][k]: part g's count of arena k (k < AR_COUNT)
 };
 

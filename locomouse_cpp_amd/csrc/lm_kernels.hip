@@ -2110,6 +2110,8 @@ __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots
   if (threadIdx.x == 0) {
     ctl->overflow = h_ctl->overflow;
     ctl->nparts = h_ctl->nparts;
+    ctl->pack_dst = h_ctl->pack_dst;
+    ctl->pack_cap = h_ctl->pack_cap;
   }
   for (int i = threadIdx.x; i < LM_SUBARENA * 32; i += blockDim.x) (&ctl->sub[0][0])[i] = 0;
 }
@@ -2119,10 +2121,17 @@ __global__ __launch_bounds__(256) void k_prep(const LmSlot* __restrict__ h_slots
 // memory; then the next batch's previous frame (storePreviousImage,
 // LocoMouse_class.cpp:1508-1513) -> the halo buffer.  Packed sizes and frame
 // sizes are multiples of 16 bytes.
+// h_pack == nullptr: the destination and its size are the batch's, in ctl
+// (k_prep copied them from the lane's mapped control block).
 __global__ __launch_bounds__(256) void k_out(const LmPackHdr* __restrict__ ph, LmPackHdr* __restrict__ h_ph,
                                              const uint8_t* __restrict__ pack, uint8_t* __restrict__ h_pack, int64_t h_cap,
+                                             const LmArenaCtl* __restrict__ ctl,
                                              const uint8_t* __restrict__ halo_arg, const uint8_t* const* __restrict__ fptr,
                                              int fidx, uint8_t* __restrict__ halo_dst, int64_t halo_bytes) {
+  if (!h_pack && ctl) {
+    h_pack = ctl->pack_dst;
+    h_cap = ctl->pack_cap;
+  }
   // halo source: halo_arg, else the batch's frame pointer fptr[fidx] (device
   // array written by k_prep, so a captured graph replays with fresh frames)
   const uint8_t* __restrict__ halo_src = halo_arg ? halo_arg : (fptr ? fptr[fidx] : nullptr);

@@ -123,7 +123,6 @@ struct Lane {
   HostBuf<LmArenaCtl> h_ctl;
   HostBuf<int32_t> h_err;
   HostBuf<LmPackHdr> h_ph;
-  HostBuf<uint8_t> h_pack;  // packed results of the lane's last batch (lm_batch_result points here)
   DevBuf<LmPackHdr> zero_ph;
   // this lane's last batch: the state a batch continuing it on this lane carries over
   bool have_state = false;
@@ -132,6 +131,7 @@ struct Lane {
   struct Pending {
     bool on = false;
     int n = 0, first = 0, s_lut0 = 1, s_proc0 = 1, plan = 0, cur = 0, prv = 0, last_n = 0;
+    int pack = -1;  // the context's result buffer the batch's k_out writes
     bool carry = false;
   } pend;
   int64_t seq = -1;               // submission number of the batch running on this lane (-1: idle)
@@ -216,11 +216,33 @@ struct lm_ctx {
   // pipeline
   std::vector<std::unique_ptr<Lane>> lanes;
   DevBuf<uint8_t> handoff;     // two frames: the last frame of submitted batch k in slot k & 1
+  // Pinned result buffers.  Each submitted batch takes a free one (k_out
+  // writes its packed results there; the address reaches the captured graph
+  // through the lane's control block), which then backs its lm_batch_result
+  // until the next lm_detect_* call after its collection -- no copy when a
+  // batch is retired from its lane early (a 1.2 MB copy per C3 batch made the
+  // single host thread of a pipelined context the bottleneck).
+  std::vector<std::unique_ptr<HostBuf<uint8_t>>> packs;
+  std::vector<char> pack_busy;
+  int take_pack(size_t cap) {
+    size_t i = 0;
+    while (i < packs.size() && pack_busy[i]) ++i;
+    if (i == packs.size()) {
+      packs.emplace_back(new HostBuf<uint8_t>());
+      pack_busy.push_back(0);
+    }
+    if (packs[i]->n < cap) packs[i]->alloc(cap);
+    pack_busy[i] = 1;
+    return (int)i;
+  }
+  void drop_pack(int i) {
+    if (i >= 0 && i < (int)pack_busy.size()) pack_busy[i] = 0;
+  }
   // Submitted batches not yet returned by lm_detect_collect, in submission
   // order.  A batch runs on a lane until it is finished: when it is
-  // collected, or earlier when a submission needs its lane (its packed
-  // results are then copied aside, "retired"), so a lane that finishes early
-  // is fed again at once while results still come back in frame order.
+  // collected, or earlier when a submission needs its lane ("retired": its
+  // results stay in its buffer), so a lane that finishes early is fed again
+  // at once while results still come back in frame order.
   struct BatchRec {
     int64_t seq = 0;
     int lane = -1;      // running there; -1 once retired
@@ -229,7 +251,7 @@ struct lm_ctx {
     int slots = 0;      // frame slots processed: n, or n + 1 when the halo frame was recomputed
     lm_status status = LM_OK;  // a failure found while retiring, reported when collected
     std::string err;
-    std::vector<uint8_t> pack;  // retired results (lm_batch_result layout)
+    int pack = -1;  // its pinned result buffer (lm_batch_result layout), lm_ctx::packs
     LmPackHdr ph{};
     std::vector<const char*> t_names;  // kernel timings (debug bit 1)
     std::vector<double> t_ms, t_t0, t_t1;
@@ -762,7 +784,6 @@ void lane_alloc(lm_ctx* c, Lane& L) {
   cap[AR_PWJC] = ns * LM_NFEAT * (64 + g.ong_nx * g.ong_ny + 1);
   cap[AR_PWNZ] = ns * LM_NFEAT * (1024 + g.ong_nx * g.ong_ny);  // an ONG column holds at least its diagonal
   for (int a = 0; a < 2; ++a) L.arena[a].alloc(cap, ns);
-  L.h_pack.alloc((size_t)L.arena[0].pack_cap);
   HIPCHK(hipEventCreateWithFlags(&L.ev_snap, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&L.ev_consumed, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&L.ev_done, hipEventDisableTiming | hipEventBlockingSync));
@@ -1094,8 +1115,8 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
                                             A.jc.p, A.ir.p, A.pr.p, A.ph.p, A.pack.p, A.side_base.p);
     T.end();
     // header + results to host memory, then frame n as the next batch's halo
-    k_out<<<128, 256, 0, st>>>(A.ph.p, L.h_ph.d, A.pack.p, L.h_pack.d, (int64_t)L.h_pack.n, nullptr, L.frame_ptr.p,
-                               n, L.halo.p, c->npix);
+    k_out<<<128, 256, 0, st>>>(A.ph.p, L.h_ph.d, A.pack.p, nullptr, 0, A.ctl.p, nullptr, L.frame_ptr.p, n, L.halo.p,
+                               c->npix);
   }
 }
 
@@ -1112,6 +1133,8 @@ void launch_attempt(lm_ctx* c, Lane& L, int attempt) {
   LmArenaCtl& hc = *L.h_ctl.p;
   std::memset(&hc, 0, sizeof(hc));
   for (int k = 0; k < AR_COUNT; ++k) hc.cap[k] = A.cap[k];
+  hc.pack_dst = c->packs[P.pack]->d;
+  hc.pack_cap = (int64_t)c->packs[P.pack]->n;
   hc.nparts = std::min(LM_SUBARENA, 2 * P.n);  // k_post has 2n blocks: every part gets used
   Timer T(c, L);
   const bool graph = graphs_env && L.use_graphs && attempt == 0 && !(c->debug & 1) && !c->kprof_on;
@@ -1178,7 +1201,6 @@ void retire(lm_ctx* c, Lane& L) {
   try {
     finish_batch(c, L);
     rec->ph = *L.h_ph.p;
-    rec->pack.assign(L.h_pack.p, L.h_pack.p + rec->ph.bytes);
   } catch (const std::invalid_argument& e) {
     rec->status = LM_ERR_INVALID_ARGUMENT;
     rec->err = e.what();
@@ -1332,7 +1354,8 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
       HIPCHK(hipMemcpy2DAsync(L.frames.p + fstride, (size_t)fstride, frames, (size_t)pitch, (size_t)c->npix, (size_t)n,
                               hipMemcpyDeviceToDevice, st));
     if (given_halo && ((uintptr_t)prev & 15) == 0)
-      k_out<<<64, 256, 0, st>>>(L.zero_ph.p, L.h_ph.d, nullptr, nullptr, 0, prev, nullptr, 0, L.halo.p, c->npix);
+      k_out<<<64, 256, 0, st>>>(L.zero_ph.p, L.h_ph.d, nullptr, nullptr, 0, nullptr, prev, nullptr, 0, L.halo.p,
+                                c->npix);
     else if (given_halo)
       HIPCHK(hipMemcpyAsync(L.halo.p, prev, (size_t)c->npix, hipMemcpyDeviceToDevice, st));
   }
@@ -1379,7 +1402,14 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   P.prv = L.last_parity;
   P.carry = carry;
   P.last_n = carry ? L.last_n : 0;
-  launch_attempt(c, L, 0);
+  P.pack = c->take_pack((size_t)L.arena[P.cur].pack_cap);
+  try {
+    launch_attempt(c, L, 0);
+  } catch (...) {
+    c->drop_pack(P.pack);
+    P.on = false;
+    throw;
+  }
   HIPCHK(hipEventRecord(L.ev_done, st));
 
   // the video position and the lane's carry state advance now; a batch that
@@ -1393,6 +1423,7 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   lm_ctx::BatchRec rec;
   rec.seq = c->nsub;
   rec.lane = L.index;
+  rec.pack = P.pack;
   rec.first = first;
   rec.n = n;
   rec.slots = n + 1 - s_proc0;
@@ -1406,7 +1437,7 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
 }
 
 // Wait for the lane's batch and rerun it while its result arena overflows;
-// its packed results are then in the lane's h_pack.
+// its packed results are then in the batch's result buffer.
 void finish_batch(lm_ctx* c, Lane& L) {
   Lane::Pending& P = L.pend;
   hipStream_t st = L.stream;
@@ -1458,14 +1489,15 @@ void finish_batch(lm_ctx* c, Lane& L) {
   }
   if (c->kprof_on) kprof_report(c, L, n);
 
-  // ---- the packed results (lm_batch_result layout) are in h_pack unless
-  // they outgrew it: then grow it and let k_out copy them (and the halo) again
+  // ---- the packed results (lm_batch_result layout) are in the batch's
+  // buffer unless they outgrew it: then grow it and let k_out copy them (and
+  // the halo) again
   Arena& A = L.arena[P.cur];
   const LmPackHdr ph = *L.h_ph.p;
-  if ((int64_t)L.h_pack.n < ph.bytes) {
-    L.drop_graphs();
-    L.h_pack.alloc((size_t)(ph.bytes + ph.bytes / 4));
-    k_out<<<128, 256, 0, st>>>(A.ph.p, L.h_ph.d, A.pack.p, L.h_pack.d, (int64_t)L.h_pack.n, nullptr, L.frame_ptr.p, n,
+  HostBuf<uint8_t>& HP = *c->packs[P.pack];
+  if ((int64_t)HP.n < ph.bytes) {
+    HP.alloc((size_t)(ph.bytes + ph.bytes / 4));
+    k_out<<<128, 256, 0, st>>>(A.ph.p, L.h_ph.d, A.pack.p, HP.d, (int64_t)HP.n, nullptr, nullptr, L.frame_ptr.p, n,
                                L.halo.p, c->npix);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
@@ -1479,9 +1511,9 @@ void finish_batch(lm_ctx* c, Lane& L) {
     std::vector<uint8_t> chk((size_t)ph.bytes);
     HIPCHK(hipMemcpy(chk.data(), A.pack.p, (size_t)ph.bytes, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < ph.bytes; ++i)
-      if (chk[i] != L.h_pack.p[i]) {
+      if (chk[i] != HP.p[i]) {
         int64_t j = ph.bytes - 1;
-        while (j > i && chk[j] == L.h_pack.p[j]) --j;
+        while (j > i && chk[j] == HP.p[j]) --j;
         fprintf(stderr, "[lm debug] D2H pack mismatch frames %d..%d: bytes [%ld, %ld] of %ld differ\n", first,
                 first + n - 1, (long)i, (long)j, (long)ph.bytes);
         break;
@@ -1521,6 +1553,10 @@ void collect_batch(lm_ctx* c, lm_batch_result* out) {
   if (c->queue.empty()) throw std::invalid_argument("no batch in flight: lm_detect_submit one first.");
   lm_ctx::BatchRec rec = std::move(c->queue.front());
   c->queue.pop_front();
+  // the previously delivered batch's arrays are no longer valid (the caller
+  // made another lm_detect_* call): its buffer is free again
+  c->drop_pack(c->delivered.pack);
+  c->delivered.pack = -1;
   if (rec.lane >= 0) {  // still on its lane: finish it there
     Lane& L = *c->lanes[rec.lane];
     rec.ran_lane = L.index;
@@ -1530,6 +1566,7 @@ void collect_batch(lm_ctx* c, lm_batch_result* out) {
       L.pend.on = false;
       L.have_state = false;
       L.seq = -1;
+      c->drop_pack(rec.pack);
       throw;
     }
     L.seq = -1;
@@ -1538,16 +1575,16 @@ void collect_batch(lm_ctx* c, lm_batch_result* out) {
     rec.t_ms = L.t_ms;
     rec.t_t0 = L.t_t0;
     rec.t_t1 = L.t_t1;
-    const LmPackHdr ph = *L.h_ph.p;
-    c->delivered = std::move(rec);
-    fill_result(out, L.h_pack.p, c->delivered.n, c->delivered.first, ph);
-    return;
+    rec.ph = *L.h_ph.p;
   }
-  if (rec.status == LM_ERR_INVALID_ARGUMENT) throw std::invalid_argument(rec.err);
-  if (rec.status == LM_ERR_HIP) throw HipError(rec.err);
-  if (rec.status != LM_OK) throw std::runtime_error(rec.err);
+  if (rec.status != LM_OK) {
+    c->drop_pack(rec.pack);
+    if (rec.status == LM_ERR_INVALID_ARGUMENT) throw std::invalid_argument(rec.err);
+    if (rec.status == LM_ERR_HIP) throw HipError(rec.err);
+    throw std::runtime_error(rec.err);
+  }
   c->delivered = std::move(rec);
-  fill_result(out, c->delivered.pack.data(), c->delivered.n, c->delivered.first, c->delivered.ph);
+  fill_result(out, c->packs[c->delivered.pack]->p, c->delivered.n, c->delivered.first, c->delivered.ph);
 }
 
 // One synchronous batch (submit + collect); nothing may be in flight.
@@ -1608,6 +1645,11 @@ LM_API lm_status lm_ctx_create(int32_t device, const lm_setup* setup, const lm_p
       lane_alloc(c, L);
     }
     if (nl > 1) c->handoff.alloc((size_t)2 * c->fstride);
+    // result buffers for every batch that can be in flight or delivered at
+    // once (2 x lanes queued + the delivered one), pinned now rather than on
+    // a timed submission
+    for (int i = 0; i < 2 * nl + 1; ++i) c->take_pack((size_t)c->lanes[0]->arena[0].pack_cap);
+    for (int i = 0; i < 2 * nl + 1; ++i) c->drop_pack(i);
   });
   if (s != LM_OK) {
     delete c;
