@@ -742,7 +742,7 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(L
     RwTiles H;
     if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) return;
     const LmDet D = K.det[d];
-    switch (D.kw) {
+    switch (D.kw_ring) {
 #define LM_KW_CASE(n)                                                                                             \
   case n:                                                                                                         \
     rw_tile<n, UNF>(K, D, H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);       \

@@ -66,6 +66,7 @@ struct LmDet {
   int32_t kind;      // 0 point detector (list), 1 tail detector (binary map)
   int32_t list;      // list id for kind 0, 0/1 (bottom/side) for kind 1
   int32_t kh, kw, kwp;
+  int32_t kw_ring;  // k_corr_rw width that runs it: kw, or a wider one <= kwp that another detector uses
   int32_t w_off;     // float offset of the kh x kwp zero-padded weights
   float delta;       // (float)(-rho): filter2D delta (LocoMouse_class.cpp:845)
   int32_t oh, ow;    // consumed output region (UNPAD)

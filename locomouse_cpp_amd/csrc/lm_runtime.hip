@@ -456,6 +456,28 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     D.m_x = out_rel[d].x;
   }
   K.n_tiles = tile;
+  // LM_RW_WIDEN=1: a ring detector whose zero-padded row (kwp) reaches the
+  // width of another ring detector of the context runs on that width's
+  // kernel: the extra taps have weight 0 and add +0 (bit-identical, the ext
+  // crops already hold kwp columns), and one launch per batch fewer ends in
+  // its own tail (C3: paw side 22 -> 24 with paw bottom).  Measured with four
+  // contexts: 466.9k vs 470.0k frames/s without (profiles/r04/widen/) -- the
+  // other contexts fill the tails anyway -- so off by default.
+  {
+    static const bool widen = [] {
+      const char* v = getenv("LM_RW_WIDEN");
+      return v && atoi(v) != 0;
+    }();
+    for (int d = 0; d < 6; ++d) {
+      LmDet& D = K.det[d];
+      D.kw_ring = D.kw;
+      if (!widen || !corr_ring(D.kw)) continue;
+      for (int e = 0; e < 6; ++e) {
+        const int w = K.det[e].kw;
+        if (e != d && corr_ring(w) && w > D.kw && w <= D.kwp && (D.kw_ring == D.kw || w < D.kw_ring)) D.kw_ring = w;
+      }
+    }
+  }
   for (int v = 0; v < 2; ++v) {
     K.ext_oy[v] = ey0[v];
     K.ext_ox[v] = ex0[v];
@@ -620,17 +642,17 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       const int d = order[oi];
       LmDet& D = K.det[d];
       const bool f16 = su->corr_precision == LM_CORR_F16;
-      const bool ring = !f16 && corr_ring(D.kw);
+      const bool ring = !f16 && corr_ring(D.kw_ring);
       const void* fn = f16 ? corr_kernel_f16(D.kw)
-                       : ring && m == 1 && rw_all_width(D.kw) ? corr_kernel_rw_all(c->unfused)
-                                                              : corr_kernel(D.kw, c->unfused);
+                       : ring && m == 1 && rw_all_width(D.kw_ring) ? corr_kernel_rw_all(c->unfused)
+                                                                   : corr_kernel(D.kw_ring, c->unfused);
       size_t need;
       if (f16) {
         D.chunk_rows = D.kh;
         need = f16_lds_bytes(f16_nch(D.kw), D.kh);
       } else if (ring) {
         D.chunk_rows = D.kh;
-        need = rw_lds_bytes(D.kw);
+        need = rw_lds_bytes(D.kw_ring);
       } else {
         const size_t row = (size_t)pk_stride(LM_TW + D.kwp - 1) * sizeof(float);
         D.chunk_rows = std::max(1, std::min(D.kh, (int)(kCorrLdsBudget / row) - (LM_TH - 1)));
@@ -651,7 +673,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       G.ids[G.n] = d;
       G.tile_end[G.n] = prev + D.tiles_x * D.tiles_y;
       ++G.n;
-      if (ring) G.ring_floats = std::max(G.ring_floats, rw_ring_floats(D.kw));
+      if (ring) G.ring_floats = std::max(G.ring_floats, rw_ring_floats(D.kw_ring));
       P.lds[gi] = std::max(P.lds[gi], need);
     }
   }
