@@ -861,7 +861,9 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
 // re-sorted from row-major order with the libstdc++ introsort replica
 // (lm_introsort.h) — then clustered: nmsMax for the bottom view,
 // peakClustering for the side view.
+#ifndef LM_NMS_THREADS
 #define LM_NMS_THREADS 512
+#endif
 #define LM_GLOB_BLOCKS 16   // grid of the global-scratch (<true>) k_nms / k_post launches: one scratch region each
 // The LDS instantiation at 36 KB and <= 64 VGPRs (8 waves per SIMD): four
 // 512-thread blocks per CU, so a batch's 1,024 (slot, list) blocks are one
@@ -931,8 +933,9 @@ DEV void rank_sort(unsigned long long* a, unsigned long long* tmp, int n) {
 // for every other run, the count of smaller keys there (binary searches, the
 // runs' probes interleaved).  A few shuffle and LDS latencies per step instead
 // of rank_sort's n / 8 rounds of loads per key.  tmp holds n keys.
-static_assert(LM_NMS_THREADS == 512, "wave_merge_sort: 8 runs of 64");
+static_assert(LM_NMS_THREADS % 64 == 0 && LM_NMS_THREADS <= 512, "wave_merge_sort: up to 8 runs of 64");
 DEV void wave_merge_sort(unsigned long long* a, unsigned long long* tmp, int n) {
+  constexpr int NR = LM_NMS_THREADS / 64;  // runs
   const int t = threadIdx.x, lane = t & 63, run = t >> 6, nruns = (n + 63) >> 6;
   unsigned long long v = t < n ? a[t] : ~0ull;
   if (run < nruns) {
@@ -949,16 +952,16 @@ DEV void wave_merge_sort(unsigned long long* a, unsigned long long* tmp, int n) 
   if (run < nruns) a[t] = v;  // sorted runs, padded with ~0 past n
   __syncthreads();
   if (t < n) {
-    int lo[8], rank = lane;
+    int lo[NR], rank = lane;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) lo[r] = 0;
+    for (int r = 0; r < NR; ++r) lo[r] = 0;
 #pragma unroll
     for (int s = 32; s >= 1; s >>= 1)
 #pragma unroll
-      for (int r = 0; r < 8; ++r)
+      for (int r = 0; r < NR; ++r)
         if (r < nruns && r != run && a[r * 64 + lo[r] + s - 1] < v) lo[r] += s;
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
+    for (int r = 0; r < NR; ++r)
       if (r < nruns && r != run) rank += lo[r] + (a[r * 64 + lo[r]] < v ? 1 : 0);
     tmp[rank] = v;
   }
