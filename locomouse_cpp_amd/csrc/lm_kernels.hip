@@ -265,7 +265,10 @@ DEV uint32_t bright_bytes(uint32_t w) {
 // 0x80 in byte i of the result for bit i of the 4-bit n
 DEV uint32_t byte_mask4(uint32_t n) { return ((n * 0x00204081u) & 0x01010101u) << 7; }
 
-__global__ __launch_bounds__(1024) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
+#ifndef LM_INGEST_WPE
+#define LM_INGEST_WPE 1  // amdgpu_waves_per_eu minimum (register budget experiments)
+#endif
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_WPE, 8))) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
                                                  const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
                                                  const uint8_t* __restrict__ luts, const LmSlot* __restrict__ slots,
                                                  int s0, int s_end, uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
