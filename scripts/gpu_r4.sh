@@ -3,7 +3,7 @@
 # oracle checks (C3 default, the drop-in 1 context x 4 lanes, C5 fp32), the
 # C4 strong-scaling mode on one GPU and rehearsed with 4 oversubscribed
 # ranks, and the launcher's refusal of --gpus 2 on a one-GPU box.
-# STEPS=tests,smoke,bench,lanes,c5,video,refuse,prof,traffic selects steps
+# STEPS=tests,smoke,bench,lanes,c5,c5f16,video,refuse,prof,traffic selects steps
 # (default: all but kprof).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
@@ -11,7 +11,7 @@ TAG=${TAG:-r4}
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp MASTER_ADDR=127.0.0.1
-S=",${STEPS:-tests,smoke,bench,lanes,c5,video,refuse,prof,traffic},"
+S=",${STEPS:-tests,smoke,bench,lanes,c5,c5f16,video,refuse,prof,traffic},"
 # kprof: phase cycles of k_nms / k_tail / k_post (LM_KPROF=1, one stream)
 on() { [[ $S == *",$1,"* ]]; }
 if on tests; then
@@ -39,6 +39,8 @@ PY
 on bench && bench c3 --steps 20 --warmup 5
 on lanes && bench lanes4 --steps 40 --warmup 5 --streams 1 --lanes 4 --no-cpu
 on c5 && bench c5 --config c5 --steps 10 --warmup 2 --no-cpu
+# C5 in the non-parity f16 mode: 8 contexts (its longer correlation launches need more streams to fill each other's tails)
+on c5f16 && bench c5f16 --config c5 --precision f16 --streams 8 --steps 12 --warmup 2 --no-cpu
 on video && bench video1 --gpus 1 --video-frames 10000 --steps 3 --warmup 2 --no-cpu
 on video && bench video4 --gpus 4 --oversubscribe --video-frames 10000 --steps 3 --warmup 2 --no-cpu
 if on refuse; then
