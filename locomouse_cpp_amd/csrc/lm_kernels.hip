@@ -881,7 +881,18 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
 #ifndef LM_NMS_WPE
 #define LM_NMS_WPE 8  // amdgpu_waves_per_eu minimum of the LDS instantiation
 #endif
-#define LM_NMS_PAIRPAR 1024   // up to this many entries: nmsMax tests every pair, spread over the block
+// nmsMax's "first earlier overlapping point": every (i < j) pair spread over
+// the block (LM_NMS_PAIRPAR entries or fewer), or each j scanning its earlier
+// points until its first hit.  All pairs balance a block's threads but test
+// ~3x the pairs; with four blocks per CU that VALU time is taken from the
+// other blocks and the correlation: the early-exit scan is 1-2 % more
+// frames/s with four contexts (profiles/r04/nms/sweep.txt), so it is used.
+#ifndef LM_NMS_PAIRPAR
+#define LM_NMS_PAIRPAR 0
+#endif
+#ifndef LM_NMS_BRANCHLESS
+#define LM_NMS_BRANCHLESS 1   // overlap test without branches (a zero factor when the rects do not intersect)
+#endif
 
 DEV float key_score(unsigned long long k) { return __uint_as_float(~(unsigned)(k >> 32)); }
 DEV unsigned key_lo(unsigned long long k) { return (unsigned)(k & 0xFFFFFFFFu); }
@@ -986,8 +997,13 @@ struct ReplicaLess {  // compareCandidate on (idx << 32 | score bits) words
 DEV bool overlaps_xy(unsigned a, unsigned b, int bw, int bh) {
   const int dx = abs((int)(a & 0xFFFFu) - (int)(b & 0xFFFFu));
   const int dy = abs((int)(a >> 16) - (int)(b >> 16));
-  if (dx >= bw || dy >= bh) return false;  // R.area() == 0
-  return 3 * (bw - dx) * (bh - dy) > 2 * bw * bh;
+  if constexpr (LM_NMS_BRANCHLESS) {
+    // no intersection (dx >= bw or dy >= bh) makes a factor 0: 0 > 2wh is false
+    return 3 * max(bw - dx, 0) * max(bh - dy, 0) > 2 * bw * bh;
+  } else {
+    if (dx >= bw || dy >= bh) return false;  // R.area() == 0
+    return 3 * (bw - dx) * (bh - dy) > 2 * bw * bh;
+  }
 }
 
 // std::sort(compareCandidate) replica in level order (lm_introsort.h
@@ -1069,7 +1085,10 @@ DEV int wave_partition(unsigned long long* a, int F, int L, int* tf, int* tr) {
   return cut;
 }
 
-DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int* leaf, int* tf, int* tr, int* s_cnt) {
+// prof (LM_KPROF=1, else null): [0] clock at the end of the partition levels,
+// [1] the number of levels
+DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int* leaf, int* tf, int* tr, int* s_cnt,
+                             long long* prof = nullptr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int i = threadIdx.x; i < n; i += blockDim.x) leaf[i] = 0;
   if (threadIdx.x == 0) {
@@ -1113,7 +1132,9 @@ DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int
     if (threadIdx.x == 0) s_cnt[sel] = 0;
     sel = 1 - sel;
     __syncthreads();
+    if (prof && threadIdx.x == 0) ++prof[1];
   }
+  if (prof && threadIdx.x == 0) prof[0] = clock64();
   // final insertion sort == stable sort of each leaf (<= 16 elements)
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     if (leaf[i] != 1) continue;
@@ -1261,7 +1282,8 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
         bitonic_sort(a, np);
       }
       NMS_PROF(9)
-      std_sort_levels_dev(a, n, s_mlist, qcap, s_assign, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt);
+      std_sort_levels_dev(a, n, s_mlist, qcap, s_assign, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt,
+                          prof ? prof + (blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 11 : nullptr);
       NMS_PROF(10)
     } else {  // rare and slow: one thread, explicit stack
       for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;

@@ -990,7 +990,8 @@ void kprof_report(lm_ctx* c, Lane& L, int n) {
       for (size_t i = 0; i < lv.size() && i < 6; ++i) {
         const long long* t = h.data() + (size_t)side * 16 * 2 * c->nslots + (size_t)lv[i].second * 16;
         fprintf(stderr, " [blk %d n=%lld %.1fus cyc=%lld:", lv[i].second, t[13], lv[i].first * 0.01, t[7] - t[0]);
-        for (int k = 1; k <= 10; ++k) fprintf(stderr, " %lld", t[k] ? t[k] - t[0] : -1);
+        for (int k = 1; k <= 11; ++k) fprintf(stderr, " %lld", t[k] ? t[k] - t[0] : -1);
+        fprintf(stderr, " levels %lld", t[12]);
         fprintf(stderr, "]");
       }
       fprintf(stderr, "\n");
