@@ -1017,9 +1017,13 @@ DEV bool overlaps_xy(unsigned a, unsigned b, int bw, int bh) {
 //    swaps a[f_k] <-> a[l_k] for k < K, K = first k with f_k >= l_k, and
 //    returns min(f_K, l_{K-1}) (f_0 when K = 0);
 //  * depth 0: heap sort by lane 0 (libstdc++'s fallback; never seen here);
-//  * leaves (<= 16 elements): the final insertion sort is a stable sort of
-//    each leaf, done in registers by one thread per leaf.
-// q: two queues of qcap (first, last, depth); leaf: n flags; tf, tr: n ints.
+//  * ranges of <= 64 elements: their whole subtree, leaves' insertion sorts
+//    included, in one wave's registers (wave_subtree).  Partitioned level
+//    by level down to the 16-element leaves, every level took ~5k cycles,
+//    latency-bound (the LDS lists, three wave syncs, the level's two block
+//    barriers), and a leaf phase another ~15k: ~64k cycles for a
+//    350-element tie list (profiles/r04/nms/kprof_tie_levels.txt).
+// q: two queues of qcap (first, last, depth); tf, tr: n ints.
 // Lanes of one wave exchanging data through memory.  k_nms reaches its
 // arrays through generic pointers (LDS, or global scratch for long lists), so
 // the accesses are FLAT instructions, which complete out of order: a
@@ -1085,12 +1089,129 @@ DEV int wave_partition(unsigned long long* a, int F, int L, int* tf, int* tr) {
   return cut;
 }
 
-// prof (LM_KPROF=1, else null): [0] clock at the end of the partition levels,
-// [1] the number of levels
-DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int* leaf, int* tf, int* tr, int* s_cnt,
+DEV unsigned long long readlane_u64(unsigned long long v, int l) {
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)v, l);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+  return ((unsigned long long)hi << 32) | lo;
+}
+DEV unsigned long long bpermute_u64(unsigned long long v, int src) {  // lane src's v
+  const unsigned lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)v);
+  const unsigned hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+DEV unsigned long long permute_u64(unsigned long long v, int dst) {  // v to lane dst (a permutation)
+  const unsigned lo = __builtin_amdgcn_ds_permute(dst << 2, (int)(unsigned)v);
+  const unsigned hi = __builtin_amdgcn_ds_permute(dst << 2, (int)(unsigned)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+// position of the k-th (0-based) set bit of m counting from bit 0 (m must
+// have more than k set bits)
+DEV int nth_set_bit(unsigned long long m, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const int c = __popcll((m >> pos) & ((1ull << w) - 1));
+    if (k >= c) {
+      k -= c;
+      pos += w;
+    }
+  }
+  return pos;
+}
+
+// One range [F, L) of <= 64 elements at depth d0, finished by one wave in
+// registers (element F + i in lane i): every partition of its introsort
+// subtree, then the final insertion sort of its leaves.  The ranges of the
+// subtree are disjoint and what happens to a range depends on its contents
+// and depth alone (lm_introsort.h, level-order formulation), so they are
+// taken one at a time, lowest first: `bnd` marks where the ranges start,
+// `pend` those of > kThreshold elements still to partition, lane s's `dep`
+// the depth of the range starting at s.  A partition is wave_partition's
+// (median of three to the front, then the k-th !(a < pivot) element from the
+// left swapped with the k-th !(pivot < a) from the right while the first is
+// left of the second) on ballots instead of LDS lists; a leaf's insertion
+// sort is its stable sort (each element's place: the leaf's elements that
+// compare before it, and the equal ones left of it).  No LDS round trip and
+// no barrier except on the depth-0 heap-sort fallback.
+DEV void wave_subtree(unsigned long long* a, int F, int L, int d0) {
+  const ReplicaLess comp;
+  constexpr int TH = lm_sort::kThreshold;
+  const int lane = threadIdx.x & 63;
+  const int m = L - F;
+  unsigned long long v = lane < m ? a[F + lane] : 0ull;
+  unsigned long long bnd = 1ull, pend = m > TH ? 1ull : 0ull;
+  int dep = d0;
+  const unsigned long long below = (1ull << lane) - 1;
+  while (pend) {
+    const int s = __builtin_ctzll(pend);  // s + TH < m <= 64
+    pend &= pend - 1;
+    const unsigned long long after = bnd & ~((2ull << s) - 1);
+    const int e = after ? __builtin_ctzll(after) : m;
+    const int d = __builtin_amdgcn_readlane(dep, s);
+    if (d == 0) {  // depth limit: libstdc++'s heap sort, by lane 0 (never seen here)
+      if (lane < m) a[F + lane] = v;
+      wave_sync();
+      if (lane == 0) lm_sort::partial_sort_full(a + F + s, a + F + e, comp);
+      wave_sync();
+      v = lane < m ? a[F + lane] : 0ull;
+      continue;  // sorted: its leaf sort below leaves it as it is
+    }
+    // move_median_to_first(s, s + 1, mid, e - 1)
+    const int mid = s + (e - s) / 2;
+    const unsigned long long x = readlane_u64(v, s + 1), y = readlane_u64(v, mid), z = readlane_u64(v, e - 1);
+    int ch;
+    if (comp(x, y)) ch = comp(y, z) ? mid : comp(x, z) ? e - 1 : s + 1;
+    else ch = comp(x, z) ? s + 1 : comp(y, z) ? e - 1 : mid;
+    const unsigned long long vs = readlane_u64(v, s), pv = readlane_u64(v, ch);
+    if (lane == s) v = pv;
+    if (lane == ch) v = vs;
+    const bool in = lane > s && lane < e;
+    const bool lf = in && !comp(v, pv), rf = in && !comp(pv, v);
+    const unsigned long long ml = __ballot(lf), mr = __ballot(rf);
+    const int nl = __popcll(ml), nr = __popcll(mr);
+    const int fk = nth_set_bit(ml, lane);           // f_k, k = lane (lane < nl)
+    const int lk = nth_set_bit(mr, nr - 1 - lane);  // l_k, k = lane (lane < nr)
+    const int K = __popcll(__ballot(lane < nl && lane < nr && fk < lk));
+    int cut;
+    if (K == 0) {
+      cut = __builtin_amdgcn_readlane(fk, 0);
+    } else {
+      cut = __builtin_amdgcn_readlane(lk, K - 1);
+      if (K < nl) cut = min(cut, __builtin_amdgcn_readlane(fk, K));
+    }
+    // swap a[f_k] <-> a[l_k], k < K (no element is both an f_k and an l_k)
+    const int rl = __popcll(ml & below), rr = __popcll(mr >> lane) - 1;
+    const int from_l = __shfl(lk, rl), from_r = __shfl(fk, rr & 63);
+    const int src = (lf && rl < K) ? from_l : (rf && rr < K) ? from_r : lane;
+    v = bpermute_u64(v, src);
+    if (lane == s || (lane == cut && cut < e)) dep = d - 1;
+    if (cut < e) bnd |= 1ull << cut;
+    if (cut - s > TH) pend |= 1ull << s;
+    if (e - cut > TH) pend |= 1ull << cut;
+  }
+  // leaves: stable sort of each (a heap-sorted range keeps its order)
+  const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1;
+  const int ls = 63 - __builtin_clzll(bnd & upto);
+  const unsigned long long aft = bnd & ~upto;
+  const int le = aft ? __builtin_ctzll(aft) : m;
+  const float sc = __uint_as_float((unsigned)v);
+  int rk = 0;
+#pragma unroll
+  for (int j = 0; j < TH; ++j) {
+    const int i = ls + j;
+    const float sj = __shfl(sc, i & 63);
+    if (i < le) rk += (sj > sc) || (i < lane && !(sc > sj));
+  }
+  const int dst = lane >= m ? lane : le - ls <= TH ? ls + rk : lane;
+  v = permute_u64(v, dst);
+  if (lane < m) a[F + lane] = v;
+}
+
+// prof (LM_KPROF=1, else null): [0] clock at the end of the levels, [1] the
+// number of levels
+DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int* tf, int* tr, int* s_cnt,
                              long long* prof = nullptr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) leaf[i] = 0;
   if (threadIdx.x == 0) {
     q[0] = 0;
     q[1] = n;
@@ -1107,13 +1228,10 @@ DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int
     int* nxt = q + (1 - sel) * 3 * qcap;
     for (int r = wid; r < qn; r += nw) {
       const int f = cur[3 * r], l = cur[3 * r + 1], d = cur[3 * r + 2];
-      if (l - f <= lm_sort::kThreshold) {
-        if (lane == 0) leaf[f] = 1;
+      if (l - f <= 64) {
+        wave_subtree(a, f, l, d);  // the whole subtree and its leaves' insertion sorts
       } else if (d == 0) {
-        if (lane == 0) {
-          lm_sort::partial_sort_full(a + f, a + l, ReplicaLess());
-          leaf[f] = 2;  // sorted; its insertion sort is a no-op
-        }
+        if (lane == 0) lm_sort::partial_sort_full(a + f, a + l, ReplicaLess());  // sorted: a leaf
       } else {
         const int cut = wave_partition(a, f, l, tf, tr);
         if (lane == 0) {
@@ -1135,30 +1253,6 @@ DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int
     if (prof && threadIdx.x == 0) ++prof[1];
   }
   if (prof && threadIdx.x == 0) prof[0] = clock64();
-  // final insertion sort == stable sort of each leaf (<= 16 elements)
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    if (leaf[i] != 1) continue;
-    int e = i + 1;
-    while (e < n && e - i < lm_sort::kThreshold && !leaf[e]) ++e;
-    const int m = e - i;
-    unsigned long long v[lm_sort::kThreshold];
-    float sc[lm_sort::kThreshold];
-#pragma unroll
-    for (int t = 0; t < lm_sort::kThreshold; ++t) {
-      v[t] = t < m ? a[i + t] : 0ull;
-      sc[t] = __uint_as_float((unsigned)(v[t] & 0xFFFFFFFFu));
-    }
-#pragma unroll
-    for (int t = 0; t < lm_sort::kThreshold; ++t) {
-      if (t >= m) break;
-      int r = 0;
-#pragma unroll
-      for (int u = 0; u < lm_sort::kThreshold; ++u)
-        if (u < m) r += (sc[u] > sc[t]) || (u < t && !(sc[t] > sc[u]));
-      a[i + r] = v[t];
-    }
-  }
-  __syncthreads();
 }
 
 // Enumerates the j in [0, n) with flag(j) in increasing order: out[r] = j.
@@ -1282,7 +1376,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
         bitonic_sort(a, np);
       }
       NMS_PROF(9)
-      std_sort_levels_dev(a, n, s_mlist, qcap, s_assign, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt,
+      std_sort_levels_dev(a, n, s_mlist, qcap, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt,
                           prof ? prof + (blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 11 : nullptr);
       NMS_PROF(10)
     } else {  // rare and slow: one thread, explicit stack
