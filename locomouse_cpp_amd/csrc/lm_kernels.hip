@@ -925,6 +925,7 @@ DEV void rank_sort(unsigned long long* a, unsigned long long* tmp, int n) {
     const unsigned long long key = a[k];
     int r = 0;
     int i = 0;
+#pragma unroll 1  // (unrolled further, the loads in flight spill at 64 VGPRs)
     for (; i + 8 <= n; i += 8) {  // 4 x 16 B loads in flight per iteration
       const ulonglong2 q0 = *reinterpret_cast<const ulonglong2*>(a + i);
       const ulonglong2 q1 = *reinterpret_cast<const ulonglong2*>(a + i + 2);
@@ -1207,44 +1208,139 @@ DEV void wave_subtree(unsigned long long* a, int F, int L, int d0) {
   if (lane < m) a[F + lane] = v;
 }
 
-// prof (LM_KPROF=1, else null): [0] clock at the end of the levels, [1] the
-// number of levels
-DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int* tf, int* tr, int* s_cnt,
-                             long long* prof = nullptr) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if (threadIdx.x == 0) {
-    q[0] = 0;
-    q[1] = n;
-    q[2] = 2 * lm_sort::lg_(n);
-    s_cnt[0] = n > 0 ? 1 : 0;
-    s_cnt[1] = 0;
+// wave_partition by the whole block: the stoppers' ranks come from per-wave
+// ballot counts (s_w: 2 nw + 1 ints), the swaps are spread over the block.
+DEV int block_partition(unsigned long long* a, int F, int L, int* tf, int* tr, int* s_w) {
+  const ReplicaLess comp;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, nw = blockDim.x >> 6;
+  if (t == 0) {
+    const int mid = F + (L - F) / 2;
+    lm_sort::move_median_to_first(a + F, a + F + 1, a + mid, a + L - 1, comp);
+    s_w[2 * nw] = 0;
   }
   __syncthreads();
+  const unsigned long long pv = a[F];
+  const int lo = F + 1, hi = L;
+  const unsigned long long below = (1ull << lane) - 1;
+  int nl = 0, nr = 0;
+  for (int b = lo; b < hi; b += blockDim.x) {
+    const int i = b + t;
+    bool lf = false, rf = false;
+    if (i < hi) {
+      const unsigned long long v = a[i];
+      lf = !comp(v, pv);
+      rf = !comp(pv, v);
+    }
+    const unsigned long long ml = __ballot(lf), mr = __ballot(rf);
+    if (lane == 0) {
+      s_w[wid] = __popcll(ml);
+      s_w[nw + wid] = __popcll(mr);
+    }
+    __syncthreads();
+    int bl = nl, br = nr, tl = 0, tr_ = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int cl = s_w[w], cr = s_w[nw + w];
+      if (w < wid) {
+        bl += cl;
+        br += cr;
+      }
+      tl += cl;
+      tr_ += cr;
+    }
+    if (lf) tf[lo + bl + __popcll(ml & below)] = i;
+    if (rf) tr[lo + br + __popcll(mr & below)] = i;
+    nl += tl;
+    nr += tr_;
+    __syncthreads();  // the lists are complete, s_w free again
+  }
+  const int kmax = min(nl, nr);
+  for (int k0 = 0; k0 < kmax; k0 += blockDim.x) {  // K: f_k < l_k holds for a prefix of k
+    const int k = k0 + t;
+    const unsigned long long m = __ballot(k < kmax && tf[lo + k] < tr[lo + nr - 1 - k]);
+    if (lane == 0 && m) atomicAdd(&s_w[2 * nw], __popcll(m));
+  }
+  __syncthreads();
+  const int K = s_w[2 * nw];
+  int cut;
+  if (K == 0) cut = tf[lo];
+  else cut = min(K < nl ? tf[lo + K] : 0x7fffffff, tr[lo + nr - K]);
+  for (int k = t; k < K; k += blockDim.x) {
+    const int i = tf[lo + k], j = tr[lo + nr - 1 - k];
+    const unsigned long long x = a[i], y = a[j];
+    a[i] = y;
+    a[j] = x;
+  }
+  __syncthreads();
+  return cut;
+}
+
+// Ranges of <= 64 elements go to a list (`small`, packed first | size << 11
+// | depth << 18) that the waves finish at the end with wave_subtree; the
+// others are partitioned level by level, by the whole block when a level
+// holds one range (the top levels, and the long chains of uneven partitions
+// that exact ties produce), else one wave per range.
+// prof (LM_KPROF=1, else null): [0] clock at the end of the levels, [1] the
+// number of levels
+DEV int small_range(int f, int l, int d) { return f | (l - f) << 11 | d << 18; }
+DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int* small, int* tf, int* tr,
+                             int* s_cnt, int* s_w, long long* prof = nullptr) {
+  static_assert(LM_NMS_CAP <= 2048, "small_range packs first in 11 bits");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int* s_small = s_w + 2 * nw + 1;
+  const ReplicaLess comp;
+  if (threadIdx.x == 0) {
+    const int d0 = 2 * lm_sort::lg_(n);
+    s_cnt[0] = n > 64 ? 1 : 0;
+    s_cnt[1] = 0;
+    *s_small = 0;
+    if (n > 64) {
+      q[0] = 0;
+      q[1] = n;
+      q[2] = d0;
+    } else if (n > 0) {
+      small[0] = small_range(0, n, d0);
+      *s_small = 1;
+    }
+  }
+  __syncthreads();
+  // children of a partitioned range: > 64 elements to the next level, the rest to `small`
+  auto push = [&](int* nxt, int sel, int f, int l, int d) {
+    if (l - f > 64) {
+      const int k = atomicAdd(&s_cnt[1 - sel], 1);
+      nxt[3 * k] = f;
+      nxt[3 * k + 1] = l;
+      nxt[3 * k + 2] = d;
+    } else if (l > f) {
+      small[atomicAdd(s_small, 1)] = small_range(f, l, d);
+    }
+  };
   int sel = 0;
   while (true) {
     const int qn = s_cnt[sel];
     if (qn == 0) break;
     const int* cur = q + sel * 3 * qcap;
     int* nxt = q + (1 - sel) * 3 * qcap;
-    for (int r = wid; r < qn; r += nw) {
-      const int f = cur[3 * r], l = cur[3 * r + 1], d = cur[3 * r + 2];
-      if (l - f <= 64) {
-        wave_subtree(a, f, l, d);  // the whole subtree and its leaves' insertion sorts
-      } else if (d == 0) {
-        if (lane == 0) lm_sort::partial_sort_full(a + f, a + l, ReplicaLess());  // sorted: a leaf
-      } else {
-        const int cut = wave_partition(a, f, l, tf, tr);
-        if (lane == 0) {
-          const int k = atomicAdd(&s_cnt[1 - sel], 2);
-          nxt[3 * k] = f;
-          nxt[3 * k + 1] = cut;
-          nxt[3 * k + 2] = d - 1;
-          nxt[3 * k + 3] = cut;
-          nxt[3 * k + 4] = l;
-          nxt[3 * k + 5] = d - 1;
-        }
+    if (qn == 1 && cur[2] > 0) {
+      const int f = cur[0], l = cur[1], d = cur[2];
+      const int cut = block_partition(a, f, l, tf, tr, s_w);
+      if (threadIdx.x == 0) {
+        push(nxt, sel, f, cut, d - 1);
+        push(nxt, sel, cut, l, d - 1);
       }
-      wave_sync();
+    } else {
+      for (int r = wid; r < qn; r += nw) {
+        const int f = cur[3 * r], l = cur[3 * r + 1], d = cur[3 * r + 2];
+        if (d == 0) {
+          if (lane == 0) lm_sort::partial_sort_full(a + f, a + l, comp);  // sorted: a leaf
+        } else {
+          const int cut = wave_partition(a, f, l, tf, tr);
+          if (lane == 0) {
+            push(nxt, sel, f, cut, d - 1);
+            push(nxt, sel, cut, l, d - 1);
+          }
+        }
+        wave_sync();
+      }
     }
     __syncthreads();
     if (threadIdx.x == 0) s_cnt[sel] = 0;
@@ -1253,6 +1349,13 @@ DEV void std_sort_levels_dev(unsigned long long* a, int n, int* q, int qcap, int
     if (prof && threadIdx.x == 0) ++prof[1];
   }
   if (prof && threadIdx.x == 0) prof[0] = clock64();
+  const int ns = *s_small;
+  for (int r = wid; r < ns; r += nw) {  // the whole subtree and its leaves' insertion sorts
+    const int e = small[r];
+    const int f = e & 0x7FF;
+    wave_subtree(a, f, f + ((e >> 11) & 0x7F), e >> 18);
+  }
+  __syncthreads();
 }
 
 // Enumerates the j in [0, n) with flag(j) in increasing order: out[r] = j.
@@ -1307,7 +1410,8 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
                  const unsigned long long* __restrict__ src, const unsigned long long* __restrict__ tailmask,
                  unsigned long long* a, int* assign, int* mlist, unsigned* xy, int* s_tmp, unsigned long long* stmp,
                  int qcap, int* s_stk, int* s_wsum,
-                 int* s_n_, int* s_flag_, int* s_qcnt, unsigned long long* __restrict__ keys, int32_t* __restrict__ err,
+                 int* s_n_, int* s_flag_, int* s_qcnt, int* s_part, unsigned long long* __restrict__ keys,
+                 int32_t* __restrict__ err,
                  long long* __restrict__ prof) -> int {
   int& s_n = *s_n_;
   int& s_flag = *s_flag_;
@@ -1376,7 +1480,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
         bitonic_sort(a, np);
       }
       NMS_PROF(9)
-      std_sort_levels_dev(a, n, s_mlist, qcap, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt,
+      std_sort_levels_dev(a, n, s_mlist, qcap, s_assign, reinterpret_cast<int*>(s_xy), s_tmp, s_qcnt, s_part,
                           prof ? prof + (blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 11 : nullptr);
       NMS_PROF(10)
     } else {  // rare and slow: one thread, explicit stack
@@ -1605,6 +1709,7 @@ DEV void nms_block(int bx, int list, const LmConst* __restrict__ Kp, int s0, uns
   __shared__ int s_stk[GLOB ? lm_sort::kStackInts : 1];
   __shared__ int s_wsum[LM_NMS_THREADS / 64 + 1];
   __shared__ int s_n, s_flag, s_qcnt[2];
+  __shared__ int s_part[2 * (LM_NMS_THREADS / 64) + 2];  // block_partition's counts + the small-range count
   static_assert(LM_NMS_RANKSORT * 8 <= LM_NMS_CAP * 4, "s_assign holds the sorts' keys");
   const int64_t npg = gscratch_slot / 3;
   // <true>: the launch's block b works its pairs one after another in scratch region b
@@ -1642,12 +1747,12 @@ DEV void nms_block(int bx, int list, const LmConst* __restrict__ Kp, int s0, uns
   const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[list];
   if constexpr (!GLOB)
     nms_run<false>(K, D, H, slot, list, side, feat, n_in, src, tailmask, s_keys, s_assign, s_mlist, s_xy, s_tmp,
-                   reinterpret_cast<unsigned long long*>(s_assign), LM_NMS_CAP / 6, s_stk, s_wsum, &s_n, &s_flag, s_qcnt,
+                   reinterpret_cast<unsigned long long*>(s_assign), LM_NMS_CAP / 6, s_stk, s_wsum, &s_n, &s_flag, s_qcnt, s_part,
                    keys, err, prof);
   else
     nms_run<true>(K, D, H, slot, list, side, feat, n_in, src, tailmask, ga, gassign, gmlist,
                   reinterpret_cast<unsigned*>(gmlist + npg), s_tmp, reinterpret_cast<unsigned long long*>(gassign), 0,
-                  s_stk, s_wsum, &s_n, &s_flag, s_qcnt, keys, err, prof);
+                  s_stk, s_wsum, &s_n, &s_flag, s_qcnt, s_part, keys, err, prof);
 }
 
 // For the <true> (global-scratch) instantiations of k_nms / k_post: a small

@@ -90,18 +90,21 @@ static void emu_wave_subtree(T* a, int m, int d0, Less comp) {
 template <class T, class Less>
 static void emu_device_sort(T* a, int n, Less comp, int depth0 = -1) {
   if (n <= 0) return;
-  std::vector<int> cur = {0, n, depth0 >= 0 ? depth0 : 2 * lm_sort::lg_(n)}, nxt;
+  // ranges of <= 64 elements are finished after the levels, in reverse order
+  // (any order gives the same result: the ranges are disjoint)
+  std::vector<int> cur = {0, n, depth0 >= 0 ? depth0 : 2 * lm_sort::lg_(n)}, nxt, small;
   while (!cur.empty()) {
     nxt.clear();
     for (size_t r = 0; r < cur.size(); r += 3) {
       const int f = cur[r], l = cur[r + 1], d = cur[r + 2];
       int cut = 0;
-      if (l - f <= 64) emu_wave_subtree(a + f, l - f, d, comp);
+      if (l - f <= 64) small.insert(small.end(), {f, l, d});
       else if (d == 0) lm_sort::partial_sort_full(a + f, a + l, comp);
       else if (lm_sort::process_range(a, f, l, d, comp, &cut)) nxt.insert(nxt.end(), {f, cut, d - 1, cut, l, d - 1});
     }
     cur.swap(nxt);
   }
+  for (size_t r = small.size(); r >= 3; r -= 3) emu_wave_subtree(a + small[r - 3], small[r - 2] - small[r - 3], small[r - 1], comp);
 }
 
 int main() {
