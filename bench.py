@@ -372,6 +372,9 @@ def main():
     ap.add_argument("--video-frames", type=int, default=0,
                     help="strong scaling (BASELINE config 4): one video of this many frames sharded over the ranks; "
                          "steps = timed passes over the shard")
+    ap.add_argument("--host-frames", action="store_true",
+                    help="frames in pinned host memory, submitted with the host API (lm_detect_batch / "
+                         "lm_detect_submit): the H2D copy is inside the timed loop (BASELINE.md §2's end-to-end figure)")
     ap.add_argument("--oversubscribe", action="store_true",
                     help="allow more ranks on a node than it has GPUs (rehearsals only: ranks share devices)")
     ap.add_argument("--check-all-ranks", action="store_true",
@@ -528,6 +531,12 @@ def run_stream(args, world, rank, device):
         # index 0 holds frame vbase-1 (the halo), index i frame vbase+i-1
         synth_frames_device(frames[k].data_ptr(), rows, cols, vbase[k] - 1, R + 1, FRAME_BYTES, device=device)
     torch.cuda.synchronize()
+    if args.host_frames:  # the same frames in page-locked host memory; the device copy is freed
+        hframes = torch.empty(frames.shape, dtype=torch.uint8, pin_memory=True)
+        hframes.copy_(frames)
+        del frames
+        torch.cuda.empty_cache()
+        frames = hframes
 
     state = [{"frame": vbase[k]} for k in range(NS)]
     kernel_ms, spans, executed = {}, {}, []
@@ -556,14 +565,21 @@ def run_stream(args, world, rank, device):
             # stream start (vbase > 0) or wrap-around: pass the previous frame
             halo = frames[k].data_ptr() + (0 if f == vbase[k] else R * FRAME_BYTES)
         c = ctxs[k]
+        ptr = frames[k].data_ptr() + i * FRAME_BYTES
         if NL == 1:
-            res = c.detect_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)
+            if args.host_frames:
+                res = c.detect_host_ptr(ptr, FRAME_BYTES, B, f, h_prev_ptr=halo)
+            else:
+                res = c.detect_device(ptr, FRAME_BYTES, B, f, d_prev_ptr=halo)
             st["last"] = res
             record(k, timing, res, None)
         else:  # pipelined: keep every lane busy (finished lanes are reused), collect in submission order
             if c.pending() == 2 * NL:
                 record(k, timing, c.collect(raw=True), None)
-            c.submit_device(frames[k].data_ptr() + i * FRAME_BYTES, FRAME_BYTES, B, f, d_prev_ptr=halo)
+            if args.host_frames:
+                c.submit_host_ptr(ptr, FRAME_BYTES, B, f, h_prev_ptr=halo)
+            else:
+                c.submit_device(ptr, FRAME_BYTES, B, f, d_prev_ptr=halo)
         st["frame"] = f + B
 
     def drain(k, timing):
@@ -635,8 +651,10 @@ def run_stream(args, world, rank, device):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f16xf16->f32 (non-parity LM_CORR_F16)" if f16 else "f32",
-        "data": "synthetic (lm_synth.h scene, resident in HBM)",
-        "config": {"workload": workload,
+        "data": ("synthetic (lm_synth.h scene, in pinned host memory: H2D inside the timed loop)" if args.host_frames
+                 else "synthetic (lm_synth.h scene, resident in HBM)"),
+        "config": {"workload": workload + ("; frames from pinned host memory through the host API "
+                                           "(lm_detect_batch / lm_detect_submit, H2D included)" if args.host_frames else ""),
                    "batch_frames": B, "streams_per_gpu": NS, "frames_per_rank": args.steps * B * NS,
                    "lanes_per_context": NL, "resident_frames_per_stream": R,
                    "stream_priorities": "alternating high/low" if os.environ.get("LM_STREAM_PRIO", "1") != "0" else "equal",
@@ -645,6 +663,7 @@ def run_stream(args, world, rank, device):
                    "dark_tiles": "skipped" if os.environ.get("LM_CORR_DARK", "1") != "0" else "computed",
                    "parallelism": f"frame shards x{world} (no collective)"},
         "hbm_gbs": round(fps * FRAME_BYTES / 1e9, 3),
+        **({"h2d_gbs": round(fps * FRAME_BYTES / 1e9, 3)} if args.host_frames else {}),
         "roofline": _roofline(ctx, f16, args.config, spans, executed, B),
         "kernel_avg_ms": {k: round(sum(v) / len(v), 5) for k, v in kernel_ms.items()},
         "kernel_busy_ms_per_batch": {k: round(union_ms(v) / len(v), 5) for k, v in spans.items()},
@@ -724,6 +743,16 @@ def video_shards(n_frames, world, rank, streams):
     return subs
 
 
+def piece_batches(n, max_batch):
+    """Batch sizes for a piece of n frames: the fewest batches of at most
+    max_batch frames, as equal as possible (larger ones first)."""
+    if n <= 0:
+        return []
+    nb = -(-n // max_batch)
+    q, r = divmod(n, nb)
+    return [q + 1] * r + [q] * (nb - r)
+
+
 def check_video(parts, n_frames):
     """Rank 0: the gathered (first frame, result dict) pieces of the whole
     video, sorted; raises unless they cover frames [0, n_frames) exactly
@@ -758,9 +787,13 @@ def run_video(args, world, rank, device):
 
     cfg, rows, cols, workload, f16 = _setup(args, device)
     N = args.video_frames
-    B = args.batch
     NL = max(1, args.lanes)
     subs = video_shards(N, world, rank, max(1, args.streams))
+    # each context's piece in equal batches of at most --batch frames (a
+    # 313-frame piece is 2 x 157, not 256 + a ragged 57 whose kernels run
+    # at a fraction of the device), one context per piece
+    cuts = [piece_batches(hi - lo, args.batch) for lo, hi in subs]
+    B = max(max(c) for c in cuts)
     FRAME_BYTES = rows * cols
     ctxs = [Context(cfg, max_batch=B, device=device, lanes=NL) for _ in subs]
     # piece k: device frames [lo - 1, hi) (index 0 = the halo frame lo - 1; unused when lo = 0)
@@ -791,8 +824,8 @@ def run_video(args, world, rank, device):
                 executed.append(executed_flops(c, c.corr_work(), c.batch_slots()))
             got.append(result_to_numpy(res))
 
-        for b0 in range(lo, hi, B):
-            n = min(B, hi - b0)
+        b0 = lo
+        for n in cuts[k]:
             ptr = base + (b0 - lo + 1) * FRAME_BYTES
             halo = base if (b0 == lo and lo > 0) else None
             if NL == 1:
@@ -801,6 +834,7 @@ def run_video(args, world, rank, device):
                 if c.pending() == 2 * NL:
                     take(c.collect(raw=True))
                 c.submit_device(ptr, FRAME_BYTES, n, b0, d_prev_ptr=halo)
+            b0 += n
         while c.pending():
             take(c.collect(raw=True))
         results[k] = got
@@ -856,7 +890,8 @@ def run_video(args, world, rank, device):
         "data": "synthetic (lm_synth.h scene, resident in HBM)",
         "config": {"workload": f"C4: one {N}-frame video sharded over {world} GPU(s) as contiguous frame ranges "
                                f"with a 1-frame halo (no collective); " + workload,
-                   "video_frames": N, "batch_frames": B, "contexts_per_gpu": len(subs), "lanes_per_context": NL,
+                   "video_frames": N, "batch_frames": B, "batches": [len(c) for c in cuts],
+                   "contexts_per_gpu": len(subs), "lanes_per_context": NL,
                    "step": "one pass over the whole video (every rank's shard, pipeline fill included, results "
                            "copied to host arrays)",
                    "shards": [list(s) for s in subs] if world == 1 else f"{world} x ceil({N}/{world}) frames",

@@ -159,7 +159,8 @@ struct LmSlotOut {
   int32_t pw_jc_off[LM_NFEAT], pw_nz_off[LM_NFEAT];
   int32_t tail[45];
   int32_t ties[LM_NLIST];        // 1 when the exact-tie std::sort replica ran
-  int32_t pad_[3];
+  int32_t bottom_kept[LM_NFEAT]; // k_tail: some bottom key of the feature survives TAIL_MASK (k_nms' side skip)
+  int32_t pad_[1];
 };
 
 // arena counters (device -> host)

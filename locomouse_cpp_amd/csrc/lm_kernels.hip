@@ -545,6 +545,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
 #include "lm_cc.h"
 
 // ------------------------------------------------------------------ k_tail
+// keys of positive scores: (~float_bits(score) << 32) | row-major output index
+DEV float key_score(unsigned long long k) { return __uint_as_float(~(unsigned)(k >> 32)); }
+DEV unsigned key_lo(unsigned long long k) { return (unsigned)(k & 0xFFFFFFFFu); }
 // detectTail (:2541-2555) -> detectLineCandidates (:2558-2742), one
 // workgroup per frame:
 //   bottom: largest component of (tail_b > 0) (selectLargestRegion :2604,
@@ -692,7 +695,8 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
                                                           unsigned long long* __restrict__ tailmask,
                                                           unsigned* __restrict__ scratch, LmSlotOut* __restrict__ hdr,
                                                           long long* __restrict__ prof, uint8_t* __restrict__ ws,
-                                                          int64_t ws_slot) {
+                                                          int64_t ws_slot, const unsigned long long* __restrict__ keys,
+                                                          const int32_t* __restrict__ n_pos) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smt_lds[];
 #define TAIL_PROF(k) \
   if (prof && threadIdx.x == 0) prof[blockIdx.x * 16 + (k)] = clock64();
@@ -781,6 +785,24 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
   TAIL_PROF(4)
   unsigned long long* __restrict__ tm = tailmask + (int64_t)slot * HB * nb64;
   for (int i = tid; i < HB * nb64; i += nt) tm[i] = mask[i];
+  // detectSideCandidates runs only when the bottom list of the feature is
+  // non-empty after the TAIL_MASK filter (:820-833).  Decided here, from the
+  // keys before k_nms stages any candidate over them: in k_nms the bottom
+  // block of a (slot, feature) overwrites its own keys while the side block
+  // would be reading them.
+  for (int feat = 0; feat < LM_NFEAT; ++feat) {
+    const LmDet& D = K.det[feat == 0 ? DET_PAW_B : DET_SNOUT_B];
+    const unsigned long long* __restrict__ src = keys + (int64_t)slot * K.keys_per_slot + K.list_off[feat];
+    const int n = n_pos[slot * LM_NLIST + feat];
+    int keep = 0;
+    for (int k = tid; k < n && !keep; k += nt) {
+      const unsigned idx = key_lo(src[k]);
+      const int y = idx / D.ow, x = idx - y * D.ow;
+      keep = !(x < TW && y < HB && ((mask[y * nb64 + (x >> 6)] >> (x & 63)) & 1));
+    }
+    keep = __syncthreads_or(keep);
+    if (tid == 0) hdr[slot].bottom_kept[feat] = keep != 0;
+  }
 
   // ---- side: (tail_s > 0) & repeat(colmax) -> largest component
   cc_bitmap_bits(bins, HS, nb64, colm, bm, rowoff);
@@ -894,8 +916,6 @@ __global__ __launch_bounds__(LM_TAIL_THREADS) void k_tail(const LmConst* __restr
 #define LM_NMS_BRANCHLESS 1   // overlap test without branches (a zero factor when the rects do not intersect)
 #endif
 
-DEV float key_score(unsigned long long k) { return __uint_as_float(~(unsigned)(k >> 32)); }
-DEV unsigned key_lo(unsigned long long k) { return (unsigned)(k & 0xFFFFFFFFu); }
 
 // in-place ascending bitonic sort of a[0..np), np a power of two, block-wide
 DEV void bitonic_sort(unsigned long long* a, int np) {
@@ -1671,24 +1691,14 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
 // One block per (slot, list): nmsMax for the bottom lists, peakClustering
 // for the side lists.  detectSideCandidates runs only when the frame's
 // bottom candidate list for the feature is non-empty (:820-833); nmsMax makes
-// at least one candidate from any non-empty point list, so a side block
-// decides that itself -- is any bottom key left after the TAIL_MASK filter --
-// and does not wait for the bottom block.  <false>: lists of at most
-// LM_NMS_CAP positives, in LDS.  <true>: the longer lists, in global scratch
-// (for_overflow_pairs, launched after <false>).
-// Some bottom key of (slot, feature) survives the TAIL_MASK filter (block-wide).
-DEV bool bottom_nonempty(const LmConst& K, const LmDet& D, const unsigned long long* __restrict__ src, int n,
-                         const unsigned long long* __restrict__ tailmask, int slot) {
-  const int tnb = (K.tail_w + 63) / 64;
-  const unsigned long long* __restrict__ tm = tailmask + (int64_t)slot * K.tail_hb * tnb;
-  int keep = 0;
-  for (int k = threadIdx.x; k < n && !keep; k += blockDim.x) {
-    const unsigned idx = key_lo(src[k]);
-    const int y = idx / D.ow, x = idx - y * D.ow;
-    keep = !(x < K.tail_w && y < K.tail_hb && ((tm[y * tnb + (x >> 6)] >> (x & 63)) & 1));
-  }
-  return __syncthreads_or(keep) != 0;
-}
+// at least one candidate from any non-empty point list, so "is any bottom
+// key left after the TAIL_MASK filter" decides it.  k_tail records that per
+// (slot, feature) in the slot header (LmSlotOut::bottom_kept) before k_nms
+// runs, so a side block neither waits for the bottom block nor reads the
+// bottom keys the bottom block overwrites with its staged candidates.
+// <false>: lists of at most LM_NMS_CAP positives, in LDS.  <true>: the
+// longer lists, in global scratch (for_overflow_pairs, launched after
+// <false>).
 
 template <bool GLOB>
 DEV void nms_block(int bx, int list, const LmConst* __restrict__ Kp, int s0, unsigned long long* __restrict__ keys,
@@ -1730,9 +1740,7 @@ DEV void nms_block(int bx, int list, const LmConst* __restrict__ Kp, int s0, uns
   const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
   const LmDet D = K.det[det];
   if (side) {
-    const int bdet = feat == 0 ? DET_PAW_B : DET_SNOUT_B;
-    const unsigned long long* __restrict__ bsrc = keys + (int64_t)slot * K.keys_per_slot + K.list_off[feat];
-    if (!bottom_nonempty(K, K.det[bdet], bsrc, n_pos[slot * LM_NLIST + feat], tailmask, slot)) {
+    if (!H->bottom_kept[feat]) {  // set by k_tail from the keys before any block stages candidates over them
       if (threadIdx.x == 0) {  // detectSideCandidates not run: an empty side list
         H->n_pos[list] = 0;
         H->cand_cnt[list] = 0;

@@ -1110,10 +1110,12 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
     if (LM_EXP_SKIP & 2) {
     } else if (c->tail_big)
       k_tail<true><<<nproc, LM_TAIL_THREADS, 0, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes, L.tailmask.p,
-                                                      L.tscratch.p, A.hdr.p, kp2, L.tail_ws.p, c->tail_ws_slot);
+                                                      L.tscratch.p, A.hdr.p, kp2, L.tail_ws.p, c->tail_ws_slot,
+                                                      L.keys.p, L.npos.p);
     else
       k_tail<false><<<nproc, LM_TAIL_THREADS, c->tail_lds, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes,
-                                                                 L.tailmask.p, L.tscratch.p, A.hdr.p, kp2, nullptr, 0);
+                                                                 L.tailmask.p, L.tscratch.p, A.hdr.p, kp2, nullptr, 0,
+                                                                 L.keys.p, L.npos.p);
     T.end();
     T.begin("k_nms");
     // one block per (slot, list); lists beyond the LDS capacity in global scratch
@@ -1428,12 +1430,16 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   P.pack = c->take_pack((size_t)L.arena[P.cur].pack_cap);
   try {
     launch_attempt(c, L, 0);
+    HIPCHK(hipEventRecord(L.ev_done, st));
   } catch (...) {
+    // kernels of this batch may already be enqueued: the lane (and the pack
+    // k_out writes into) is free only once its stream has drained
+    (void)hipStreamSynchronize(st);
+    (void)hipGetLastError();
     c->drop_pack(P.pack);
     P.on = false;
     throw;
   }
-  HIPCHK(hipEventRecord(L.ev_done, st));
 
   // the video position and the lane's carry state advance now; a batch that
   // fails at collection clears the lane's state (a later batch on another

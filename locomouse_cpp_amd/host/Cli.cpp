@@ -321,6 +321,25 @@ int run(int argc, char** argv) {
   li.rewind = [reader] { reader->rewind(); };
   li.output_file = in.OUTPUT_PATH + "/output_" + in.FILE_STEM + ".yml";
   if (const char* d = std::getenv("LM_DEVICE")) li.device = std::atoi(d);
+  // LM_DEVICES=0,1,...: detection sharded over these GPUs (LocoMouse_Inputs::devices);
+  // LM_OVERSUBSCRIBE=1 lets a device appear more than once (rehearsals on fewer GPUs)
+  if (const char* ds = std::getenv("LM_DEVICES")) {
+    std::stringstream ss(ds);
+    std::string tok;
+    while (std::getline(ss, tok, ','))
+      if (!tok.empty()) {
+        size_t used = 0;
+        int d = -1;
+        try {
+          d = std::stoi(tok, &used);
+        } catch (const std::exception&) {
+          used = 0;
+        }
+        if (used != tok.size()) throw std::invalid_argument("LM_DEVICES: not a device index: " + tok);
+        li.devices.push_back(d);
+      }
+  }
+  if (const char* o = std::getenv("LM_OVERSUBSCRIBE")) li.oversubscribe = std::atoi(o) != 0;
   if (const char* b = std::getenv("LM_BATCH")) li.batch = std::max(1, std::atoi(b));
   if (const char* l = std::getenv("LM_LANES")) li.lanes = std::max(1, std::atoi(l));
   if (std::getenv("LM_PRINT_INPUTS")) {  // diagnostics: the parsed inputs, nothing run on the GPU

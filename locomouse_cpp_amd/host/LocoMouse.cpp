@@ -4,9 +4,13 @@
 #include "LocoMouse.hpp"
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
 #include <iostream>
+#include <mutex>
+#include <set>
 #include <stdexcept>
+#include <thread>
 
 namespace locomouse {
 
@@ -135,6 +139,173 @@ void throw_on_error(lm_status s) {
   throw std::runtime_error(lm_last_error());
 }
 
+// ------------------------------------------------------- multi-GPU shards
+//
+// main.cpp:54-82 is a loop over frames whose only cross-frame state is the
+// previous frame (pairwise costs read frame f-1's candidates, the motion
+// check its pixels), so contiguous frame ranges run independently given
+// their predecessor frame as a 1-frame halo.  The reader
+// delivers frames in order, so the shards are the batches themselves: batch
+// k goes to device k mod D with the last frame of batch k-1 as its halo.
+// One host thread per device owns that device's context; it submits its
+// batches (lm_detect_submit copies host frames before returning, so the
+// pinned buffer goes straight back to the pool) and collects them into a
+// FrameResults chunk, which the caller's thread appends in frame order.
+struct LocoMouse::DevicePool {
+  struct Job {
+    int first = 0, n = 0;
+    uint8_t* frames = nullptr;     // pinned batch buffer (returned to the pool once submitted)
+    std::vector<uint8_t> halo;     // frame first-1 (empty for the video's first batch)
+    std::vector<int32_t> bb;       // per-frame corners, halo frame first when present
+    std::promise<std::unique_ptr<FrameResults>> done;
+  };
+  struct Worker {
+    int device = 0;
+    lm_ctx* ctx = nullptr;
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<std::shared_ptr<Job>> queue;
+    bool stop = false;
+  };
+
+  size_t frame_bytes = 0;
+  int batch = 0, lanes = 1;
+  std::vector<std::unique_ptr<Worker>> workers;
+  std::mutex free_m;
+  std::condition_variable free_cv;
+  std::vector<uint8_t*> free_bufs;
+  std::vector<uint8_t*> all_bufs;
+  std::deque<std::future<std::unique_ptr<FrameResults>>> results;  // oldest batch first
+  size_t next = 0;                                                  // the next batch's worker
+
+  DevicePool(const std::vector<int>& devices, const lm_setup& setup, const lm_params& params, const lm_model& model,
+             int batch_, size_t frame_bytes_)
+      : frame_bytes(frame_bytes_), batch(batch_), lanes(std::max(1, setup.pipeline_lanes)) {
+    try {
+      for (int d : devices) {
+        auto w = std::make_unique<Worker>();
+        w->device = d;
+        throw_on_error(lm_ctx_create(d, &setup, &params, &model, batch, &w->ctx));
+        workers.push_back(std::move(w));
+      }
+      // two buffers per device: one being filled by the reader while another waits for its worker
+      for (size_t i = 0; i < 2 * workers.size(); ++i) {
+        void* q = nullptr;
+        throw_on_error(lm_host_alloc(frame_bytes * (size_t)batch, &q));
+        all_bufs.push_back(static_cast<uint8_t*>(q));
+      }
+    } catch (...) {
+      release();
+      throw;
+    }
+    free_bufs = all_bufs;
+    for (auto& w : workers) w->th = std::thread([this, p = w.get()] { run(*p); });
+  }
+  ~DevicePool() {
+    for (auto& w : workers) {
+      {
+        std::lock_guard<std::mutex> g(w->m);
+        w->stop = true;
+      }
+      w->cv.notify_all();
+    }
+    for (auto& w : workers)
+      if (w->th.joinable()) w->th.join();
+    release();
+  }
+  void release() {
+    for (auto& w : workers)
+      if (w->ctx) {
+        lm_ctx_destroy(w->ctx);
+        w->ctx = nullptr;
+      }
+    for (uint8_t* p : all_bufs) lm_host_free(p);
+    all_bufs.clear();
+  }
+  lm_ctx* first_ctx() const { return workers.front()->ctx; }
+  size_t capacity() const { return workers.size() * 2 * (size_t)lanes; }
+
+  uint8_t* take_buffer() {
+    std::unique_lock<std::mutex> g(free_m);
+    free_cv.wait(g, [this] { return !free_bufs.empty(); });
+    uint8_t* p = free_bufs.back();
+    free_bufs.pop_back();
+    return p;
+  }
+  void give_buffer(uint8_t* p) {
+    {
+      std::lock_guard<std::mutex> g(free_m);
+      free_bufs.push_back(p);
+    }
+    free_cv.notify_one();
+  }
+
+  void submit(std::shared_ptr<Job> j) {
+    results.push_back(j->done.get_future());
+    Worker& w = *workers[next];
+    next = (next + 1) % workers.size();
+    {
+      std::lock_guard<std::mutex> g(w.m);
+      w.queue.push_back(std::move(j));
+    }
+    w.cv.notify_one();
+  }
+
+  // A device's thread: submit queued batches while fewer than 2 x lanes are
+  // waiting for collection, otherwise collect the oldest.
+  void run(Worker& w) {
+    std::deque<std::shared_ptr<Job>> inflight;
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> g(w.m);
+        w.cv.wait(g, [&] { return w.stop || !w.queue.empty() || !inflight.empty(); });
+        if (w.stop) {  // the object is going away: batches not yet submitted are dropped
+          for (auto& q : w.queue) give_buffer(q->frames);
+          w.queue.clear();
+        }
+        if (!w.queue.empty() && (int)inflight.size() < 2 * lanes) {
+          j = std::move(w.queue.front());
+          w.queue.pop_front();
+        } else if (inflight.empty()) {
+          return;  // stopped, nothing queued or in flight
+        }
+      }
+      if (j) {
+        try {
+          throw_on_error(lm_detect_submit(w.ctx, j->frames, (int64_t)frame_bytes, j->n, j->first,
+                                          j->halo.empty() ? nullptr : j->halo.data(), j->bb.data()));
+          give_buffer(j->frames);
+          inflight.push_back(std::move(j));
+        } catch (...) {
+          give_buffer(j->frames);
+          j->done.set_exception(std::current_exception());
+        }
+        continue;
+      }
+      std::shared_ptr<Job> o = std::move(inflight.front());
+      inflight.pop_front();
+      try {
+        lm_batch_result r{};
+        throw_on_error(lm_detect_collect(w.ctx, &r));
+        auto fr = std::make_unique<FrameResults>();
+        fr->append(r);
+        o->done.set_value(std::move(fr));
+      } catch (...) {
+        o->done.set_exception(std::current_exception());
+      }
+    }
+  }
+};
+
+namespace {
+template <class T>
+void move_append(std::vector<T>& dst, std::vector<T>& src) {
+  dst.insert(dst.end(), std::make_move_iterator(src.begin()), std::make_move_iterator(src.end()));
+}
+}  // namespace
+
 LocoMouse::LocoMouse(const LocoMouse_Inputs& inputs) : IN(inputs), METHOD(0), N_FRAMES(inputs.n_frames) {
   if (!IN.read_frame && !IN.read_frames) throw std::invalid_argument("LocoMouse: no frame reader (V) given.");
   if (IN.batch < 1) throw std::invalid_argument("LocoMouse: batch must be >= 1.");
@@ -142,11 +313,23 @@ LocoMouse::LocoMouse(const LocoMouse_Inputs& inputs) : IN(inputs), METHOD(0), N_
     throw std::invalid_argument("LocoMouse: video size must be positive.");
   FRAME_BYTES = (size_t)IN.setup.video_rows * IN.setup.video_cols;
   IN.setup.method = 0;
+  if (IN.devices.empty()) IN.devices.push_back(IN.device);
+  if (!IN.oversubscribe && std::set<int>(IN.devices.begin(), IN.devices.end()).size() != IN.devices.size())
+    throw std::invalid_argument("LocoMouse: a device is listed twice (set oversubscribe to share devices).");
+  for (int d : IN.devices)
+    if (d < 0) throw std::invalid_argument("LocoMouse: invalid device index " + std::to_string(d) + ".");
+  IN.device = IN.devices.front();  // the BB pass and the geometry queries
   if (IN.verbose_debug && !IN.debug_text.empty()) DEBUG_TEXT.open(IN.debug_text);  // :341-343
 }
 
 LocoMouse::~LocoMouse() {
-  if (CTX) lm_ctx_destroy(CTX);  // waits for the batches in flight; their errors die with the object
+  // both wait for the batches in flight; their errors die with the object
+  if (POOL) {
+    PENDING.p = nullptr;  // a pool buffer: the pool frees it
+    POOL.reset();
+  } else if (CTX) {
+    lm_ctx_destroy(CTX);
+  }
 }
 
 // :543-569: with use_provided_bounding_box the bottom-right corners are the
@@ -230,8 +413,14 @@ void LocoMouse::initializeFeatureLoop() {
                << "BB_SIDE_MOUSE: " << debug_rect(BB_SIDE_MOUSE) << std::endl
                << "BB_BOTTOM_MOUSE: " << debug_rect(BB_BOTTOM_MOUSE) << std::endl;
   IN.setup.pipeline_lanes = std::max(1, std::min(IN.lanes, LM_MAX_LANES));
-  throw_on_error(lm_ctx_create(IN.device, &IN.setup, &IN.params, &IN.model, IN.batch, &CTX));
-  PENDING.allocate(FRAME_BYTES * (size_t)IN.batch);
+  if (IN.devices.size() > 1) {
+    POOL = std::make_unique<DevicePool>(IN.devices, IN.setup, IN.params, IN.model, IN.batch, FRAME_BYTES);
+    CTX = POOL->first_ctx();
+    PENDING.p = POOL->take_buffer();  // pool-owned: handed to the workers and swapped at every flush
+  } else {
+    throw_on_error(lm_ctx_create(IN.device, &IN.setup, &IN.params, &IN.model, IN.batch, &CTX));
+    PENDING.allocate(FRAME_BYTES * (size_t)IN.batch);
+  }
   N_PENDING = 0;
   if (DEBUG_TEXT.is_open()) {  // :700-704, :766
     const lm_geometry g = geometry();
@@ -302,9 +491,26 @@ void LocoMouse::sync() {
 void LocoMouse::collect_oldest() {
   const std::pair<int, int> b = INFLIGHT.front();
   INFLIGHT.pop_front();
-  lm_batch_result r{};
-  throw_on_error(lm_detect_collect(CTX, &r));
-  append(r);
+  if (POOL) {  // the batch's device thread collected it into a chunk of containers
+    auto fut = std::move(POOL->results.front());
+    POOL->results.pop_front();
+    std::unique_ptr<FrameResults> R = fut.get();
+    move_append(CANDIDATES_BOTTOM_PAW, R->CANDIDATES_BOTTOM_PAW);
+    move_append(CANDIDATES_BOTTOM_SNOUT, R->CANDIDATES_BOTTOM_SNOUT);
+    move_append(CANDIDATES_SIDE_PAW, R->CANDIDATES_SIDE_PAW);
+    move_append(CANDIDATES_SIDE_SNOUT, R->CANDIDATES_SIDE_SNOUT);
+    move_append(CANDIDATES_MATCHED_VIEWS_PAW, R->CANDIDATES_MATCHED_VIEWS_PAW);
+    move_append(CANDIDATES_MATCHED_VIEWS_SNOUT, R->CANDIDATES_MATCHED_VIEWS_SNOUT);
+    move_append(UNARY_BOTTOM_PAW, R->UNARY_BOTTOM_PAW);
+    move_append(UNARY_BOTTOM_SNOUT, R->UNARY_BOTTOM_SNOUT);
+    move_append(PAIRWISE_BOTTOM_PAW, R->PAIRWISE_BOTTOM_PAW);
+    move_append(PAIRWISE_BOTTOM_SNOUT, R->PAIRWISE_BOTTOM_SNOUT);
+    move_append(TRACKS_TAIL, R->TRACKS_TAIL);
+  } else {
+    lm_batch_result r{};
+    throw_on_error(lm_detect_collect(CTX, &r));
+    append(r);
+  }
   if (DEBUG_TEXT.is_open()) debug_frames(b.first, b.second);
 }
 
@@ -321,22 +527,40 @@ lm_geometry LocoMouse::geometry() const {
 // to be appended (oldest first, so results are appended in frame order).
 void LocoMouse::flush() {
   const int n = N_PENDING, first = CURRENT_FRAME + 1 - n;
-  std::vector<int32_t> bb((size_t)3 * n);
-  for (int i = 0; i < n; ++i) {
-    bb[3 * i] = (int32_t)BB_X_POS[first + i];
-    bb[3 * i + 1] = (int32_t)BB_Y_BOTTOM_POS[first + i];
-    bb[3 * i + 2] = (int32_t)BB_Y_SIDE_POS[first + i];
+  // multi-GPU: every batch but the video's first carries its predecessor frame (and its corners) as a halo
+  const int h = (POOL && first > 0) ? 1 : 0;
+  std::vector<int32_t> bb((size_t)3 * (n + h));
+  for (int i = -h; i < n; ++i) {
+    bb[3 * (i + h)] = (int32_t)BB_X_POS[first + i];
+    bb[3 * (i + h) + 1] = (int32_t)BB_Y_BOTTOM_POS[first + i];
+    bb[3 * (i + h) + 2] = (int32_t)BB_Y_SIDE_POS[first + i];
   }
-  while ((int)INFLIGHT.size() >= 2 * lm_ctx_lanes(CTX)) collect_oldest();
-  throw_on_error(lm_detect_submit(CTX, PENDING.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data()));
-  INFLIGHT.push_back({first, n});
   // Frames already read ahead past this batch (read_frames fills up to a whole
   // batch; a caller that reads results mid-batch flushes early) move to the
   // front of the pending buffer, so the reader's position and the frame
   // numbering stay in step.
   const int ahead = std::max(0, N_READ_AHEAD - n);
-  if (ahead)
-    std::memmove(PENDING.data(), PENDING.data() + (size_t)n * FRAME_BYTES, (size_t)ahead * FRAME_BYTES);
+  if (POOL) {
+    while (INFLIGHT.size() >= POOL->capacity()) collect_oldest();
+    auto j = std::make_shared<DevicePool::Job>();
+    j->first = first;
+    j->n = n;
+    j->frames = PENDING.p;
+    j->bb = std::move(bb);
+    if (h) j->halo = LAST_FRAME;
+    LAST_FRAME.assign(PENDING.p + (size_t)(n - 1) * FRAME_BYTES, PENDING.p + (size_t)n * FRAME_BYTES);
+    uint8_t* fresh = POOL->take_buffer();
+    if (ahead) std::memcpy(fresh, PENDING.p + (size_t)n * FRAME_BYTES, (size_t)ahead * FRAME_BYTES);
+    PENDING.p = fresh;
+    POOL->submit(std::move(j));
+    INFLIGHT.push_back({first, n});
+  } else {
+    while ((int)INFLIGHT.size() >= 2 * lm_ctx_lanes(CTX)) collect_oldest();
+    throw_on_error(lm_detect_submit(CTX, PENDING.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data()));
+    INFLIGHT.push_back({first, n});
+    if (ahead)
+      std::memmove(PENDING.data(), PENDING.data() + (size_t)n * FRAME_BYTES, (size_t)ahead * FRAME_BYTES);
+  }
   N_PENDING = 0;
   N_READ_AHEAD = ahead;
 }

@@ -67,6 +67,16 @@ struct LocoMouse_Inputs {
   int device = 0;      // HIP device of this instance (one per GPU / host thread)
   int batch = 256;     // frames per lm_detect_submit / lm_bb_push call
   int lanes = 4;       // batches in flight on the device (lm_setup.pipeline_lanes)
+  // Multi-GPU detection: with more than one
+  // entry, the video is cut into contiguous shards of `batch` frames dealt to
+  // the devices in turn, each shard run with its predecessor frame as a
+  // 1-frame halo (the per-frame path has no other cross-frame state); one
+  // host thread per device submits and collects, and the results are
+  // appended in frame order into the same containers.  Empty: {device}.
+  // The whole-video BB pass runs on the first device.  A device listed twice
+  // is refused unless `oversubscribe` (rehearsals on fewer GPUs).
+  std::vector<int> devices;
+  bool oversubscribe = false;
   // Whole-video BB pass (use_provided_bounding_box = 0): config.yml's
   // median_filter_size / min_pixel_visible / moving_average_window /
   // conn_comp_connectivity, and V.set(CV_CAP_PROP_POS_FRAMES, 0) (:761-762)
@@ -153,7 +163,10 @@ class LocoMouse : protected FrameResults {
   TrackSetup track_setup();
 
  private:
-  lm_ctx* CTX = nullptr;
+  lm_ctx* CTX = nullptr;  // the (first) device's context
+  struct DevicePool;      // per-device contexts and host threads of a multi-GPU run
+  std::unique_ptr<DevicePool> POOL;
+  std::vector<uint8_t> LAST_FRAME;  // multi-GPU: the last raw frame handed over, the next shard's halo
  protected:
   void runBoundingBoxPass(int method);  // lm_bb_* over the whole video, then rewind
  private:

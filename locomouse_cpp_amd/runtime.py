@@ -258,6 +258,20 @@ class Context:
                                      pp, bbp, C.byref(res)))
         return res if raw else result_to_numpy(res)
 
+    def detect_host_ptr(self, h_frames_ptr, pitch, n, first_frame, h_prev_ptr=None, raw=True):
+        """lm_detect_batch on frames at a host address (e.g. a pinned torch
+        tensor's data_ptr()): the H2D copy is part of the call."""
+        res = lm_batch_result()
+        _check(lib().lm_detect_batch(self._h, C.c_void_p(h_frames_ptr), pitch, n, first_frame,
+                                     C.c_void_p(h_prev_ptr) if h_prev_ptr else None, None, C.byref(res)))
+        return res if raw else result_to_numpy(res)
+
+    def submit_host_ptr(self, h_frames_ptr, pitch, n, first_frame, h_prev_ptr=None):
+        """Pipelined lm_detect_submit of frames at a host address (copied to
+        the device before it returns)."""
+        _check(lib().lm_detect_submit(self._h, C.c_void_p(h_frames_ptr), pitch, n, first_frame,
+                                      C.c_void_p(h_prev_ptr) if h_prev_ptr else None, None))
+
     def detect_device(self, d_frames_ptr, pitch, n, first_frame, d_prev_ptr=None, bb=None, raw=True):
         """Frames already in device memory (e.g. a torch.cuda uint8 tensor's data_ptr())."""
         res = lm_batch_result()

@@ -25,6 +25,8 @@ struct Flat {
 
 locomouse::TrackResults g_tracks;
 std::string g_output_file;
+std::vector<int> g_devices;  // LocoMouse_Inputs::devices of the next lmh_run (empty: the device argument)
+bool g_oversubscribe = false;
 
 int fail(const std::exception& e, int code, char* err, int errlen) {
   if (err && errlen > 0) {
@@ -35,6 +37,11 @@ int fail(const std::exception& e, int code, char* err, int errlen) {
 }
 
 }  // namespace
+
+extern "C" void lmh_set_devices(const int* devices, int n, int oversubscribe) {
+  g_devices.assign(devices, devices + (n > 0 ? n : 0));
+  g_oversubscribe = oversubscribe != 0;
+}
 
 extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_model* model,
                        const lm_bb_params* bb_params, const uint8_t* frames, int n_frames, int n_read, int batch,
@@ -47,6 +54,8 @@ extern "C" int lmh_run(const lm_setup* setup, const lm_params* params, const lm_
     in.model = *model;
     in.n_frames = (uint32_t)n_frames;
     in.device = device;
+    in.devices = g_devices;
+    in.oversubscribe = g_oversubscribe;
     in.batch = batch;
     in.output_file = g_output_file;
     const size_t fb = (size_t)setup->video_rows * setup->video_cols;

@@ -36,6 +36,7 @@ def lib():
                               C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_int]
         L.lmh_run.restype = C.c_int
         L.lmh_set_output.argtypes = [C.c_char_p]
+        L.lmh_set_devices.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.lmh_read_png.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
         L.lmh_read_avi.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int]
         L.lmh_fs_node.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -54,12 +55,14 @@ class HostError(RuntimeError):
         self.code = code
 
 
-def run_video(cfg, frames, batch=8, device=0, n_frames=None, call_order=0, bb_params=None, with_bb=False):
+def run_video(cfg, frames, batch=8, device=0, n_frames=None, call_order=0, bb_params=None, with_bb=False,
+              devices=None, oversubscribe=False):
     """LocoMouse_Initialize + main.cpp's loop over `frames`; returns the
     result containers as a result dict (abi.result_to_numpy layout).
     bb_params: lm_bb_params for the whole-video BB pass (used when
     cfg.params.use_provided_bounding_box == 0); with_bb also returns the
-    corners [n][3] (x, y_bottom, y_side) and the (side, bottom) box sizes."""
+    corners [n][3] (x, y_bottom, y_side) and the (side, bottom) box sizes.
+    devices / oversubscribe: LocoMouse_Inputs::devices (multi-GPU shards)."""
     import numpy as np
     from locomouse_cpp_amd.abi import lm_batch_result, lm_rect, result_to_numpy
     frames = np.ascontiguousarray(frames, dtype=np.uint8)
@@ -68,9 +71,15 @@ def run_video(cfg, frames, batch=8, device=0, n_frames=None, call_order=0, bb_pa
     n = frames.shape[0] if n_frames is None else n_frames
     corners = np.zeros((n, 3), dtype=np.uint32)
     sizes = (lm_rect * 2)()
-    rc = lib().lmh_run(C.byref(cfg.setup), C.byref(cfg.params), C.byref(cfg.model),
-                       C.byref(bb_params) if bb_params is not None else None, frames.ctypes.data, n,
-                       frames.shape[0], batch, device, call_order, C.byref(out), corners.ctypes.data, sizes, err, 512)
+    devs = np.ascontiguousarray(devices or [], dtype=np.int32)
+    lib().lmh_set_devices(devs.ctypes.data, len(devs), int(oversubscribe))
+    try:
+        rc = lib().lmh_run(C.byref(cfg.setup), C.byref(cfg.params), C.byref(cfg.model),
+                           C.byref(bb_params) if bb_params is not None else None, frames.ctypes.data, n,
+                           frames.shape[0], batch, device, call_order, C.byref(out), corners.ctypes.data, sizes, err,
+                           512)
+    finally:
+        lib().lmh_set_devices(None, 0, 0)
     if rc:
         raise HostError(rc, err.value.decode())
     res = result_to_numpy(out)
@@ -79,14 +88,15 @@ def run_video(cfg, frames, batch=8, device=0, n_frames=None, call_order=0, bb_pa
     return res
 
 
-def run_video_tracks(cfg, frames, batch=8, device=0, output_file=None):
+def run_video_tracks(cfg, frames, batch=8, device=0, output_file=None, devices=None, oversubscribe=False):
     """run_video with main.cpp's post-loop calls (computeBottomTracks,
     computeSideTracks, exportResults): returns (result dict, tracks dict,
     corners)."""
     import numpy as np
     lib().lmh_set_output(os.fsencode(output_file) if output_file else None)
     try:
-        res, corners, _ = run_video(cfg, frames, batch=batch, device=device, call_order=4, with_bb=True)
+        res, corners, _ = run_video(cfg, frames, batch=batch, device=device, call_order=4, with_bb=True,
+                                    devices=devices, oversubscribe=oversubscribe)
     finally:
         lib().lmh_set_output(None)
     n = res["n_frames"]

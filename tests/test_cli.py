@@ -223,7 +223,7 @@ def test_cli_reads_every_input(tmp_path):
 
 
 @pytest.mark.parametrize("case", ["calibration", "connectivity", "median", "prior", "flip", "method", "video",
-                                  "background", "size", "args"])
+                                  "background", "size", "args", "devices_twice", "devices_text"])
 def test_cli_errors_match_the_reference(tmp_path, case):
     cfg = S.SyntheticConfig()
     paths = MW.write_inputs(str(tmp_path), cfg, 2)
@@ -262,7 +262,14 @@ def test_cli_errors_match_the_reference(tmp_path, case):
     elif case == "args":
         args = args[:3]
         want = "Invalid inputs: Error: Could not open the calibration file: "
-    rc, out = run_cli(args)
+    env = None
+    if case == "devices_twice":  # LocoMouse_Inputs::devices: refused before any device is touched
+        env = {"LM_DEVICES": "0,1,0"}
+        want = "Invalid inputs: LocoMouse: a device is listed twice"
+    elif case == "devices_text":
+        env = {"LM_DEVICES": "0,gpu1"}
+        want = "Invalid inputs: LM_DEVICES: not a device index: gpu1"
+    rc, out = run_cli(args, env=env)
     assert rc == 1, out
     assert want in out, out
     assert "Total Elapsed time:" in out
@@ -272,13 +279,18 @@ def test_cli_errors_match_the_reference(tmp_path, case):
 
 # ------------------------------------------------------------- GPU: full run
 
+MULTI_DEVICE_ENV = {"LM_DEVICES": "0,0,0,0", "LM_OVERSUBSCRIBE": "1"}  # 4 "devices" on the one GPU
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["R24", "L8", "RJ"])
+@pytest.mark.parametrize("variant", ["R24", "L8", "RJ", "R24-4dev"])
 def test_cli_end_to_end_matches_oracle(tmp_path, variant):
     """The whole program on synthetic files: its output YAML holds the
     oracle's tracks (oracle detection on the same frames + the restated
     tracker).  "RJ": an MJPEG video (4:2:0 colour JPEG frames), the oracle
-    fed Pillow's decoding of the same frames."""
+    fed Pillow's decoding of the same frames.  "-4dev": LM_DEVICES with four
+    entries (one GPU, oversubscribed): shards of 7 frames dealt to four
+    device threads, each with its halo frame."""
     from oracle import oracle as O
     from oracle import track_oracle as TO
     flip = variant.startswith("L")
@@ -286,8 +298,11 @@ def test_cli_end_to_end_matches_oracle(tmp_path, variant):
     cfg = S.SyntheticConfig(flip=flip)
     stem = "mouse_" + variant[0]
     jpeg = dict(mode="RGB", quality=92, subsampling=2) if variant.endswith("J") else None
-    paths = MW.write_inputs(str(tmp_path), cfg, n, stem=stem, bits=24 if jpeg else int(variant[1:]), jpeg=jpeg)
-    rc, out = run_cli(cli_args(paths, side=variant[0], outdir=str(tmp_path)), env={"LM_BATCH": "16"})
+    multi = variant.endswith("-4dev")
+    bits = 24 if jpeg else int(variant[1:].split("-")[0])
+    paths = MW.write_inputs(str(tmp_path), cfg, n, stem=stem, bits=bits, jpeg=jpeg)
+    env = dict(MULTI_DEVICE_ENV, LM_BATCH="7") if multi else {"LM_BATCH": "16"}
+    rc, out = run_cli(cli_args(paths, side=variant[0], outdir=str(tmp_path)), env=env)
     assert rc == 0, out
     res = O.OracleRun(cfg, paths["decoded"] if jpeg else cfg.frames(0, n)).result
     p = cfg.params
@@ -324,11 +339,15 @@ def _load_cv_yaml(path):
 
 
 @pytest.mark.gpu
-def test_cli_verbose_debug_outputs(tmp_path):
+@pytest.mark.parametrize("devices", [1, 4])
+def test_cli_verbose_debug_outputs(tmp_path, devices):
     """verbose_debug: 1 with N_debug_frames: 30 of a 40-frame video — the run
     stops after 30 frames (loadVideo :380-389), and debug_<stem>.yml holds
     exportDebugVariables' content (:2769-2920) equal to the oracle's
-    containers and tracks; debug_<stem>.txt logs each frame's stages."""
+    containers and tracks; debug_<stem>.txt logs each frame's stages.
+    devices=4: the same through LM_DEVICES (four device threads on the one
+    GPU, 6-frame shards): every container of the debug YAML still equals the
+    oracle's."""
     import re
 
     from oracle import oracle as O
@@ -338,7 +357,8 @@ def test_cli_verbose_debug_outputs(tmp_path):
     stem = "dbg_R"
     paths = MW.write_inputs(str(tmp_path), cfg, n, stem=stem,
                             config_overrides={"verbose_debug": 1, "N_debug_frames": nd})
-    rc, out = run_cli(cli_args(paths, outdir=str(tmp_path)), env={"LM_BATCH": "16"})
+    env = dict(MULTI_DEVICE_ENV, LM_BATCH="6") if devices > 1 else {"LM_BATCH": "16"}
+    rc, out = run_cli(cli_args(paths, outdir=str(tmp_path)), env=env)
     assert rc == 0, out
     res = O.OracleRun(cfg, cfg.frames(0, nd)).result
     p = cfg.params

@@ -159,9 +159,10 @@ def test_error_mapping(cfg):
         assert e.value.code == 2
 
 
-def _quantized_config(rank):
+def _quantized_config(rank, side_rank=None):
     """Detector weights on a 2^-12 grid, so the fp32 correlation is exact and
-    equal-sum windows tie exactly; biases put ~`rank` pixels above zero."""
+    equal-sum windows tie exactly; biases put ~`rank` pixels above zero
+    (`side_rank` for the side detectors when given)."""
     from oracle import oracle as O
     base = S.SyntheticConfig()
     W = {}
@@ -172,9 +173,10 @@ def _quantized_config(rank):
     r0 = O.OracleRun(c0, c0.frames(0, 1), flags=O.KEEP_DEBUG)
     biases, dups = {}, 0
     for det, name in ((0, "paw_bottom"), (1, "snout_bottom"), (3, "paw_side"), (4, "snout_side")):
+        rk = side_rank if (side_rank is not None and det >= 3) else rank
         v = np.sort(r0.scores(0, det).ravel())[::-1]
-        biases[name] = float(v[rank])
-        pos = v[v > v[rank]]
+        biases[name] = float(v[rk])
+        pos = v[v > v[rk]]
         dups += len(pos) - len(np.unique(pos))
     return S.SyntheticConfig(weights=W, biases=biases), dups
 
@@ -279,3 +281,20 @@ def test_global_tier_few_overflowing_pairs():
         got = ctx.detect(frames, 0)
         ctx.close()
         assert_same(got, ref, "few overflowing pairs: ")
+
+
+def test_side_global_tier_bottom_lds_tier():
+    """Side lists beyond LM_NMS_CAP (global-scratch k_nms) with short bottom
+    lists (LDS k_nms): the side skip (detectSideCandidates runs only for a
+    non-empty bottom list, :820-833) must not read bottom keys the bottom
+    block has already overwritten with its staged candidates -- k_tail
+    records the decision before k_nms runs.  Blank frames make some bottom
+    lists empty, so both outcomes of the skip occur."""
+    c, dups = _quantized_config(300, side_rank=2500)
+    frames = c.frames(0, 10)
+    frames[[2, 6]] = 0
+    ref = _oracle(c, frames).result
+    ctx = _ctx(c, max_batch=10)
+    got = ctx.detect(frames, 0)
+    ctx.close()
+    assert_same(got, ref, "mixed tiers: ")

@@ -111,3 +111,74 @@ def test_tm_de_computed_bounding_box_then_main_loop_matches_oracle():
     cfg2.params.bounding_box_side = abi.lm_rect(*r["bb_side_mouse"])
     cfg2.params.bounding_box_bottom = abi.lm_rect(*r["bb_bottom_mouse"])
     assert_same(got, O.OracleRun(cfg2, frames, bb=ref_corners.astype(np.int32)).result, "host TM_DE bb: ")
+
+
+# ---------------------------------------------------- multi-GPU shards (§8(e))
+
+def test_device_list_refusals():
+    """LocoMouse_Inputs::devices: a device listed twice is refused unless
+    oversubscribe is set, and a negative index is refused -- both by the
+    constructor, before any device is touched (runs without a GPU)."""
+    cfg = S.SyntheticConfig()
+    with pytest.raises(H.HostError, match="listed twice") as e:
+        H.run_video(cfg, cfg.frames(0, 2), devices=[0, 1, 0])
+    assert e.value.code == 1
+    with pytest.raises(H.HostError, match="invalid device index") as e:
+        H.run_video(cfg, cfg.frames(0, 2), devices=[0, -1])
+    assert e.value.code == 1
+
+
+@pytest.mark.parametrize("n,batch,ndev", [(3, 8, 4), (23, 5, 4), (20, 5, 4), (9, 1, 3)])
+def test_shard_plan_equals_unsharded_oracle(n, batch, ndev):
+    """The multi-device plan of the host mirror -- batch k of `batch` frames
+    on device k mod ndev, every batch but the first run with its predecessor
+    frame as a 1-frame halo -- gives the unsharded results, on the oracle
+    (CPU): fewer batches than devices, a ragged last batch, one-frame shards."""
+    import numpy as np
+    from locomouse_cpp_amd.results import concat_results, slice_results
+    from oracle import oracle as O
+    from test_gpu_parity import assert_same
+    cfg = S.SyntheticConfig()
+    frames = cfg.frames(0, n)
+    ref = O.OracleRun(cfg, frames).result
+    per_dev = {}
+    parts = []
+    for k, a in enumerate(range(0, n, batch)):
+        b = min(n, a + batch)
+        per_dev.setdefault(k % ndev, []).append(a)
+        if a == 0:
+            parts.append(O.OracleRun(cfg, frames[a:b]).result)
+        else:
+            parts.append(slice_results(O.OracleRun(cfg, frames[a - 1:b]).result, 1))
+    assert sum(len(v) for v in per_dev.values()) == (n + batch - 1) // batch
+    assert_same(concat_results(parts), ref, f"plan n{n} b{batch} d{ndev}: ")
+    assert np.array_equal(concat_results(parts)["tail"], ref["tail"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,batch,order", [(23, 5, 0), (23, 5, 1 | 8), (3, 8, 0), (40, 7, 8)])
+def test_main_loop_on_four_devices_matches_oracle(n, batch, order):
+    """LocoMouse_Inputs::devices = four entries of the one GPU (oversubscribe):
+    shards of `batch` frames dealt to four device threads, each shard with its
+    halo frame, results appended in frame order -- every container equals the
+    oracle's (incl. mid-batch reads, the read-ahead reader, and fewer shards
+    than devices)."""
+    from oracle import oracle as O
+    from test_gpu_parity import assert_same
+    cfg = S.SyntheticConfig()
+    frames = cfg.frames(0, n)
+    got = H.run_video(cfg, frames, batch=batch, call_order=order, devices=[0, 0, 0, 0], oversubscribe=True)
+    assert_same(got, O.OracleRun(cfg, frames).result, f"host 4 devices n{n} b{batch} o{order}: ")
+
+
+@pytest.mark.gpu
+def test_tracks_on_four_devices_match_single_device():
+    """main.cpp's post-loop stage on the four-device containers: the tracks
+    equal those of the one-device run."""
+    import numpy as np
+    cfg = S.SyntheticConfig()
+    frames = cfg.frames(0, 30)
+    r1, t1, _ = H.run_video_tracks(cfg, frames, batch=8)
+    r4, t4, _ = H.run_video_tracks(cfg, frames, batch=4, devices=[0, 0, 0, 0], oversubscribe=True)
+    for k in t1:
+        assert np.array_equal(t1[k], t4[k]), k
