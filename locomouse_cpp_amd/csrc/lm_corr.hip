@@ -385,6 +385,45 @@ DEV lm_f2 corr_tap_h(lm_f2 acc, lm_f2 w2, lm_f2 p) {
   }
 }
 
+// Both taps (halves 0 and 1) of one weight pair in ONE inline-asm block, for
+// pair 0 (acc a, weights wa) and/or pair 1 (acc b, weights wb); px: the six
+// pixel pairs p .. p + 5 the two taps read.  The compiler cannot see inside
+// an asm statement, so it separates any two that touch the same registers by
+// an s_nop (the wait states an MFMA result would need): one statement per
+// tap put 30 s_nops into a kw-30 step, one per pair halves that.  Per
+// accumulator the taps keep their order (half 0, then half 1).
+#ifndef LM_RW_PAIRASM
+#define LM_RW_PAIRASM 1
+#endif
+#define LM_RWF(a, w, p, sel) "v_pk_fma_f32 %" #a ", %" #w ", %" #p ", %" #a " " sel "\n"
+#define LM_RW_S0 "op_sel_hi:[0,1,1]"
+#define LM_RW_S1 "op_sel:[1,0,0] op_sel_hi:[1,1,1]"
+DEV void rw_pair_ab(lm_f2 (&a)[PK_C], lm_f2 (&b)[PK_C], lm_f2 wa, lm_f2 wb, const lm_f2* px) {
+  static_assert(PK_C == 5, "the asm block is written for 5 columns");
+  asm volatile(LM_RWF(0, 10, 12, LM_RW_S0) LM_RWF(1, 10, 13, LM_RW_S0) LM_RWF(2, 10, 14, LM_RW_S0)
+                   LM_RWF(3, 10, 15, LM_RW_S0) LM_RWF(4, 10, 16, LM_RW_S0)
+               LM_RWF(5, 11, 12, LM_RW_S0) LM_RWF(6, 11, 13, LM_RW_S0) LM_RWF(7, 11, 14, LM_RW_S0)
+                   LM_RWF(8, 11, 15, LM_RW_S0) LM_RWF(9, 11, 16, LM_RW_S0)
+               LM_RWF(0, 10, 13, LM_RW_S1) LM_RWF(1, 10, 14, LM_RW_S1) LM_RWF(2, 10, 15, LM_RW_S1)
+                   LM_RWF(3, 10, 16, LM_RW_S1) LM_RWF(4, 10, 17, LM_RW_S1)
+               LM_RWF(5, 11, 13, LM_RW_S1) LM_RWF(6, 11, 14, LM_RW_S1) LM_RWF(7, 11, 15, LM_RW_S1)
+                   LM_RWF(8, 11, 16, LM_RW_S1) LM_RWF(9, 11, 17, LM_RW_S1)
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(b[0]), "+v"(b[1]), "+v"(b[2]),
+                 "+v"(b[3]), "+v"(b[4])
+               : "s"(wa), "s"(wb), "v"(px[0]), "v"(px[1]), "v"(px[2]), "v"(px[3]), "v"(px[4]), "v"(px[5]));
+}
+DEV void rw_pair_1(lm_f2 (&a)[PK_C], lm_f2 w, const lm_f2* px) {
+  asm volatile(LM_RWF(0, 5, 6, LM_RW_S0) LM_RWF(1, 5, 7, LM_RW_S0) LM_RWF(2, 5, 8, LM_RW_S0)
+                   LM_RWF(3, 5, 9, LM_RW_S0) LM_RWF(4, 5, 10, LM_RW_S0)
+               LM_RWF(0, 5, 7, LM_RW_S1) LM_RWF(1, 5, 8, LM_RW_S1) LM_RWF(2, 5, 9, LM_RW_S1)
+                   LM_RWF(3, 5, 10, LM_RW_S1) LM_RWF(4, 5, 11, LM_RW_S1)
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4])
+               : "s"(w), "v"(px[0]), "v"(px[1]), "v"(px[2]), "v"(px[3]), "v"(px[4]), "v"(px[5]));
+}
+#undef LM_RWF
+#undef LM_RW_S0
+#undef LM_RW_S1
+
 template <int KW, bool UNF>
 struct RwPipe {
   using P = RwPlan<KW>;
@@ -412,7 +451,14 @@ struct RwPipe {
   }
   template <int J, int C, bool A, bool B>
   DEV void compute_from() {
-    if constexpr (J < P::end(C)) {
+    if constexpr (J < P::end(C) && LM_RW_PAIRASM && LM_RW_ASMFMA && !UNF && (J & 1) == 0 && J + 1 < P::end(C) &&
+                  (A || B)) {
+      constexpr int q = J / 2 - P::qb(C);
+      if constexpr (A && B) rw_pair_ab(acc[0], acc[1], wa[q], wb[q], &px[J]);
+      else if constexpr (A) rw_pair_1(acc[0], wa[q], &px[J]);
+      else rw_pair_1(acc[1], wb[q], &px[J]);
+      compute_from<J + 2, C, A, B>();
+    } else if constexpr (J < P::end(C)) {
       constexpr int q = J / 2 - P::qb(C), h = J & 1;
       if constexpr (A) {
 #pragma unroll

@@ -6,8 +6,9 @@ The ring correlation (k_corr_rw) loads its pixel pairs with inline-asm
 ds_read2_b32 and waits for them with an explicit s_waitcnt at each chunk
 start; a spill or register copy of those pairs between issue and wait would
 read stale LDS data unnoticed by the compiler.  So no kernel may spill VGPRs
-or use scratch, the width-specialised ring kernels must hold 5 waves per SIMD
-(<= 96 VGPRs) with no SGPR spills either, and in every ring kernel no
+or use scratch, the width-specialised ring kernels must hold the 4 waves per
+SIMD their LDS rings allow (<= 128 VGPRs) with no SGPR spills
+either, and in every ring kernel no
 instruction may read a VGPR a ds_read2_b32 wrote before the next
 s_waitcnt lgkmcnt(0) (test_ring_reads_wait_for_lds)."""
 import os
@@ -43,8 +44,8 @@ def test_ring_correlation_budget(kernels):
     for k, r in ring.items():
         kw = int(re.match(r"_Z9k_corr_rwILi(\d+)E", k).group(1))
         assert r["sgpr_spill_count"] == 0, (k, r)
-        # four 40 x 8 sub-tiles per wave: the rings (>= 8.6 KB of LDS per
-        # wave) allow at most 4 waves per SIMD, which 128 VGPRs allow
+        # eight 40 x 4 sub-tiles per wave: the rings (~9.5 KB of LDS per wave
+        # at kw 30) allow at most 4 waves per SIMD, which 128 VGPRs allow
         assert r["vgpr_count"] <= 128, (k, r)
 
 
