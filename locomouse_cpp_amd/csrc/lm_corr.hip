@@ -332,6 +332,9 @@ DEV bool corr_tile_dark(const LmConst& K, const LmDet& D, const uint8_t* __restr
 #ifndef LM_RW_ASMFMA
 #define LM_RW_ASMFMA 1
 #endif
+#ifndef LM_RW_PREF
+#define LM_RW_PREF 1  // steps ahead a window row's global load is issued (1 or 2)
+#endif
 #ifndef LM_RW_PMAX
 #define LM_RW_PMAX 4
 #endif
@@ -474,7 +477,11 @@ struct RwPipe {
   // step t, chunk C onwards.  On entry chunk C's pairs and weights are in
   // flight; on exit the next step's first chunk is.  `base_n` addresses the
   // next step's pixel rows, rows_n its weight rows.
-  template <int C, bool A, bool B, typename F>
+  // NEXT = false (a wave's last step): nothing is prefetched for a step that
+  // does not come -- an LDS read whose result nobody uses leaves its
+  // destination registers free to the compiler, which may write them before
+  // the read returns and is overwritten by it.
+  template <int C, bool A, bool B, bool NEXT = true, typename F>
   DEV void chunks(unsigned base, unsigned base_n, const lm_f2* __restrict__ ra, const lm_f2* __restrict__ rb,
                   const lm_f2* __restrict__ ra_n, const lm_f2* __restrict__ rb_n, F&& at_start) {
     // lgkmcnt(0) through the builtin (vmcnt / expcnt left at their maxima), so
@@ -486,19 +493,21 @@ struct RwPipe {
     if constexpr (C + 1 < P::N) {
       load_w<C + 1>(na, nb, ra, rb);
       issue<P::pbeg(C + 1), P::pend(C + 1)>(base);
-    } else {
+    } else if constexpr (NEXT) {
       load_w<0>(na, nb, ra_n, rb_n);
       issue<P::pbeg(0), P::pend(0)>(base_n);
     }
     __builtin_amdgcn_sched_barrier(0);
     compute_from<P::beg(C), C, A, B>();
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (C + 1 < P::N || NEXT) {
 #pragma unroll
-    for (int q = 0; q < P::PMAX; ++q) {
-      wa[q] = na[q];
-      wb[q] = nb[q];
+      for (int q = 0; q < P::PMAX; ++q) {
+        wa[q] = na[q];
+        wb[q] = nb[q];
+      }
     }
-    if constexpr (C + 1 < P::N) chunks<C + 1, A, B>(base, base_n, ra, rb, ra_n, rb_n, at_start);
+    if constexpr (C + 1 < P::N) chunks<C + 1, A, B, NEXT>(base, base_n, ra, rb, ra_n, rb_n, at_start);
   }
 };
 
@@ -556,7 +565,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     const int e = lane + 64 * k, qk = e / NL, dk = e - qk * NL;
     lk[k] = qk < H.nvalid;
     int sk, yk, xk;
-    H.get(qk, sk, yk, xk);
+    H.get(min(qk, NQ - 1), sk, yk, xk);  // lanes past the last sub-tile: a valid address, the value unused
     const uint8_t* s = corr_src(K, D, ext, ext_slot_bytes, sk, yk, xk);
     la[k] = reinterpret_cast<const unsigned*>(s - ((uintptr_t)s & 3)) + dk;
     lo[k] = qk * QP + 4 * dk;
@@ -578,12 +587,21 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   struct Row {
     unsigned v[NLD];
   };
+  // LM_RW_PREF = 2: every lane loads unconditionally (rows past the window
+  // clamped to its last, lanes without a sub-tile at a valid address; those
+  // values are never stored), so the loads of a step are not behind branches
+  // and the compiler can wait for the older row with vmcnt(NLD) while the
+  // newer one stays in flight.
   auto load_row = [&](int r) -> Row {
     Row w;
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
+#if LM_RW_PREF >= 2
+      w.v[k] = la[k][(int64_t)min(r, nrows - 1) * ew4];
+#else
       w.v[k] = 0u;
       if (lk[k] && r < nrows) w.v[k] = la[k][(int64_t)r * ew4];
+#endif
     }
     return w;
   };
@@ -633,11 +651,48 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   auto wrow = [&](int i) { return W + min(max(i, 0), kh - 1) * kwp2; };
   S.template load_w<0>(S.wa, S.wb, wrow(0), wrow(-2));
   S.template issue<RwPlan<KW>::pbeg(0), RwPlan<KW>::pend(0)>(row_base(0));
-  // Step t reads ring rows t .. t + 5 and prefetches step t + 1's rows in its
-  // last chunk; it loads row t + HS at its start and stores it at its end
-  // into the slot of row t (dead by then: a wave's LDS operations run in
-  // order).  The load has a whole step to land, and no register carries a
-  // row from one step to the next.
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+#if LM_RW_PREF >= 2
+  // Step t reads ring rows t and t + 1 and prefetches step t + 1's pixel
+  // pairs in its last chunk; at its end it stores row t + HS into the slot
+  // of row t (dead by then: a wave's LDS operations run in order).  That
+  // row's global load was issued at the start of step t - 1, so it has two
+  // steps to land: step t loads row t + HS + 1 into one register set while
+  // it stores the other (even steps store r0 and load r1, odd steps the
+  // reverse -- the step loop is unrolled by two by hand, so no register copy
+  // makes the wave wait for the load just issued).
+  auto stepx = [&](int t, auto A, auto B, Row& st, Row& ld, auto N) {
+    S.template chunks<0, decltype(A)::value, decltype(B)::value, decltype(N)::value>(
+        row_base(t), row_base(t + 1), wrow(t), wrow(t - 2), wrow(t + 1), wrow(t - 1),
+        [&]() { if constexpr (decltype(N)::value) ld = load_row(t + HS + 1); });
+    if constexpr (decltype(N)::value) store_row(t + HS, st);  // the last step stores no row (t + HS >= nrows)
+  };
+  Row r0 = load_row(HS), r1;
+  {  // kh >= 2: the host runs one-row detectors on k_corr_gen
+    // pair 0 (tap row t) runs while t < kh, pair 1 (tap row t - 2) from t = 2
+    stepx(0, T1{}, F0{}, r0, r1, T1{});
+    stepx(1, T1{}, F0{}, r1, r0, T1{});
+    int t = 2;
+    for (; t + 1 < kh; t += 2) {
+      stepx(t, T1{}, T1{}, r0, r1, T1{});
+      stepx(t + 1, T1{}, T1{}, r1, r0, T1{});
+    }
+    if (t < kh) {
+      stepx(t, T1{}, T1{}, r0, r1, T1{});
+      stepx(kh, F0{}, T1{}, r1, r0, T1{});
+      stepx(kh + 1, F0{}, T1{}, r0, r1, F0{});
+    } else {
+      stepx(kh, F0{}, T1{}, r0, r1, T1{});
+      stepx(kh + 1, F0{}, T1{}, r1, r0, F0{});
+    }
+  }
+#else
+  // Step t reads ring rows t and t + 1 and prefetches step t + 1's pixel
+  // pairs in its last chunk; it loads row t + HS at its start and stores it
+  // at its end into the slot of row t (dead by then: a wave's LDS operations
+  // run in order).  The load has a whole step to land, and no register
+  // carries a row from one step to the next.
   auto step = [&](int t, auto A, auto B) {
     Row nx;
     S.template chunks<0, decltype(A)::value, decltype(B)::value>(row_base(t), row_base(t + 1), wrow(t), wrow(t - 2),
@@ -645,15 +700,17 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
                                                                   [&]() { nx = load_row(t + HS); });
     store_row(t + HS, nx);
   };
-  using T1 = std::true_type;
-  using F0 = std::false_type;
   // pair 0 (tap row t) runs while t < kh, pair 1 (tap row t - 2) from t = 2
+  // (the last step's prefetch is dead; the wait below drains it before any
+  // register it names is reused: tests/test_kernel_resources.py checks the
+  // code for such writes)
   const int e1 = min(2, kh);
   int t = 0;
   for (; t < e1; ++t) step(t, T1{}, F0{});
   for (; t < 2; ++t) step(t, F0{}, F0{});
   for (; t < kh; ++t) step(t, T1{}, T1{});
   for (; t < kh + 2; ++t) step(t, F0{}, T1{});
+#endif
   __builtin_amdgcn_s_waitcnt(0xC07F);  // the last (unused) prefetch
 #pragma unroll
   for (int p = 0; p < 2; ++p)

@@ -265,6 +265,28 @@ DEV uint32_t bright_bytes(uint32_t w) {
 // 0x80 in byte i of the result for bit i of the 4-bit n
 DEV uint32_t byte_mask4(uint32_t n) { return ((n * 0x00204081u) & 0x01010101u) << 7; }
 
+// The five aligned dwords that cover the 16 source bytes [lo, lo + 16) of a
+// run: one dwordx4 (gfx950 global loads need only dword alignment) plus one
+// dword -- two vector-memory instructions instead of five.
+#ifndef LM_INGEST_X4
+#define LM_INGEST_X4 1
+#endif
+typedef uint32_t lm_u4a4 __attribute__((ext_vector_type(4), aligned(4)));
+DEV void ingest_run_load(const lm_gu8* F, int lo, uint32_t (&d)[5]) {
+  const lm_gu32* w = reinterpret_cast<const lm_gu32*>(F + (lo & ~3));
+#if LM_INGEST_X4
+  const lm_u4a4 a = *reinterpret_cast<const __attribute__((address_space(1))) lm_u4a4*>(w);
+  d[0] = a.x;
+  d[1] = a.y;
+  d[2] = a.z;
+  d[3] = a.w;
+  d[4] = w[4];
+#else
+#pragma unroll
+  for (int u = 0; u < 5; ++u) d[u] = w[u];
+#endif
+}
+
 #ifndef LM_INGEST_WPE
 #define LM_INGEST_WPE 1  // amdgpu_waves_per_eu minimum (register budget experiments)
 #endif
@@ -343,11 +365,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       if (m.y != 0) {
 #pragma unroll
         for (int f = 0; f < LM_INGEST_FB; ++f)
-          if (f < nf) {
-            const lm_gu32* w = reinterpret_cast<const lm_gu32*>(as_global(frame_ptr[sb + f]) + (m.x & ~3));
-#pragma unroll
-            for (int u = 0; u < 5; ++u) d[f][u] = w[u];
-          }
+          if (f < nf) ingest_run_load(as_global(frame_ptr[sb + f]), m.x, d[f]);
       }
     }
   };
@@ -458,11 +476,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       // loads are issued before any is used.
 #pragma unroll
       for (int f = 0; f < LM_INGEST_FB; ++f)
-        if (f < nf) {
-          const lm_gu32* w = reinterpret_cast<const lm_gu32*>(as_global(frame_ptr[sb + f]) + (lo & ~3));
-#pragma unroll
-          for (int u = 0; u < 5; ++u) d[f][u] = w[u];
-        }
+        if (f < nf) ingest_run_load(as_global(frame_ptr[sb + f]), lo, d[f]);
 #pragma unroll
       for (int f = 0; f < LM_INGEST_FB; ++f)
         if (f < nf) {
@@ -487,10 +501,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       const lm_gu8* __restrict__ F = as_global(frame_ptr[slot]);
       uint32_t pw[4] = {0, 0, 0, 0};
       if (run != 0) {
-        const lm_gu32* w = reinterpret_cast<const lm_gu32*>(F + (lo & ~3));
         uint32_t d1[5];
-#pragma unroll
-        for (int u = 0; u < 5; ++u) d1[u] = w[u];
+        ingest_run_load(F, lo, d1);
         run_bytes(d1, pw);
       } else {
 #pragma unroll

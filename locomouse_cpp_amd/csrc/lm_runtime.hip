@@ -433,7 +433,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     D.oh = out_rel[d].h;
     D.ow = out_rel[d].w;
     const bool f16 = su->corr_precision == LM_CORR_F16;
-    const bool ring = !f16 && corr_ring(D.kw);
+    const bool ring = !f16 && corr_ring(D.kw) && D.kh >= 2;  // one-row detectors: k_corr_gen
     D.tile_w = f16 ? LM_F16_TW : LM_TW;
     D.tile_h = f16 ? LM_F16_TH : ring ? LM_RW_TH : LM_TH;
     D.tiles_x = (D.ow + D.tile_w - 1) / D.tile_w;
@@ -471,7 +471,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
     for (int d = 0; d < 6; ++d) {
       LmDet& D = K.det[d];
       D.kw_ring = D.kw;
-      if (!widen || !corr_ring(D.kw)) continue;
+      if (!widen || !corr_ring(D.kw) || D.kh < 2) continue;
       for (int e = 0; e < 6; ++e) {
         const int w = K.det[e].kw;
         if (e != d && corr_ring(w) && w > D.kw && w <= D.kwp && (D.kw_ring == D.kw || w < D.kw_ring)) D.kw_ring = w;
@@ -642,7 +642,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       const int d = order[oi];
       LmDet& D = K.det[d];
       const bool f16 = su->corr_precision == LM_CORR_F16;
-      const bool ring = !f16 && corr_ring(D.kw_ring);
+      const bool ring = !f16 && corr_ring(D.kw_ring) && D.kh >= 2;
       const void* fn = f16 ? corr_kernel_f16(D.kw)
                        : ring && m == 1 && rw_all_width(D.kw_ring) ? corr_kernel_rw_all(c->unfused)
                                                                    : corr_kernel(D.kw_ring, c->unfused);

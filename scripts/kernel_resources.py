@@ -170,6 +170,14 @@ def _lds_pair_step(ins, pending, bad):
             else (_vregs(ops[1].split()[0]) if len(ops) > 1 else set())
     if srcs & pending and bad is not None:
         bad.append(ins)
+    # a write to a pending destination (WAW): the late LDS return would
+    # overwrite the new value (a dead read's registers reused by the
+    # compiler).  Another LDS read into them is fine: a wave's LDS reads
+    # return in order.
+    if ops and bad is not None and (op.startswith("v_") or
+                                    op.startswith(("global_load", "buffer_load", "flat_load"))):
+        if _vregs(ops[0].split()[0]) & pending:
+            bad.append("WAW " + ins)
     if op == "ds_read2_b32" and ops:
         return pending | _vregs(ops[0])
     if ops and op.startswith("v_"):
@@ -178,9 +186,9 @@ def _lds_pair_step(ins, pending, bad):
 
 
 def early_reads_of_lds_pairs(instrs):
-    """Instructions that read a VGPR written by a ds_read2_b32 before an
-    s_waitcnt that drains the LDS counter (lgkmcnt(0)) has executed, on some
-    control-flow path.  The ring correlation issues those reads as inline asm
+    """Instructions that read -- or write ("WAW ...", except another LDS read) --
+    a VGPR written by a ds_read2_b32 before an s_waitcnt that drains the LDS
+    counter (lgkmcnt(0)) has executed, on some control-flow path.  The ring correlation issues those reads as inline asm
     the compiler's wait insertion does not see, so a register copy or use
     before the explicit wait would read stale data.  instrs: disassemble_cfg
     items (address, text, branch target) -- a forward may-analysis over the

@@ -10,7 +10,8 @@ or use scratch, the width-specialised ring kernels must hold the 4 waves per
 SIMD their LDS rings allow (<= 128 VGPRs) with no SGPR spills
 either, and in every ring kernel no
 instruction may read a VGPR a ds_read2_b32 wrote before the next
-s_waitcnt lgkmcnt(0) (test_ring_reads_wait_for_lds)."""
+s_waitcnt lgkmcnt(0), nor write it (a dead read's registers reused by the
+compiler are overwritten when the read returns; test_ring_reads_wait_for_lds)."""
 import os
 import re
 import sys
