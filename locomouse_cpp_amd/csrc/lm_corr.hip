@@ -333,7 +333,7 @@ DEV bool corr_tile_dark(const LmConst& K, const LmDet& D, const uint8_t* __restr
 #define LM_RW_ASMFMA 1
 #endif
 #ifndef LM_RW_PREF
-#define LM_RW_PREF 1  // steps ahead a window row's global load is issued (1 or 2)
+#define LM_RW_PREF 2  // steps ahead a window row's global load is issued (1 or 2)
 #endif
 #ifndef LM_RW_PMAX
 #define LM_RW_PMAX 4
@@ -798,6 +798,30 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
       }
 }
 
+// XCD-aware work order: workgroups are dispatched to the 8 XCDs round-robin
+// (block b on XCD b mod 8), each XCD with its own L2.  Block b takes logical
+// block xcd_block(b): the logical blocks come in runs of LM_RW_XCD
+// consecutive ones, and each run goes to one XCD (runs dealt to the XCDs in
+// turn, so the empty waves at the grid's end stay spread over all eight).
+// Consecutive work items are neighbouring bright tiles of one frame, so the
+// sub-tiles that re-read each other's window rows (the (kh - 1)-row vertical
+// halo, the (kw - 1)-column horizontal one) fetch them from one L2.
+#ifndef LM_RW_XCD
+#define LM_RW_XCD 0  // run length in workgroups (0: the hardware order)
+#endif
+DEV int xcd_block(int b, int nb) {
+#if LM_RW_XCD
+  constexpr int C = LM_RW_XCD;
+  const int full = nb / (8 * C) * (8 * C);
+  if (b >= full) return b;  // the last partial round: hardware order
+  const int k = b >> 3, x = b & 7;
+  return (k / C) * (8 * C) + x * C + (k % C);
+#else
+  (void)nb;
+  return b;
+#endif
+}
+
 // One launch per width group (LM_KW_LIST widths).
 template <int KW, bool UNF>
 // waves per SIMD: LDS allows 5 (80-column sub-tiles, kw <= 32) or 4
@@ -814,7 +838,7 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
   // LM_RW_ITEMS work items per wave, strided by the launch's wave count (the
   // host sizes the grid for that many)
   const int nwaves = gridDim.x * LM_RW_WAVES;
-  for (int g = blockIdx.x * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
+  for (int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
     int d;
     RwTiles H;
     if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) return;
@@ -840,7 +864,7 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(L
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * G.ring_floats;
   const int nwaves = gridDim.x * LM_RW_WAVES;
-  for (int g = blockIdx.x * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
+  for (int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
     int d;
     RwTiles H;
     if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) return;
