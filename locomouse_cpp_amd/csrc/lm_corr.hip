@@ -807,7 +807,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
 // sub-tiles that re-read each other's window rows (the (kh - 1)-row vertical
 // halo, the (kw - 1)-column horizontal one) fetch them from one L2.
 #ifndef LM_RW_XCD
-#define LM_RW_XCD 0  // run length in workgroups (0: the hardware order)
+#define LM_RW_XCD 16  // run length in workgroups (0: the hardware order)
 #endif
 DEV int xcd_block(int b, int nb) {
 #if LM_RW_XCD

@@ -297,8 +297,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
                                                  unsigned* __restrict__ tailbm, const int2* __restrict__ smap,
                                                  const uint4* __restrict__ sbkg, const int32_t* __restrict__ skey,
                                                  uint8_t* __restrict__ flags, int32_t* __restrict__ tl_cnt,
-                                                 uint32_t* __restrict__ tl_list) {
+                                                 uint32_t* __restrict__ tl_list, long long* __restrict__ prof) {
   const LmConst& K = *Kp;
+  // LM_KPROF=1: clock64() of thread 0 at the phase ends, wall clock at start / end
+  long long* pb = prof ? prof + (int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 16 : nullptr;
+#define ING_PROF(k) \
+  if (pb && threadIdx.x == 0) pb[k] = clock64();
+  ING_PROF(0)
+  if (pb && threadIdx.x == 0) pb[14] = wall_clock64();
   const int sb = s0 + blockIdx.y * LM_INGEST_FB;
   const int nf = min(LM_INGEST_FB, s_end - sb);
   const int T = (int)blockDim.x, tid = (int)threadIdx.x;
@@ -365,12 +371,20 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       if (m.y != 0) {
 #pragma unroll
         for (int f = 0; f < LM_INGEST_FB; ++f)
-          if (f < nf) ingest_run_load(as_global(frame_ptr[sb + f]), m.x, d[f]);
+          if (f < nf) {
+#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 512)  // timing experiment: no frame loads (wrong pixels)
+            for (int u = 0; u < 5; ++u) d[f][u] = (uint32_t)(m.x * (u + 1));
+#else
+            ingest_run_load(as_global(frame_ptr[sb + f]), m.x, d[f]);
+#endif
+          }
       }
     }
   };
+  ING_PROF(1)
   fast_loads(tid);
   __syncthreads();
+  ING_PROF(2)
 
   for (int i = tid; i < nch; i += T) {
     if (i != tid) fast_loads(i);
@@ -437,6 +451,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
         }
         word[k >> 2] |= o << (8 * (k & 3));
       }
+#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 256)  // timing experiment: no crop stores unless the word is a sentinel
+      if ((word[0] ^ word[1] ^ word[2] ^ word[3]) == 0x9E3779B9u)
+#endif
       *reinterpret_cast<uint4*>(ext + (int64_t)(sb + f) * ext_slot_bytes + q) = make_uint4(word[0], word[1], word[2], word[3]);
       if (flag_chunk) {
         uint32_t ha = 0u, hb = 0u;
@@ -512,9 +529,16 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       emit(f, pw, sl, Rf, Cf);
     }
   }
+  ING_PROF(3)
 #if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 128)  // timing experiment: no flags, no lists
   return;
 #endif
+  if (!fl_band || !tl_list) {
+    if (pb && threadIdx.x == 0) {
+      pb[4] = clock64();
+      pb[15] = wall_clock64();
+    }
+  }
   if (!fl_band) return;
   // the band's flag bytes (each written by this block only: no zeroing pass)
   // and its bright tiles appended to the view's list (any order: the
@@ -550,6 +574,11 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
   uint32_t* __restrict__ out = tl_list + (int64_t)v * K.tl_stride +
                                (int64_t)lm_tl_y0(c, G) * LM_INGEST_FB * K.fl_tx[v] * K.fl_ty[v] + s_base;
   for (int p = tid; p < s_n; p += T) out[p] = s_ent[p];
+  if (pb && threadIdx.x == 0) {
+    pb[4] = clock64();
+    pb[15] = wall_clock64();
+  }
+#undef ING_PROF
 }
 
 #include "lm_corr.h"  // the correlation kernels are their own translation unit (lm_corr.hip)
@@ -1475,19 +1504,49 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 13] = n;
   int np = 1;
   while (np < n) np <<= 1;
-  if (!glob && n <= LM_NMS_THREADS) {
-    wave_merge_sort(a, stmp, n);
-  } else if (n <= LM_NMS_RANKSORT) {
-    rank_sort(a, stmp, n);
-  } else {
-    for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
+  // Exact score ties, found before sorting (an LDS hash set of the score
+  // bits, linear probing, at most half full): a tie list is re-sorted from
+  // row-major order by the std::sort replica below, so its (score, index)
+  // sort would be thrown away -- ~20k cycles of the slowest blocks.
+  const bool pre = !glob && 2 * n <= LM_NMS_CAP;
+  if (pre) {
+    int tb = 64;
+    while (tb < 2 * n) tb <<= 1;
+    unsigned* tab = reinterpret_cast<unsigned*>(s_tmp);
+    for (int k = threadIdx.x; k < tb; k += blockDim.x) tab[k] = 0u;  // 0: empty (a positive score's key is not 0)
     __syncthreads();
-    bitonic_sort(a, np);
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+      const unsigned h = (unsigned)(a[k] >> 32);
+      unsigned sl = (h * 2654435761u) & (unsigned)(tb - 1);
+      while (true) {
+        const unsigned old = atomicCAS(&tab[sl], 0u, h);
+        if (old == 0u) break;
+        if (old == h) {
+          s_flag = 1;
+          break;
+        }
+        sl = (sl + 1) & (unsigned)(tb - 1);
+      }
+    }
+    __syncthreads();
+  }
+  if (!(pre && s_flag)) {
+    if (!glob && n <= LM_NMS_THREADS) {
+      wave_merge_sort(a, stmp, n);
+    } else if (n <= LM_NMS_RANKSORT) {
+      rank_sort(a, stmp, n);
+    } else {
+      for (int k = n + threadIdx.x; k < np; k += blockDim.x) a[k] = ~0ull;
+      __syncthreads();
+      bitonic_sort(a, np);
+    }
   }
   NMS_PROF(2)
-  for (int k = threadIdx.x; k + 1 < n; k += blockDim.x)
-    if ((a[k] >> 32) == (a[k + 1] >> 32)) s_flag = 1;
-  __syncthreads();
+  if (!pre) {
+    for (int k = threadIdx.x; k + 1 < n; k += blockDim.x)
+      if ((a[k] >> 32) == (a[k + 1] >> 32)) s_flag = 1;
+    __syncthreads();
+  }
   const int tie = s_flag;
   if (tie) {  // (GLOB: the row-major re-sort below is the single-thread replica)
     // exact score tie: std::sort from the row-major order nmsMax builds (:1638-1648)

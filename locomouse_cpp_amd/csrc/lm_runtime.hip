@@ -115,6 +115,7 @@ struct Lane {
   DevBuf<uint32_t> dark_list;
   DevBuf<int32_t> dark_cnt;
   DevBuf<long long> kprof;  // LM_KPROF=1: kernel phase timestamps
+  DevBuf<long long> kprof_ing;  // LM_KPROF=1: k_ingest's, 16 per workgroup
   Arena arena[2];
   int parity = 0;
   // host
@@ -903,6 +904,36 @@ int corr_plan_for(const lm_ctx* c) {
 void kprof_report(lm_ctx* c, Lane& L, int n) {
   std::vector<long long> h((size_t)4 * 16 * 2 * c->nslots);
   COPY_SYNC(h.data(), L.kprof.p, h.size() * sizeof(long long), hipMemcpyDeviceToHost, L.stream);
+  if (L.kprof_ing.p) {  // k_ingest: phases 1-4 per workgroup, start spread (launch rounds)
+    const LmConst& K = c->K;
+    const size_t nb = (size_t)(K.ing_nb[0] + K.ing_nb[1]) * ((c->nslots + LM_INGEST_FB - 1) / LM_INGEST_FB);
+    std::vector<long long> g(16 * nb);
+    COPY_SYNC(g.data(), L.kprof_ing.p, g.size() * sizeof(long long), hipMemcpyDeviceToHost, L.stream);
+    double acc[8] = {0}, life = 0;
+    int cntb = 0;
+    long long t_min = 0, t_max = 0, s_max = 0;
+    std::vector<long long> starts;
+    for (size_t b = 0; b < nb; ++b) {
+      const long long* t = g.data() + b * 16;
+      if (!t[0] || !t[4]) continue;
+      for (int k = 1; k <= 4; ++k) acc[k] += (double)(t[k] - t[k - 1]);
+      life += (double)(t[4] - t[0]);
+      t_min = t_min ? std::min(t_min, t[14]) : t[14];
+      t_max = std::max(t_max, t[15]);
+      starts.push_back(t[14]);
+      ++cntb;
+    }
+    for (long long st0 : starts) s_max = std::max(s_max, st0 - t_min);
+    std::sort(starts.begin(), starts.end());
+    const double p50 = starts.empty() ? 0.0 : (starts[starts.size() / 2] - t_min) * 0.01;
+    const double p90 = starts.empty() ? 0.0 : (starts[starts.size() * 9 / 10] - t_min) * 0.01;
+    if (cntb) {
+      fprintf(stderr, "kprof k_ingest: blocks=%d life=%.0f cyc, span=%.1f us, start p50 %.1f p90 %.1f last %.1f us:", cntb,
+              life / cntb, (t_max - t_min) * 0.01, p50, p90, s_max * 0.01);
+      for (int k = 1; k <= 4; ++k) fprintf(stderr, " p%d=%.0f", k, acc[k] / cntb);
+      fprintf(stderr, "\n");
+    }
+  }
   {  // k_post (LDS instantiation): region 3, one block per (frame, feature)
     const long long* base = h.data() + (size_t)3 * 16 * 2 * c->nslots;
     double acc[8] = {0}, life = 0;
@@ -1068,10 +1099,17 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
     // ext crops of both views, and (dark tiles) the bright-tile flags and lists
     T.begin("k_ingest");
     const CorrDark dk = lane_dark(c, L);
+    long long* kpi = nullptr;
+    const size_t ing_blocks = (size_t)(K.ing_nb[0] + K.ing_nb[1]) * ((c->nslots + LM_INGEST_FB - 1) / LM_INGEST_FB);
+    if (c->kprof_on) {
+      if (!L.kprof_ing.p) L.kprof_ing.alloc(16 * ing_blocks);
+      HIPCHK(hipMemsetAsync(L.kprof_ing.p, 0, sizeof(long long) * 16 * ing_blocks, st));
+      kpi = L.kprof_ing.p;
+    }
     k_ingest<<<dim3((unsigned)(K.ing_nb[0] + K.ing_nb[1]), (unsigned)((nproc + LM_INGEST_FB - 1) / LM_INGEST_FB)),
                K.ing_threads, 0, st>>>(dK, L.frame_ptr.p, c->bkg.p, c->cal.p, L.luts.p, L.slots.p, s_proc0, n + 1, L.ext.p,
                                         c->ext_slot_bytes, reinterpret_cast<unsigned*>(L.tailbin.p), L.smap.p, L.sbkg.p,
-                                        L.skey.p, dk.flags, dk.cnt, dk.list);
+                                        L.skey.p, dk.flags, dk.cnt, dk.list, kpi);
     T.end();
   }
   if ((part == 1 || part < 0) && !(LM_EXP_SKIP & 16)) {
