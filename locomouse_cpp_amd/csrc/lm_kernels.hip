@@ -167,7 +167,11 @@ __global__ __launch_bounds__(256) void k_lut(const unsigned* __restrict__ mm, in
 // the frame's bottom crop I_BOTTOM_MOUSE in place (LUT(I_BOTTOM_MOUSE, table,
 // I_BOTTOM_MOUSE), LocoMouse_class.cpp:1445-1448), so that rectangle of I_PAD
 // holds table[v] for the rest of the frame and in I_PREV_PAD for the next.
-DEV bool in_gray_rect(const LmConst& K, const LmSlot& sl, int R, int C) {
+struct GrayRect {  // the LmConst fields in_gray_rect reads
+  int32_t unpad_y[1], unpad_x[1], bb_bottom_h, bb_bottom_w;
+};
+template <class KT>
+DEV bool in_gray_rect(const KT& K, const LmSlot& sl, int R, int C) {
   const int y = R - sl.crop_y[0] - K.unpad_y[0], x = C - sl.crop_x[0] - K.unpad_x[0];
   return (unsigned)y < (unsigned)K.bb_bottom_h && (unsigned)x < (unsigned)K.bb_bottom_w;
 }
@@ -200,37 +204,72 @@ DEV uint8_t ipad_pixel_t(FP __restrict__ F, const uint8_t* __restrict__ bkg, con
 static_assert(LM_FW >= LM_INGEST_VEC, "a 16-byte chunk spans at most two flag tiles");
 #define LM_INGEST_MAXTX 128  // flag-grid columns a band's workgroup can hold (ow <= 128 LM_FW)
 
-// Gather indices and background bytes of the 16 crop pixels that start at
-// I_PAD (R, C0) (-1 / 0 outside I_UNPAD); returns 1 when idx[k] = idx[0] + k
-// for all k, -1 when idx[k] = idx[0] - k (a flipped translation), else 0, and
-// sets lo to the first source byte of such a run.
-DEV int ingest_locate(const LmConst& K, const int32_t* __restrict__ cal, const uint8_t* __restrict__ bkg, int R, int C0,
-                      int (&idx)[LM_INGEST_VEC], uint32_t (&bw)[4], int& lo) {
+// Gather index of crop pixel I_PAD (R, C) (-1 outside I_UNPAD).
+DEV int ingest_index(const LmConst& K, const int32_t* __restrict__ cal, int R, int C) {
   const int r = R - K.pad_pre_rows;
-  bool up = true, down = true;
+  int c = C - K.pad_pre_cols;
+  if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) return -1;
+  if (K.flip) c = K.n_cols - 1 - c;
+  return cal[r * K.n_cols + c];
+}
+
+// Gather indices and background bytes of the 16 crop pixels that start at
+// I_PAD (R, C0) (0 background outside I_UNPAD).  inside: bit k set when
+// pixel k lies inside I_UNPAD.  Returns 1 when the inside pixels are a run
+// idx[k] = lo + k, -1 when idx[k] = lo + 15 - k (a flipped translation) --
+// a chunk at the pad's edge is a run too, its outside bytes masked to 0
+// after the LUT (I_PAD is zero outside I_UNPAD), and a chunk with no inside
+// pixel is an empty run -- else 0 (a gather).  lo is the first source byte
+// of the 20 the run's five dwords cover; a run whose dwords would leave the
+// frame is a gather.  (k_ingest keeps only run, lo, inside and the
+// background bytes: a gather re-reads the indices per frame, ingest_index,
+// so no 16-register index array stays live.)
+DEV int ingest_locate(const LmConst& K, const int32_t* __restrict__ cal, const uint8_t* __restrict__ bkg, int R, int C0,
+                      uint32_t (&bw)[4], int& lo, unsigned& inside) {
+  const int r = R - K.pad_pre_rows;
+  inside = 0u;
 #pragma unroll
   for (int j = 0; j < 4; ++j) bw[j] = 0u;
+  // one pass, no index array: the first inside pixel fixes the candidate
+  // runs' virtual idx[0] (up0 for a run, dn0 for a flipped one), the later
+  // ones are tested against them
+  int up0 = 0, dn0 = 0;
+  bool any = false, up = true, down = true;
 #pragma unroll
   for (int k = 0; k < LM_INGEST_VEC; ++k) {
     int c = C0 + k - K.pad_pre_cols;
-    if (r < 0 || r >= K.n_rows || c < 0 || c >= K.n_cols) {
-      idx[k] = -1;
-    } else {
+    if (r >= 0 && r < K.n_rows && c >= 0 && c < K.n_cols) {
       if (K.flip) c = K.n_cols - 1 - c;
-      idx[k] = cal[r * K.n_cols + c];
-      bw[k >> 2] |= (uint32_t)bkg[idx[k]] << (8 * (k & 3));
+      const int ix = cal[r * K.n_cols + c];
+      bw[k >> 2] |= (uint32_t)bkg[ix] << (8 * (k & 3));
+      inside |= 1u << k;
+      if (!any) {
+        up0 = ix - k;
+        dn0 = ix + k;
+        any = true;
+      } else {
+        up = up && ix == up0 + k;
+        down = down && ix == dn0 - k;
+      }
     }
-    up = up && idx[k] >= 0 && idx[k] == idx[0] + k;
-    down = down && idx[k] >= 0 && idx[k] == idx[0] - k;
+  }
+  if (!any) {  // no pixel inside I_UNPAD: all zeros
+    lo = 0;
+    return 1;
   }
   int run = up ? 1 : (down ? -1 : 0);
-  lo = up ? idx[0] : idx[0] - (LM_INGEST_VEC - 1);
-  if (run != 0 && (lo & ~3) + 20 > K.video_rows * K.video_cols) run = 0;  // the fifth dword would pass the frame end
+  lo = up ? up0 : dn0 - (LM_INGEST_VEC - 1);
+  if (run != 0 && (lo < 0 || (lo & ~3) + 20 > K.video_rows * K.video_cols)) run = 0;  // the dwords would leave the frame
   return run;
 }
 
+// 0xFF in byte j of the result for bit j of the 4-bit n (masking a word's
+// outside bytes)
+DEV uint32_t byte_keep4(uint32_t n) { return ((n * 0x00204081u) & 0x01010101u) * 0xFFu; }
+
 // Source map of one view's crop at a fixed position (cx, cy): per 16-byte
-// ext-crop chunk, {first source byte, run} and the 16 background bytes, so
+// ext-crop chunk, {first source byte, run code | inside mask} and the 16
+// background bytes, so
 // k_ingest's batches with their crop there (always, with a provided bounding
 // box) skip the calibration and background gathers (frame-invariant data,
 // LocoMouse_class.cpp:1337-1406).  key[2 v], key[2 v + 1] = the position.
@@ -248,12 +287,13 @@ __global__ __launch_bounds__(256) void k_srcmap(const LmConst* __restrict__ Kp, 
   }
   if (qq >= nv) return;
   const int er = (int)(qq / K.ext_w[v]), ec = (int)(qq % K.ext_w[v]);
-  int idx[LM_INGEST_VEC];
   uint32_t w[4];
   int lo;
-  const int run = ingest_locate(K, cal, bkg, cy + K.ext_oy[v] + er, cx + K.ext_ox[v] + ec, idx, w, lo);
+  unsigned inside;
+  const int run = ingest_locate(K, cal, bkg, cy + K.ext_oy[v] + er, cx + K.ext_ox[v] + ec, w, lo, inside);
   const int64_t ci = ((v ? e0 : 0) + qq) / LM_INGEST_VEC;
-  smap[ci] = make_int2(lo, run);
+  // y: run code (1 up, 2 down, 0 a gather) | inside mask << 16
+  smap[ci] = make_int2(lo, (run > 0 ? 1 : run < 0 ? 2 : 0) | (int)(inside << 16));
   sbkg[ci] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
@@ -287,8 +327,11 @@ DEV void ingest_run_load(const lm_gu8* F, int lo, uint32_t (&d)[5]) {
 #endif
 }
 
+#ifndef LM_INGEST_PIPE
+#define LM_INGEST_PIPE 3  // frames whose run loads are in flight at once
+#endif
 #ifndef LM_INGEST_WPE
-#define LM_INGEST_WPE 1  // amdgpu_waves_per_eu minimum (register budget experiments)
+#define LM_INGEST_WPE 5  // amdgpu_waves_per_eu minimum: <= 96 VGPRs, so 5 four-wave groups per CU (one round at C3)
 #endif
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_WPE, 8))) void k_ingest(const LmConst* __restrict__ Kp, const uint8_t* const* __restrict__ frame_ptr,
                                                  const uint8_t* __restrict__ bkg, const int32_t* __restrict__ cal,
@@ -344,6 +387,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
     s_n = 0;
     s_outs = 0;
   }
+  // the grey LUT's switch and rectangle, read once (in_gray_rect takes them from gk)
+  const bool gray_on = K.gray_lut_on != 0;
+  GrayRect gk;
+  gk.unpad_y[0] = K.unpad_y[0];
+  gk.unpad_x[0] = K.unpad_x[0];
+  gk.bb_bottom_h = K.bb_bottom_h;
+  gk.bb_bottom_w = K.bb_bottom_w;
   const LmSlot sl0 = slots[sb];
   bool same = true;
   for (int f = 1; f < nf; ++f)
@@ -356,10 +406,22 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
     ec = (i - rr * cw) * LM_INGEST_VEC;
     return i < nch && er >= 0 && er < K.ext_h[v];
   };
-  uint32_t d[LM_INGEST_FB][5];
+  // the run loads of frames f .. f + LM_INGEST_PIPE - 1 in flight at once:
+  // frame f's registers take frame f + LM_INGEST_PIPE's loads as soon as they
+  // are consumed, so the group needs LM_INGEST_PIPE x 5 registers for them,
+  // not LM_INGEST_FB x 5 (five waves per SIMD: the grid is one round)
+  constexpr int PIPE = LM_INGEST_PIPE;
+  uint32_t d[PIPE][5];
   int2 m = make_int2(0, 0);
   uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
-  // the fast path's loads of chunk i (source map entry, then the run's dwords)
+  auto frame_load = [&](int f, int lo_, uint32_t (&dd)[5]) {
+#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 512)  // timing experiment: no frame loads (wrong pixels)
+    for (int u = 0; u < 5; ++u) dd[u] = (uint32_t)(lo_ * (u + 1));
+#else
+    ingest_run_load(as_global(frame_ptr[sb + f]), lo_, dd);
+#endif
+  };
+  // the fast path's loads of chunk i (source map entry, then the first frames' run dwords)
   auto fast_loads = [&](int i) {
     int er, ec;
     const bool act = chunk_pos(i, er, ec);
@@ -368,16 +430,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       const int64_t ci = ((v ? e0 : 0) + (int64_t)er * ew + ec) / LM_INGEST_VEC;
       m = smap[ci];
       b4 = sbkg[ci];
-      if (m.y != 0) {
+      if ((m.y & 3) != 0) {
 #pragma unroll
-        for (int f = 0; f < LM_INGEST_FB; ++f)
-          if (f < nf) {
-#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 512)  // timing experiment: no frame loads (wrong pixels)
-            for (int u = 0; u < 5; ++u) d[f][u] = (uint32_t)(m.x * (u + 1));
-#else
-            ingest_run_load(as_global(frame_ptr[sb + f]), m.x, d[f]);
-#endif
-          }
+        for (int f = 0; f < PIPE; ++f)
+          if (f < nf) frame_load(f, m.x, d[f]);
       }
     }
   };
@@ -413,11 +469,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       }
     }
     const bool flag_chunk = (ma[0] | ma[1] | ma[2] | ma[3] | mb[0] | mb[1] | mb[2] | mb[3]) != 0u;
-    int idx[LM_INGEST_VEC];
     uint32_t bw[4];  // background bytes, packed
     int run = 0;  // 1: idx[k] = idx[0] + k, -1: idx[k] = idx[0] - k, 0: gather
     int lo = 0;   // a run's first source byte
-    bool allv = false;  // every pixel inside I_UNPAD (a run; idx[] not filled on the source-map path)
+    unsigned inside = 0xFFFFu;  // bit k: pixel k inside I_UNPAD (the others are masked to 0 after the LUT)
     // the 16 source bytes of a run span [lo, lo + 16): five aligned dwords cover them
     // (funnel shifts by the byte offset, then a byte reversal for a flipped run:
     // no register array is indexed with a run-time value, so nothing spills)
@@ -437,20 +492,26 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
     // background subtraction, the slot's LUT, the grey LUT, the 16-byte store
     // and the chunk's bright-tile bits (pixels and background bytes stay
     // packed four to a register)
-    auto emit = [&](int f, const uint32_t (&pw)[4], const LmSlot& sl, int R, int C0) {
+    // Pixels outside I_UNPAD (inside bit clear: the pad, or the background-
+    // and-LUT of a don't-care byte) are zeroed after the LUT, once per word.
+    // The grey LUT is a separate instantiation (GRAY, chosen once per
+    // kernel): a K field tested per byte made the compiler re-load it per
+    // byte and wait for it -- with the LUT read just issued, whose wait
+    // counter the scalar load shares -- so every byte's LDS read was waited
+    // for on its own.
+    auto emit = [&](int f, const uint32_t (&pw)[4], const LmSlot& sl, int R, int C0, unsigned in_mask, auto gray_c) {
+      constexpr bool GRAY = decltype(gray_c)::value;
       uint32_t word[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int k = 0; k < LM_INGEST_VEC; ++k) {
-        uint32_t o = 0;
-        if (allv || idx[k] >= 0) {
-          const uint32_t pk = (pw[k >> 2] >> (8 * (k & 3))) & 0xFFu, bk = (bw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-          o = lut[f][pk > bk ? pk - bk : 0];
-          if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) o = glut[o];
-        } else if (K.gray_lut_on && in_gray_rect(K, sl, R, C0 + k)) {
-          o = glut[0];  // only reachable through the pad (rejected on the host)
-        }
+        const uint32_t pk = (pw[k >> 2] >> (8 * (k & 3))) & 0xFFu, bk = (bw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        uint32_t o = lut[f][pk > bk ? pk - bk : 0];
+        // (the grey LUT's rectangle never reaches the pad: the host rejects that)
+        if (GRAY && in_gray_rect(gk, sl, R, C0 + k)) o = glut[o];
         word[k >> 2] |= o << (8 * (k & 3));
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) word[j] &= byte_keep4((in_mask >> (4 * j)) & 0xFu);
 #if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 256)  // timing experiment: no crop stores unless the word is a sentinel
       if ((word[0] ^ word[1] ^ word[2] ^ word[3]) == 0x9E3779B9u)
 #endif
@@ -469,10 +530,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
     };
 
     const int R = sl0.crop_y[v] + K.ext_oy[v] + er, C0 = sl0.crop_x[v] + K.ext_ox[v] + ec;
-    if (mapped && m.y != 0) {  // the source map holds this crop position: no calibration / background gathers
-      run = m.y;
+    if (mapped && (m.y & 3) != 0) {  // the source map holds this crop position: no calibration / background gathers
+      run = (m.y & 3) == 1 ? 1 : -1;
       lo = m.x;
-      allv = true;
+      inside = (unsigned)m.y >> 16;
       bw[0] = b4.x;
       bw[1] = b4.y;
       bw[2] = b4.z;
@@ -481,28 +542,35 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       for (int f = 0; f < LM_INGEST_FB; ++f)
         if (f < nf) {
           uint32_t pw[4];
-          run_bytes(d[f], pw);
-          emit(f, pw, slots[sb + f], R, C0);
+          run_bytes(d[f % PIPE], pw);
+          if (f + PIPE < nf) frame_load(f + PIPE, lo, d[f % PIPE]);
+          if (gray_on) emit(f, pw, slots[sb + f], R, C0, inside, std::true_type{});
+          else emit(f, pw, sl0, R, C0, inside, std::false_type{});
         }
       continue;
     }
-    run = ingest_locate(K, cal, bkg, R, C0, idx, bw, lo);
+    run = ingest_locate(K, cal, bkg, R, C0, bw, lo, inside);
     if (same && run != 0) {
       // Every slot of the group has its crop at the same place and the pixels
-      // are a run, but the source map does not hold it: all the group's frame
-      // loads are issued before any is used.
+      // are a run, but the source map does not hold it: the group's frame
+      // loads are issued PIPE ahead of their use.
 #pragma unroll
-      for (int f = 0; f < LM_INGEST_FB; ++f)
-        if (f < nf) ingest_run_load(as_global(frame_ptr[sb + f]), lo, d[f]);
+      for (int f = 0; f < PIPE; ++f)
+        if (f < nf) frame_load(f, lo, d[f]);
 #pragma unroll
       for (int f = 0; f < LM_INGEST_FB; ++f)
         if (f < nf) {
           uint32_t pw[4];
-          run_bytes(d[f], pw);
-          emit(f, pw, slots[sb + f], R, C0);
+          run_bytes(d[f % PIPE], pw);
+          if (f + PIPE < nf) frame_load(f + PIPE, lo, d[f % PIPE]);
+          if (gray_on) emit(f, pw, slots[sb + f], R, C0, inside, std::true_type{});
+          else emit(f, pw, sl0, R, C0, inside, std::false_type{});
         }
       continue;
     }
+#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 1024)  // timing experiment: no general-path chunks (wrong pixels)
+    continue;
+#endif
     // General case: frame by frame, the indices recomputed whenever the crop moves.
     int px = sl0.crop_x[v], py = sl0.crop_y[v];
     for (int f = 0; f < nf; ++f) {
@@ -513,7 +581,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       if (sl.crop_x[v] != px || sl.crop_y[v] != py) {  // crop moved: recompute the gather indices
         px = sl.crop_x[v];
         py = sl.crop_y[v];
-        run = ingest_locate(K, cal, bkg, Rf, Cf, idx, bw, lo);
+        run = ingest_locate(K, cal, bkg, Rf, Cf, bw, lo, inside);
       }
       const lm_gu8* __restrict__ F = as_global(frame_ptr[slot]);
       uint32_t pw[4] = {0, 0, 0, 0};
@@ -524,9 +592,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       } else {
 #pragma unroll
         for (int k = 0; k < LM_INGEST_VEC; ++k)
-          if (idx[k] >= 0) pw[k >> 2] |= (uint32_t)F[idx[k]] << (8 * (k & 3));
+          if ((inside >> k) & 1u) pw[k >> 2] |= (uint32_t)F[ingest_index(K, cal, Rf, Cf + k)] << (8 * (k & 3));
       }
-      emit(f, pw, sl, Rf, Cf);
+      if (gray_on) emit(f, pw, sl, Rf, Cf, inside, std::true_type{});
+      else emit(f, pw, sl, Rf, Cf, inside, std::false_type{});
     }
   }
   ING_PROF(3)
