@@ -1533,6 +1533,9 @@ DEV double readlane_f64(double v, int lane) {
 // Kept as two instantiations so the common case never goes through generic
 // (FLAT) pointers, which cost several times the latency of LDS accesses.
 // optional phase timestamps (LM_KPROF=1): clock64() of thread 0 per phase
+#ifndef LM_NMS_PREHASH
+#define LM_NMS_PREHASH 1
+#endif
 #define NMS_PROF(k) \
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + (k)] = clock64();
 template <bool GLOB>
@@ -1577,19 +1580,25 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   // bits, linear probing, at most half full): a tie list is re-sorted from
   // row-major order by the std::sort replica below, so its (score, index)
   // sort would be thrown away -- ~20k cycles of the slowest blocks.
-  const bool pre = !glob && 2 * n <= LM_NMS_CAP;
+  const bool pre = LM_NMS_PREHASH && !glob && 2 * n <= LM_NMS_CAP;
   if (pre) {
-    int tb = 64;
-    while (tb < 2 * n) tb <<= 1;
+    int tb = 64, lg = 6;
+    while (tb < 2 * n) {
+      tb <<= 1;
+      ++lg;
+    }
     unsigned* tab = reinterpret_cast<unsigned*>(s_tmp);
-    for (int k = threadIdx.x; k < tb; k += blockDim.x) tab[k] = 0u;  // 0: empty (a positive score's key is not 0)
+    for (int k = threadIdx.x; k < tb; k += blockDim.x) tab[k] = ~0u;  // empty: a NaN pattern no score has
     __syncthreads();
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
       const unsigned h = (unsigned)(a[k] >> 32);
-      unsigned sl = (h * 2654435761u) & (unsigned)(tb - 1);
+      // Fibonacci hashing: the product's HIGH bits, which every bit of the
+      // score feeds (scores of a smooth map often share their low mantissa
+      // bits, and the low bits of the product only see those)
+      unsigned sl = (h * 2654435761u) >> (32 - lg);
       while (true) {
-        const unsigned old = atomicCAS(&tab[sl], 0u, h);
-        if (old == 0u) break;
+        const unsigned old = atomicCAS(&tab[sl], ~0u, h);
+        if (old == ~0u) break;
         if (old == h) {
           s_flag = 1;
           break;
