@@ -51,6 +51,12 @@ def main(root, batch, out=None):
                           "calibrated for the kernel's 4-B/lane and 16-B/lane loads in profiles/r03/fetch_calib.json"
                        for k in corr},
         "write_correction": "WRITE_SIZE as reported",
+        # k_ingest per batch (one dispatch): its 16-B and 4-B run loads and byte
+        # loads are calibrated at 0.50 too (profiles/r03/fetch_calib.json)
+        "k_ingest": ({"fetch_bytes_per_batch": int(2 * fetch["k_ingest"] * 1024),
+                      "write_bytes_per_batch": int(write.get("k_ingest", 0.0) * 1024),
+                      "hbm_bytes_per_batch": int((2 * fetch["k_ingest"] + write.get("k_ingest", 0.0)) * 1024),
+                      "correction": "FETCH_SIZE x2, WRITE_SIZE as reported"} if "k_ingest" in fetch else None),
         "all_kernels_kib_per_dispatch": {k: {"fetch": round(fetch[k], 1), "write": round(write.get(k, 0.0), 1)}
                                          for k in sorted(fetch)},
     }
