@@ -119,6 +119,7 @@ static inline float f16_bfrag_weight(const double* w, int kw, int i, int c, int 
 // k_corr_rw's ring does not depend on the detector height: every width of
 // LM_KW_LIST, any kh; other widths run k_corr_gen
 bool corr_ring(int kw);
+void rwprof_report();  // LM_RW_PROF builds: ring-kernel wave summary (stderr)
 const void* corr_kernel(int kw, bool unf);     // k_corr_rw<kw> or k_corr_gen
 const void* corr_kernel_rw_all(bool unf);      // every ring width in one launch
 const void* corr_kernel_f16(int kw);           // nullptr when kw is too wide

@@ -26,7 +26,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <map>
 #include <type_traits>
+#include <vector>
 
 #include "lm_corr.h"
 
@@ -427,6 +431,9 @@ DEV void rw_pair_1(lm_f2 (&a)[PK_C], lm_f2 w, const lm_f2* px) {
 #undef LM_RW_S0
 #undef LM_RW_S1
 
+#ifndef LM_RW_EXP
+#define LM_RW_EXP 0  // timing experiments (wrong scores): 1 no weight loads, 2 no pixel reads, 4 no chunk-start wait
+#endif
 template <int KW, bool UNF>
 struct RwPipe {
   using P = RwPlan<KW>;
@@ -437,7 +444,7 @@ struct RwPipe {
 
   template <int Q0, int Q1>
   DEV void issue(unsigned base) {
-    if constexpr (Q0 < Q1) {
+    if constexpr (Q0 < Q1 && !(LM_RW_EXP & 2)) {  // (timing experiment 2: no pixel reads)
       lds_pair_nw<STR, Q0>(px[Q0], base);
       issue<Q0 + 1, Q1>(base);
     }
@@ -448,8 +455,13 @@ struct RwPipe {
                   const lm_f2* __restrict__ rb) {
 #pragma unroll
     for (int q = 0; q < P::qe(C) - P::qb(C); ++q) {
+#if LM_RW_EXP & 1  // timing experiment: no weight loads (wrong scores)
+      na[q] = wa[q];
+      nb[q] = wb[q];
+#else
       na[q] = ra[P::qb(C) + q];
       nb[q] = rb[P::qb(C) + q];
+#endif
     }
   }
   template <int J, int C, bool A, bool B>
@@ -486,7 +498,7 @@ struct RwPipe {
                   const lm_f2* __restrict__ ra_n, const lm_f2* __restrict__ rb_n, F&& at_start) {
     // lgkmcnt(0) through the builtin (vmcnt / expcnt left at their maxima), so
     // the compiler's own wait insertion knows the scalar loads are done too
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if constexpr (!(LM_RW_EXP & 4)) __builtin_amdgcn_s_waitcnt(0xC07F);  // (timing experiment 4: no wait here)
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (C == 0) at_start();
     lm_f2 na[P::PMAX], nb[P::PMAX];
@@ -822,6 +834,47 @@ DEV int xcd_block(int b, int nb) {
 #endif
 }
 
+// LM_RW_PROF=1 (experiment builds only): one record per ring-kernel wave --
+// wall-clock start and end, its cycles, the SIMD it ran on and its tap-steps
+// -- read back and summarised by rwprof_report() (after each batch under
+// LM_KPROF=1): how much of a launch the SIMDs hold waves, and how fast the
+// waves run while they do.
+#ifndef LM_RW_PROF
+#define LM_RW_PROF 0
+#endif
+#if LM_RW_PROF
+#define LM_RWPROF_CAP (1 << 17)
+__device__ unsigned long long g_rwprof[4 * LM_RWPROF_CAP];
+__device__ unsigned g_rwprof_n;
+DEV void rwprof_record(long long t0w, long long t0c, int work, int items) {
+  if ((threadIdx.x & 63) != 0) return;
+  unsigned hw, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const long long t1c = clock64(), t1w = wall_clock64();
+  const unsigned i = atomicAdd(&g_rwprof_n, 1u);
+  if (i >= LM_RWPROF_CAP) return;
+  unsigned long long* r = g_rwprof + 4 * (size_t)i;
+  r[0] = (unsigned long long)t0w;
+  r[1] = (unsigned long long)t1w;
+  r[2] = (unsigned long long)(t1c - t0c) | ((unsigned long long)items << 40);
+  r[3] = (unsigned long long)hw | ((unsigned long long)(xcc & 15) << 32) | ((unsigned long long)work << 36);
+}
+#define RWPROF_BEGIN                                     \
+  const long long rwp_t0w = wall_clock64(), rwp_t0c = clock64(); \
+  int rwp_work = 0, rwp_items = 0;
+#define RWPROF_ITEM(D) \
+  rwp_work += ((D).kh + 2) * (D).kw;    \
+  ++rwp_items;
+#define RWPROF_END rwprof_record(rwp_t0w, rwp_t0c, rwp_work, rwp_items);
+#define RWPROF_STOP break
+#else
+#define RWPROF_BEGIN
+#define RWPROF_ITEM(D)
+#define RWPROF_END
+#define RWPROF_STOP return
+#endif
+
 // One launch per width group (LM_KW_LIST widths).
 template <int KW, bool UNF>
 // waves per SIMD: LDS allows 5 (80-column sub-tiles, kw <= 32) or 4
@@ -838,12 +891,15 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
   // LM_RW_ITEMS work items per wave, strided by the launch's wave count (the
   // host sizes the grid for that many)
   const int nwaves = gridDim.x * LM_RW_WAVES;
+  RWPROF_BEGIN
   for (int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
     int d;
     RwTiles H;
-    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) return;
+    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) RWPROF_STOP;
+    RWPROF_ITEM(K.det[d])
     rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);
   }
+  RWPROF_END
 }
 
 // Every ring detector of the context in ONE launch (longest first), so the
@@ -864,11 +920,13 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(L
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * G.ring_floats;
   const int nwaves = gridDim.x * LM_RW_WAVES;
+  RWPROF_BEGIN
   for (int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
     int d;
     RwTiles H;
-    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) return;
+    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) RWPROF_STOP;
     const LmDet D = K.det[d];
+    RWPROF_ITEM(D)
     switch (D.kw_ring) {
 #define LM_KW_CASE(n)                                                                                             \
   case n:                                                                                                         \
@@ -880,6 +938,7 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(L
         break;
     }
   }
+  RWPROF_END
 }
 
 // ---------------------------------------------------------------- k_corr_gen
@@ -1291,4 +1350,66 @@ hipError_t launch_corr_dbg(bool unf, dim3 grid, hipStream_t st, const LmConst* K
   else
     k_corr_dbg<false><<<grid, 256, 0, st>>>(K, ext, ext_slot_bytes, weights, s0, dbg, dbg_off, dbg_slot_floats);
   return hipGetLastError();
+}
+
+// LM_RW_PROF builds: summary of the ring-kernel wave records since the last
+// call (stderr), then the record counter reset.  Work unit: a wave's tap
+// steps, sum over its items of (kh + 2) kw; each is 10 v_pk_fma_f32 per lane
+// (5 columns x 2 row pairs), 4 cycles each on a SIMD.
+void rwprof_report() {
+#if LM_RW_PROF
+  unsigned n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_rwprof_n), sizeof n) != hipSuccess) return;
+  n = n < LM_RWPROF_CAP ? n : LM_RWPROF_CAP;
+  std::vector<unsigned long long> r(4 * (size_t)n);
+  if (n && hipMemcpyFromSymbol(r.data(), HIP_SYMBOL(g_rwprof), r.size() * sizeof(unsigned long long)) != hipSuccess)
+    return;
+  const unsigned zero = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rwprof_n), &zero, sizeof zero);
+  if (!n) return;
+  unsigned long long w0 = ~0ull, w1 = 0;
+  double cyc = 0, wall = 0, work = 0;
+  long items = 0;
+  std::map<unsigned long long, std::vector<std::pair<unsigned long long, unsigned long long>>> simd;
+  std::vector<double> life;
+  for (unsigned i = 0; i < n; ++i) {
+    const unsigned long long* q = &r[4 * (size_t)i];
+    w0 = std::min(w0, q[0]);
+    w1 = std::max(w1, q[1]);
+    cyc += (double)(q[2] & ((1ull << 40) - 1));
+    items += (long)(q[2] >> 40);
+    wall += (double)(q[1] - q[0]);
+    work += (double)(q[3] >> 36);
+    life.push_back((double)(q[1] - q[0]));
+    // SIMD key: XCC, SE, SH, CU, SIMD (HW_ID bits 15:4)
+    const unsigned long long key = (((q[3] >> 32) & 15) << 16) | ((q[3] >> 4) & 0xFFF);
+    simd[key].push_back({q[0], q[1]});
+  }
+  double active = 0;  // sum over SIMDs of the union of their waves' lifetimes (wall ticks)
+  for (auto& kv : simd) {
+    auto& v = kv.second;
+    std::sort(v.begin(), v.end());
+    unsigned long long a = v[0].first, b = v[0].second;
+    for (auto& iv : v) {
+      if (iv.first > b) {
+        active += (double)(b - a);
+        a = iv.first;
+        b = iv.second;
+      } else {
+        b = std::max(b, iv.second);
+      }
+    }
+    active += (double)(b - a);
+  }
+  std::sort(life.begin(), life.end());
+  const double clk = cyc / wall;  // shader cycles per wall tick (100 MHz)
+  const double span = (double)(w1 - w0);
+  const double fma_cyc = work * 10 * 4;
+  fprintf(stderr,
+          "rwprof: waves %u items %ld span %.1f us clock %.2f GHz simds %zu | simd-active %.3f of 1024 x span | "
+          "waves per active simd %.2f | pk-fma busy while active %.3f, over span %.3f | life p50 %.1f p90 %.1f max %.1f us\n",
+          n, items, span / 100.0, clk / 10.0, simd.size(), active / (1024.0 * span), wall / active,
+          fma_cyc / (active * clk), fma_cyc / (1024.0 * span * clk), life[life.size() / 2] / 100.0,
+          life[life.size() * 9 / 10] / 100.0, life.back() / 100.0);
+#endif
 }

@@ -1533,14 +1533,6 @@ DEV double readlane_f64(double v, int lane) {
 // Kept as two instantiations so the common case never goes through generic
 // (FLAT) pointers, which cost several times the latency of LDS accesses.
 // optional phase timestamps (LM_KPROF=1): clock64() of thread 0 per phase
-// lists of at most this many keys sorted by rank_sort instead of
-// wave_merge_sort (score sort; row-major re-sort of a tie list)
-#ifndef LM_NMS_RANK_SMALL
-#define LM_NMS_RANK_SMALL 0
-#endif
-#ifndef LM_NMS_RANK_SMALL_TIE
-#define LM_NMS_RANK_SMALL_TIE 0
-#endif
 #ifndef LM_NMS_PREHASH
 #define LM_NMS_PREHASH 1
 #endif
@@ -1617,9 +1609,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
     __syncthreads();
   }
   if (!(pre && s_flag)) {
-    if (!glob && n <= LM_NMS_RANK_SMALL) {
-      rank_sort(a, stmp, n);
-    } else if (!glob && n <= LM_NMS_THREADS) {
+    if (!glob && n <= LM_NMS_THREADS) {
       wave_merge_sort(a, stmp, n);
     } else if (n <= LM_NMS_RANKSORT) {
       rank_sort(a, stmp, n);
@@ -1649,9 +1639,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
     __syncthreads();
     NMS_PROF(8)
     if (!glob) {
-      if (n <= LM_NMS_RANK_SMALL_TIE) {  // back to row-major order
-        rank_sort(a, stmp, n);
-      } else if (n <= LM_NMS_THREADS) {
+      if (n <= LM_NMS_THREADS) {  // back to row-major order
         wave_merge_sort(a, stmp, n);
       } else if (n <= LM_NMS_RANKSORT) {
         rank_sort(a, stmp, n);

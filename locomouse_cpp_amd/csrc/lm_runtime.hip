@@ -1554,7 +1554,10 @@ void finish_batch(lm_ctx* c, Lane& L) {
     L.t_ev.clear();
     for (int k = 0; k < 4; ++k) L.t_work[k] = -1;
   }
-  if (c->kprof_on) kprof_report(c, L, n);
+  if (c->kprof_on) {
+    kprof_report(c, L, n);
+    rwprof_report();
+  }
 
   // ---- the packed results (lm_batch_result layout) are in the batch's
   // buffer unless they outgrew it: then grow it and let k_out copy them (and
