@@ -224,9 +224,10 @@ struct RwTiles {
   int nvalid;         // sub-tiles 0 .. nvalid - 1 hold a tile
   int ftx;            // listed: flag-grid columns of the view
   int slot, oy, ox;   // one tile: its slot and origin
-  DEV void get(int i, int& s, int& y, int& x) const {
+  // sub-tile i's list entry (listed; 0 otherwise), and its decoding
+  DEV uint32_t raw(int i) const { return l ? l[i < nvalid ? i : 0] : 0u; }
+  DEV void dec(uint32_t e, int i, int& s, int& y, int& x) const {
     if (l) {
-      const uint32_t e = l[i < nvalid ? i : 0];
       const int lt = (int)(e & 0xFFFFu);
       s = (int)(e >> 16);
       y = (lt / ftx) * LM_FH;
@@ -237,6 +238,7 @@ struct RwTiles {
       x = ox + (i % LM_RW_NQX) * LM_FW;
     }
   }
+  DEV void get(int i, int& s, int& y, int& x) const { dec(raw(i), i, s, y, x); }
 };
 
 // Wave g of a ring launch -> its detector and sub-tiles.  The batch's work
@@ -254,7 +256,7 @@ struct RwTiles {
 // (row-major).  Called by every lane of the wave; false: past the last wave.
 static_assert(LM_TL_NC == 64, "one list counter per lane");
 DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, const int32_t* tl_cnt,
-                        const uint32_t* tl_list, int& d, RwTiles& H) {
+                        const uint32_t* tl_list, int& d, RwTiles& H, const int* cnc = nullptr) {
   constexpr int NQ = LM_RW_NQ;
   const int lane = threadIdx.x & 63;
   int base = 0;
@@ -266,7 +268,7 @@ DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s
     const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
     if (tl_cnt != nullptr && D.kind == 0) {
       const int v = D.view;
-      const int cn = tl_cnt[v * LM_TL_NC + lane];  // segment `lane`'s bright tiles
+      const int cn = cnc ? cnc[v] : tl_cnt[v * LM_TL_NC + lane];  // segment `lane`'s bright tiles (cnc: read before)
       const int wv = (cn + NQ - 1) / NQ;
       int P = wv;  // inclusive scan: waves of segments 0 .. lane
 #pragma unroll
@@ -533,12 +535,54 @@ struct RwPipe {
 // so rows t .. t + 5 are live; row t + HS is loaded at the step's start and
 // stored at its end into row t's slot.  A wave's LDS operations run in order,
 // so no barrier anywhere.
-template <int KW, bool UNF>
+struct RwNoHook {
+  DEV void operator()() const {}
+};
+// The list entries a wave of width KW reads for one work item: its lane's
+// sub-tile (pe[0]) and the sub-tile of each of its window-row loads
+// (pe[1 + k]).  rw_tile takes them read ahead (LM_RW_NEXT), so an item's
+// first global reads are its window rows, not entries then rows.
+template <int KW>
+struct RwGeom {
+  static constexpr int NQ = LM_RW_NQ;
+  static constexpr int QX = LM_FW / PK_C;  // lanes across a sub-tile
+  static constexpr int QY = LM_FH / PK_R;  // row groups (lanes down) of a sub-tile
+  static constexpr int LG = 64 / QY;       // lanes per row group of the wave
+  static constexpr int NL = (3 + LM_FW + KW - 1 + 3) / 4;  // dwords of a sub-tile's window row
+  static constexpr int NLD = (NQ * NL + 63) / 64;          // dwords a lane loads per row
+  static constexpr int NE = NLD + 1;                       // list entries per lane and item
+};
+template <int KW>
+DEV void rw_fetch_entries(const RwTiles& H, uint32_t (&pe)[RwGeom<KW>::NE]) {
+  using Gm = RwGeom<KW>;
+  const int lane = threadIdx.x & 63;
+  pe[0] = H.raw((lane % Gm::LG) / Gm::QX);
+#pragma unroll
+  for (int k = 0; k < Gm::NLD; ++k) pe[1 + k] = H.raw(min((lane + 64 * k) / Gm::NL, Gm::NQ - 1));
+}
+
+// the same for a width known at run time (the merged launch's next item):
+// entries for up to 4 row loads per lane (the widest layout; the unused ones
+// are valid reads)
+DEV void rw_fetch_entries_rt(const RwTiles& H, int kw, uint32_t (&pe)[5]) {
+  using Gm = RwGeom<16>;
+  const int lane = threadIdx.x & 63, nl = (3 + LM_FW + kw - 1 + 3) / 4;
+  pe[0] = H.raw((lane % Gm::LG) / Gm::QX);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) pe[1 + k] = H.raw(min((lane + 64 * k) / nl, Gm::NQ - 1));
+}
+
+template <int KW, bool UNF, typename Hook = RwNoHook>
 DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D, const RwTiles& H, float* ring,
                                                 const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
                                                 const float* __restrict__ weights,
                                                 unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes) {
+                                                uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
+                                                long long* ph = nullptr, const uint32_t* pe = nullptr,
+                                                Hook hook = Hook{}) {
+  (void)ph;  // LM_RW_PROF builds: clocks at the step loop's start and end
+  // pe: this item's list entries read ahead (rw_fetch_entries), or null;
+  // hook: called once, right after the first window rows' reads are issued
   constexpr int NQ = LM_RW_NQ, NQX = LM_RW_NQX;
   constexpr int QX = LM_FW / PK_C;  // lanes across a sub-tile
   constexpr int QY = LM_FH / PK_R;  // row groups (lanes down) of a sub-tile
@@ -564,7 +608,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   // the lane's sub-tile (in VGPRs from here on: the merged kernel's SGPRs
   // are full)
   int slot, oy0, ox0;
-  H.get(q, slot, oy0, ox0);
+  H.dec(pe ? pe[0] : H.raw(q), q, slot, oy0, ox0);
   const bool valid = q < H.nvalid;
   const int mis = (int)((uintptr_t)corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0) & 3);
   // row loads: load k of a lane is dword dk of sub-tile qk's window row
@@ -577,7 +621,8 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     const int e = lane + 64 * k, qk = e / NL, dk = e - qk * NL;
     lk[k] = qk < H.nvalid;
     int sk, yk, xk;
-    H.get(min(qk, NQ - 1), sk, yk, xk);  // lanes past the last sub-tile: a valid address, the value unused
+    const int ik = min(qk, NQ - 1);  // lanes past the last sub-tile: a valid address, the value unused
+    H.dec(pe ? pe[1 + k] : H.raw(ik), ik, sk, yk, xk);
     const uint8_t* s = corr_src(K, D, ext, ext_slot_bytes, sk, yk, xk);
     la[k] = reinterpret_cast<const unsigned*>(s - ((uintptr_t)s & 3)) + dk;
     lo[k] = qk * QP + 4 * dk;
@@ -634,6 +679,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     Row v0[HS];
 #pragma unroll
     for (int r = 0; r < HS; ++r) v0[r] = load_row(r);
+    hook();  // the next item's entry reads, queued behind this item's rows
 #pragma unroll
     for (int r = 0; r < HS; ++r) store_row(r, v0[r]);
   }
@@ -681,6 +727,9 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     if constexpr (decltype(N)::value) store_row(t + HS, st);  // the last step stores no row (t + HS >= nrows)
   };
   Row r0 = load_row(HS), r1;
+#if LM_RW_PROF
+  ph[0] = clock64();
+#endif
   {  // kh >= 2: the host runs one-row detectors on k_corr_gen
     // pair 0 (tap row t) runs while t < kh, pair 1 (tap row t - 2) from t = 2
     stepx(0, T1{}, F0{}, r0, r1, T1{});
@@ -724,6 +773,9 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   for (; t < kh + 2; ++t) step(t, F0{}, T1{});
 #endif
   __builtin_amdgcn_s_waitcnt(0xC07F);  // the last (unused) prefetch
+#if LM_RW_PROF
+  ph[1] = clock64();
+#endif
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -844,9 +896,9 @@ DEV int xcd_block(int b, int nb) {
 #endif
 #if LM_RW_PROF
 #define LM_RWPROF_CAP (1 << 17)
-__device__ unsigned long long g_rwprof[4 * LM_RWPROF_CAP];
+__device__ unsigned long long g_rwprof[8 * LM_RWPROF_CAP];
 __device__ unsigned g_rwprof_n;
-DEV void rwprof_record(long long t0w, long long t0c, int work, int items) {
+DEV void rwprof_record(long long t0w, long long t0c, int work, int items, const long long* ph3) {
   if ((threadIdx.x & 63) != 0) return;
   unsigned hw, xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -854,32 +906,54 @@ DEV void rwprof_record(long long t0w, long long t0c, int work, int items) {
   const long long t1c = clock64(), t1w = wall_clock64();
   const unsigned i = atomicAdd(&g_rwprof_n, 1u);
   if (i >= LM_RWPROF_CAP) return;
-  unsigned long long* r = g_rwprof + 4 * (size_t)i;
+  unsigned long long* r = g_rwprof + 8 * (size_t)i;
   r[0] = (unsigned long long)t0w;
   r[1] = (unsigned long long)t1w;
   r[2] = (unsigned long long)(t1c - t0c) | ((unsigned long long)items << 40);
   r[3] = (unsigned long long)hw | ((unsigned long long)(xcc & 15) << 32) | ((unsigned long long)work << 36);
+  r[4] = (unsigned long long)ph3[0];  // cycles in rw_tile before its step loop (window rows, mask bytes)
+  r[5] = (unsigned long long)ph3[1];  // in the step loop
+  r[6] = (unsigned long long)ph3[2];  // after it (keys / tail bits)
+  r[7] = 0;
 }
 #define RWPROF_BEGIN                                     \
   const long long rwp_t0w = wall_clock64(), rwp_t0c = clock64(); \
-  int rwp_work = 0, rwp_items = 0;
+  int rwp_work = 0, rwp_items = 0;                                 \
+  long long rwp_ph[2], rwp_acc[3] = {0, 0, 0}, rwp_te = 0;
 #define RWPROF_ITEM(D) \
   rwp_work += ((D).kh + 2) * (D).kw;    \
-  ++rwp_items;
-#define RWPROF_END rwprof_record(rwp_t0w, rwp_t0c, rwp_work, rwp_items);
+  ++rwp_items;                          \
+  rwp_te = clock64();
+#define RWPROF_PH rwp_ph
+#define RWPROF_AFTER                     \
+  {                                      \
+    const long long tx = clock64();      \
+    rwp_acc[0] += rwp_ph[0] - rwp_te;    \
+    rwp_acc[1] += rwp_ph[1] - rwp_ph[0]; \
+    rwp_acc[2] += tx - rwp_ph[1];        \
+  }
+#define RWPROF_END rwprof_record(rwp_t0w, rwp_t0c, rwp_work, rwp_items, rwp_acc);
 #define RWPROF_STOP break
 #else
 #define RWPROF_BEGIN
 #define RWPROF_ITEM(D)
 #define RWPROF_END
+#define RWPROF_PH nullptr
+#define RWPROF_AFTER
 #define RWPROF_STOP return
 #endif
 
+#ifndef LM_RW_NEXT
+#define LM_RW_NEXT 0  // per-width launches: next item's list entries read during the current one
+#endif
 // One launch per width group (LM_KW_LIST widths).
 template <int KW, bool UNF>
 // waves per SIMD: LDS allows 5 (80-column sub-tiles, kw <= 32) or 4
 // (40-column); the register budget is set to match
-__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? (LM_FW == 40 ? 4 : 5) : 1, 8))) void k_corr_rw(
+#ifndef LM_RW_WPE
+#define LM_RW_WPE (LM_FW == 40 ? 4 : 5)
+#endif
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? LM_RW_WPE : 1, 8))) void k_corr_rw(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
     int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
@@ -892,13 +966,52 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
   // host sizes the grid for that many)
   const int nwaves = gridDim.x * LM_RW_WAVES;
   RWPROF_BEGIN
+#if LM_RW_NEXT
+  // Each wave works up to LM_RW_ITEMS items one after another and reads the
+  // next item's list entries during the current one, right after the
+  // current item's first window rows, so an item's start waits for one
+  // global read (its rows) instead of two (entries, then rows).  Waves that
+  // all started together otherwise stall together at every item's start.
+  // Only g and the entries cross an item.
+  constexpr int NE = RwGeom<KW>::NE;
+  const int lane = threadIdx.x & 63;
+  int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave;
+  uint32_t pe[NE];
+  for (int it = 0;; ++it) {
+    int cnc[2] = {0, 0};  // the dark-tile counters (L1 hits after the first item)
+    if (tl_cnt != nullptr) {
+      cnc[0] = tl_cnt[lane];
+      cnc[1] = tl_cnt[LM_TL_NC + lane];
+    }
+    const int* cp = tl_cnt != nullptr ? cnc : nullptr;
+    int d, dn;
+    RwTiles H, Hn;
+    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H, cp)) break;
+    if (it == 0) rw_fetch_entries<KW>(H, pe);
+    const bool okn = it + 1 < LM_RW_ITEMS && corr_locate_rw(K, G, nslots, s0, g + nwaves, tl_cnt, tl_list, dn, Hn, cp);
+    uint32_t pen[NE];
+    RWPROF_ITEM(K.det[d])
+    rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes,
+                     RWPROF_PH, pe, [&]() {
+                       if (okn) rw_fetch_entries<KW>(Hn, pen);
+                     });
+    RWPROF_AFTER
+    if (!okn) break;
+    g += nwaves;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) pe[k] = pen[k];
+  }
+#else
   for (int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
     int d;
     RwTiles H;
     if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) RWPROF_STOP;
     RWPROF_ITEM(K.det[d])
-    rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);
+    rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes,
+                     RWPROF_PH);
+    RWPROF_AFTER
   }
+#endif
   RWPROF_END
 }
 
@@ -921,6 +1034,49 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(L
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * G.ring_floats;
   const int nwaves = gridDim.x * LM_RW_WAVES;
   RWPROF_BEGIN
+#if LM_RW_NEXT
+  // as k_corr_rw's LM_RW_NEXT loop; the next item may have another width, so
+  // its entries are read for the widest row-load layout (4 loads per lane)
+  const int lane = threadIdx.x & 63;
+  int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave;
+  uint32_t pe[5];
+  for (int it = 0;; ++it) {
+    int cnc[2] = {0, 0};
+    if (tl_cnt != nullptr) {
+      cnc[0] = tl_cnt[lane];
+      cnc[1] = tl_cnt[LM_TL_NC + lane];
+    }
+    const int* cp = tl_cnt != nullptr ? cnc : nullptr;
+    int d, dn;
+    RwTiles H, Hn;
+    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H, cp)) break;
+    const LmDet D = K.det[d];
+    if (it == 0) rw_fetch_entries_rt(H, D.kw_ring, pe);
+    const bool okn = it + 1 < LM_RW_ITEMS && corr_locate_rw(K, G, nslots, s0, g + nwaves, tl_cnt, tl_list, dn, Hn, cp);
+    const int kwn = okn ? K.det[dn].kw_ring : 0;
+    uint32_t pen[5];
+    auto hook = [&]() {
+      if (okn) rw_fetch_entries_rt(Hn, kwn, pen);
+    };
+    RWPROF_ITEM(D)
+    switch (D.kw_ring) {
+#define LM_KW_CASE(n)                                                                                             \
+  case n:                                                                                                         \
+    rw_tile<n, UNF>(K, D, H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes,         \
+                    RWPROF_PH, pe, hook);                                                                         \
+    break;
+      LM_KW_LIST_RW_ALL(LM_KW_CASE)
+#undef LM_KW_CASE
+      default:
+        break;
+    }
+    RWPROF_AFTER
+    if (!okn) break;
+    g += nwaves;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) pe[k] = pen[k];
+  }
+#else
   for (int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
     int d;
     RwTiles H;
@@ -930,14 +1086,17 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(L
     switch (D.kw_ring) {
 #define LM_KW_CASE(n)                                                                                             \
   case n:                                                                                                         \
-    rw_tile<n, UNF>(K, D, H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes);       \
+    rw_tile<n, UNF>(K, D, H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes,         \
+                    RWPROF_PH);                                                                                   \
     break;
       LM_KW_LIST_RW_ALL(LM_KW_CASE)
 #undef LM_KW_CASE
       default:
         break;
     }
+    RWPROF_AFTER
   }
+#endif
   RWPROF_END
 }
 
@@ -1361,19 +1520,22 @@ void rwprof_report() {
   unsigned n = 0;
   if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_rwprof_n), sizeof n) != hipSuccess) return;
   n = n < LM_RWPROF_CAP ? n : LM_RWPROF_CAP;
-  std::vector<unsigned long long> r(4 * (size_t)n);
+  std::vector<unsigned long long> r(8 * (size_t)n);
   if (n && hipMemcpyFromSymbol(r.data(), HIP_SYMBOL(g_rwprof), r.size() * sizeof(unsigned long long)) != hipSuccess)
     return;
   const unsigned zero = 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rwprof_n), &zero, sizeof zero);
   if (!n) return;
   unsigned long long w0 = ~0ull, w1 = 0;
-  double cyc = 0, wall = 0, work = 0;
+  double cyc = 0, wall = 0, work = 0, ph_pro = 0, ph_loop = 0, ph_epi = 0;
   long items = 0;
   std::map<unsigned long long, std::vector<std::pair<unsigned long long, unsigned long long>>> simd;
   std::vector<double> life;
   for (unsigned i = 0; i < n; ++i) {
-    const unsigned long long* q = &r[4 * (size_t)i];
+    const unsigned long long* q = &r[8 * (size_t)i];
+    ph_pro += (double)q[4];
+    ph_loop += (double)q[5];
+    ph_epi += (double)q[6];
     w0 = std::min(w0, q[0]);
     w1 = std::max(w1, q[1]);
     cyc += (double)(q[2] & ((1ull << 40) - 1));
@@ -1411,5 +1573,9 @@ void rwprof_report() {
           n, items, span / 100.0, clk / 10.0, simd.size(), active / (1024.0 * span), wall / active,
           fma_cyc / (active * clk), fma_cyc / (1024.0 * span * clk), life[life.size() / 2] / 100.0,
           life[life.size() * 9 / 10] / 100.0, life.back() / 100.0);
+  fprintf(stderr,
+          "rwprof items: cycles per item before the step loop %.0f, in it %.0f, after %.0f; wave cycles outside "
+          "items %.0f per wave; pk-fma cycles / step-loop cycles %.3f (x waves sharing a SIMD)\n",
+          ph_pro / items, ph_loop / items, ph_epi / items, (cyc - ph_pro - ph_loop - ph_epi) / n, fma_cyc / ph_loop);
 #endif
 }
