@@ -106,8 +106,12 @@ __host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
 __host__ __device__ constexpr int f16_nch(int kw) { return (kw + 31 + 15) / 16; }
 __host__ __device__ constexpr int f16_cols(int nch) { return LM_F16_TW - 32 + 16 * nch; }
 __host__ __device__ constexpr int f16_stride(int cols) { return (cols + 7) / 16 * 16 + 8; }
+#ifndef LM_F16_BLDS
+#define LM_F16_BLDS 0  // B fragments staged once per workgroup in three LDS row slots
+#endif
 __host__ __device__ constexpr size_t f16_lds_bytes(int nch, int kh) {
-  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2;  // the f16 window (B fragments come from global)
+  // the f16 window (+ three B row slots of nch KiB with LM_F16_BLDS; else B comes from global)
+  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2 + (LM_F16_BLDS ? (size_t)3 * nch * 1024 : 0);
 }
 // Host: the B fragment of (row i, chunk c) for lane l, element j (0 off the band).
 static inline float f16_bfrag_weight(const double* w, int kw, int i, int c, int l, int j) {

@@ -1357,8 +1357,103 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
             if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[t], bf[q][c], acc[t], 0, 0, 0);
         }
   };
+#if LM_F16_BLDS
+  // LM_F16_BLDS: each detector row's NCH KiB of B fragments is read from
+  // global memory ONCE per workgroup (by all its threads, one row ahead in
+  // registers) into one of three LDS slots (row i in slot i % 3), and the
+  // waves read their fragments from there: a quarter of the L1 traffic of
+  // every wave fetching them itself.  One barrier per detector row (every
+  // wave runs the row loop, also when its tiles are all skipped); slot
+  // (i + 2) % 3 is refilled after row i, when every wave has left row i - 1.
+  auto mma_b = [&](auto c0, auto c1) {
+    constexpr bool ONG[2] = {decltype(c0)::value, decltype(c1)::value};
+    constexpr int NF = NCH * 64;  // fragments per detector row
+    constexpr int U = (NF + LM_F16_THREADS - 1) / LM_F16_THREADS;
+    lm_h8* __restrict__ bl = reinterpret_cast<lm_h8*>(img + rows * STR);
+    const lm_h8* __restrict__ bg = reinterpret_cast<const lm_h8*>(bfrag + D.w16_off);
+    lm_h8 sb[U];
+    auto sload = [&](int i) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int f = (int)threadIdx.x + u * LM_F16_THREADS;
+        if (f < NF) sb[u] = bg[(int64_t)i * NF + f];
+      }
+    };
+    auto sstore = [&](int slot) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int f = (int)threadIdx.x + u * LM_F16_THREADS;
+        if (f < NF) bl[slot * NF + f] = sb[u];
+      }
+    };
+    auto load_a = [&](lm_h8 (&a)[LM_F16_T], int i, int c) {
+      const _Float16* __restrict__ ai = arow + min(i, kh - 1) * STR + 16 * c;
+#pragma unroll
+      for (int t = 0; t < LM_F16_T; ++t)
+        if (ONG[t / TG]) a[t] = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR);
+    };
+    // B fragment (row slot q, chunk c) of this lane
+    auto load_bl = [&](int q, int c) -> lm_h8 { return bl[(q % 3) * NF + c * 64 + lane]; };
+    sload(0);
+    sstore(0);
+    if (kh > 1) {
+      sload(1);
+      sstore(1);
+    }
+    __syncthreads();
+    if (kh > 2) sload(2);
+    lm_h8 br[3];
+    load_a(ar[0], 0, 0);
+    br[0] = load_bl(0, 0);
+    load_a(ar[1], 1 / NCH, 1 % NCH);
+    br[1] = load_bl(1 / NCH, 1 % NCH);
+    int i = 0;
+    for (; i + 2 < kh; i += 3) {  // rows i, i + 1, i + 2 in slots 0, 1, 2 (i is a multiple of 3)
+#pragma unroll
+      for (int k = 0; k < 3 * NCH; ++k) {
+        const int q = k / NCH, c = k % NCH, k2 = k + 2;
+        load_a(ar[k2 % 3], i + k2 / NCH, k2 % NCH);
+        br[k2 % 3] = load_bl(k2 / NCH, k2 % NCH);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < LM_F16_T; ++t)
+          if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[k % 3][t], br[k % 3], acc[t], 0, 0, 0);
+        if (c == NCH - 1) {  // row i + q done: refill slot (q + 2) % 3 with row i + q + 2
+          if (i + q + 2 < kh) sstore((q + 2) % 3);
+          if (i + q + 3 < kh) sload(i + q + 3);
+          __syncthreads();
+        }
+      }
+    }
+    // the last kh % 3 rows (slots 0, 1)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (i + q < kh) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          lm_h8 a[LM_F16_T];
+          load_a(a, i + q, c);
+          const lm_h8 b = load_bl(q, c);
+#pragma unroll
+          for (int t = 0; t < LM_F16_T; ++t)
+            if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[t], b, acc[t], 0, 0, 0);
+        }
+      }
+  };
+#endif
   using T1 = std::true_type;
   using F0 = std::false_type;
+#if LM_F16_BLDS
+  if (LM_F16_EXP == 2) {
+  } else if (on[0] && on[1])
+    mma_b(T1{}, T1{});
+  else if (on[0])
+    mma_b(T1{}, F0{});
+  else if (on[1])
+    mma_b(F0{}, T1{});
+  else
+    mma_b(F0{}, F0{});  // staging and barriers with the workgroup
+#else
   if (LM_F16_EXP == 2) {
   } else if (on[0] && on[1])
     mma_all(T1{}, T1{});
@@ -1366,6 +1461,7 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
     mma_all(T1{}, F0{});
   else if (on[1])
     mma_all(F0{}, T1{});
+#endif
 
   if (D.kind != 0) {
     // bits straight from a ballot: this wave owns u32 word (ox0 / 32 + wave) of
