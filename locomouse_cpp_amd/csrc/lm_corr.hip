@@ -1205,14 +1205,18 @@ typedef float lm_f32x16 __attribute__((ext_vector_type(16)));
 // global load at any alignment, one 16-byte LDS store: the row stride is a
 // multiple of 8 halfs); up to 7 columns past `cols` are written (inside the
 // row's stride) and never read.
+#ifndef LM_F16_FILLU
+#define LM_F16_FILLU 4  // 8-byte window loads in flight per thread
+#endif
 DEV void tile_fill_f16(_Float16* __restrict__ lds, int stride, const uint8_t* __restrict__ src, int ew, int rows,
                        int cols) {
+  constexpr int UF = LM_F16_FILLU;
   const int ng = (cols + 7) >> 3;
   const int total = rows * ng;
-  for (int e0 = 0; e0 < total; e0 += 4 * (int)blockDim.x) {
-    uint2 v[4];
+  for (int e0 = 0; e0 < total; e0 += UF * (int)blockDim.x) {
+    uint2 v[UF];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < UF; ++u) {
       const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
       if (e < total) {
         const int r = e / ng, g = e - r * ng;
@@ -1220,7 +1224,7 @@ DEV void tile_fill_f16(_Float16* __restrict__ lds, int stride, const uint8_t* __
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < UF; ++u) {
       const int e = e0 + u * (int)blockDim.x + (int)threadIdx.x;
       if (e < total) {
         const int r = e / ng, g = e - r * ng;
