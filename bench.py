@@ -45,7 +45,7 @@ CONFIGS = {  # BASELINE.json configs with a GPU bench line: (rows, cols, descrip
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
 F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16 MFMA peak (MI355X_MICROARCH.md: ~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc_k_corr.json")  # this tree's PMC passes (scripts/gpu_r5.sh step traffic on the final tree, profiles/r05/final2/)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc_k_corr.json")  # this tree's PMC passes at the default shape (scripts/gpu_r5.sh step traffic, profiles/r05/final3/)
 
 
 def algorithmic_flops_per_frame(ctx):
@@ -362,10 +362,12 @@ def main():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c3")
     ap.add_argument("--precision", choices=["fp32", "f16"], default="fp32",
                     help="f16: the non-parity LM_CORR_F16 correlation (BASELINE config 5)")
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per batch (default: 320 for the C3 resident stream, else 256)")
     ap.add_argument("--resident", type=int, default=6400, help="frames resident in HBM per stream (cycled)")
-    ap.add_argument("--streams", type=int, default=4,
-                    help="contexts per GPU (each with its own host thread)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="contexts per GPU, each with its own host thread (default: 8 for the C3 resident stream, "
+                         "else 4)")
     ap.add_argument("--lanes", type=int, default=1,
                     help="pipeline lanes per context (lm_setup.pipeline_lanes: batches in flight on their own HIP "
                          "streams, driven with lm_detect_submit / lm_detect_collect)")
@@ -387,6 +389,17 @@ def main():
                     help="bb: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) instead of the headline path")
     ap.add_argument("--bb-semantics", type=int, default=0, help="firstLastOverT: 0 as executed, 1 integer sums")
     args = ap.parse_args()
+    # The C3 resident stream (the headline line) runs 8 contexts x 320-frame
+    # batches: 491.0k vs 478.4k frames/s for 4 x 256 over three same-box
+    # repetitions (profiles/r05/sweep/shape_b.txt; 5 or 6 contexts were
+    # slower).  The other configs and modes keep the shapes they were
+    # measured with.
+    c3_stream = (args.config == "c3" and args.video_frames == 0 and not args.host_frames and args.lanes == 1
+                 and args.precision == "fp32" and args.workload == "detect")
+    if args.streams is None:
+        args.streams = 8 if c3_stream else 4
+    if args.batch is None:
+        args.batch = 320 if c3_stream else 256
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     if args.workload == "bb":
@@ -456,7 +469,10 @@ def _roofline(ctx, f16, config, spans, executed, B):
     traffic = None  # HBM bytes per launch from this tree's PMC passes (scripts/pmc_traffic.py)
     if os.path.exists(PMC_TRAFFIC) and not f16 and config == "c3":
         with open(PMC_TRAFFIC) as fh:
-            traffic = json.load(fh).get("hbm_bytes_per_launch")
+            pmc = json.load(fh)
+        # measured at the default shape; per frame x this launch's frames otherwise
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc.get("batch_frames") == B else \
+            int(pmc["hbm_bytes_per_frame"] * B)
     return {"bound": "mfma" if f16 else "valu",
             "compute_roof": "dense f16 MFMA (v_mfma_f32_32x32x16_f16)" if f16 else
             "fp32 VALU (v_pk_fma_f32; equals the f32 MFMA peak)",
