@@ -45,7 +45,7 @@ CONFIGS = {  # BASELINE.json configs with a GPU bench line: (rows, cols, descrip
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
 F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16 MFMA peak (MI355X_MICROARCH.md: ~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc_k_corr.json")  # this tree's PMC passes at the default shape (scripts/gpu_r5.sh step traffic, profiles/r05/final3/)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc_k_corr.json")  # this tree's PMC passes at the default shape (scripts/gpu_r5.sh step traffic, profiles/r05/final4/)
 
 
 def algorithmic_flops_per_frame(ctx):
@@ -363,7 +363,7 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "f16"], default="fp32",
                     help="f16: the non-parity LM_CORR_F16 correlation (BASELINE config 5)")
     ap.add_argument("--batch", type=int, default=None,
-                    help="frames per batch (default: 320 for the C3 resident stream, else 256)")
+                    help="frames per batch (default: 448 for the C3 resident stream, else 256)")
     ap.add_argument("--resident", type=int, default=6400, help="frames resident in HBM per stream (cycled)")
     ap.add_argument("--streams", type=int, default=None,
                     help="contexts per GPU, each with its own host thread (default: 8 for the C3 resident stream, "
@@ -389,17 +389,18 @@ def main():
                     help="bb: the whole-video bounding-box pass (SURVEY.md §8(f) row 1) instead of the headline path")
     ap.add_argument("--bb-semantics", type=int, default=0, help="firstLastOverT: 0 as executed, 1 integer sums")
     args = ap.parse_args()
-    # The C3 resident stream (the headline line) runs 8 contexts x 320-frame
-    # batches: 491.0k vs 478.4k frames/s for 4 x 256 over three same-box
-    # repetitions (profiles/r05/sweep/shape_b.txt; 5 or 6 contexts were
-    # slower).  The other configs and modes keep the shapes they were
-    # measured with.
+    # The C3 resident stream (the headline line) runs 8 contexts x 448-frame
+    # batches: 4 x 256 478.4k, 8 x 320 491.0k frames/s over three same-box
+    # repetitions (profiles/r05/sweep/shape_b.txt; 5, 6, 10 contexts
+    # slower), then 8 x 448 493.9k vs 8 x 320 486.6k over six
+    # (shape_c.txt, shape_d.txt; 512 and 640 no better).  The other configs
+    # and modes keep the shapes they were measured with.
     c3_stream = (args.config == "c3" and args.video_frames == 0 and not args.host_frames and args.lanes == 1
                  and args.precision == "fp32" and args.workload == "detect")
     if args.streams is None:
         args.streams = 8 if c3_stream else 4
     if args.batch is None:
-        args.batch = 320 if c3_stream else 256
+        args.batch = 448 if c3_stream else 256
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     if args.workload == "bb":
