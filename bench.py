@@ -393,7 +393,8 @@ def main():
     # batches: 4 x 256 478.4k, 8 x 320 491.0k frames/s over three same-box
     # repetitions (profiles/r05/sweep/shape_b.txt; 5, 6, 10 contexts
     # slower), then 8 x 448 493.9k vs 8 x 320 486.6k over six
-    # (shape_c.txt, shape_d.txt; 512 and 640 no better).  The other configs
+    # (shape_c.txt, shape_d.txt; 512 and 640 no better; 12 or 16 contexts,
+    # or 2 lanes each, no better either: shape_e.txt).  The other configs
     # and modes keep the shapes they were measured with.
     c3_stream = (args.config == "c3" and args.video_frames == 0 and not args.host_frames and args.lanes == 1
                  and args.precision == "fp32" and args.workload == "detect")
