@@ -354,6 +354,19 @@ def rank_env(args):
 
 # ------------------------------------------------------------ one rank
 
+def resolve_shape(args):
+    """Contexts per GPU and frames per batch left unset on the command line:
+    8 x 448 for the C3 resident stream (the headline line), 4 x 256 for every
+    other config and mode."""
+    c3_stream = (args.config == "c3" and args.video_frames == 0 and not args.host_frames and args.lanes == 1
+                 and args.precision == "fp32" and args.workload == "detect")
+    if args.streams is None:
+        args.streams = 8 if c3_stream else 4
+    if args.batch is None:
+        args.batch = 448 if c3_stream else 256
+    return args
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -396,12 +409,7 @@ def main():
     # (shape_c.txt, shape_d.txt; 512 and 640 no better; 12 or 16 contexts,
     # or 2 lanes each, no better either: shape_e.txt).  The other configs
     # and modes keep the shapes they were measured with.
-    c3_stream = (args.config == "c3" and args.video_frames == 0 and not args.host_frames and args.lanes == 1
-                 and args.precision == "fp32" and args.workload == "detect")
-    if args.streams is None:
-        args.streams = 8 if c3_stream else 4
-    if args.batch is None:
-        args.batch = 448 if c3_stream else 256
+    resolve_shape(args)
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
     if args.workload == "bb":

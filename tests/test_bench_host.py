@@ -116,3 +116,27 @@ def test_executed_flops_counts_halo_slots():
     assert bench.executed_flops(Ctx(), work, None) is None
     assert np.isclose(bench.executed_flops(Ctx(), {"outputs": (1, 0)}, 0),
                       2 * (w["paw_bottom"].size + w["snout_bottom"].size))
+
+
+def test_default_shape_by_mode():
+    """Unset --streams / --batch: 8 contexts x 448 frames for the C3 resident
+    stream only (profiles/r05/sweep/), 4 x 256 for every other config and
+    mode; explicit values are kept."""
+    from types import SimpleNamespace
+
+    def shape(**kw):
+        a = dict(config="c3", video_frames=0, host_frames=False, lanes=1, precision="fp32", workload="detect",
+                 streams=None, batch=None)
+        a.update(kw)
+        r = bench.resolve_shape(SimpleNamespace(**a))
+        return r.streams, r.batch
+
+    assert shape() == (8, 448)
+    assert shape(config="c5") == (4, 256)
+    assert shape(video_frames=1250) == (4, 256)
+    assert shape(host_frames=True) == (4, 256)
+    assert shape(lanes=4) == (4, 256)
+    assert shape(precision="f16") == (4, 256)
+    assert shape(workload="bb") == (4, 256)
+    assert shape(streams=2, batch=100) == (2, 100)
+    assert shape(streams=2) == (2, 448)
