@@ -22,7 +22,12 @@ struct LmDetGroup {
   int32_t n;
   int32_t ids[LM_NDET];
   int32_t tile_end[LM_NDET];  // cumulative tile counts
-  int32_t ring_floats;        // k_corr_rw_all: LDS floats per wave
+  int32_t ring_floats;        // k_corr_rw_all: LDS floats per wave (the widest detector's rings)
+  // ring launches: a point detector's dark-tile grid tiles per slot (0 for the
+  // tail detectors), and the launch's cumulative workgroup counts per
+  // detector (filled per launch by launch_corr: they depend on the slot count)
+  int32_t ftiles[LM_NDET];
+  int32_t wg_end[LM_NDET];
 };
 
 // Widths with a width-specialised k_corr_rw (any height); every other
@@ -56,8 +61,16 @@ __host__ __device__ constexpr bool rw_all_width(int kw) {
 #define LM_RW_WAVES 4
 #endif
 #define LM_RW_THREADS (64 * LM_RW_WAVES)
-#ifndef LM_RW_ITEMS
-#define LM_RW_ITEMS 1  // work items (LM_RW_NQ sub-tiles each) per wave, one after another
+// one work item (LM_RW_NQ sub-tiles) per wave; RwRun can describe passes
+// j = 0 .. npass - 1, LM_RW_PSTR list entries apart
+#define LM_RW_PASSES 1
+#define LM_RW_PSTR (LM_RW_WAVES * LM_RW_NQ)
+#ifndef LM_RW_IMAJOR
+#define LM_RW_IMAJOR 0  // 0: workgroups slot-group-major; n: runs of n per slot group, runs interleaved
+#endif
+#define LM_RW_IMAJOR_B (LM_RW_IMAJOR > 0 ? LM_RW_IMAJOR : 1)
+#ifndef LM_RW_ALL_WPE
+#define LM_RW_ALL_WPE 4  // waves per SIMD of the merged launch (k_corr_rw_all)
 #endif
 #define LM_RW_TH 16     // output rows of a wave's 80 x 16 tile (tail detectors)
 #define LM_RW_HTH LM_FH  // output rows per sub-tile (the dark-tile grid's rows)
@@ -106,12 +119,10 @@ __host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
 __host__ __device__ constexpr int f16_nch(int kw) { return (kw + 31 + 15) / 16; }
 __host__ __device__ constexpr int f16_cols(int nch) { return LM_F16_TW - 32 + 16 * nch; }
 __host__ __device__ constexpr int f16_stride(int cols) { return (cols + 7) / 16 * 16 + 8; }
-#ifndef LM_F16_BLDS
-#define LM_F16_BLDS 0  // B fragments staged once per workgroup in three LDS row slots
-#endif
 __host__ __device__ constexpr size_t f16_lds_bytes(int nch, int kh) {
-  // the f16 window (+ three B row slots of nch KiB with LM_F16_BLDS; else B comes from global)
-  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2 + (LM_F16_BLDS ? (size_t)3 * nch * 1024 : 0);
+  // the f16 window (the B fragments come from global memory)
+  (void)nch;
+  return (size_t)(LM_F16_TH + kh - 1) * f16_stride(f16_cols(nch)) * 2;
 }
 // Host: the B fragment of (row i, chunk c) for lane l, element j (0 off the band).
 static inline float f16_bfrag_weight(const double* w, int kw, int i, int c, int l, int j) {
@@ -123,8 +134,8 @@ static inline float f16_bfrag_weight(const double* w, int kw, int i, int c, int 
 // k_corr_rw's ring does not depend on the detector height: every width of
 // LM_KW_LIST, any kh; other widths run k_corr_gen
 bool corr_ring(int kw);
-void rwprof_report();  // LM_RW_PROF builds: ring-kernel wave summary (stderr)
 const void* corr_kernel(int kw, bool unf);     // k_corr_rw<kw> or k_corr_gen
+const void* corr_kernel_gen(bool unf);         // k_corr_gen (any size)
 const void* corr_kernel_rw_all(bool unf);      // every ring width in one launch
 const void* corr_kernel_f16(int kw);           // nullptr when kw is too wide
 // Dark tiles of a batch (written by k_ingest, lm_kernels.hip): flag bytes

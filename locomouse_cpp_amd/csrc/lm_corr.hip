@@ -215,18 +215,18 @@ DEV const uint8_t* corr_src(const LmConst& K, const LmDet& D, const uint8_t* ext
 // for another and a wave's LDS operations execute in order, so the rings need
 // no barrier.
 
-// A ring wave's sub-tiles (see rw_tile): LM_RW_NQ entries of a bright-tile
-// list, or the parts of one 80 x 16 tile.  Each lane looks up the sub-tiles
-// it needs (get: a vector load of the list entry or arithmetic) -- a
-// per-lane pick out of wave-uniform arrays compiled to a private-memory copy.
-struct RwTiles {
+// A ring wave's work (see rw_tile): LM_RW_NQ sub-tiles of LM_FW x LM_FH
+// outputs -- LM_RW_NQ bright tiles from a segment of a dark-tile list (the
+// entries at l), or the 8 parts of one 80 x 16 tile.
+struct RwRun {
   const uint32_t* l;  // listed: the wave's first entry; nullptr: one 80 x 16 tile
   int nvalid;         // sub-tiles 0 .. nvalid - 1 hold a tile
   int ftx;            // listed: flag-grid columns of the view
   int slot, oy, ox;   // one tile: its slot and origin
-  // sub-tile i's list entry (listed; 0 otherwise), and its decoding
-  DEV uint32_t raw(int i) const { return l ? l[i < nvalid ? i : 0] : 0u; }
-  DEV void dec(uint32_t e, int i, int& s, int& y, int& x) const {
+  // list entry of sub-tile i (a valid one for i past the last)
+  DEV uint32_t entry(int i) const { return l ? l[min(i, nvalid - 1)] : 0u; }
+  // slot and output origin of sub-tile i (e: its entry)
+  DEV void tile(int i, uint32_t e, int& s, int& y, int& x) const {
     if (l) {
       const int lt = (int)(e & 0xFFFFu);
       s = (int)(e >> 16);
@@ -238,76 +238,74 @@ struct RwTiles {
       x = ox + (i % LM_RW_NQX) * LM_FW;
     }
   }
-  DEV void get(int i, int& s, int& y, int& x) const { dec(raw(i), i, s, y, x); }
 };
 
-// Wave g of a ring launch -> its detector and sub-tiles.  The batch's work
-// is flattened detector-major (all slots of the group's first detector, then
-// the next ...), so no wave idles at a frame's end and the host can put the
-// longest detectors first.  With dark-tile lists (tl_cnt != nullptr) a point
-// detector's waves take its view's bright LM_FW x 8 tiles LM_RW_NQ at a time
-// from the list segments k_ingest filled (segment c: tl_cnt[view LM_TL_NC +
-// c] tiles, ceil(/ LM_RW_NQ) waves; a wave finds its segment with a scan over
-// the 64 counters, one per lane), so the group's wave count is known on the
-// device only: the grid is sized for every 80 x 16 tile (as many outputs as a
-// wave's sub-tiles, and each segment's waves <= its slots' 80 x 16 tiles) and
-// the waves past the last group's count (whole workgroups at the grid's end)
-// return.  Otherwise a wave takes the sub-tiles of one 80 x 16 tile
-// (row-major).  Called by every lane of the wave; false: past the last wave.
-static_assert(LM_TL_NC == 64, "one list counter per lane");
-DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, const int32_t* tl_cnt,
-                        const uint32_t* tl_list, int& d, RwTiles& H, const int* cnc = nullptr) {
-  constexpr int NQ = LM_RW_NQ;
-  const int lane = threadIdx.x & 63;
-  int base = 0;
+// Workgroup b (logical, after the XCD remap) and wave `wave` of a ring launch
+// -> its detector and work.  The launch is flattened detector-major (the
+// host puts the longest detectors first) in whole workgroups per detector
+// (LmDetGroup::wg_end, from launch_corr); a workgroup takes LM_RW_PSTR
+// LM_RW_PASSES consecutive list entries (or LM_RW_WAVES LM_RW_PASSES tiles).
+//
+// Point detectors with dark-tile lists: the list of view v is cut into
+// LM_TL_NC segments, segment c holding the bright tiles of slot groups
+// y0(c) .. y0(c + 1) - 1 (lm_tl_y0) in the order k_ingest appended them, with
+// room for every tile of those groups.  The workgroups are laid out by that
+// room: CG = ceil(tiles per slot group / entries per workgroup) per slot
+// group, so workgroup b of the detector lies in slot group y = b / CG, hence
+// in segment c = floor(LM_TL_NC y / G) (the inverse of y0), at workgroup
+// i = b - y0(c) CG of the segment.  All of it is arithmetic on wave-uniform
+// values: a wave's first global reads are its list entries and the
+// segment's counter, together (round 5 scanned the 64 counters first, then
+// read the entries: one dependent global read more per wave).  Waves past
+// the counter return (whole workgroups but for a segment's last one).
+// False: nothing for this wave.
+DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int b, int wave,
+                        const int32_t* tl_cnt, const uint32_t* tl_list, int& d, RwRun& R) {
+  constexpr int WE = LM_RW_PSTR * LM_RW_PASSES, WT = LM_RW_WAVES * LM_RW_PASSES;
+  // the detector: the first whose workgroup range ends past b (selected
+  // with constant indices: a kernel-argument array indexed at run time is
+  // copied to scratch)
+  int prev = 0, end = G.wg_end[0], nt = G.tile_end[0], ft = G.ftiles[0];
+  d = G.ids[0];
 #pragma unroll
-  for (int k = 0; k < LM_NDET; ++k) {
-    if (k >= G.n) return false;
-    d = G.ids[k];
-    const LmDet& D = K.det[d];
-    const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
-    if (tl_cnt != nullptr && D.kind == 0) {
-      const int v = D.view;
-      const int cn = cnc ? cnc[v] : tl_cnt[v * LM_TL_NC + lane];  // segment `lane`'s bright tiles (cnc: read before)
-      const int wv = (cn + NQ - 1) / NQ;
-      int P = wv;  // inclusive scan: waves of segments 0 .. lane
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(P, o);
-        if (lane >= o) P += u;
-      }
-      const int cnt = __builtin_amdgcn_readlane(P, 63);  // (readlane: wave-uniform values stay scalar)
-      if (g < base + cnt) {
-        const int local = g - base;
-        const int c = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(P > local)) - 1);
-        const int w = local - (__builtin_amdgcn_readlane(P, c) - __builtin_amdgcn_readlane(wv, c));  // place in segment c
-        const int ng = (nslots + LM_INGEST_FB - 1) / LM_INGEST_FB;
-        H.l = tl_list + (int64_t)v * K.tl_stride +
-              (int64_t)lm_tl_y0(c, ng) * LM_INGEST_FB * K.fl_tx[v] * K.fl_ty[v] + NQ * w;
-        H.nvalid = min(NQ, __builtin_amdgcn_readlane(cn, c) - NQ * w);
-        H.ftx = K.fl_tx[v];
-        H.slot = H.oy = H.ox = 0;
-        return true;
-      }
-      base += cnt;
-    } else {
-      const int cnt = nt * nslots;
-      if (g < base + cnt) {
-        const int local = g - base;
-        const int tx = D.tiles_x;
-        const int lt = local - (local / nt) * nt;
-        H.l = nullptr;
-        H.nvalid = NQ;
-        H.ftx = 0;
-        H.slot = s0 + local / nt;
-        H.oy = (lt / tx) * LM_RW_TH;
-        H.ox = (lt % tx) * LM_TW;
-        return true;
-      }
-      base += cnt;
+  for (int j = 0; j < LM_NDET - 1; ++j)
+    if (j + 1 < G.n && b >= G.wg_end[j]) {
+      prev = G.wg_end[j];
+      end = G.wg_end[j + 1];
+      nt = G.tile_end[j + 1] - G.tile_end[j];
+      ft = G.ftiles[j + 1];
+      d = G.ids[j + 1];
     }
+  if (b >= end) return false;
+  const LmDet& D = K.det[d];
+  const int lb = b - prev;
+  if (tl_cnt != nullptr && D.kind == 0) {
+    const int v = D.view, ng = (nslots + LM_INGEST_FB - 1) / LM_INGEST_FB;
+    const int cg = (ft * LM_INGEST_FB + WE - 1) / WE;
+#if LM_RW_IMAJOR
+    // runs of LM_RW_IMAJOR workgroups per slot group, the slot groups'
+    // first runs first: the workgroups past a segment's count sit at the
+    // grid's end
+    constexpr int IB = LM_RW_IMAJOR;
+    const int y = (lb / IB) % ng, i = lb / (IB * ng) * IB + lb % IB;
+    const int c = LM_TL_NC * y / ng, y0 = lm_tl_y0(c, ng);
+    if (i >= cg) return false;
+    const int first = WE * ((y - y0) * cg + i) + LM_RW_NQ * wave;
+#else
+    const int y = lb / cg, c = LM_TL_NC * y / ng, y0 = lm_tl_y0(c, ng);
+    const int first = WE * (lb - y0 * cg) + LM_RW_NQ * wave;  // the wave's first entry in the segment
+#endif
+    const int cnt = tl_cnt[v * LM_TL_NC + c];
+    if (first >= cnt) return false;
+    R = RwRun{tl_list + (int64_t)v * K.tl_stride + (int64_t)y0 * LM_INGEST_FB * K.fl_tx[v] * K.fl_ty[v] + first,
+              min(LM_RW_NQ, cnt - first), K.fl_tx[v], 0, 0, 0};
+    return true;
   }
-  return false;
+  const int local = WT * lb + wave, total = nt * nslots;
+  if (local >= total) return false;
+  const int lt = local % nt, tx = D.tiles_x;
+  R = RwRun{nullptr, LM_RW_NQ, 0, s0 + local / nt, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
+  return true;
 }
 
 // A workgroup tile of a point detector (k_corr_gen, k_corr_f16) whose flag
@@ -332,15 +330,9 @@ DEV bool corr_tile_dark(const LmConst& K, const LmDet& D, const uint8_t* __restr
 // at most 12 + 4 pairs are live.  Weights are read as 64-bit pairs (taps 2q,
 // 2q + 1 of a row; rows are zero-padded to a multiple of 4) into aligned SGPR
 // pairs, and each tap's v_pk_fma_f32 broadcasts its half of the pair with
-// op_sel (LM_RW_ASMFMA): with single-float weights the compiler copied every
+// op_sel: with single-float weights the compiler copied every
 // odd SGPR into an even one, and the copies of the next step's first chunk
 // forced an lgkmcnt(0) wait right after that chunk's loads were issued.
-#ifndef LM_RW_ASMFMA
-#define LM_RW_ASMFMA 1
-#endif
-#ifndef LM_RW_PREF
-#define LM_RW_PREF 2  // steps ahead a window row's global load is issued (1 or 2)
-#endif
 #ifndef LM_RW_PMAX
 #define LM_RW_PMAX 4
 #endif
@@ -374,10 +366,7 @@ DEV void lds_pair_nw(lm_f2& dst, unsigned base) {
 // behind the chunk's s_waitcnt.
 template <bool UNF, int H>
 DEV lm_f2 corr_tap_h(lm_f2 acc, lm_f2 w2, lm_f2 p) {
-  if constexpr (!LM_RW_ASMFMA) {
-    const float w = H ? w2.y : w2.x;
-    return corr_tap<UNF>(acc, (lm_f2){w, w}, p);
-  } else if constexpr (UNF) {  // rounded product, then rounded sum (OpenCV's scalar / SSE2 build)
+  if constexpr (UNF) {  // rounded product, then rounded sum (OpenCV's scalar / SSE2 build)
     lm_f2 prod;
     if constexpr (H == 0)
       asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(prod) : "s"(w2), "v"(p));
@@ -401,9 +390,6 @@ DEV lm_f2 corr_tap_h(lm_f2 acc, lm_f2 w2, lm_f2 p) {
 // an s_nop (the wait states an MFMA result would need): one statement per
 // tap put 30 s_nops into a kw-30 step, one per pair halves that.  Per
 // accumulator the taps keep their order (half 0, then half 1).
-#ifndef LM_RW_PAIRASM
-#define LM_RW_PAIRASM 1
-#endif
 #define LM_RWF(a, w, p, sel) "v_pk_fma_f32 %" #a ", %" #w ", %" #p ", %" #a " " sel "\n"
 #define LM_RW_S0 "op_sel_hi:[0,1,1]"
 #define LM_RW_S1 "op_sel:[1,0,0] op_sel_hi:[1,1,1]"
@@ -433,9 +419,6 @@ DEV void rw_pair_1(lm_f2 (&a)[PK_C], lm_f2 w, const lm_f2* px) {
 #undef LM_RW_S0
 #undef LM_RW_S1
 
-#ifndef LM_RW_EXP
-#define LM_RW_EXP 0  // timing experiments (wrong scores): 1 no weight loads, 2 no pixel reads, 4 no chunk-start wait
-#endif
 template <int KW, bool UNF>
 struct RwPipe {
   using P = RwPlan<KW>;
@@ -443,10 +426,9 @@ struct RwPipe {
   lm_f2 px[PK_C + KW - 1];
   lm_f2 acc[2][PK_C];
   lm_f2 wa[P::PMAX], wb[P::PMAX];  // weight pairs of the chunk being computed (rows t, t - 2)
-
   template <int Q0, int Q1>
   DEV void issue(unsigned base) {
-    if constexpr (Q0 < Q1 && !(LM_RW_EXP & 2)) {  // (timing experiment 2: no pixel reads)
+    if constexpr (Q0 < Q1) {
       lds_pair_nw<STR, Q0>(px[Q0], base);
       issue<Q0 + 1, Q1>(base);
     }
@@ -457,18 +439,13 @@ struct RwPipe {
                   const lm_f2* __restrict__ rb) {
 #pragma unroll
     for (int q = 0; q < P::qe(C) - P::qb(C); ++q) {
-#if LM_RW_EXP & 1  // timing experiment: no weight loads (wrong scores)
-      na[q] = wa[q];
-      nb[q] = wb[q];
-#else
       na[q] = ra[P::qb(C) + q];
       nb[q] = rb[P::qb(C) + q];
-#endif
     }
   }
   template <int J, int C, bool A, bool B>
   DEV void compute_from() {
-    if constexpr (J < P::end(C) && LM_RW_PAIRASM && LM_RW_ASMFMA && !UNF && (J & 1) == 0 && J + 1 < P::end(C) &&
+    if constexpr (J < P::end(C) && !UNF && (J & 1) == 0 && J + 1 < P::end(C) &&
                   (A || B)) {
       constexpr int q = J / 2 - P::qb(C);
       if constexpr (A && B) rw_pair_ab(acc[0], acc[1], wa[q], wb[q], &px[J]);
@@ -500,7 +477,7 @@ struct RwPipe {
                   const lm_f2* __restrict__ ra_n, const lm_f2* __restrict__ rb_n, F&& at_start) {
     // lgkmcnt(0) through the builtin (vmcnt / expcnt left at their maxima), so
     // the compiler's own wait insertion knows the scalar loads are done too
-    if constexpr (!(LM_RW_EXP & 4)) __builtin_amdgcn_s_waitcnt(0xC07F);  // (timing experiment 4: no wait here)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (C == 0) at_start();
     lm_f2 na[P::PMAX], nb[P::PMAX];
@@ -525,92 +502,65 @@ struct RwPipe {
   }
 };
 
+// The ring kernels' arguments, gathered for rw_tile.
+struct RwArgs {
+  const LmConst* K;
+  LmDetGroup G;
+  const uint8_t* ext;
+  int64_t ext_slot_bytes;
+  const float* weights;
+  int32_t s0, nslots;
+  unsigned long long* keys;
+  int32_t* n_pos;
+  uint8_t* tailbin;
+  int64_t tailbin_slot_bytes;
+  const int32_t* tl_cnt;
+  const uint32_t* tl_list;
+};
+
 // One wave's work (the body of k_corr_rw and k_corr_rw_all): LM_RW_NQ
-// sub-tiles of LM_FW x 8 outputs, 64 / LM_RW_NQ lanes each (lane 32 ly +
-// QX q + lx), each sub-tile streaming its own window through its own ring of LM_RW_HSLOTS
-// rows + 1 mirror.  The sub-tiles are bright tiles from the dark-tile list
-// (any slots, any places) or the parts of one 80 x 16 tile (tail detectors,
-// skip off).  Per sub-tile: lane (ly, lx) owns 5 columns x 4 rows as two
-// packed row pairs; at step t it reads window rows t + 4 ly and t + 4 ly + 1,
-// so rows t .. t + 5 are live; row t + HS is loaded at the step's start and
-// stored at its end into row t's slot.  A wave's LDS operations run in order,
-// so no barrier anywhere.
-struct RwNoHook {
-  DEV void operator()() const {}
-};
-// The list entries a wave of width KW reads for one work item: its lane's
-// sub-tile (pe[0]) and the sub-tile of each of its window-row loads
-// (pe[1 + k]).  rw_tile takes them read ahead (LM_RW_NEXT), so an item's
-// first global reads are its window rows, not entries then rows.
-template <int KW>
-struct RwGeom {
-  static constexpr int NQ = LM_RW_NQ;
-  static constexpr int QX = LM_FW / PK_C;  // lanes across a sub-tile
-  static constexpr int QY = LM_FH / PK_R;  // row groups (lanes down) of a sub-tile
-  static constexpr int LG = 64 / QY;       // lanes per row group of the wave
-  static constexpr int NL = (3 + LM_FW + KW - 1 + 3) / 4;  // dwords of a sub-tile's window row
-  static constexpr int NLD = (NQ * NL + 63) / 64;          // dwords a lane loads per row
-  static constexpr int NE = NLD + 1;                       // list entries per lane and item
-};
-template <int KW>
-DEV void rw_fetch_entries(const RwTiles& H, uint32_t (&pe)[RwGeom<KW>::NE]) {
-  using Gm = RwGeom<KW>;
-  const int lane = threadIdx.x & 63;
-  pe[0] = H.raw((lane % Gm::LG) / Gm::QX);
-#pragma unroll
-  for (int k = 0; k < Gm::NLD; ++k) pe[1 + k] = H.raw(min((lane + 64 * k) / Gm::NL, Gm::NQ - 1));
-}
-
-// the same for a width known at run time (the merged launch's next item):
-// entries for up to 4 row loads per lane (the widest layout; the unused ones
-// are valid reads)
-DEV void rw_fetch_entries_rt(const RwTiles& H, int kw, uint32_t (&pe)[5]) {
-  using Gm = RwGeom<16>;
-  const int lane = threadIdx.x & 63, nl = (3 + LM_FW + kw - 1 + 3) / 4;
-  pe[0] = H.raw((lane % Gm::LG) / Gm::QX);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) pe[1 + k] = H.raw(min((lane + 64 * k) / nl, Gm::NQ - 1));
-}
-
-template <int KW, bool UNF, typename Hook = RwNoHook>
-DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D, const RwTiles& H, float* ring,
-                                                const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
-                                                const float* __restrict__ weights,
-                                                unsigned long long* __restrict__ keys, int32_t* __restrict__ n_pos,
-                                                uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
-                                                long long* ph = nullptr, const uint32_t* pe = nullptr,
-                                                Hook hook = Hook{}) {
-  (void)ph;  // LM_RW_PROF builds: clocks at the step loop's start and end
-  // pe: this item's list entries read ahead (rw_fetch_entries), or null;
-  // hook: called once, right after the first window rows' reads are issued
+// sub-tiles of 40 x 4 outputs, 8 lanes each (lane 8 q + lx), each sub-tile
+// streaming its window (kh + 3 rows of 40 + kw - 1 pixels) through its own
+// LDS ring of 3 rows + 1 mirror.  Lane lx of sub-tile q owns 5 columns x 4
+// rows as two packed row pairs; at step t (t = 0 .. kh + 1) it reads window
+// rows t and t + 1 (pair 0 with weight row t, pair 1 with weight row t - 2);
+// row t + 3 is stored at the end of step t into row t's slot, its global
+// load issued two steps earlier.  A wave's LDS operations run in order, so
+// no barrier anywhere.  The sub-tiles' row loads: load k of a lane is dword
+// dk of sub-tile qk's window row (lane + 64 k = qk NL + dk).
+template <int KW, bool UNF>
+DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const RwRun& R, float* ring) {
   constexpr int NQ = LM_RW_NQ, NQX = LM_RW_NQX;
   constexpr int QX = LM_FW / PK_C;  // lanes across a sub-tile
-  constexpr int QY = LM_FH / PK_R;  // row groups (lanes down) of a sub-tile
-  constexpr int LG = 64 / QY;       // lanes per row group of the wave
-  static_assert(QX * QY * NQ == 64, "sub-tile lanes");
+  static_assert(LM_FH == PK_R && QX * NQ == 64, "one row of 8 lanes per 40 x 4 sub-tile");
   constexpr int STR = rw_stride(KW);
   constexpr int QP = rw_qpitch(KW);
   constexpr int NL = (3 + LM_FW + KW - 1 + 3) / 4;  // dwords of a sub-tile's window row
   constexpr int NLD = (NQ * NL + 63) / 64;          // dwords a lane loads per row
   static_assert(NLD <= 4, "window rows wider than four loads per lane");
   constexpr int HS = LM_RW_HSLOTS;
+  const LmConst& K = *A.K;
+  const LmDet& D = K.det[dix];
   const int lane = threadIdx.x & 63;
+  const int q = lane / QX, lx = lane % QX;
   const int kh = D.kh, kwp = D.kwp;
+  // the host runs one-row detectors on k_corr_gen: without this the compiler
+  // also lays out kh < 2 paths, on which a prefetched pixel pair could reach
+  // the epilogue without its wait (infeasible, but the LDS-wait checker of
+  // tests/test_kernel_resources.py cannot tell)
+  __builtin_assume(kh >= 2);
   const int nrows = LM_RW_HTH + kh - 1;
   const int ew = K.ext_w[D.view];
   const int ew4 = ew >> 2;  // ext rows are padded to 16 bytes
-  // lane = LG ly + QX q + lx: the lanes of each ds_read_b32 lane group share
-  // ly (one ring row per sub-tile), and the sub-tiles' rings start QX (mod 32)
-  // floats apart, so the group's 32 reads hit 32 banks (rw_qpitch); with the
-  // two ly of 8-row sub-tiles in one group, rings of 7 rows put them 4 or -3
-  // rows apart and no pitch avoided conflicts for both
-  const int ly = lane / LG, q = (lane % LG) / QX, lx = lane % QX;
-  // the lane's sub-tile (in VGPRs from here on: the merged kernel's SGPRs
-  // are full)
+  const uint8_t* __restrict__ vext = A.ext + (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0);
+  // the ext crops start 256-byte aligned per slot, views and rows are
+  // multiples of 16 bytes and tile origins of 4, so every window row starts
+  // in_x & 3 bytes past a dword
+  const int mis = D.in_x & 3;
+  // the lane's sub-tile
   int slot, oy0, ox0;
-  H.dec(pe ? pe[0] : H.raw(q), q, slot, oy0, ox0);
-  const bool valid = q < H.nvalid;
-  const int mis = (int)((uintptr_t)corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0) & 3);
+  R.tile(q, R.entry(q), slot, oy0, ox0);
+  const bool valid = q < R.nvalid;
   // row loads: load k of a lane is dword dk of sub-tile qk's window row
   // (e = lane + 64 k = qk NL + dk), stored at float lo[k] of the rings
   const unsigned* __restrict__ la[NLD];
@@ -619,47 +569,51 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
 #pragma unroll
   for (int k = 0; k < NLD; ++k) {
     const int e = lane + 64 * k, qk = e / NL, dk = e - qk * NL;
-    lk[k] = qk < H.nvalid;
+    lk[k] = qk < R.nvalid;
     int sk, yk, xk;
     const int ik = min(qk, NQ - 1);  // lanes past the last sub-tile: a valid address, the value unused
-    H.dec(pe ? pe[1 + k] : H.raw(ik), ik, sk, yk, xk);
-    const uint8_t* s = corr_src(K, D, ext, ext_slot_bytes, sk, yk, xk);
-    la[k] = reinterpret_cast<const unsigned*>(s - ((uintptr_t)s & 3)) + dk;
+    R.tile(ik, R.entry(ik), sk, yk, xk);
+    la[k] = reinterpret_cast<const unsigned*>(vext + (int64_t)sk * A.ext_slot_bytes + (int64_t)(D.in_y + yk) * ew +
+                                              (D.in_x + xk - mis)) +
+            dk;
     lo[k] = qk * QP + 4 * dk;
   }
 
   // brightness mask of the point detectors' outputs (crop pixel > 25), read
-  // from the ext crop now so the loads are long done by the epilogue
+  // from the ext crop now so the loads are long done by the epilogue: per
+  // output row the lane's 5 bytes, from the two aligned dwords they lie in
   unsigned mbits = 0;
   if (D.kind == 0 && valid) {
-    const uint8_t* __restrict__ m = ext + (int64_t)slot * ext_slot_bytes +
-                                    (D.view ? (int64_t)K.ext_h[0] * K.ext_w[0] : 0) + (int64_t)(D.m_y + oy0 + ly * PK_R) * ew +
-                                    (D.m_x + ox0 + lx * PK_C);
+    const uint8_t* __restrict__ m =
+        vext + (int64_t)slot * A.ext_slot_bytes + (int64_t)(D.m_y + oy0) * ew + (D.m_x + ox0 + lx * PK_C);
+    const int mo = (int)((uintptr_t)m & 3);  // the same for every row (ew is a multiple of 16)
+    const unsigned* __restrict__ m4 = reinterpret_cast<const unsigned*>(m - mo);
+    unsigned mw[PK_R][2];
 #pragma unroll
-    for (int r = 0; r < PK_R; ++r)
+    for (int r = 0; r < PK_R; ++r) {
+      mw[r][0] = m4[(int64_t)r * ew4];
+      mw[r][1] = m4[(int64_t)r * ew4 + 1];
+    }
 #pragma unroll
-      for (int c = 0; c < PK_C; ++c) mbits |= (m[(int64_t)r * ew + c] > 25 ? 1u : 0u) << (r * PK_C + c);
+    for (int r = 0; r < PK_R; ++r) {
+      const unsigned long long row = ((unsigned long long)mw[r][1] << 32 | mw[r][0]) >> (8 * mo);
+#pragma unroll
+      for (int c = 0; c < PK_C; ++c) mbits |= (((unsigned)(row >> (8 * c)) & 0xFFu) > 25u ? 1u : 0u) << (r * PK_C + c);
+    }
   }
 
   struct Row {
     unsigned v[NLD];
   };
-  // LM_RW_PREF = 2: every lane loads unconditionally (rows past the window
-  // clamped to its last, lanes without a sub-tile at a valid address; those
-  // values are never stored), so the loads of a step are not behind branches
-  // and the compiler can wait for the older row with vmcnt(NLD) while the
-  // newer one stays in flight.
+  // Every lane loads unconditionally (rows past the window clamped to its
+  // last, lanes without a sub-tile at a valid address; those values are never
+  // stored), so the loads of a step are not behind branches and the compiler
+  // can wait for the older row with vmcnt(NLD) while the newer one stays in
+  // flight.
   auto load_row = [&](int r) -> Row {
     Row w;
 #pragma unroll
-    for (int k = 0; k < NLD; ++k) {
-#if LM_RW_PREF >= 2
-      w.v[k] = la[k][(int64_t)min(r, nrows - 1) * ew4];
-#else
-      w.v[k] = 0u;
-      if (lk[k] && r < nrows) w.v[k] = la[k][(int64_t)r * ew4];
-#endif
-    }
+    for (int k = 0; k < NLD; ++k) w.v[k] = la[k][(int64_t)min(r, nrows - 1) * ew4];
     return w;
   };
   auto store_row = [&](int r, Row w) {
@@ -679,27 +633,17 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
     Row v0[HS];
 #pragma unroll
     for (int r = 0; r < HS; ++r) v0[r] = load_row(r);
-    hook();  // the next item's entry reads, queued behind this item's rows
 #pragma unroll
     for (int r = 0; r < HS; ++r) store_row(r, v0[r]);
   }
 
-  lm_f2 acc[PK_R / 2][PK_C];
-  const lm_f2* __restrict__ W = reinterpret_cast<const lm_f2*>(weights + D.w_off);  // kwp is a multiple of 4
+  const lm_f2* __restrict__ W = reinterpret_cast<const lm_f2*>(A.weights + D.w_off);  // kwp is a multiple of 4
   const int kwp2 = kwp >> 1;
   const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring +
                              (unsigned)(q * QP * (int)sizeof(float));
   const unsigned lane_off = (unsigned)((lx * PK_C + mis) * (int)sizeof(float));
-  // ring slot of window row t + 4 ly (t wave-uniform: both candidates are
-  // scalar, the lane picks one)
   auto row_base = [&](int t) -> unsigned {
-    const int a = t % HS;
-    if constexpr (QY == 1) {
-      return ring_base + (unsigned)(a * STR * (int)sizeof(float)) + lane_off;
-    } else {
-      const int b = a + PK_R >= HS ? a + PK_R - HS : a + PK_R;
-      return ring_base + (unsigned)((ly ? b : a) * STR * (int)sizeof(float)) + lane_off;
-    }
+    return ring_base + (unsigned)((t % HS) * STR * (int)sizeof(float)) + lane_off;
   };
   RwPipe<KW, UNF> S;
 #pragma unroll
@@ -711,7 +655,6 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   S.template issue<RwPlan<KW>::pbeg(0), RwPlan<KW>::pend(0)>(row_base(0));
   using T1 = std::true_type;
   using F0 = std::false_type;
-#if LM_RW_PREF >= 2
   // Step t reads ring rows t and t + 1 and prefetches step t + 1's pixel
   // pairs in its last chunk; at its end it stores row t + HS into the slot
   // of row t (dead by then: a wave's LDS operations run in order).  That
@@ -720,16 +663,13 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   // it stores the other (even steps store r0 and load r1, odd steps the
   // reverse -- the step loop is unrolled by two by hand, so no register copy
   // makes the wave wait for the load just issued).
-  auto stepx = [&](int t, auto A, auto B, Row& st, Row& ld, auto N) {
-    S.template chunks<0, decltype(A)::value, decltype(B)::value, decltype(N)::value>(
+  auto stepx = [&](int t, auto B0, auto B1, Row& st, Row& ld, auto N) {
+    S.template chunks<0, decltype(B0)::value, decltype(B1)::value, decltype(N)::value>(
         row_base(t), row_base(t + 1), wrow(t), wrow(t - 2), wrow(t + 1), wrow(t - 1),
         [&]() { if constexpr (decltype(N)::value) ld = load_row(t + HS + 1); });
     if constexpr (decltype(N)::value) store_row(t + HS, st);  // the last step stores no row (t + HS >= nrows)
   };
   Row r0 = load_row(HS), r1;
-#if LM_RW_PROF
-  ph[0] = clock64();
-#endif
   {  // kh >= 2: the host runs one-row detectors on k_corr_gen
     // pair 0 (tap row t) runs while t < kh, pair 1 (tap row t - 2) from t = 2
     stepx(0, T1{}, F0{}, r0, r1, T1{});
@@ -748,38 +688,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
       stepx(kh + 1, F0{}, T1{}, r1, r0, F0{});
     }
   }
-#else
-  // Step t reads ring rows t and t + 1 and prefetches step t + 1's pixel
-  // pairs in its last chunk; it loads row t + HS at its start and stores it
-  // at its end into the slot of row t (dead by then: a wave's LDS operations
-  // run in order).  The load has a whole step to land, and no register
-  // carries a row from one step to the next.
-  auto step = [&](int t, auto A, auto B) {
-    Row nx;
-    S.template chunks<0, decltype(A)::value, decltype(B)::value>(row_base(t), row_base(t + 1), wrow(t), wrow(t - 2),
-                                                                  wrow(t + 1), wrow(t - 1),
-                                                                  [&]() { nx = load_row(t + HS); });
-    store_row(t + HS, nx);
-  };
-  // pair 0 (tap row t) runs while t < kh, pair 1 (tap row t - 2) from t = 2
-  // (the last step's prefetch is dead; the wait below drains it before any
-  // register it names is reused: tests/test_kernel_resources.py checks the
-  // code for such writes)
-  const int e1 = min(2, kh);
-  int t = 0;
-  for (; t < e1; ++t) step(t, T1{}, F0{});
-  for (; t < 2; ++t) step(t, F0{}, F0{});
-  for (; t < kh; ++t) step(t, T1{}, T1{});
-  for (; t < kh + 2; ++t) step(t, F0{}, T1{});
-#endif
   __builtin_amdgcn_s_waitcnt(0xC07F);  // the last (unused) prefetch
-#if LM_RW_PROF
-  ph[1] = clock64();
-#endif
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int c = 0; c < PK_C; ++c) acc[p][c] = S.acc[p][c];
 
   // epilogue (the ring is dead: this wave's reads were issued first)
   unsigned bits = 0;
@@ -789,19 +698,19 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
 #pragma unroll
       for (int c = 0; c < PK_C; ++c) {
         const int x = ox0 + lx * PK_C + c;
-        const int y0 = oy0 + ly * PK_R + 2 * p;
-        if (x < D.ow && y0 < D.oh && acc[p][c].x > 0.0f) bits |= 1u << ((2 * p) * PK_C + c);
-        if (x < D.ow && y0 + 1 < D.oh && acc[p][c].y > 0.0f) bits |= 1u << ((2 * p + 1) * PK_C + c);
+        const int y0 = oy0 + 2 * p;
+        if (x < D.ow && y0 < D.oh && S.acc[p][c].x > 0.0f) bits |= 1u << ((2 * p) * PK_C + c);
+        if (x < D.ow && y0 + 1 < D.oh && S.acc[p][c].y > 0.0f) bits |= 1u << ((2 * p + 1) * PK_C + c);
       }
   }
   if (D.kind != 0) {
-    // tail map (the sub-tiles are one 80 x 16 tile with sub-tile 0 at its
-    // top left): 16 rows x <= 4 u32 words (the tile's origin is a multiple of
-    // 80, so 80 columns touch at most 4 words) = one word per lane, gathered
-    // in the ring, then ORed into the slot's bitmap
+    // tail map (the sub-tiles are one 80 x 16 tile with sub-tile 0 at its top
+    // left): 16 rows x <= 4 u32 words (the tile's origin is a multiple of 80,
+    // so 80 columns touch at most 4 words) = one word per lane, gathered in
+    // the ring, then ORed into the slot's bitmap
     unsigned* s_tb = reinterpret_cast<unsigned*>(ring);
     const int w0 = (ox0 - (q % NQX) * LM_FW) >> 5;  // the tile's first word
-    const int ty = (q / NQX) * LM_FH + ly * PK_R;   // the lane's first row in the tile
+    const int ty = (q / NQX) * LM_FH;               // the lane's first row in the tile
     s_tb[lane] = 0u;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -814,7 +723,7 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
         }
     __builtin_amdgcn_wave_barrier();
     const unsigned v = s_tb[lane];
-    unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(tailbin + (int64_t)slot * tailbin_slot_bytes) +
+    unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(A.tailbin + (int64_t)slot * A.tailbin_slot_bytes) +
                                 (D.list ? (int64_t)K.tail_hb * K.tail_nw : 0);
     const int y = oy0 - (q / NQX) * LM_FH + (lane >> 2), gw = w0 + (lane & 3);  // rows from the tile's top
     if (v && y < D.oh && gw < K.tail_nw) atomicOr(&tb[(int64_t)y * K.tail_nw + gw], v);
@@ -823,29 +732,22 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
   bits &= mbits;
   // keys: each lane's set bits at consecutive places after the lanes of its
   // sub-tile before it (popcount, then an inclusive scan over the sub-tile's
-  // lanes), one global atomic per sub-tile (keys are sorted later: their
+  // 8 lanes), one global atomic per sub-tile (keys are sorted later: their
   // order in the list does not matter)
   const int cnt = __popc(bits);
-  int incl = cnt;  // inclusive scan over the lane's QX-lane segment (its sub-tile's lanes of one ly)
+  int incl = cnt;
 #pragma unroll
   for (int o = 1; o < QX; o <<= 1) {
     const int u = __shfl_up(incl, o, QX);
     if (lx >= o) incl += u;
   }
-  const int seg = __shfl(incl, QX - 1, QX);  // the segment's count
-  int before = incl - cnt, tot = seg, last = (lane & ~(QX - 1)) + QX - 1;
-  if constexpr (QY == 2) {  // the sub-tile's ly = 0 segment first
-    const int seg_lo = __shfl(seg, lane & 31);
-    tot = seg_lo + __shfl(seg, lane | 32);
-    before += ly ? seg_lo : 0;
-    last |= 32;
-  }
+  const int tot = __shfl(incl, QX - 1, QX);  // the sub-tile's count
+  const int before = incl - cnt, lastl = (lane & ~(QX - 1)) + QX - 1;
   if (__ballot(tot != 0) == 0) return;
-  // one atomic per sub-tile (its last lane), the base to all its lanes
   int base_k = 0;
-  if (lane == last && tot) base_k = atomicAdd(&n_pos[slot * LM_NLIST + D.list], tot);
-  base_k = __shfl(base_k, last);
-  unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k + before;
+  if (lane == lastl && tot) base_k = atomicAdd(&A.n_pos[slot * LM_NLIST + D.list], tot);
+  base_k = __shfl(base_k, lastl);
+  unsigned long long* __restrict__ kl = A.keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + base_k + before;
   int pos = 0;
 #pragma unroll
   for (int p = 0; p < PK_R / 2; ++p)
@@ -855,8 +757,8 @@ DEV __attribute__((always_inline)) void rw_tile(const LmConst& K, const LmDet& D
       for (int hh = 0; hh < 2; ++hh) {
         const int r = 2 * p + hh, k = r * PK_C + c;
         if (bits & (1u << k)) {
-          const int y = oy0 + ly * PK_R + r, x = ox0 + lx * PK_C + c;
-          const float sc = hh ? acc[p][c].y : acc[p][c].x;
+          const int y = oy0 + r, x = ox0 + lx * PK_C + c;
+          const float sc = hh ? S.acc[p][c].y : S.acc[p][c].x;
           kl[pos++] = ((unsigned long long)(~__float_as_uint(sc)) << 32) | (unsigned)(y * D.ow + x);
         }
       }
@@ -886,218 +788,57 @@ DEV int xcd_block(int b, int nb) {
 #endif
 }
 
-// LM_RW_PROF=1 (experiment builds only): one record per ring-kernel wave --
-// wall-clock start and end, its cycles, the SIMD it ran on and its tap-steps
-// -- read back and summarised by rwprof_report() (after each batch under
-// LM_KPROF=1): how much of a launch the SIMDs hold waves, and how fast the
-// waves run while they do.
-#ifndef LM_RW_PROF
-#define LM_RW_PROF 0
-#endif
-#if LM_RW_PROF
-#define LM_RWPROF_CAP (1 << 17)
-__device__ unsigned long long g_rwprof[8 * LM_RWPROF_CAP];
-__device__ unsigned g_rwprof_n;
-DEV void rwprof_record(long long t0w, long long t0c, int work, int items, const long long* ph3) {
-  if ((threadIdx.x & 63) != 0) return;
-  unsigned hw, xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  const long long t1c = clock64(), t1w = wall_clock64();
-  const unsigned i = atomicAdd(&g_rwprof_n, 1u);
-  if (i >= LM_RWPROF_CAP) return;
-  unsigned long long* r = g_rwprof + 8 * (size_t)i;
-  r[0] = (unsigned long long)t0w;
-  r[1] = (unsigned long long)t1w;
-  r[2] = (unsigned long long)(t1c - t0c) | ((unsigned long long)items << 40);
-  r[3] = (unsigned long long)hw | ((unsigned long long)(xcc & 15) << 32) | ((unsigned long long)work << 36);
-  r[4] = (unsigned long long)ph3[0];  // cycles in rw_tile before its step loop (window rows, mask bytes)
-  r[5] = (unsigned long long)ph3[1];  // in the step loop
-  r[6] = (unsigned long long)ph3[2];  // after it (keys / tail bits)
-  r[7] = 0;
-}
-#define RWPROF_BEGIN                                     \
-  const long long rwp_t0w = wall_clock64(), rwp_t0c = clock64(); \
-  int rwp_work = 0, rwp_items = 0;                                 \
-  long long rwp_ph[2], rwp_acc[3] = {0, 0, 0}, rwp_te = 0;
-#define RWPROF_ITEM(D) \
-  rwp_work += ((D).kh + 2) * (D).kw;    \
-  ++rwp_items;                          \
-  rwp_te = clock64();
-#define RWPROF_PH rwp_ph
-#define RWPROF_AFTER                     \
-  {                                      \
-    const long long tx = clock64();      \
-    rwp_acc[0] += rwp_ph[0] - rwp_te;    \
-    rwp_acc[1] += rwp_ph[1] - rwp_ph[0]; \
-    rwp_acc[2] += tx - rwp_ph[1];        \
-  }
-#define RWPROF_END rwprof_record(rwp_t0w, rwp_t0c, rwp_work, rwp_items, rwp_acc);
-#define RWPROF_STOP break
-#else
-#define RWPROF_BEGIN
-#define RWPROF_ITEM(D)
-#define RWPROF_END
-#define RWPROF_PH nullptr
-#define RWPROF_AFTER
-#define RWPROF_STOP return
-#endif
-
-#ifndef LM_RW_NEXT
-#define LM_RW_NEXT 0  // per-width launches: next item's list entries read during the current one
-#endif
 // One launch per width group (LM_KW_LIST widths).
-template <int KW, bool UNF>
-// waves per SIMD: LDS allows 5 (80-column sub-tiles, kw <= 32) or 4
-// (40-column); the register budget is set to match
+// Waves per SIMD: the 40-column sub-tiles' rings allow 4 (80-column ones: 5
+// at kw <= 32); the register budget is set to match.
 #ifndef LM_RW_WPE
 #define LM_RW_WPE (LM_FW == 40 ? 4 : 5)
 #endif
+template <int KW, bool UNF>
 __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(KW <= 32 ? LM_RW_WPE : 1, 8))) void k_corr_rw(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
     int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
     const int32_t* __restrict__ tl_cnt, const uint32_t* __restrict__ tl_list) {
-  const LmConst& K = *Kp;
   extern __shared__ uint4 lds_rw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * rw_ring_floats(KW);
-  // LM_RW_ITEMS work items per wave, strided by the launch's wave count (the
-  // host sizes the grid for that many)
-  const int nwaves = gridDim.x * LM_RW_WAVES;
-  RWPROF_BEGIN
-#if LM_RW_NEXT
-  // Each wave works up to LM_RW_ITEMS items one after another and reads the
-  // next item's list entries during the current one, right after the
-  // current item's first window rows, so an item's start waits for one
-  // global read (its rows) instead of two (entries, then rows).  Waves that
-  // all started together otherwise stall together at every item's start.
-  // Only g and the entries cross an item.
-  constexpr int NE = RwGeom<KW>::NE;
-  const int lane = threadIdx.x & 63;
-  int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave;
-  uint32_t pe[NE];
-  for (int it = 0;; ++it) {
-    int cnc[2] = {0, 0};  // the dark-tile counters (L1 hits after the first item)
-    if (tl_cnt != nullptr) {
-      cnc[0] = tl_cnt[lane];
-      cnc[1] = tl_cnt[LM_TL_NC + lane];
-    }
-    const int* cp = tl_cnt != nullptr ? cnc : nullptr;
-    int d, dn;
-    RwTiles H, Hn;
-    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H, cp)) break;
-    if (it == 0) rw_fetch_entries<KW>(H, pe);
-    const bool okn = it + 1 < LM_RW_ITEMS && corr_locate_rw(K, G, nslots, s0, g + nwaves, tl_cnt, tl_list, dn, Hn, cp);
-    uint32_t pen[NE];
-    RWPROF_ITEM(K.det[d])
-    rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes,
-                     RWPROF_PH, pe, [&]() {
-                       if (okn) rw_fetch_entries<KW>(Hn, pen);
-                     });
-    RWPROF_AFTER
-    if (!okn) break;
-    g += nwaves;
-#pragma unroll
-    for (int k = 0; k < NE; ++k) pe[k] = pen[k];
-  }
-#else
-  for (int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
-    int d;
-    RwTiles H;
-    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) RWPROF_STOP;
-    RWPROF_ITEM(K.det[d])
-    rw_tile<KW, UNF>(K, K.det[d], H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes,
-                     RWPROF_PH);
-    RWPROF_AFTER
-  }
-#endif
-  RWPROF_END
+  const RwArgs a{Kp, G, ext, ext_slot_bytes, weights, s0, nslots, keys, n_pos, tailbin, tailbin_slot_bytes, tl_cnt, tl_list};
+  int d;
+  RwRun R;
+  if (!corr_locate_rw(*a.K, a.G, a.nslots, a.s0, xcd_block(blockIdx.x, gridDim.x), wave, a.tl_cnt, a.tl_list, d, R))
+    return;
+  rw_tile<KW, UNF>(a, d, R, ring);
 }
 
 // Every ring detector of the context in ONE launch (longest first), so the
 // widths share the launch's tail instead of each ending its own; each wave
 // branches to its width's body.  G.ring_floats: LDS floats per wave (the
-// widest detector's ring).
-// Register budget: with 40-column sub-tiles the widths' bodies together need
-// ~154 VGPRs (each alone <= 99: the dispatch's SGPRs spill into VGPR lanes),
-// so three waves per SIMD instead of four, without spills.
+// widest detector's rings and the tail scratch words).
 template <bool UNF>
-__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(LM_FW == 40 ? 3 : 4, 8))) void k_corr_rw_all(
+__global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(LM_RW_ALL_WPE, 8))) void k_corr_rw_all(
     const LmConst* __restrict__ Kp, const LmDetGroup G, const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
     const float* __restrict__ weights, int s0, int nslots, unsigned long long* __restrict__ keys,
     int32_t* __restrict__ n_pos, uint8_t* __restrict__ tailbin, int64_t tailbin_slot_bytes,
     const int32_t* __restrict__ tl_cnt, const uint32_t* __restrict__ tl_list) {
-  const LmConst& K = *Kp;
   extern __shared__ uint4 lds_rw[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   float* ring = reinterpret_cast<float*>(lds_rw) + wave * G.ring_floats;
-  const int nwaves = gridDim.x * LM_RW_WAVES;
-  RWPROF_BEGIN
-#if LM_RW_NEXT
-  // as k_corr_rw's LM_RW_NEXT loop; the next item may have another width, so
-  // its entries are read for the widest row-load layout (4 loads per lane)
-  const int lane = threadIdx.x & 63;
-  int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave;
-  uint32_t pe[5];
-  for (int it = 0;; ++it) {
-    int cnc[2] = {0, 0};
-    if (tl_cnt != nullptr) {
-      cnc[0] = tl_cnt[lane];
-      cnc[1] = tl_cnt[LM_TL_NC + lane];
-    }
-    const int* cp = tl_cnt != nullptr ? cnc : nullptr;
-    int d, dn;
-    RwTiles H, Hn;
-    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H, cp)) break;
-    const LmDet D = K.det[d];
-    if (it == 0) rw_fetch_entries_rt(H, D.kw_ring, pe);
-    const bool okn = it + 1 < LM_RW_ITEMS && corr_locate_rw(K, G, nslots, s0, g + nwaves, tl_cnt, tl_list, dn, Hn, cp);
-    const int kwn = okn ? K.det[dn].kw_ring : 0;
-    uint32_t pen[5];
-    auto hook = [&]() {
-      if (okn) rw_fetch_entries_rt(Hn, kwn, pen);
-    };
-    RWPROF_ITEM(D)
-    switch (D.kw_ring) {
-#define LM_KW_CASE(n)                                                                                             \
-  case n:                                                                                                         \
-    rw_tile<n, UNF>(K, D, H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes,         \
-                    RWPROF_PH, pe, hook);                                                                         \
+  const RwArgs a{Kp, G, ext, ext_slot_bytes, weights, s0, nslots, keys, n_pos, tailbin, tailbin_slot_bytes, tl_cnt, tl_list};
+  int d;
+  RwRun R;
+  if (!corr_locate_rw(*a.K, a.G, a.nslots, a.s0, xcd_block(blockIdx.x, gridDim.x), wave, a.tl_cnt, a.tl_list, d, R))
+    return;
+  switch (a.K->det[d].kw_ring) {
+#define LM_KW_CASE(n)           \
+  case n:                       \
+    rw_tile<n, UNF>(a, d, R, ring); \
     break;
-      LM_KW_LIST_RW_ALL(LM_KW_CASE)
+    LM_KW_LIST_RW_ALL(LM_KW_CASE)
 #undef LM_KW_CASE
-      default:
-        break;
-    }
-    RWPROF_AFTER
-    if (!okn) break;
-    g += nwaves;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) pe[k] = pen[k];
+    default:
+      break;
   }
-#else
-  for (int g = xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, it = 0; it < LM_RW_ITEMS; g += nwaves, ++it) {
-    int d;
-    RwTiles H;
-    if (!corr_locate_rw(K, G, nslots, s0, g, tl_cnt, tl_list, d, H)) RWPROF_STOP;
-    const LmDet D = K.det[d];
-    RWPROF_ITEM(D)
-    switch (D.kw_ring) {
-#define LM_KW_CASE(n)                                                                                             \
-  case n:                                                                                                         \
-    rw_tile<n, UNF>(K, D, H, ring, ext, ext_slot_bytes, weights, keys, n_pos, tailbin, tailbin_slot_bytes,         \
-                    RWPROF_PH);                                                                                   \
-    break;
-      LM_KW_LIST_RW_ALL(LM_KW_CASE)
-#undef LM_KW_CASE
-      default:
-        break;
-    }
-    RWPROF_AFTER
-  }
-#endif
-  RWPROF_END
 }
 
 // ---------------------------------------------------------------- k_corr_gen
@@ -1262,11 +1003,7 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
   constexpr int cols = f16_cols(NCH), STR = f16_stride(cols);
   const int rows = LM_F16_TH + kh - 1;
   _Float16* __restrict__ img = reinterpret_cast<_Float16*>(lds_f16);
-#ifndef LM_F16_EXP  // timing experiments (scripts/build_variant.sh): 1 no window fill, 2 no MFMA; both ignore the mask
-#define LM_F16_EXP 0
-#endif
-  if (LM_F16_EXP != 1)
-    tile_fill_f16(img, STR, corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0), K.ext_w[D.view], rows, cols);
+  tile_fill_f16(img, STR, corr_src(K, D, ext, ext_slot_bytes, slot, oy0, ox0), K.ext_w[D.view], rows, cols);
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
 
@@ -1291,7 +1028,6 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
   // every ring index is static.
   lm_h8 bf[3][NCH], ar[3][LM_F16_T];
   auto load_b = [&](lm_h8 (&b)[NCH], int i) {
-    if (LM_F16_EXP == 4 && (i & 1)) return;  // experiment: half the B fragment loads (stale data)
 #pragma unroll
     for (int c = 0; c < NCH; ++c) b[c] = bsrc[(int64_t)(i * NCH + c) * 64];
   };
@@ -1310,7 +1046,7 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
     for (int t = g * TG; t < (g + 1) * TG; ++t)
       if (x < D.ow && oy0 + 32 * t < D.oh) {
-        if (D.kind != 0 || LM_F16_EXP != 0) {
+        if (D.kind != 0) {
           any = true;
         } else {
 #pragma unroll
@@ -1361,111 +1097,14 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
             if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[t], bf[q][c], acc[t], 0, 0, 0);
         }
   };
-#if LM_F16_BLDS
-  // LM_F16_BLDS: each detector row's NCH KiB of B fragments is read from
-  // global memory ONCE per workgroup (by all its threads, one row ahead in
-  // registers) into one of three LDS slots (row i in slot i % 3), and the
-  // waves read their fragments from there: a quarter of the L1 traffic of
-  // every wave fetching them itself.  One barrier per detector row (every
-  // wave runs the row loop, also when its tiles are all skipped); slot
-  // (i + 2) % 3 is refilled after row i, when every wave has left row i - 1.
-  auto mma_b = [&](auto c0, auto c1) {
-    constexpr bool ONG[2] = {decltype(c0)::value, decltype(c1)::value};
-    constexpr int NF = NCH * 64;  // fragments per detector row
-    constexpr int U = (NF + LM_F16_THREADS - 1) / LM_F16_THREADS;
-    lm_h8* __restrict__ bl = reinterpret_cast<lm_h8*>(img + rows * STR);
-    const lm_h8* __restrict__ bg = reinterpret_cast<const lm_h8*>(bfrag + D.w16_off);
-    lm_h8 sb[U];
-    auto sload = [&](int i) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int f = (int)threadIdx.x + u * LM_F16_THREADS;
-        if (f < NF) sb[u] = bg[(int64_t)i * NF + f];
-      }
-    };
-    auto sstore = [&](int slot) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int f = (int)threadIdx.x + u * LM_F16_THREADS;
-        if (f < NF) bl[slot * NF + f] = sb[u];
-      }
-    };
-    auto load_a = [&](lm_h8 (&a)[LM_F16_T], int i, int c) {
-      const _Float16* __restrict__ ai = arow + min(i, kh - 1) * STR + 16 * c;
-#pragma unroll
-      for (int t = 0; t < LM_F16_T; ++t)
-        if (ONG[t / TG]) a[t] = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR);
-    };
-    // B fragment (row slot q, chunk c) of this lane
-    auto load_bl = [&](int q, int c) -> lm_h8 { return bl[(q % 3) * NF + c * 64 + lane]; };
-    sload(0);
-    sstore(0);
-    if (kh > 1) {
-      sload(1);
-      sstore(1);
-    }
-    __syncthreads();
-    if (kh > 2) sload(2);
-    lm_h8 br[3];
-    load_a(ar[0], 0, 0);
-    br[0] = load_bl(0, 0);
-    load_a(ar[1], 1 / NCH, 1 % NCH);
-    br[1] = load_bl(1 / NCH, 1 % NCH);
-    int i = 0;
-    for (; i + 2 < kh; i += 3) {  // rows i, i + 1, i + 2 in slots 0, 1, 2 (i is a multiple of 3)
-#pragma unroll
-      for (int k = 0; k < 3 * NCH; ++k) {
-        const int q = k / NCH, c = k % NCH, k2 = k + 2;
-        load_a(ar[k2 % 3], i + k2 / NCH, k2 % NCH);
-        br[k2 % 3] = load_bl(k2 / NCH, k2 % NCH);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 0; t < LM_F16_T; ++t)
-          if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[k % 3][t], br[k % 3], acc[t], 0, 0, 0);
-        if (c == NCH - 1) {  // row i + q done: refill slot (q + 2) % 3 with row i + q + 2
-          if (i + q + 2 < kh) sstore((q + 2) % 3);
-          if (i + q + 3 < kh) sload(i + q + 3);
-          __syncthreads();
-        }
-      }
-    }
-    // the last kh % 3 rows (slots 0, 1)
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (i + q < kh) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          lm_h8 a[LM_F16_T];
-          load_a(a, i + q, c);
-          const lm_h8 b = load_bl(q, c);
-#pragma unroll
-          for (int t = 0; t < LM_F16_T; ++t)
-            if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[t], b, acc[t], 0, 0, 0);
-        }
-      }
-  };
-#endif
   using T1 = std::true_type;
   using F0 = std::false_type;
-#if LM_F16_BLDS
-  if (LM_F16_EXP == 2) {
-  } else if (on[0] && on[1])
-    mma_b(T1{}, T1{});
-  else if (on[0])
-    mma_b(T1{}, F0{});
-  else if (on[1])
-    mma_b(F0{}, T1{});
-  else
-    mma_b(F0{}, F0{});  // staging and barriers with the workgroup
-#else
-  if (LM_F16_EXP == 2) {
-  } else if (on[0] && on[1])
+  if (on[0] && on[1])
     mma_all(T1{}, T1{});
   else if (on[0])
     mma_all(T1{}, F0{});
   else if (on[1])
     mma_all(F0{}, T1{});
-#endif
 
   if (D.kind != 0) {
     // bits straight from a ballot: this wave owns u32 word (ox0 / 32 + wave) of
@@ -1577,6 +1216,8 @@ const void* corr_kernel(int kw, bool unf) {
   }
 }
 
+const void* corr_kernel_gen(bool unf) { return unf ? (const void*)&k_corr_gen<true> : (const void*)&k_corr_gen<false>; }
+
 const void* corr_kernel_rw_all(bool unf) {
   return unf ? (const void*)&k_corr_rw_all<true> : (const void*)&k_corr_rw_all<false>;
 }
@@ -1587,13 +1228,26 @@ hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t
                        const CorrDark& dk) {
   if (ring) {
     int nslots = (int)grid.y;
-    const unsigned waves = (unsigned)(G.tile_end[G.n - 1] * nslots);
-    void* args[] = {(void*)&K,       (void*)&G,    (void*)&ext,     (void*)&ext_slot_bytes,
+    // workgroups per detector (corr_locate_rw): listed point detectors by the
+    // room of their view's list (CG per slot group), the others one wave per
+    // 80 x 16 tile
+    LmDetGroup Gl = G;
+    const int ng = (nslots + LM_INGEST_FB - 1) / LM_INGEST_FB;
+    constexpr int WE = LM_RW_PSTR * LM_RW_PASSES, WT = LM_RW_WAVES * LM_RW_PASSES;
+    int wg = 0;
+    for (int k = 0; k < G.n; ++k) {
+      const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
+      if (dk.cnt != nullptr && G.ftiles[k] > 0)
+        wg += ng * (((G.ftiles[k] * LM_INGEST_FB + WE - 1) / WE + LM_RW_IMAJOR_B - 1) / LM_RW_IMAJOR_B * LM_RW_IMAJOR_B);
+      else
+        wg += (nt * nslots + WT - 1) / WT;
+      Gl.wg_end[k] = wg;
+    }
+    void* args[] = {(void*)&K,       (void*)&Gl,   (void*)&ext,     (void*)&ext_slot_bytes,
                     (void*)&weights, (void*)&s0,   (void*)&nslots,  (void*)&keys,
                     (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes, (void*)&dk.cnt,
                     (void*)&dk.list};
-    const unsigned per_block = LM_RW_WAVES * LM_RW_ITEMS;  // work items per workgroup
-    return hipLaunchKernel(fn, dim3((waves + per_block - 1) / per_block), dim3(LM_RW_THREADS), args, lds, st);
+    return hipLaunchKernel(fn, dim3((unsigned)wg), dim3(LM_RW_THREADS), args, lds, st);
   }
   void* args[] = {(void*)&K,     (void*)&G,       (void*)&ext,     (void*)&ext_slot_bytes,           (void*)&weights,
                   (void*)&s0,    (void*)&keys,    (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes,
@@ -1611,71 +1265,3 @@ hipError_t launch_corr_dbg(bool unf, dim3 grid, hipStream_t st, const LmConst* K
   return hipGetLastError();
 }
 
-// LM_RW_PROF builds: summary of the ring-kernel wave records since the last
-// call (stderr), then the record counter reset.  Work unit: a wave's tap
-// steps, sum over its items of (kh + 2) kw; each is 10 v_pk_fma_f32 per lane
-// (5 columns x 2 row pairs), 4 cycles each on a SIMD.
-void rwprof_report() {
-#if LM_RW_PROF
-  unsigned n = 0;
-  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_rwprof_n), sizeof n) != hipSuccess) return;
-  n = n < LM_RWPROF_CAP ? n : LM_RWPROF_CAP;
-  std::vector<unsigned long long> r(8 * (size_t)n);
-  if (n && hipMemcpyFromSymbol(r.data(), HIP_SYMBOL(g_rwprof), r.size() * sizeof(unsigned long long)) != hipSuccess)
-    return;
-  const unsigned zero = 0;
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rwprof_n), &zero, sizeof zero);
-  if (!n) return;
-  unsigned long long w0 = ~0ull, w1 = 0;
-  double cyc = 0, wall = 0, work = 0, ph_pro = 0, ph_loop = 0, ph_epi = 0;
-  long items = 0;
-  std::map<unsigned long long, std::vector<std::pair<unsigned long long, unsigned long long>>> simd;
-  std::vector<double> life;
-  for (unsigned i = 0; i < n; ++i) {
-    const unsigned long long* q = &r[8 * (size_t)i];
-    ph_pro += (double)q[4];
-    ph_loop += (double)q[5];
-    ph_epi += (double)q[6];
-    w0 = std::min(w0, q[0]);
-    w1 = std::max(w1, q[1]);
-    cyc += (double)(q[2] & ((1ull << 40) - 1));
-    items += (long)(q[2] >> 40);
-    wall += (double)(q[1] - q[0]);
-    work += (double)(q[3] >> 36);
-    life.push_back((double)(q[1] - q[0]));
-    // SIMD key: XCC, SE, SH, CU, SIMD (HW_ID bits 15:4)
-    const unsigned long long key = (((q[3] >> 32) & 15) << 16) | ((q[3] >> 4) & 0xFFF);
-    simd[key].push_back({q[0], q[1]});
-  }
-  double active = 0;  // sum over SIMDs of the union of their waves' lifetimes (wall ticks)
-  for (auto& kv : simd) {
-    auto& v = kv.second;
-    std::sort(v.begin(), v.end());
-    unsigned long long a = v[0].first, b = v[0].second;
-    for (auto& iv : v) {
-      if (iv.first > b) {
-        active += (double)(b - a);
-        a = iv.first;
-        b = iv.second;
-      } else {
-        b = std::max(b, iv.second);
-      }
-    }
-    active += (double)(b - a);
-  }
-  std::sort(life.begin(), life.end());
-  const double clk = cyc / wall;  // shader cycles per wall tick (100 MHz)
-  const double span = (double)(w1 - w0);
-  const double fma_cyc = work * 10 * 4;
-  fprintf(stderr,
-          "rwprof: waves %u items %ld span %.1f us clock %.2f GHz simds %zu | simd-active %.3f of 1024 x span | "
-          "waves per active simd %.2f | pk-fma busy while active %.3f, over span %.3f | life p50 %.1f p90 %.1f max %.1f us\n",
-          n, items, span / 100.0, clk / 10.0, simd.size(), active / (1024.0 * span), wall / active,
-          fma_cyc / (active * clk), fma_cyc / (1024.0 * span * clk), life[life.size() / 2] / 100.0,
-          life[life.size() * 9 / 10] / 100.0, life.back() / 100.0);
-  fprintf(stderr,
-          "rwprof items: cycles per item before the step loop %.0f, in it %.0f, after %.0f; wave cycles outside "
-          "items %.0f per wave; pk-fma cycles / step-loop cycles %.3f (x waves sharing a SIMD)\n",
-          ph_pro / items, ph_loop / items, ph_epi / items, (cyc - ph_pro - ph_loop - ph_epi) / n, fma_cyc / ph_loop);
-#endif
-}

@@ -415,11 +415,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
   int2 m = make_int2(0, 0);
   uint4 b4 = make_uint4(0u, 0u, 0u, 0u);
   auto frame_load = [&](int f, int lo_, uint32_t (&dd)[5]) {
-#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 512)  // timing experiment: no frame loads (wrong pixels)
-    for (int u = 0; u < 5; ++u) dd[u] = (uint32_t)(lo_ * (u + 1));
-#else
     ingest_run_load(as_global(frame_ptr[sb + f]), lo_, dd);
-#endif
   };
   // the fast path's loads of chunk i (source map entry, then the first frames' run dwords)
   auto fast_loads = [&](int i) {
@@ -512,9 +508,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) word[j] &= byte_keep4((in_mask >> (4 * j)) & 0xFu);
-#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 256)  // timing experiment: no crop stores unless the word is a sentinel
-      if ((word[0] ^ word[1] ^ word[2] ^ word[3]) == 0x9E3779B9u)
-#endif
       *reinterpret_cast<uint4*>(ext + (int64_t)(sb + f) * ext_slot_bytes + q) = make_uint4(word[0], word[1], word[2], word[3]);
       if (flag_chunk) {
         uint32_t ha = 0u, hb = 0u;
@@ -568,9 +561,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
         }
       continue;
     }
-#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 1024)  // timing experiment: no general-path chunks (wrong pixels)
-    continue;
-#endif
     // General case: frame by frame, the indices recomputed whenever the crop moves.
     int px = sl0.crop_x[v], py = sl0.crop_y[v];
     for (int f = 0; f < nf; ++f) {
@@ -599,9 +589,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
     }
   }
   ING_PROF(3)
-#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 128)  // timing experiment: no flags, no lists
-  return;
-#endif
   if (!fl_band || !tl_list) {
     if (pb && threadIdx.x == 0) {
       pb[4] = clock64();
@@ -631,14 +618,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(LM_INGEST_
   // this workgroup's list segment and its counter (tl_cnt: bright tiles of
   // view v at v LM_TL_NC + c, their outputs at (2 + v) LM_TL_NC + c)
   const int G = (int)gridDim.y, c = (int)blockIdx.y * LM_TL_NC / G;
-#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 64)  // timing experiment: no global list atomics (lists come out empty)
-  if (tid == 0) s_base = 0;
-#else
   if (tid == 0) {
     s_base = s_n ? atomicAdd(&tl_cnt[v * LM_TL_NC + c], s_n) : 0;
     if (s_outs) atomicAdd(&tl_cnt[(2 + v) * LM_TL_NC + c], s_outs);
   }
-#endif
   __syncthreads();
   uint32_t* __restrict__ out = tl_list + (int64_t)v * K.tl_stride +
                                (int64_t)lm_tl_y0(c, G) * LM_INGEST_FB * K.fl_tx[v] * K.fl_ty[v] + s_base;
@@ -1580,13 +1563,17 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   // bits, linear probing, at most half full): a tie list is re-sorted from
   // row-major order by the std::sort replica below, so its (score, index)
   // sort would be thrown away -- ~20k cycles of the slowest blocks.
-  const bool pre = LM_NMS_PREHASH && !glob && 2 * n <= LM_NMS_CAP;
+  // The table is the next power of two >= 2n and lives in s_tmp
+  // (LM_NMS_CAP ints), so it is used only when that power fits: n <= 512 at
+  // LM_NMS_CAP = 1536 (2n <= CAP alone would let 513..768 keys write a
+  // 2048-entry table past s_tmp).
+  int tb = 64, lg = 6;
+  while (tb < 2 * n) {
+    tb <<= 1;
+    ++lg;
+  }
+  const bool pre = LM_NMS_PREHASH && !glob && tb <= LM_NMS_CAP;
   if (pre) {
-    int tb = 64, lg = 6;
-    while (tb < 2 * n) {
-      tb <<= 1;
-      ++lg;
-    }
     unsigned* tab = reinterpret_cast<unsigned*>(s_tmp);
     for (int k = threadIdx.x; k < tb; k += blockDim.x) tab[k] = ~0u;  // empty: a NaN pattern no score has
     __syncthreads();
@@ -1877,14 +1864,6 @@ DEV void nms_block(int bx, int list, const LmConst* __restrict__ Kp, int s0, uns
   int* gmlist = gassign + npg;
   const int n_in = n_pos[slot * LM_NLIST + list];
   if (side && slot < 1) return;  // the previous frame (halo slot): bottom lists only
-#if defined(LM_EXP_SKIP) && (LM_EXP_SKIP & 1)
-  if (threadIdx.x == 0) {
-    H->n_pos[list] = 0;
-    H->cand_cnt[list] = 0;
-    H->ties[list] = 0;
-  }
-  return;
-#endif
   if (GLOB != (n_in > LM_NMS_CAP)) return;  // the other instantiation's list
   const int det = side ? (feat == 0 ? DET_PAW_S : DET_SNOUT_S) : (feat == 0 ? DET_PAW_B : DET_SNOUT_B);
   const LmDet D = K.det[det];

@@ -30,13 +30,6 @@
 
 namespace {
 
-// Timing experiments only (scripts/build_variant_rt.sh -DLM_EXP_SKIP=...;
-// results are wrong): 1 k_nms writes empty lists, 2 no k_tail, 16 no correlation launch,
-// 64 k_ingest without its global list atomics, 128 k_ingest without flags and lists.
-#ifndef LM_EXP_SKIP
-#define LM_EXP_SKIP 0
-#endif
-
 // LDS window of one k_corr_gen workgroup (row chunks are sized to fit it)
 constexpr size_t kCorrLdsBudget = 64 * 1024;
 constexpr size_t kF16LdsMax = 160 * 1024;  // one k_corr_f16 workgroup per CU at most
@@ -644,9 +637,13 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       LmDet& D = K.det[d];
       const bool f16 = su->corr_precision == LM_CORR_F16;
       const bool ring = !f16 && corr_ring(D.kw_ring) && D.kh >= 2;
-      const void* fn = f16 ? corr_kernel_f16(D.kw)
-                       : ring && m == 1 && rw_all_width(D.kw_ring) ? corr_kernel_rw_all(c->unfused)
-                                                                   : corr_kernel(D.kw_ring, c->unfused);
+      // a detector that is not a ring detector (a width without an
+      // instantiation, or one row at a ring width) runs k_corr_gen explicitly:
+      // corr_kernel() picks by width alone
+      const void* fn = f16     ? corr_kernel_f16(D.kw)
+                       : !ring ? corr_kernel_gen(c->unfused)
+                       : m == 1 && rw_all_width(D.kw_ring) ? corr_kernel_rw_all(c->unfused)
+                                                           : corr_kernel(D.kw_ring, c->unfused);
       size_t need;
       if (f16) {
         D.chunk_rows = D.kh;
@@ -673,6 +670,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       const int prev = G.n ? G.tile_end[G.n - 1] : 0;
       G.ids[G.n] = d;
       G.tile_end[G.n] = prev + D.tiles_x * D.tiles_y;
+      G.ftiles[G.n] = D.kind == 0 ? K.fl_tx[D.view] * K.fl_ty[D.view] : 0;
       ++G.n;
       if (ring) G.ring_floats = std::max(G.ring_floats, rw_ring_floats(D.kw_ring));
       P.lds[gi] = std::max(P.lds[gi], need);
@@ -1112,7 +1110,7 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
                                         L.skey.p, dk.flags, dk.cnt, dk.list, kpi);
     T.end();
   }
-  if ((part == 1 || part < 0) && !(LM_EXP_SKIP & 16)) {
+  if (part == 1 || part < 0) {
     T.begin("k_corr");
     const lm_ctx::CorrPlan& CP = c->corr_plan[P.plan];
     for (size_t gi = 0; gi < CP.groups.size(); ++gi) {
@@ -1145,8 +1143,7 @@ void enqueue_chain(lm_ctx* c, Lane& L, Arena& A, const Lane::Pending& P, Timer& 
       kp3 = L.kprof.p + 3 * 16 * 2 * c->nslots;
     }
     T.begin("k_tail");
-    if (LM_EXP_SKIP & 2) {
-    } else if (c->tail_big)
+    if (c->tail_big)
       k_tail<true><<<nproc, LM_TAIL_THREADS, 0, st>>>(dK, s_proc0, L.tailbin.p, c->tailbin_slot_bytes, L.tailmask.p,
                                                       L.tscratch.p, A.hdr.p, kp2, L.tail_ws.p, c->tail_ws_slot,
                                                       L.keys.p, L.npos.p);
@@ -1554,10 +1551,7 @@ void finish_batch(lm_ctx* c, Lane& L) {
     L.t_ev.clear();
     for (int k = 0; k < 4; ++k) L.t_work[k] = -1;
   }
-  if (c->kprof_on) {
-    kprof_report(c, L, n);
-    rwprof_report();
-  }
+  if (c->kprof_on) kprof_report(c, L, n);
 
   // ---- the packed results (lm_batch_result layout) are in the batch's
   // buffer unless they outgrew it: then grow it and let k_out copy them (and

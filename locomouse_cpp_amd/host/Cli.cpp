@@ -107,6 +107,7 @@ class VideoFrames {
       : V(std::move(v)), T(threads), FB((size_t)V->rows() * V->cols()) {}
   bool read(uint8_t* dst) { return pos < V->frame_count() && V->read_at(pos++, dst); }
   int read(uint8_t* dst, int n) {
+    const auto t0 = std::chrono::steady_clock::now();
     n = (int)std::min<size_t>((size_t)std::max(n, 0), V->frame_count() - pos);
     std::vector<char> ok((size_t)n, 0);
     std::atomic<int> next{0};
@@ -120,8 +121,11 @@ class VideoFrames {
     int got = 0;
     while (got < n && ok[got]) ++got;
     pos += (size_t)got;
+    decode_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return got;
   }
+  int threads() const { return T; }
+  double decode_s = 0;  // wall seconds in read(dst, n): file reads + decoding on T threads
   void rewind() { pos = 0; }  // V.set(CV_CAP_PROP_POS_FRAMES, 0)
 
  private:
@@ -386,6 +390,8 @@ int run(int argc, char** argv) {
   std::unique_ptr<LocoMouse> L = LocoMouse_Initialize(li);  // main.cpp:45-91
   L->getBoundingBox();
   L->initializeFeatureLoop();
+  const auto t_init = std::chrono::steady_clock::now();
+  const double decode_init = reader->decode_s;  // the bounding-box pass's reads, when it runs
   for (unsigned int i = 0; i < L->N_frames(); ++i) {
     L->readFrame();
     L->cropBoundingBox();
@@ -404,8 +410,12 @@ int run(int argc, char** argv) {
   L->exportResults();
   if (std::getenv("LM_TIMING")) {  // stage times (not in the reference)
     const auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    std::cout << "LM_TIMING loop_ms " << ms(t_start, t_loop) << " tracks_ms " << ms(t_loop, t_tracks) << " export_ms "
-              << ms(t_tracks, std::chrono::steady_clock::now()) << std::endl;
+    const LocoMouse::StageTimes st = L->stage_times();
+    std::cout << "LM_TIMING init_ms " << ms(t_start, t_init) << " loop_ms " << ms(t_init, t_loop) << " tracks_ms "
+              << ms(t_loop, t_tracks) << " export_ms " << ms(t_tracks, std::chrono::steady_clock::now())
+              << " decode_ms " << 1e3 * (reader->decode_s - decode_init) << " decode_threads " << reader->threads()
+              << " submit_ms " << 1e3 * st.submit_s << " wait_ms " << 1e3 * st.wait_s << " batches " << st.batches
+              << " frames " << L->N_frames() << std::endl;
   }
   return EXIT_SUCCESS;
 }

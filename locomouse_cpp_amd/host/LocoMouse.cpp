@@ -10,6 +10,7 @@
 #include <mutex>
 #include <set>
 #include <stdexcept>
+#include <chrono>
 #include <thread>
 
 namespace locomouse {
@@ -489,6 +490,12 @@ void LocoMouse::sync() {
 // errors (the reference's exceptions) surface here: at the per-frame call
 // that hands over a batch while every lane is busy, or at sync().
 void LocoMouse::collect_oldest() {
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Tally {  // wall time of this call, also when it throws
+    std::chrono::steady_clock::time_point t0;
+    double& acc;
+    ~Tally() { acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+  } tally{t0, TIMES.wait_s};
   const std::pair<int, int> b = INFLIGHT.front();
   INFLIGHT.pop_front();
   if (POOL) {  // the batch's device thread collected it into a chunk of containers
@@ -540,6 +547,7 @@ void LocoMouse::flush() {
   // front of the pending buffer, so the reader's position and the frame
   // numbering stay in step.
   const int ahead = std::max(0, N_READ_AHEAD - n);
+  ++TIMES.batches;
   if (POOL) {
     while (INFLIGHT.size() >= POOL->capacity()) collect_oldest();
     auto j = std::make_shared<DevicePool::Job>();
@@ -549,14 +557,18 @@ void LocoMouse::flush() {
     j->bb = std::move(bb);
     if (h) j->halo = LAST_FRAME;
     LAST_FRAME.assign(PENDING.p + (size_t)(n - 1) * FRAME_BYTES, PENDING.p + (size_t)n * FRAME_BYTES);
-    uint8_t* fresh = POOL->take_buffer();
+    const auto t0 = std::chrono::steady_clock::now();
+    uint8_t* fresh = POOL->take_buffer();  // waits while every buffer is queued or being submitted
     if (ahead) std::memcpy(fresh, PENDING.p + (size_t)n * FRAME_BYTES, (size_t)ahead * FRAME_BYTES);
     PENDING.p = fresh;
     POOL->submit(std::move(j));
+    TIMES.submit_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     INFLIGHT.push_back({first, n});
   } else {
     while ((int)INFLIGHT.size() >= 2 * lm_ctx_lanes(CTX)) collect_oldest();
+    const auto t0 = std::chrono::steady_clock::now();
     throw_on_error(lm_detect_submit(CTX, PENDING.data(), (int64_t)FRAME_BYTES, n, first, nullptr, bb.data()));
+    TIMES.submit_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     INFLIGHT.push_back({first, n});
     if (ahead)
       std::memmove(PENDING.data(), PENDING.data() + (size_t)n * FRAME_BYTES, (size_t)ahead * FRAME_BYTES);

@@ -140,6 +140,17 @@ class LocoMouse : protected FrameResults {
   // Processes the frames read so far (called by every accessor above).
   void sync();
 
+  // Wall seconds the caller's thread spent handing batches to the device
+  // (lm_detect_submit: the pinned staging copy and the H2D issue, or the
+  // queue to a device thread) and waiting for results (lm_detect_collect, or
+  // a device thread's chunk), and the batches handed over.  Not in the
+  // reference: the LocoMouse program prints them under LM_TIMING.
+  struct StageTimes {
+    double submit_s = 0, wait_s = 0;
+    int batches = 0;
+  };
+  StageTimes stage_times() const { return TIMES; }
+
  protected:
   LocoMouse_Inputs IN;
   int METHOD = 0;
@@ -190,6 +201,7 @@ class LocoMouse : protected FrameResults {
   size_t FRAME_BYTES = 0;
   void flush();
   void collect_oldest();
+  StageTimes TIMES;
 };
 
 // LocoMouse_TM (LocoMouse_TM.hpp:30-55): readFrame adds imadjust

@@ -185,6 +185,49 @@ def _lds_pair_step(ins, pending, bad):
     return pending
 
 
+def _sregs(operand):
+    """SGPR numbers an operand names (s7, s[4:5])."""
+    m = re.fullmatch(r"s(\d+)", operand)
+    if m:
+        return {int(m.group(1))}
+    m = re.fullmatch(r"s\[(\d+):(\d+)\]", operand)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    return set()
+
+
+def _flag_step(ins, consts, vcc):
+    """Constant tracking for the compiler's boolean-flag branches: an SGPR
+    pair set to 0 / -1 (s_mov_b64), VCC computed from it with EXEC
+    (s_and_b64 / s_andn2_b64 vcc, exec, s[a:b]).  Returns (consts, vcc): vcc
+    is "zero", "nonzero" or None (unknown).  Conservative: any other
+    instruction naming VCC makes it unknown, and any instruction naming an
+    SGPR of a tracked pair (as its first operand, or any operand of a vector
+    instruction) forgets that pair."""
+    op, _, rest = ins.partition(" ")
+    ops = [o.strip().split(" ")[0] for o in rest.split(",")] if rest else []
+    if not ops:
+        return consts, vcc
+    if op == "s_mov_b64" and len(ops) == 2 and ops[1] in ("0", "-1") and ops[0].startswith("s["):
+        d = _sregs(ops[0])
+        keep = frozenset(kv for kv in consts if not (_sregs(kv[0]) & d))
+        return keep | {(ops[0], int(ops[1]))}, vcc
+    if op in ("s_and_b64", "s_andn2_b64") and len(ops) == 3 and ops[0] == "vcc" and ops[1] == "exec":
+        c = dict(consts).get(ops[2])
+        if c is None:
+            return consts, None
+        on = (c == -1) if op == "s_and_b64" else (c == 0)  # EXEC is never zero where the branch executes
+        return consts, "nonzero" if on else "zero"
+    if any(o.startswith("vcc") for o in ops):
+        vcc = None
+    touched = set()
+    for o in (ops if op.startswith("v_") else ops[:1]):
+        touched |= _sregs(o)
+    if touched:
+        consts = frozenset(kv for kv in consts if not (_sregs(kv[0]) & touched))
+    return consts, vcc
+
+
 def early_reads_of_lds_pairs(instrs):
     """Instructions that read -- or write ("WAW ...", except another LDS read) --
     a VGPR written by a ds_read2_b32 before an s_waitcnt that drains the LDS
@@ -192,7 +235,12 @@ def early_reads_of_lds_pairs(instrs):
     the compiler's wait insertion does not see, so a register copy or use
     before the explicit wait would read stale data.  instrs: disassemble_cfg
     items (address, text, branch target) -- a forward may-analysis over the
-    branches -- or plain instruction texts (scanned in program order)."""
+    branches -- or plain instruction texts (scanned in program order).  The
+    CFG analysis is path-sensitive for one pattern the compiler uses to merge
+    control flow: a flag SGPR pair set to 0 or -1 on each incoming path and a
+    VCC branch on it (s_mov_b64 s[a:b], -1 / s_andn2_b64 vcc, exec, s[a:b] /
+    s_cbranch_vccnz); a path whose flag decides the branch the other way is
+    not followed."""
     if not instrs or isinstance(instrs[0], str):
         pending, bad = frozenset(), []
         for ins in instrs:
@@ -201,29 +249,46 @@ def early_reads_of_lds_pairs(instrs):
     idx = {a: i for i, (a, _, _) in enumerate(instrs)}
     n = len(instrs)
 
-    def succs(i):
+    def succs(i, vcc):
         _, t, tgt = instrs[i]
         op = t.split(" ")[0]
         if op in ("s_endpgm", "s_setpc_b64", "s_trap"):
             return []
         nxt = [i + 1] if i + 1 < n else []
         if tgt is not None and tgt in idx:
-            return [idx[tgt]] if op == "s_branch" else [idx[tgt]] + nxt
+            if op == "s_branch":
+                return [idx[tgt]]
+            if op == "s_cbranch_vccnz" and vcc is not None:
+                return [idx[tgt]] if vcc == "nonzero" else nxt
+            if op == "s_cbranch_vccz" and vcc is not None:
+                return [idx[tgt]] if vcc == "zero" else nxt
+            return [idx[tgt]] + nxt
         return nxt
 
-    state = [None] * n  # pending set on entry
-    state[0] = frozenset()
-    work = [0]
+    CAP = 64  # states kept per instruction before they are merged (the analysis stays sound)
+    states = [set() for _ in range(n)]
+    states[0].add((frozenset(), frozenset(), None))
+    work = [(0, (frozenset(), frozenset(), None))]
     while work:
-        i = work.pop()
-        out = _lds_pair_step(instrs[i][1], state[i], None)
-        for j in succs(i):
-            merged = out if state[j] is None else state[j] | out
-            if merged != state[j]:
-                state[j] = merged
-                work.append(j)
+        i, (pend, consts, vcc) = work.pop()
+        out = _lds_pair_step(instrs[i][1], pend, None)
+        c2, v2 = _flag_step(instrs[i][1], consts, vcc)
+        for j in succs(i, v2):
+            st = (out, c2, v2)
+            if st in states[j]:
+                continue
+            if len(states[j]) >= CAP:  # collapse: one state with every pending register, no flags
+                allp = frozenset().union(out, *[s_[0] for s_ in states[j]])
+                st = (allp, frozenset(), None)
+                if st in states[j]:
+                    continue
+                states[j] = {st}
+            else:
+                states[j].add(st)
+            work.append((j, st))
     bad = []
     for i in range(n):
-        if state[i] is not None:
-            _lds_pair_step(instrs[i][1], state[i], bad)
+        pend = frozenset().union(*[s_[0] for s_ in states[i]]) if states[i] else None
+        if pend is not None:
+            _lds_pair_step(instrs[i][1], pend, bad)
     return bad

@@ -354,3 +354,52 @@ def test_long_candidate_lists_take_the_global_paths():
     co = ref["cand_offset"]
     assert min(int(co[4 * f + 1] - co[4 * f]) for f in range(4)) > 1500
     assert_same(_batched(cfg, frames, 3), ref, "long lists: ")
+
+
+@pytest.mark.parametrize("plan", [0, 1])
+def test_one_row_detectors_at_ring_widths(plan):
+    """1 x 24 and 1 x 30 detectors: ring-kernel widths, but one row, so they
+    must run k_corr_gen (the ring's two-step-ahead loop needs kh >= 2) in the
+    per-width and the merged plans alike, beside ring detectors of the same
+    widths (the ring kernel was picked by width alone)."""
+    w = {"paw_side": S.dog_detector(1, 24, 4.0, 61), "tail_side": S.line_detector(1, 30, 0.5, 62),
+         "snout_bottom": S.dog_detector(30, 30, 5.0, 12)}
+    base = S.SyntheticConfig(weights=w)
+    cfg = S.SyntheticConfig(weights=w, biases=E._bias_for_rate(base, ["paw_side", "snout_bottom"]))
+    frames = cfg.frames(0, 4)
+    ctx = _ctx(cfg, max_batch=4)
+    ctx.set_debug(1 | (abi.LM_DEBUG_PLAN_MERGED if plan else abi.LM_DEBUG_PLAN_PER_WIDTH))
+    got = ctx.detect(frames, 0)
+    from oracle import oracle as O
+    ref = _oracle(cfg, frames, flags=O.KEEP_DEBUG)
+    assert_same(got, ref.result, f"one-row plan {plan}: ")
+    for f in range(4):
+        for det in range(6):
+            s = ctx.debug_scores(f, det)
+            assert np.array_equal(s.view(np.uint32), ref.scores(f, det, s.shape).view(np.uint32)), (f, det)
+    ctx.close()
+
+
+@pytest.mark.parametrize("quantized", [True, False])
+@pytest.mark.parametrize("rank", [600, 750, 900])
+def test_nms_lists_of_513_to_768_keys(quantized, rank):
+    """Bottom and side lists of 513..768 kept keys: k_nms's tie pre-hash
+    table (next power of two >= 2n) would be 2,048 entries, past its
+    1,536-int LDS array, so such lists must skip the pre-hash (ADVICE r05);
+    with and without exact score ties.  `rank`: positive scores of frame 0
+    before the brightness and tail masks, so the kept lists land in or just
+    below the range."""
+    if quantized:
+        c, _ = _quantized_config(rank)
+    else:
+        from oracle import oracle as O
+        base = S.SyntheticConfig()
+        c0 = S.SyntheticConfig(biases={n: 0.0 for n in S.DETECTOR_SPECS})
+        r0 = O.OracleRun(c0, c0.frames(0, 1), flags=O.KEEP_DEBUG)
+        b = dict(base.biases)
+        for det, name in ((0, "paw_bottom"), (1, "snout_bottom"), (3, "paw_side"), (4, "snout_side")):
+            b[name] = float(np.sort(r0.scores(0, det).ravel())[::-1][rank])
+        c = S.SyntheticConfig(biases=b)
+    frames = c.frames(0, 6)
+    got = _ctx(c, max_batch=6).detect(frames, 0)
+    assert_same(got, _oracle(c, frames).result, f"nms 513..768 rank {rank} q {quantized}: ")

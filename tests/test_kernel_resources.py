@@ -100,3 +100,27 @@ def test_lds_wait_checker_follows_branches():
     assert kernel_resources.early_reads_of_lds_pairs(ok) == []
     assert kernel_resources.early_reads_of_lds_pairs(bad) == ["v_mov_b32_e32 v10, v3"]
     assert kernel_resources.early_reads_of_lds_pairs(laid_out) == []  # program order alone would flag it
+
+
+def test_lds_wait_checker_flag_branches():
+    """The compiler merges paths through a flag SGPR pair (s_mov_b64 s[6:7],
+    0 / -1; s_andn2_b64 vcc, exec, s[6:7]; s_cbranch_vccnz): a path whose
+    flag sends the branch the other way is not followed, one whose flag is
+    unknown is."""
+    import kernel_resources
+    rd = "ds_read2_b32 v[24:25], v9 offset0:1 offset1:117"
+
+    def prog(flag_init):
+        # 0: ds_read2 in flight; 1: flag; 2: branch to 4 (the merge) ...
+        return [(0, rd, None), (4, flag_init, None), (8, "s_branch 1", 16),
+                (12, "s_waitcnt lgkmcnt(0)", None),
+                (16, "s_andn2_b64 vcc, exec, s[6:7]", None), (20, "s_cbranch_vccnz 2", 32),
+                (24, "s_waitcnt lgkmcnt(0)", None), (28, "s_endpgm", None),
+                (32, "v_mov_b32_e32 v24, 0", None), (36, "s_endpgm", None)]
+    # flag -1: vcc = exec & ~(-1) = 0, the branch to the write is not taken
+    assert kernel_resources.early_reads_of_lds_pairs(prog("s_mov_b64 s[6:7], -1")) == []
+    # flag 0: vcc = exec, the write follows the pending read
+    assert kernel_resources.early_reads_of_lds_pairs(prog("s_mov_b64 s[6:7], 0")) == ["WAW v_mov_b32_e32 v24, 0"]
+    # flag unknown (a compare result): both ways
+    assert kernel_resources.early_reads_of_lds_pairs(prog("v_cmp_ne_u32_e64 s[6:7], v1, v2")) == \
+        ["WAW v_mov_b32_e32 v24, 0"]
