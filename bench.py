@@ -476,20 +476,24 @@ def _roofline(ctx, f16, config, spans, executed, B):
     exec_per_launch = (sum(executed) / len(executed)) if executed and None not in executed else flops * B
     achieved_tf = exec_per_launch / (corr_avg_ms * 1e-3) / 1e12 if corr_avg_ms > 0 else 0.0
     peak_tf = F16_PEAK_TFLOPS if f16 else FP32_PEAK_TFLOPS
-    traffic = None  # HBM bytes per launch from this tree's PMC passes (scripts/pmc_traffic.py)
+    traffic, measured, pmc = None, False, {}  # HBM bytes per launch from this tree's PMC passes (scripts/pmc_traffic.py)
     if os.path.exists(PMC_TRAFFIC) and not f16 and config == "c3":
         with open(PMC_TRAFFIC) as fh:
             pmc = json.load(fh)
-        # measured at the default shape; per frame x this launch's frames otherwise
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc.get("batch_frames") == B else \
-            int(pmc["hbm_bytes_per_frame"] * B)
+        # measured at the default shape; per frame x this launch's frames
+        # otherwise -- an estimate (per-launch weight and L2 traffic does not
+        # scale with the frame count), labelled as such in traffic_source
+        measured = pmc.get("batch_frames") == B
+        traffic = pmc.get("hbm_bytes_per_launch") if measured else int(pmc["hbm_bytes_per_frame"] * B)
     return {"bound": "mfma" if f16 else "valu",
             "compute_roof": "dense f16 MFMA (v_mfma_f32_32x32x16_f16)" if f16 else
             "fp32 VALU (v_pk_fma_f32; equals the f32 MFMA peak)",
             "kernel": "k_corr", "achieved": round(achieved_tf, 3), "peak": peak_tf,
             "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
             "traffic": traffic,
-            "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if traffic else None,
+            "traffic_source": (os.path.relpath(PMC_TRAFFIC, ROOT) + ("" if measured else
+                               f" (scaled from its {pmc.get('batch_frames')}-frame PMC launch to {B} frames: an estimate)"))
+            if traffic else None,
             "executed_flop_per_launch": int(exec_per_launch),
             "algorithmic_flop_per_launch": flops * B,
             "executed_fraction": round(exec_per_launch / (flops * B), 4),

@@ -23,11 +23,6 @@ struct LmDetGroup {
   int32_t ids[LM_NDET];
   int32_t tile_end[LM_NDET];  // cumulative tile counts
   int32_t ring_floats;        // k_corr_rw_all: LDS floats per wave (the widest detector's rings)
-  // ring launches: a point detector's dark-tile grid tiles per slot (0 for the
-  // tail detectors), and the launch's cumulative workgroup counts per
-  // detector (filled per launch by launch_corr: they depend on the slot count)
-  int32_t ftiles[LM_NDET];
-  int32_t wg_end[LM_NDET];
 };
 
 // Widths with a width-specialised k_corr_rw (any height); every other
@@ -61,14 +56,6 @@ __host__ __device__ constexpr bool rw_all_width(int kw) {
 #define LM_RW_WAVES 4
 #endif
 #define LM_RW_THREADS (64 * LM_RW_WAVES)
-// one work item (LM_RW_NQ sub-tiles) per wave; RwRun can describe passes
-// j = 0 .. npass - 1, LM_RW_PSTR list entries apart
-#define LM_RW_PASSES 1
-#define LM_RW_PSTR (LM_RW_WAVES * LM_RW_NQ)
-#ifndef LM_RW_IMAJOR
-#define LM_RW_IMAJOR 0  // 0: workgroups slot-group-major; n: runs of n per slot group, runs interleaved
-#endif
-#define LM_RW_IMAJOR_B (LM_RW_IMAJOR > 0 ? LM_RW_IMAJOR : 1)
 #ifndef LM_RW_ALL_WPE
 #define LM_RW_ALL_WPE 4  // waves per SIMD of the merged launch (k_corr_rw_all)
 #endif

@@ -240,72 +240,76 @@ struct RwRun {
   }
 };
 
-// Workgroup b (logical, after the XCD remap) and wave `wave` of a ring launch
-// -> its detector and work.  The launch is flattened detector-major (the
-// host puts the longest detectors first) in whole workgroups per detector
-// (LmDetGroup::wg_end, from launch_corr); a workgroup takes LM_RW_PSTR
-// LM_RW_PASSES consecutive list entries (or LM_RW_WAVES LM_RW_PASSES tiles).
+// Wave g of a ring launch -> its detector and sub-tiles.  The batch's work
+// is flattened detector-major (all slots of the group's first detector, then
+// the next ...; the host puts the longest detectors first), so no wave idles
+// at a frame's end.  With dark-tile lists (tl_cnt != nullptr) a point
+// detector's waves take its view's bright LM_FW x LM_FH tiles LM_RW_NQ at a
+// time from the list segments k_ingest filled (segment c: tl_cnt[view
+// LM_TL_NC + c] tiles, ceil(/ LM_RW_NQ) waves), packed densely: a wave finds
+// its segment with one scan over the 64 counters, one per lane.  The group's
+// wave count is known on the device only, so the grid is sized for every
+// 80 x 16 tile and the waves past the last group's count (whole workgroups
+// at the grid's end) return.  Otherwise a wave takes the sub-tiles of one
+// 80 x 16 tile (row-major per slot).  Called by every lane of the wave;
+// false: past the last wave.
 //
-// Point detectors with dark-tile lists: the list of view v is cut into
-// LM_TL_NC segments, segment c holding the bright tiles of slot groups
-// y0(c) .. y0(c + 1) - 1 (lm_tl_y0) in the order k_ingest appended them, with
-// room for every tile of those groups.  The workgroups are laid out by that
-// room: CG = ceil(tiles per slot group / entries per workgroup) per slot
-// group, so workgroup b of the detector lies in slot group y = b / CG, hence
-// in segment c = floor(LM_TL_NC y / G) (the inverse of y0), at workgroup
-// i = b - y0(c) CG of the segment.  All of it is arithmetic on wave-uniform
-// values: a wave's first global reads are its list entries and the
-// segment's counter, together (round 5 scanned the 64 counters first, then
-// read the entries: one dependent global read more per wave).  Waves past
-// the counter return (whole workgroups but for a segment's last one).
-// False: nothing for this wave.
-DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int b, int wave,
-                        const int32_t* tl_cnt, const uint32_t* tl_list, int& d, RwRun& R) {
-  constexpr int WE = LM_RW_PSTR * LM_RW_PASSES, WT = LM_RW_WAVES * LM_RW_PASSES;
-  // the detector: the first whose workgroup range ends past b (selected
-  // with constant indices: a kernel-argument array indexed at run time is
-  // copied to scratch)
-  int prev = 0, end = G.wg_end[0], nt = G.tile_end[0], ft = G.ftiles[0];
-  d = G.ids[0];
+// Round 6 tried an arithmetic map instead (workgroup b -> the room of its
+// slot group's segment, the counter and the entries read together: one
+// dependent global read less per wave): 2-3 % fewer frames/s at 8 contexts
+// (profiles/r06/corr_ab/).  The room-based layout puts a segment's working
+// waves in whole workgroups, so every segment's last workgroup idles up to
+// three wave slots while its LDS is held, and the empty workgroups sit
+// between the working ones; the dense layout has neither.
+static_assert(LM_TL_NC == 64, "one list counter per lane");
+DEV bool corr_locate_rw(const LmConst& K, const LmDetGroup& G, int nslots, int s0, int g, const int32_t* tl_cnt,
+                        const uint32_t* tl_list, int& d, RwRun& R) {
+  constexpr int NQ = LM_RW_NQ;
+  const int lane = threadIdx.x & 63;
+  int base = 0;
 #pragma unroll
-  for (int j = 0; j < LM_NDET - 1; ++j)
-    if (j + 1 < G.n && b >= G.wg_end[j]) {
-      prev = G.wg_end[j];
-      end = G.wg_end[j + 1];
-      nt = G.tile_end[j + 1] - G.tile_end[j];
-      ft = G.ftiles[j + 1];
-      d = G.ids[j + 1];
+  for (int k = 0; k < LM_NDET; ++k) {
+    if (k >= G.n) return false;
+    const int dk = G.ids[k];
+    const LmDet& D = K.det[dk];
+    const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
+    if (tl_cnt != nullptr && D.kind == 0) {
+      const int v = D.view;
+      const int cn = tl_cnt[v * LM_TL_NC + lane];  // segment `lane`'s bright tiles
+      const int wv = (cn + NQ - 1) / NQ;
+      int P = wv;  // inclusive scan: waves of segments 0 .. lane
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(P, o);
+        if (lane >= o) P += u;
+      }
+      const int cnt = __builtin_amdgcn_readlane(P, 63);  // (readlane: wave-uniform values stay scalar)
+      if (g < base + cnt) {
+        const int local = g - base;
+        const int c = __builtin_amdgcn_readfirstlane(__ffsll((long long)__ballot(P > local)) - 1);
+        const int w = local - (__builtin_amdgcn_readlane(P, c) - __builtin_amdgcn_readlane(wv, c));  // place in segment c
+        const int ng = (nslots + LM_INGEST_FB - 1) / LM_INGEST_FB;
+        d = dk;
+        R = RwRun{tl_list + (int64_t)v * K.tl_stride + (int64_t)lm_tl_y0(c, ng) * LM_INGEST_FB * K.fl_tx[v] * K.fl_ty[v] +
+                      NQ * w,
+                  min(NQ, __builtin_amdgcn_readlane(cn, c) - NQ * w), K.fl_tx[v], 0, 0, 0};
+        return true;
+      }
+      base += cnt;
+    } else {
+      const int cnt = nt * nslots;
+      if (g < base + cnt) {
+        const int local = g - base;
+        const int tx = D.tiles_x;
+        const int lt = local - (local / nt) * nt;
+        d = dk;
+        R = RwRun{nullptr, NQ, 0, s0 + local / nt, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
+        return true;
+      }
+      base += cnt;
     }
-  if (b >= end) return false;
-  const LmDet& D = K.det[d];
-  const int lb = b - prev;
-  if (tl_cnt != nullptr && D.kind == 0) {
-    const int v = D.view, ng = (nslots + LM_INGEST_FB - 1) / LM_INGEST_FB;
-    const int cg = (ft * LM_INGEST_FB + WE - 1) / WE;
-#if LM_RW_IMAJOR
-    // runs of LM_RW_IMAJOR workgroups per slot group, the slot groups'
-    // first runs first: the workgroups past a segment's count sit at the
-    // grid's end
-    constexpr int IB = LM_RW_IMAJOR;
-    const int y = (lb / IB) % ng, i = lb / (IB * ng) * IB + lb % IB;
-    const int c = LM_TL_NC * y / ng, y0 = lm_tl_y0(c, ng);
-    if (i >= cg) return false;
-    const int first = WE * ((y - y0) * cg + i) + LM_RW_NQ * wave;
-#else
-    const int y = lb / cg, c = LM_TL_NC * y / ng, y0 = lm_tl_y0(c, ng);
-    const int first = WE * (lb - y0 * cg) + LM_RW_NQ * wave;  // the wave's first entry in the segment
-#endif
-    const int cnt = tl_cnt[v * LM_TL_NC + c];
-    if (first >= cnt) return false;
-    R = RwRun{tl_list + (int64_t)v * K.tl_stride + (int64_t)y0 * LM_INGEST_FB * K.fl_tx[v] * K.fl_ty[v] + first,
-              min(LM_RW_NQ, cnt - first), K.fl_tx[v], 0, 0, 0};
-    return true;
   }
-  const int local = WT * lb + wave, total = nt * nslots;
-  if (local >= total) return false;
-  const int lt = local % nt, tx = D.tiles_x;
-  R = RwRun{nullptr, LM_RW_NQ, 0, s0 + local / nt, (lt / tx) * LM_RW_TH, (lt % tx) * LM_TW};
-  return true;
+  return false;
 }
 
 // A workgroup tile of a point detector (k_corr_gen, k_corr_f16) whose flag
@@ -806,7 +810,8 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(K
   const RwArgs a{Kp, G, ext, ext_slot_bytes, weights, s0, nslots, keys, n_pos, tailbin, tailbin_slot_bytes, tl_cnt, tl_list};
   int d;
   RwRun R;
-  if (!corr_locate_rw(*a.K, a.G, a.nslots, a.s0, xcd_block(blockIdx.x, gridDim.x), wave, a.tl_cnt, a.tl_list, d, R))
+  if (!corr_locate_rw(*a.K, a.G, a.nslots, a.s0, xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, a.tl_cnt,
+                      a.tl_list, d, R))
     return;
   rw_tile<KW, UNF>(a, d, R, ring);
 }
@@ -827,7 +832,8 @@ __global__ __launch_bounds__(LM_RW_THREADS) __attribute__((amdgpu_waves_per_eu(L
   const RwArgs a{Kp, G, ext, ext_slot_bytes, weights, s0, nslots, keys, n_pos, tailbin, tailbin_slot_bytes, tl_cnt, tl_list};
   int d;
   RwRun R;
-  if (!corr_locate_rw(*a.K, a.G, a.nslots, a.s0, xcd_block(blockIdx.x, gridDim.x), wave, a.tl_cnt, a.tl_list, d, R))
+  if (!corr_locate_rw(*a.K, a.G, a.nslots, a.s0, xcd_block(blockIdx.x, gridDim.x) * LM_RW_WAVES + wave, a.tl_cnt,
+                      a.tl_list, d, R))
     return;
   switch (a.K->det[d].kw_ring) {
 #define LM_KW_CASE(n)           \
@@ -1228,26 +1234,12 @@ hipError_t launch_corr(const void* fn, bool ring, dim3 grid, int threads, size_t
                        const CorrDark& dk) {
   if (ring) {
     int nslots = (int)grid.y;
-    // workgroups per detector (corr_locate_rw): listed point detectors by the
-    // room of their view's list (CG per slot group), the others one wave per
-    // 80 x 16 tile
-    LmDetGroup Gl = G;
-    const int ng = (nslots + LM_INGEST_FB - 1) / LM_INGEST_FB;
-    constexpr int WE = LM_RW_PSTR * LM_RW_PASSES, WT = LM_RW_WAVES * LM_RW_PASSES;
-    int wg = 0;
-    for (int k = 0; k < G.n; ++k) {
-      const int nt = G.tile_end[k] - (k ? G.tile_end[k - 1] : 0);
-      if (dk.cnt != nullptr && G.ftiles[k] > 0)
-        wg += ng * (((G.ftiles[k] * LM_INGEST_FB + WE - 1) / WE + LM_RW_IMAJOR_B - 1) / LM_RW_IMAJOR_B * LM_RW_IMAJOR_B);
-      else
-        wg += (nt * nslots + WT - 1) / WT;
-      Gl.wg_end[k] = wg;
-    }
-    void* args[] = {(void*)&K,       (void*)&Gl,   (void*)&ext,     (void*)&ext_slot_bytes,
+    const unsigned waves = (unsigned)(G.tile_end[G.n - 1] * nslots);  // every 80 x 16 tile (corr_locate_rw)
+    void* args[] = {(void*)&K,       (void*)&G,    (void*)&ext,     (void*)&ext_slot_bytes,
                     (void*)&weights, (void*)&s0,   (void*)&nslots,  (void*)&keys,
                     (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes, (void*)&dk.cnt,
                     (void*)&dk.list};
-    return hipLaunchKernel(fn, dim3((unsigned)wg), dim3(LM_RW_THREADS), args, lds, st);
+    return hipLaunchKernel(fn, dim3((waves + LM_RW_WAVES - 1) / LM_RW_WAVES), dim3(LM_RW_THREADS), args, lds, st);
   }
   void* args[] = {(void*)&K,     (void*)&G,       (void*)&ext,     (void*)&ext_slot_bytes,           (void*)&weights,
                   (void*)&s0,    (void*)&keys,    (void*)&n_pos,   (void*)&tailbin, (void*)&tailbin_slot_bytes,

@@ -670,7 +670,6 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
       const int prev = G.n ? G.tile_end[G.n - 1] : 0;
       G.ids[G.n] = d;
       G.tile_end[G.n] = prev + D.tiles_x * D.tiles_y;
-      G.ftiles[G.n] = D.kind == 0 ? K.fl_tx[D.view] * K.fl_ty[D.view] : 0;
       ++G.n;
       if (ring) G.ring_floats = std::max(G.ring_floats, rw_ring_floats(D.kw_ring));
       P.lds[gi] = std::max(P.lds[gi], need);
@@ -939,8 +938,15 @@ void kprof_report(lm_ctx* c, Lane& L, int n) {
     long long t_min = 0, t_max = 0, worst = 0;
     int wb = -1;
     for (int b = 0; b < 2 * n; ++b) {
-      const long long* t = base + (size_t)b * 16;
-      if (!t[0] || !t[6]) continue;
+      const long long* t0 = base + (size_t)b * 16;
+      if (!t0[0] || !t0[6]) continue;
+      // a phase a block skips (e.g. phase 2 of a feature without side
+      // candidates) leaves its stamp at 0: it took no time (round 5 printed
+      // p2 = 0 - t1 and p3 = t3 - 0 for such blocks)
+      long long t[16];
+      for (int k = 0; k < 16; ++k) t[k] = t0[k];
+      for (int k = 1; k <= 6; ++k)
+        if (!t[k]) t[k] = t[k - 1];
       for (int k = 1; k <= 6; ++k) acc[k] += (double)(t[k] - t[k - 1]);
       life += (double)(t[6] - t[0]);
       if (t[6] - t[0] > worst) {
@@ -954,7 +960,10 @@ void kprof_report(lm_ctx* c, Lane& L, int n) {
     if (nb) {
       fprintf(stderr, "kprof k_post: blocks=%d life=%.0f cyc, span=%.1f us:", nb, life / nb, (t_max - t_min) * 0.01);
       for (int k = 1; k <= 6; ++k) fprintf(stderr, " p%d=%.0f", k, acc[k] / nb);
-      const long long* t = base + (size_t)wb * 16;
+      long long t[16];
+      for (int k = 0; k < 16; ++k) t[k] = base[(size_t)wb * 16 + k];
+      for (int k = 1; k <= 6; ++k)
+        if (!t[k]) t[k] = t[k - 1];
       fprintf(stderr, " | slowest blk %d cyc=%lld:", wb, worst);
       for (int k = 1; k <= 6; ++k) fprintf(stderr, " %lld", t[k] - t[k - 1]);
       fprintf(stderr, "\n");
