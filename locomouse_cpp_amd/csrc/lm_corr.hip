@@ -616,8 +616,11 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
   // flight.
   auto load_row = [&](int r) -> Row {
     Row w;
+    // the row offset is wave-uniform: keep it scalar (the compiler otherwise
+    // forms it with 64-bit vector multiplies in every step)
+    const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(min(r, nrows - 1) * ew4);
 #pragma unroll
-    for (int k = 0; k < NLD; ++k) w.v[k] = la[k][(int64_t)min(r, nrows - 1) * ew4];
+    for (int k = 0; k < NLD; ++k) w.v[k] = la[k][ro];
     return w;
   };
   auto store_row = [&](int r, Row w) {
