@@ -355,15 +355,26 @@ def rank_env(args):
 # ------------------------------------------------------------ one rank
 
 def resolve_shape(args):
-    """Contexts per GPU and frames per batch left unset on the command line:
-    8 x 448 for the C3 resident stream (the headline line), 4 x 256 for every
-    other config and mode."""
-    c3_stream = (args.config == "c3" and args.video_frames == 0 and not args.host_frames and args.lanes == 1
-                 and args.precision == "fp32" and args.workload == "detect")
+    """Contexts per GPU, pipeline lanes per context and frames per batch left
+    unset on the command line.  C3 fp32 detection: 8 contexts x 448 frames for
+    the resident stream (the headline line); for one video (--video-frames,
+    BASELINE config 4) by the rank's share of it -- up to 2,500 frames (the
+    8-GPU shard of the 10,000-frame video is 1,250): one context x 4 lanes in
+    6 equal batches, else 4 contexts x 2 lanes x 313 frames.  4 x 1 x 256 for
+    every other config and mode."""
+    c3 = args.config == "c3" and args.precision == "fp32" and args.workload == "detect" and not args.host_frames
+    shape = (4, 1, 256)
+    if c3 and args.video_frames == 0 and args.lanes in (None, 1):
+        shape = (8, 1, 448)
+    elif c3 and args.video_frames > 0:
+        share = -(-args.video_frames // max(1, args.gpus))
+        shape = (1, 4, max(1, -(-share // 6))) if share <= 2500 else (4, 2, 313)
     if args.streams is None:
-        args.streams = 8 if c3_stream else 4
+        args.streams = shape[0]
+    if args.lanes is None:
+        args.lanes = shape[1]
     if args.batch is None:
-        args.batch = 448 if c3_stream else 256
+        args.batch = shape[2]
     return args
 
 
@@ -381,9 +392,10 @@ def main():
     ap.add_argument("--streams", type=int, default=None,
                     help="contexts per GPU, each with its own host thread (default: 8 for the C3 resident stream, "
                          "else 4)")
-    ap.add_argument("--lanes", type=int, default=1,
+    ap.add_argument("--lanes", type=int, default=None,
                     help="pipeline lanes per context (lm_setup.pipeline_lanes: batches in flight on their own HIP "
-                         "streams, driven with lm_detect_submit / lm_detect_collect)")
+                         "streams, driven with lm_detect_submit / lm_detect_collect; default: 1, or for one C3 "
+                         "video 4 / 2 by the rank's share, see resolve_shape)")
     ap.add_argument("--video-frames", type=int, default=0,
                     help="strong scaling (BASELINE config 4): one video of this many frames sharded over the ranks; "
                          "steps = timed passes over the shard")
@@ -407,8 +419,11 @@ def main():
     # repetitions (profiles/r05/sweep/shape_b.txt; 5, 6, 10 contexts
     # slower), then 8 x 448 493.9k vs 8 x 320 486.6k over six
     # (shape_c.txt, shape_d.txt; 512 and 640 no better; 12 or 16 contexts,
-    # or 2 lanes each, no better either: shape_e.txt).  The other configs
-    # and modes keep the shapes they were measured with.
+    # or 2 lanes each, no better either: shape_e.txt).  One C3 video
+    # (profiles/r06/c4/): the whole 10,000 frames on one GPU 410k at
+    # 4 x 1 x 256, 440-447k at 4 x 2 x 256 / 313; the 1,250-frame shard
+    # 3.32 ms at 1 x 4 x 250, 3.08 ms at 1 x 4 x 209.  The other configs and
+    # modes keep the shapes they were measured with.
     resolve_shape(args)
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")

@@ -119,24 +119,30 @@ def test_executed_flops_counts_halo_slots():
 
 
 def test_default_shape_by_mode():
-    """Unset --streams / --batch: 8 contexts x 448 frames for the C3 resident
-    stream only (profiles/r05/sweep/), 4 x 256 for every other config and
-    mode; explicit values are kept."""
+    """Unset --streams / --lanes / --batch: 8 contexts x 448 frames for the C3
+    resident stream (profiles/r05/sweep/), by the rank's share for one C3
+    video (profiles/r06/c4/), 4 x 1 x 256 for every other config and mode;
+    explicit values are kept."""
     from types import SimpleNamespace
 
     def shape(**kw):
-        a = dict(config="c3", video_frames=0, host_frames=False, lanes=1, precision="fp32", workload="detect",
-                 streams=None, batch=None)
+        a = dict(config="c3", video_frames=0, host_frames=False, lanes=None, precision="fp32", workload="detect",
+                 streams=None, batch=None, gpus=1)
         a.update(kw)
         r = bench.resolve_shape(SimpleNamespace(**a))
-        return r.streams, r.batch
+        return r.streams, r.lanes, r.batch
 
-    assert shape() == (8, 448)
-    assert shape(config="c5") == (4, 256)
-    assert shape(video_frames=1250) == (4, 256)
-    assert shape(host_frames=True) == (4, 256)
-    assert shape(lanes=4) == (4, 256)
-    assert shape(precision="f16") == (4, 256)
-    assert shape(workload="bb") == (4, 256)
-    assert shape(streams=2, batch=100) == (2, 100)
-    assert shape(streams=2) == (2, 448)
+    assert shape() == (8, 1, 448)
+    assert shape(config="c5") == (4, 1, 256)
+    assert shape(video_frames=10000) == (4, 2, 313)
+    assert shape(video_frames=10000, gpus=8) == (1, 4, 209)  # a 1,250-frame shard: 6 batches
+    assert shape(video_frames=1250) == (1, 4, 209)
+    assert shape(video_frames=10000, config="c5") == (4, 1, 256)
+    assert shape(host_frames=True) == (4, 1, 256)
+    assert shape(lanes=4) == (4, 4, 256)
+    assert shape(lanes=1) == (8, 1, 448)
+    assert shape(precision="f16") == (4, 1, 256)
+    assert shape(workload="bb") == (4, 1, 256)
+    assert shape(streams=2, batch=100) == (2, 1, 100)
+    assert shape(streams=2) == (2, 1, 448)
+    assert shape(video_frames=10000, streams=8, batch=448) == (8, 2, 448)

@@ -85,9 +85,9 @@ def test_bench_video_mode_shards_whole_video(ranks, lanes):
 
 @pytest.mark.timeout(600)
 def test_bench_c4_eight_ranks_full_shape():
-    """BASELINE config 4 at its own shape: a 10,000-frame video as 8
-    contiguous 1,250-frame shards, one bench.py rank each (spawned by
-    bench.py --gpus 8, oversubscribed on this box's one GPU; the driver's
+    """BASELINE config 4 at its own shape and bench.py's default shape for it:
+    a 10,000-frame video as 8 contiguous 1,250-frame shards, one bench.py rank
+    each (spawned by bench.py --gpus 8, oversubscribed on this box's one GPU; the driver's
     node gives each rank its own GPU), every shard but the first with its
     predecessor frame as the halo.  Rank 0 gathers all 10,000 frames, checks
     them whole and disjoint, and compares every one with the oracle."""
@@ -97,12 +97,16 @@ def test_bench_c4_eight_ranks_full_shape():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--oversubscribe",
-                        "--video-frames", "10000", "--streams", "1", "--lanes", "4",
-                        "--steps", "1", "--warmup", "2", "--no-cpu"], env=env, capture_output=True, text=True,
+                        "--video-frames", "10000", "--steps", "1", "--warmup", "2", "--no-cpu"], env=env,
+                       capture_output=True, text=True,
                        timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 8 and line["scaling"] == "strong"
     assert line["config"]["shards"] == "8 x ceil(10000/8) frames"
+    # the default shape for a 1,250-frame share (bench.resolve_shape): one
+    # context x 4 lanes, 6 batches of <= 209 frames
+    assert (line["config"]["contexts_per_gpu"], line["config"]["lanes_per_context"]) == (1, 4)
+    assert line["config"]["batch_frames"] == 209 and line["config"]["batches"] == [6]
     assert line["gathered"]["frames"] == 10000 and line["gathered"]["whole_and_disjoint"]
     assert line["video_check"]["frames"] == 10000 and line["video_check"]["bit_exact"], line["video_check"]
