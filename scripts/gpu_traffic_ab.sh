@@ -21,7 +21,7 @@ for f in locomouse_cpp_amd/exp/liblocomouse_hip_*.so; do
     timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -f csv -d $O/$v/p$i -o run -- python3 bench.py --steps 4 --warmup 1 --no-cpu --no-check > $O/$v.p$i.out 2>&1 || { echo "$v pass $c failed"; tail -5 $O/$v.p$i.out; cp $O/orig.so $LIB; exit 1; }
   done
   mkdir -p $O/$v/pmc && cp -r $O/$v/p1 $O/$v/pmc/FETCH_SIZE && cp -r $O/$v/p2 $O/$v/pmc/WRITE_SIZE
-  python3 scripts/pmc_traffic.py $O/$v/pmc 256 $O/$v/pmc_k_corr.json > $O/$v/traffic.txt && echo "$v" && tail -3 $O/$v/traffic.txt
+  python3 scripts/pmc_traffic.py $O/$v/pmc ${TRAFFIC_BATCH:-448} $O/$v/pmc_k_corr.json > $O/$v/traffic.txt && echo "$v" && tail -3 $O/$v/traffic.txt
   python3 - $O/$v/p3 <<'PY'
 import csv, glob, sys
 from collections import defaultdict
