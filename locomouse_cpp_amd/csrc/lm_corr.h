@@ -87,9 +87,9 @@ __host__ __device__ constexpr int rw_qpitch(int kw) {
          ((LM_FW / 5 - ((LM_RW_HSLOTS + 1) * rw_stride(kw)) % 32) + 32) % 32;
 }
 __host__ __device__ constexpr int rw_ring_floats(int kw) { return LM_RW_NQ * rw_qpitch(kw); }
-__host__ __device__ constexpr size_t rw_lds_bytes(int kw) {
-  return (size_t)LM_RW_WAVES * rw_ring_floats(kw) * sizeof(float);
-}
+// LDS of one ring workgroup at width kw (defined in lm_corr.hip, so it
+// follows the LM_RW_WAVES that the ring kernels were built with)
+size_t corr_rw_lds(int kw);
 
 // k_corr_f16 (non-parity LM_CORR_F16 mode)
 #ifndef LM_F16_WAVES

@@ -1225,6 +1225,8 @@ const void* corr_kernel(int kw, bool unf) {
   }
 }
 
+size_t corr_rw_lds(int kw) { return (size_t)LM_RW_WAVES * rw_ring_floats(kw) * sizeof(float); }
+
 const void* corr_kernel_gen(bool unf) { return unf ? (const void*)&k_corr_gen<true> : (const void*)&k_corr_gen<false>; }
 
 const void* corr_kernel_rw_all(bool unf) {

@@ -650,7 +650,7 @@ void validate_and_build(lm_ctx* c, const lm_setup* su, const lm_params* P, const
         need = f16_lds_bytes(f16_nch(D.kw), D.kh);
       } else if (ring) {
         D.chunk_rows = D.kh;
-        need = rw_lds_bytes(D.kw_ring);
+        need = corr_rw_lds(D.kw_ring);
       } else {
         const size_t row = (size_t)pk_stride(LM_TW + D.kwp - 1) * sizeof(float);
         D.chunk_rows = std::max(1, std::min(D.kh, (int)(kCorrLdsBudget / row) - (LM_TH - 1)));
