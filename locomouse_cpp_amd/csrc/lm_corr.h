@@ -91,15 +91,13 @@ __host__ __device__ constexpr int rw_ring_floats(int kw) { return LM_RW_NQ * rw_
 // follows the LM_RW_WAVES that the ring kernels were built with)
 size_t corr_rw_lds(int kw);
 
-// k_corr_f16 (non-parity LM_CORR_F16 mode)
-#ifndef LM_F16_WAVES
-#define LM_F16_WAVES 4  // waves side by side, 32 output columns each (5: -4 % k_corr at C5 but fewer frames/s; C3 worse)
-#endif
-#define LM_F16_TW (32 * LM_F16_WAVES)
-#ifndef LM_F16_T
-#define LM_F16_T 2  // 32-row accumulator tiles per wave (2 or 4)
-#endif
-#define LM_F16_TH (32 * LM_F16_T)
+// k_corr_f16 (non-parity LM_CORR_F16 mode): 2 x 2 waves per workgroup, each
+// with two 32 x 32 accumulator tiles side by side -> a 128 x 64 output tile
+// (round 4: 5 waves of 32 columns, -4 % k_corr at C5 but fewer frames/s;
+// four 32-row tiles per wave, 130k vs 150k C5 frames/s at two waves per SIMD)
+#define LM_F16_WAVES 4
+#define LM_F16_TW 128
+#define LM_F16_TH 64
 #define LM_F16_THREADS (64 * LM_F16_WAVES)
 #define LM_F16_MAX_NCH 10
 

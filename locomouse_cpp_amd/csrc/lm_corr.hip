@@ -945,7 +945,10 @@ __global__ __launch_bounds__(LM_CORR_THREADS) void k_corr_gen(const LmConst* __r
 // L1 / L2 hits) into registers while it multiplies with row i's, using each
 // for its two 32 x 32 output tiles; the LDS holds only the window, and the
 // row loop has no barrier.
-// Four waves side by side: a 128 x 64 output tile per workgroup.
+// 2 x 2 waves: a 128 x 64 output tile per workgroup; each wave holds two
+// 32 x 32 tiles side by side, which share their A fragments (tile 1 at
+// window chunk m + 2 is tile 0 at chunk m: NCH + 2 LDS reads per detector row
+// for 2 NCH MFMAs instead of 2 NCH) and every B fragment.
 // Accumulator layout (32x32 MFMA): column = lane & 31, row = (reg & 3) +
 // 8 (reg >> 2) + 4 (lane >> 5).
 typedef _Float16 lm_h8 __attribute__((ext_vector_type(8)));
@@ -991,7 +994,7 @@ DEV void tile_fill_f16(_Float16* __restrict__ lds, int stride, const uint8_t* __
 }
 
 template <int NCH>
-__global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(NCH <= 7 && LM_F16_T == 2 ? 3 : 2))) void k_corr_f16(const LmConst* __restrict__ Kp, const LmDetGroup G,
+__global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(NCH <= 7 ? 3 : 2))) void k_corr_f16(const LmConst* __restrict__ Kp, const LmDetGroup G,
                                                             const uint8_t* __restrict__ ext, int64_t ext_slot_bytes,
                                                             const uint4* __restrict__ bfrag, int s0,
                                                             unsigned long long* __restrict__ keys,
@@ -1017,80 +1020,79 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  // 2 x 2 waves; wave (wx, wy) owns output columns 64 wx .. + 63 (two 32 x 32
+  // accumulator tiles side by side) of rows 32 wy .. + 31.  Tile 1's A
+  // fragment at window chunk m + 2 is tile 0's at chunk m, so a row's
+  // NCH + 2 A fragments feed both tiles: A_m x B_m into tile 0 (m < NCH),
+  // A_m x B_(m-2) into tile 1 (m >= 2).
+  static_assert(LM_F16_WAVES == 4 && LM_F16_TW == 128 && LM_F16_TH == 64, "2 x 2 waves of two 32 x 32 tiles");
+  const int wx = wave & 1, wy = wave >> 1;
+  constexpr int NS = NCH + 2;  // A steps per detector row
   const float init = D.delta * D.wscale;
-  lm_f32x16 acc[LM_F16_T];
+  lm_f32x16 acc[2];
 #pragma unroll
-  for (int t = 0; t < LM_F16_T; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[t][q] = init;
-  const _Float16* __restrict__ arow = img + r * STR + 32 * wave + 8 * h;
-  // B fragments straight from global memory (the same NCH KiB per detector
-  // row for every workgroup: L1/L2 hits), one row ahead in registers, so the
-  // row loop has no barrier (round 2 staged them through LDS with one
-  // __syncthreads per row)
+  const _Float16* __restrict__ arow = img + (32 * wy + r) * STR + 64 * wx + 8 * h;
   const lm_h8* __restrict__ bsrc = reinterpret_cast<const lm_h8*>(bfrag + D.w16_off) + lane;
-  // Detector rows in groups of three, flattened to 3 NCH (row, chunk) steps:
-  // step k's A fragments were read two steps earlier (a 3-deep register
+  // Detector rows in groups of three, flattened to 3 NM (row, A step)
+  // steps: step k's A fragment was read two steps earlier (a 3-deep register
   // ring), so an MFMA never waits on the LDS read issued right before it; B
-  // fragments of row i + 3 load while rows i + 1, i + 2 multiply (one row's
-  // MFMAs are shorter than an L2 hit under load).  With the group unrolled,
-  // every ring index is static.
-  lm_h8 bf[3][NCH], ar[3][LM_F16_T];
+  // fragments of row i + 3 load while rows i + 1, i + 2 multiply.  With the
+  // group unrolled, every ring index is static.
+  lm_h8 bf[3][NCH], ar[3];
   auto load_b = [&](lm_h8 (&b)[NCH], int i) {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) b[c] = bsrc[(int64_t)(i * NCH + c) * 64];
   };
-  // A wave's 32 x 32 accumulator tile t runs only when it holds an output
-  // (inside oh x ow) and, for a point detector, some output whose mouse pixel
-  // is > 25 (the rest are zeroed by the reference's mask and produce no key)
-  const int x = ox0 + 32 * wave + r;
-  const _Float16* __restrict__ mrow = img + (D.m_y - D.in_y) * STR + 32 * wave + r + (D.m_x - D.in_x);
-  // skip groups: the wave's upper and lower LM_F16_T / 2 tiles
-  static_assert(LM_F16_T == 2 || LM_F16_T == 4, "2 or 4 accumulator tiles per wave");
-  constexpr int TG = LM_F16_T / 2;
+  const int xb = ox0 + 64 * wx + r;  // tile t: column xb + 32 t
+  const int yb = oy0 + 32 * wy;
+  const _Float16* __restrict__ mrow = img + (D.m_y - D.in_y + 32 * wy) * STR + 64 * wx + r + (D.m_x - D.in_x);
+  // tile t runs only when it holds an output (inside oh x ow) and, for a
+  // point detector, some output whose mouse pixel is > 25 (the rest are
+  // zeroed by the reference's mask and produce no key)
   bool on[2];
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
+  for (int t = 0; t < 2; ++t) {
     bool any = false;
+    if (xb + 32 * t < D.ow && yb < D.oh) {
+      if (D.kind != 0) {
+        any = true;
+      } else {
 #pragma unroll
-    for (int t = g * TG; t < (g + 1) * TG; ++t)
-      if (x < D.ow && oy0 + 32 * t < D.oh) {
-        if (D.kind != 0) {
-          any = true;
-        } else {
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int ly = 32 * t + 16 * h + q;
-            any |= oy0 + ly < D.oh && (float)mrow[ly * STR] > 25.0f;
-          }
+        for (int q = 0; q < 16; ++q) {
+          const int ly = 16 * h + q;
+          any |= yb + ly < D.oh && (float)mrow[ly * STR + 32 * t] > 25.0f;
         }
       }
-    on[g] = __builtin_amdgcn_readfirstlane(__ballot(any) != 0 ? 1 : 0) != 0;
+    }
+    on[t] = __builtin_amdgcn_readfirstlane(__ballot(any) != 0 ? 1 : 0) != 0;
   }
   auto mma_all = [&](auto c0, auto c1) {
-    constexpr bool ONG[2] = {decltype(c0)::value, decltype(c1)::value};
-    auto load_a = [&](lm_h8 (&a)[LM_F16_T], int i, int c) {
-      const _Float16* __restrict__ ai = arow + min(i, kh - 1) * STR + 16 * c;
-#pragma unroll
-      for (int t = 0; t < LM_F16_T; ++t)
-        if (ONG[t / TG]) a[t] = *reinterpret_cast<const lm_h8*>(ai + 32 * t * STR);
+    constexpr bool ON0 = decltype(c0)::value, ON1 = decltype(c1)::value;
+    constexpr int M0 = ON0 ? 0 : 2, M1 = ON1 ? NS : NCH;  // the A steps a row needs
+    constexpr int NM = M1 - M0;
+    auto load_a = [&](lm_h8& a, int i, int m) { a = *reinterpret_cast<const lm_h8*>(arow + min(i, kh - 1) * STR + 16 * (M0 + m)); };
+    auto mma = [&](const lm_h8& a, lm_h8 (&b)[NCH], int m) {
+      const int mm = M0 + m;
+      if (ON0 && mm < NCH) acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[mm < NCH ? mm : 0], acc[0], 0, 0, 0);
+      if (ON1 && mm >= 2) acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[mm >= 2 ? mm - 2 : 0], acc[1], 0, 0, 0);
     };
 #pragma unroll
     for (int q = 0; q < 3; ++q)
       if (q < kh) load_b(bf[q], q);
     load_a(ar[0], 0, 0);
-    load_a(ar[1], 1 / NCH, 1 % NCH);
+    load_a(ar[1], 1 / NM, 1 % NM);
     int i = 0;
     for (; i + 2 < kh; i += 3) {
 #pragma unroll
-      for (int k = 0; k < 3 * NCH; ++k) {
-        const int q = k / NCH, c = k % NCH, k2 = k + 2;
-        load_a(ar[k2 % 3], i + k2 / NCH, k2 % NCH);
+      for (int k = 0; k < 3 * NM; ++k) {
+        const int q = k / NM, m = k % NM, k2 = k + 2;
+        load_a(ar[k2 % 3], i + k2 / NM, k2 % NM);
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 0; t < LM_F16_T; ++t)
-          if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ar[k % 3][t], bf[q][c], acc[t], 0, 0, 0);
-        if (c == NCH - 1 && i + q + 3 < kh) load_b(bf[q], i + q + 3);
+        mma(ar[k % 3], bf[q], m);
+        if (m == NM - 1 && i + q + 3 < kh) load_b(bf[q], i + q + 3);
       }
     }
     // the last kh % 3 rows (their B fragments are in bf[0], bf[1])
@@ -1098,12 +1100,10 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
     for (int q = 0; q < 2; ++q)
       if (i + q < kh)
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          lm_h8 a[LM_F16_T];
-          load_a(a, i + q, c);
-#pragma unroll
-          for (int t = 0; t < LM_F16_T; ++t)
-            if (ONG[t / TG]) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[t], bf[q][c], acc[t], 0, 0, 0);
+        for (int m = 0; m < NM; ++m) {
+          lm_h8 a;
+          load_a(a, i + q, m);
+          mma(a, bf[q], m);
         }
   };
   using T1 = std::true_type;
@@ -1116,33 +1116,33 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
     mma_all(F0{}, T1{});
 
   if (D.kind != 0) {
-    // bits straight from a ballot: this wave owns u32 word (ox0 / 32 + wave) of
-    // each of its rows (lanes 0-31: row y, lanes 32-63: row y + 4)
+    // bits straight from a ballot: this wave owns u32 words (ox0 / 32 + 2 wx + t)
+    // of its rows (lanes 0-31: row y, lanes 32-63: row y + 4)
     unsigned* __restrict__ tb = reinterpret_cast<unsigned*>(tailbin + (int64_t)slot * tailbin_slot_bytes) +
                                 (D.list ? (int64_t)K.tail_hb * K.tail_nw : 0);
-    const int gw = (ox0 >> 5) + wave;
 #pragma unroll
-    for (int t = 0; t < LM_F16_T; ++t)
+    for (int t = 0; t < 2; ++t) {
+      const int gw = (ox0 >> 5) + 2 * wx + t, x = xb + 32 * t;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int y = oy0 + 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const int y = yb + (q & 3) + 8 * (q >> 2) + 4 * h;
         const unsigned long long m = __ballot(y < D.oh && x < D.ow && acc[t][q] > 0.0f);
         if ((lane & 31) == 0 && y < D.oh && gw < K.tail_nw) tb[(int64_t)y * K.tail_nw + gw] = (unsigned)(m >> (32 * h));
       }
+    }
     return;
   }
-  using Bits = std::conditional_t<(LM_F16_T > 2), unsigned long long, unsigned>;
-  Bits bits = 0;
+  unsigned bits = 0;
 #pragma unroll
-  for (int t = 0; t < LM_F16_T; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int ly = 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
-      const int y = oy0 + ly;
-      const float pix = (float)mrow[ly * STR];
-      if (y < D.oh && x < D.ow && pix > 25.0f && acc[t][q] > 0.0f) bits |= (Bits)1 << (16 * t + q);
+      const int ly = (q & 3) + 8 * (q >> 2) + 4 * h;
+      const int y = yb + ly, x = xb + 32 * t;
+      const float pix = (float)mrow[ly * STR + 32 * t];
+      if (y < D.oh && x < D.ow && pix > 25.0f && acc[t][q] > 0.0f) bits |= 1u << (16 * t + q);
     }
-  const int nk = LM_F16_T > 2 ? __popcll((unsigned long long)bits) : __popc((unsigned)bits);
+  const int nk = __popc(bits);
   const int off = nk ? atomicAdd(&s_cnt, nk) : 0;
   __syncthreads();
   if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&n_pos[slot * LM_NLIST + D.list], s_cnt) : 0;
@@ -1150,11 +1150,11 @@ __global__ __launch_bounds__(LM_F16_THREADS) __attribute__((amdgpu_waves_per_eu(
   unsigned long long* __restrict__ kl = keys + (int64_t)slot * K.keys_per_slot + K.list_off[D.list] + s_base + off;
   int k = 0;
 #pragma unroll
-  for (int t = 0; t < LM_F16_T; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int q = 0; q < 16; ++q)
-      if (bits & ((Bits)1 << (16 * t + q))) {
-        const int y = oy0 + 32 * t + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (bits & (1u << (16 * t + q))) {
+        const int y = yb + (q & 3) + 8 * (q >> 2) + 4 * h, x = xb + 32 * t;
         const float score = acc[t][q] * D.inv_wscale;
         kl[k++] = ((unsigned long long)(~__float_as_uint(score)) << 32) | (unsigned)(y * D.ow + x);
       }
