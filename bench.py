@@ -45,7 +45,7 @@ CONFIGS = {  # BASELINE.json configs with a GPU bench line: (rows, cols, descrip
 FP32_PEAK_TFLOPS = 157.3   # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
 F16_PEAK_TFLOPS = 2500.0   # MI355X dense f16 MFMA peak (MI355X_MICROARCH.md: ~2.5 PF dense)
 HBM_PEAK_GBS = 8000.0
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc_k_corr.json")  # this tree's PMC passes at the default shape (scripts/gpu_r5.sh step traffic, profiles/r05/final4/)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r06", "pmc_k_corr.json")  # this tree's PMC passes at the default shape (scripts/gpu_r6.sh step traffic)
 
 
 def algorithmic_flops_per_frame(ctx):
