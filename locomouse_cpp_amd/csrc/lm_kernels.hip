@@ -1519,6 +1519,9 @@ DEV double readlane_f64(double v, int lane) {
 #ifndef LM_NMS_PREHASH
 #define LM_NMS_PREHASH 1
 #endif
+#ifndef LM_NMS_TIE_PRIO
+#define LM_NMS_TIE_PRIO 3  // s_setprio of a tie block's waves (0: as every block)
+#endif
 #define NMS_PROF(k) \
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + (k)] = clock64();
 template <bool GLOB>
@@ -1614,6 +1617,11 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   }
   const int tie = s_flag;
   if (tie) {  // (GLOB: the row-major re-sort below is the single-thread replica)
+    // A tie block is the launch's slowest (the replica's levels, then the
+    // same clustering as every block) and shares its CU with three others
+    // that end far earlier: its waves take issue priority for the rest of
+    // the block, so the span is more nearly its own length.
+    __builtin_amdgcn_s_setprio(LM_NMS_TIE_PRIO);
     // exact score tie: std::sort from the row-major order nmsMax builds (:1638-1648)
     for (int k = threadIdx.x; k < n; k += blockDim.x) {
       const unsigned long long v = a[k];
