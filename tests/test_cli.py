@@ -321,6 +321,36 @@ def test_cli_end_to_end_matches_oracle(tmp_path, variant):
     assert np.array_equal(m.astype(np.int32), np.array(ref["tracks_tail"], np.int32))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("multi", [False, True])
+def test_cli_timing_split(tmp_path, multi):
+    """LM_TIMING=1 (not in the reference): the program prints one LM_TIMING
+    line with its wall split (scripts/cli_e2e_mjpeg.py reads it for the
+    10,000-frame MJPEG run).  On a 40-frame MJPEG video in 16-frame batches
+    (or 7-frame shards over four "devices"): every field present and >= 0,
+    the decode inside the frame loop, every frame counted, the batches
+    handed over, and the output YAML written as without the variable."""
+    n = 40
+    cfg = S.SyntheticConfig()
+    paths = MW.write_inputs(str(tmp_path), cfg, n, stem="mouse_R", bits=24,
+                            jpeg=dict(mode="RGB", quality=92, subsampling=2))
+    env = dict(MULTI_DEVICE_ENV, LM_BATCH="7", LM_TIMING="1") if multi else {"LM_BATCH": "16", "LM_TIMING": "1"}
+    rc, out = run_cli(cli_args(paths, side="R", outdir=str(tmp_path)), env=env)
+    assert rc == 0, out
+    lines = [ln for ln in out.splitlines() if ln.startswith("LM_TIMING ")]
+    assert len(lines) == 1, out
+    f = lines[0].split()[1:]
+    t = {k: float(v) for k, v in zip(f[::2], f[1::2])}
+    keys = ("init_ms", "loop_ms", "tracks_ms", "export_ms", "decode_ms", "decode_threads", "submit_ms", "wait_ms",
+            "batches", "frames")
+    assert set(keys) <= set(t), t
+    assert all(t[k] >= 0 for k in keys), t
+    assert t["frames"] == n and t["decode_threads"] >= 1
+    assert t["batches"] == (6 if multi else 3), t  # ceil(40 / 7) shards, ceil(40 / 16) batches
+    assert t["decode_ms"] <= t["loop_ms"] + 1e-6, t
+    assert os.path.exists(tmp_path / "output_mouse_R.yml")
+
+
 def _load_cv_yaml(path):
     """An independent reader for the FileStorage YAML (PyYAML, safe loader with
     a constructor for !!opencv-matrix)."""
