@@ -566,8 +566,19 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
   R.tile(q, R.entry(q), slot, oy0, ox0);
   const bool valid = q < R.nvalid;
   // row loads: load k of a lane is dword dk of sub-tile qk's window row
-  // (e = lane + 64 k = qk NL + dk), stored at float lo[k] of the rings
-  const unsigned* __restrict__ la[NLD];
+  // (e = lane + 64 k = qk NL + dk), stored at float lo[k] of the rings.  They
+  // are buffer loads from the wave's lowest slot: the base in a buffer
+  // resource (SGPRs), the row offset a scalar, and a 32-bit byte offset per
+  // lane, so no load needs vector address arithmetic.  A wave's sub-tiles
+  // come from one list segment (the slots of one k_ingest workgroup per 64 of
+  // them) or one slot, so the lane offsets stay far below 4 GiB.
+  int smin = slot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) smin = min(smin, __shfl_xor(smin, o));
+  smin = __builtin_amdgcn_readfirstlane(smin);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(vext + (int64_t)smin * A.ext_slot_bytes), 0, (int)0xFFFFFFFF, 0x00020000);
+  unsigned la[NLD];
   int lo[NLD];
   bool lk[NLD];
 #pragma unroll
@@ -577,9 +588,8 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
     int sk, yk, xk;
     const int ik = min(qk, NQ - 1);  // lanes past the last sub-tile: a valid address, the value unused
     R.tile(ik, R.entry(ik), sk, yk, xk);
-    la[k] = reinterpret_cast<const unsigned*>(vext + (int64_t)sk * A.ext_slot_bytes + (int64_t)(D.in_y + yk) * ew +
-                                              (D.in_x + xk - mis)) +
-            dk;
+    la[k] = (unsigned)((int64_t)(sk - smin) * A.ext_slot_bytes + (int64_t)(D.in_y + yk) * ew + (D.in_x + xk - mis)) +
+            4u * (unsigned)dk;
     lo[k] = qk * QP + 4 * dk;
   }
 
@@ -618,9 +628,9 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
     Row w;
     // the row offset is wave-uniform: keep it scalar (the compiler otherwise
     // forms it with 64-bit vector multiplies in every step)
-    const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(min(r, nrows - 1) * ew4);
+    const int ro = __builtin_amdgcn_readfirstlane(min(r, nrows - 1) * ew);
 #pragma unroll
-    for (int k = 0; k < NLD; ++k) w.v[k] = la[k][ro];
+    for (int k = 0; k < NLD; ++k) w.v[k] = __builtin_amdgcn_raw_buffer_load_b32(wrsrc, (int)la[k], ro, 0);
     return w;
   };
   auto store_row = [&](int r, Row w) {
