@@ -566,7 +566,7 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
   R.tile(q, R.entry(q), slot, oy0, ox0);
   const bool valid = q < R.nvalid;
   // row loads: load k of a lane is dword dk of sub-tile qk's window row
-  // (e = lane + 64 k = qk NL + dk), stored at float lo[k] of the rings.  They
+  // (e = lane + 64 k = qk NL + dk), stored at LDS byte address lo[k] of the rings.  They
   // are buffer loads from the wave's lowest slot: the base in a buffer
   // resource (SGPRs), the row offset a scalar, and a 32-bit byte offset per
   // lane, so no load needs vector address arithmetic.  A wave's sub-tiles
@@ -579,7 +579,7 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
   const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint8_t*>(vext + (int64_t)smin * A.ext_slot_bytes), 0, (int)0xFFFFFFFF, 0x00020000);
   unsigned la[NLD];
-  int lo[NLD];
+  int lo[NLD];  // LDS byte address of the load's ring column (row 0)
   bool lk[NLD];
 #pragma unroll
   for (int k = 0; k < NLD; ++k) {
@@ -590,7 +590,7 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
     R.tile(ik, R.entry(ik), sk, yk, xk);
     la[k] = (unsigned)((int64_t)(sk - smin) * A.ext_slot_bytes + (int64_t)(D.in_y + yk) * ew + (D.in_x + xk - mis)) +
             4u * (unsigned)dk;
-    lo[k] = qk * QP + 4 * dk;
+    lo[k] = (int)(unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)(ring + qk * QP + 4 * dk);
   }
 
   // brightness mask of the point detectors' outputs (crop pixel > 25), read
@@ -636,14 +636,17 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
   auto store_row = [&](int r, Row w) {
     if (r >= nrows) return;
     const int s = r % HS;  // r is wave-uniform: scalar arithmetic
+    // the slot's byte offset as one scalar (else the compiler adds two per store)
+    const int so = __builtin_amdgcn_readfirstlane(s * STR * (int)sizeof(float));
 #pragma unroll
     for (int k = 0; k < NLD; ++k)
       if (lk[k]) {
         const unsigned v = w.v[k];
-        const float4 f = make_float4((float)(v & 0xFFu), (float)((v >> 8) & 0xFFu), (float)((v >> 16) & 0xFFu),
-                                     (float)(v >> 24));
-        *reinterpret_cast<float4*>(ring + lo[k] + s * STR) = f;
-        if (s == 0) *reinterpret_cast<float4*>(ring + lo[k] + HS * STR) = f;
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v f = {(float)(v & 0xFFu), (float)((v >> 8) & 0xFFu), (float)((v >> 16) & 0xFFu), (float)(v >> 24)};
+        typedef __attribute__((address_space(3))) f4v lds_f4;
+        *reinterpret_cast<lds_f4*>((uintptr_t)(unsigned)(lo[k] + so)) = f;
+        if (s == 0) *reinterpret_cast<lds_f4*>((uintptr_t)(unsigned)(lo[k] + HS * STR * (int)sizeof(float))) = f;
       }
   };
   {
