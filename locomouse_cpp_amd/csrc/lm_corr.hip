@@ -662,8 +662,9 @@ DEV __attribute__((always_inline)) void rw_tile(const RwArgs& A, int dix, const 
   const unsigned ring_base = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) float*)ring +
                              (unsigned)(q * QP * (int)sizeof(float));
   const unsigned lane_off = (unsigned)((lx * PK_C + mis) * (int)sizeof(float));
-  auto row_base = [&](int t) -> unsigned {
-    return ring_base + (unsigned)((t % HS) * STR * (int)sizeof(float)) + lane_off;
+  const unsigned ring_lane = ring_base + lane_off;
+  auto row_base = [&](int t) -> unsigned {  // the slot offset as one scalar: one vector add per row
+    return ring_lane + (unsigned)__builtin_amdgcn_readfirstlane((t % HS) * STR * (int)sizeof(float));
   };
   RwPipe<KW, UNF> S;
 #pragma unroll
