@@ -107,6 +107,8 @@ struct Lane {
   DevBuf<uint8_t> dark_flags;  // dark tiles (CorrDark): flag bytes, bright-tile lists and counts
   DevBuf<uint32_t> dark_list;
   DevBuf<int32_t> dark_cnt;
+  HostBuf<int32_t> h_cnt;   // debug bit 1: dark_cnt of the submitted batch, copied on its stream
+  bool h_cnt_valid = false;
   DevBuf<long long> kprof;  // LM_KPROF=1: kernel phase timestamps
   DevBuf<long long> kprof_ing;  // LM_KPROF=1: k_ingest's, 16 per workgroup
   Arena arena[2];
@@ -785,6 +787,7 @@ void lane_alloc(lm_ctx* c, Lane& L) {
     SET_SYNC(L.dark_flags.p, 0, (size_t)K.fl_slot * ns, st);
     L.dark_list.alloc((size_t)2 * K.tl_stride);
     L.dark_cnt.alloc(4 * LM_TL_NC);
+    L.h_cnt.alloc(4 * LM_TL_NC);
   }
   L.err.alloc(16);
   L.frame_ptr.alloc(ns);
@@ -871,8 +874,14 @@ struct Timer {  // HIP events around the timed kernels of a lane's batch (debug 
     L.t_ev.clear();
     for (int k = 0; k < 4; ++k) L.t_work[k] = -1;
     if (L.dark_cnt.p) {  // the segment counters summed per view
+      // normally copied on the batch's stream when it was submitted (no
+      // synchronous copy on the host's path); the timing was switched on
+      // after that submit: copy now
       int32_t h[4 * LM_TL_NC];
-      COPY_SYNC(h, L.dark_cnt.p, sizeof(h), hipMemcpyDeviceToHost, L.stream);
+      if (L.h_cnt_valid)
+        std::copy(L.h_cnt.p, L.h_cnt.p + 4 * LM_TL_NC, h);
+      else
+        COPY_SYNC(h, L.dark_cnt.p, sizeof(h), hipMemcpyDeviceToHost, L.stream);
       for (int k = 0; k < 4; ++k) L.t_work[k] = std::accumulate(h + k * LM_TL_NC, h + (k + 1) * LM_TL_NC, 0);
     }
   }
@@ -1474,6 +1483,9 @@ void submit_batch(lm_ctx* c, const uint8_t* frames, int64_t pitch, int n, int fi
   P.pack = c->take_pack((size_t)L.arena[P.cur].pack_cap);
   try {
     launch_attempt(c, L, 0);
+    L.h_cnt_valid = (c->debug & 2) && L.dark_cnt.p;
+    if (L.h_cnt_valid)
+      HIPCHK(hipMemcpyAsync(L.h_cnt.p, L.dark_cnt.p, 4 * LM_TL_NC * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(L.ev_done, st));
   } catch (...) {
     // kernels of this batch may already be enqueued: the lane (and the pack
@@ -1517,7 +1529,10 @@ void finish_batch(lm_ctx* c, Lane& L) {
   const int n = P.n, first = P.first;
   HIPCHK(hipSetDevice(c->device));
   for (int attempt = 0;; ++attempt) {
-    if (attempt > 0) launch_attempt(c, L, attempt);
+    if (attempt > 0) {
+      launch_attempt(c, L, attempt);
+      L.h_cnt_valid = false;  // (the counters of the rerun: read synchronously)
+    }
     HIPCHK(hipStreamSynchronize(st));
     Arena& A = L.arena[P.cur];
     const LmPackHdr& ph = *L.h_ph.p;
