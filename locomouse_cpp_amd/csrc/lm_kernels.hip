@@ -1519,12 +1519,6 @@ DEV double readlane_f64(double v, int lane) {
 #ifndef LM_NMS_PREHASH
 #define LM_NMS_PREHASH 1
 #endif
-#ifndef LM_NMS_BIG_PRIO
-#define LM_NMS_BIG_PRIO 0  // s_setprio of blocks with >= LM_NMS_BIG_N keys (0: off)
-#endif
-#ifndef LM_NMS_BIG_N
-#define LM_NMS_BIG_N 256
-#endif
 #ifndef LM_NMS_TIE_PRIO
 #define LM_NMS_TIE_PRIO 3  // s_setprio of a tie block's waves (0: as every block)
 #endif
@@ -1566,11 +1560,7 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   NMS_PROF(1)
   const int n = s_n;
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 13] = n;
-#if LM_NMS_BIG_PRIO
-  // long lists are the launch's slowest blocks: issue priority over the
-  // short ones sharing their CU
-  if (n >= LM_NMS_BIG_N) __builtin_amdgcn_s_setprio(LM_NMS_BIG_PRIO);
-#endif
+
   int np = 1;
   while (np < n) np <<= 1;
   // Exact score ties, found before sorting (an LDS hash set of the score
