@@ -1560,7 +1560,6 @@ DEV auto nms_run(const LmConst& K, const LmDet& D, LmSlotOut* H, int slot, int l
   NMS_PROF(1)
   const int n = s_n;
   if (prof && threadIdx.x == 0) prof[(blockIdx.x * 2 + (blockIdx.y & 1)) * 16 + 13] = n;
-
   int np = 1;
   while (np < n) np <<= 1;
   // Exact score ties, found before sorting (an LDS hash set of the score
