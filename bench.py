@@ -419,7 +419,9 @@ def main():
     # repetitions (profiles/r05/sweep/shape_b.txt; 5, 6, 10 contexts
     # slower), then 8 x 448 493.9k vs 8 x 320 486.6k over six
     # (shape_c.txt, shape_d.txt; 512 and 640 no better; 12 or 16 contexts,
-    # or 2 lanes each, no better either: shape_e.txt).  One C3 video
+    # or 2 lanes each, no better either: shape_e.txt; re-checked on round 6's
+    # final kernels, 8 x 512 and 10 x 448 within noise:
+    # profiles/r06/corr_ab/r6s_c3_shape.txt).  One C3 video
     # (profiles/r06/c4/): the whole 10,000 frames on one GPU 410k at
     # 4 x 1 x 256, 440-447k at 4 x 2 x 256 / 313; the 1,250-frame shard
     # 3.32 ms at 1 x 4 x 250, 3.08 ms at 1 x 4 x 209.  The other configs and
